@@ -1,0 +1,156 @@
+/*
+ * rtsn.h -- C ABI of the MI355X-native S_n radiative-transfer solver
+ * (librtsn.so).  Drop-in for the Solver / ParameterHandler surface of
+ * Helblindi/radiative-transfer; plain pointers and sizes, no C++/torch types.
+ *
+ * The reference has no C ABI: its boundary is the C++ classes
+ *   ParameterHandler(const string)                 include/ParameterHandler.h:67
+ *   Solver(ParameterHandler&, Tensor3& psi, Ref<MatrixXd> phi, Ref<MatrixXd> F)
+ *                                                  include/solver.h:79-83
+ *   void solve()                                   include/solver.h:92
+ *   compute_angle_integrated_intensity / compute_positive_angle_integrated_intensity /
+ *   compute_radiative_flux / compute_balance       include/solver.h:85-88
+ *   get_balance / get_phi_plus / get_e_ave / compute_group_ends / get_ends
+ *                                                  include/solver.h:89-97
+ * Each entry point below names the member it replaces.  Where the reference
+ * asserts or exit(1)s, these functions return an rt_status instead.
+ *
+ * Array layouts are the reference's Eigen ColMajor layouts:
+ *   psi  (M, G, N)    index i + M*(g + G*c)          main.cc:88
+ *   ends (M, G, N, 2) index i + M*(g + G*(c + N*s))  solver.h:135
+ *   phi / F / phi_plus (G, N) index g + G*c          main.cc:91-92, solver.h:131
+ * where G is the number of groups held by the handle (all groups, or the
+ * [g_lo, g_hi) shard given to rt_create_from_params).
+ *
+ * Threading: one handle per host thread; every call on a handle is ordered on
+ * the handle's own HIP stream (rt_stream).  Host-buffer getters synchronise.
+ */
+#ifndef RTSN_H
+#define RTSN_H
+
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum {
+  RT_OK = 0,
+  RT_ERR_IO = 1,          /* a group table could not be opened (ParameterHandler.cpp:146-149 exit(1)) */
+  RT_ERR_PARSE = 2,       /* std::stoi / std::stod would throw (param.cpp:452,466) */
+  RT_ERR_PARAM = 3,       /* invalid configuration (odd M -> mu = 0 assert solver.cpp:402, bad BC :660, ...) */
+  RT_ERR_VALIDATION = 4,  /* assert(validate_correction()) would fire (solver.cpp:609-612) */
+  RT_ERR_NOMEM = 5,       /* host or device allocation failed */
+  RT_ERR_DEVICE = 6,      /* HIP runtime error / no usable gfx950 device */
+  RT_ERR_TIMEOUT = 7,     /* an in-kernel inter-workgroup wait timed out (never expected) */
+  RT_ERR_ARG = 8          /* NULL handle / bad argument */
+} rt_status;
+
+/* Every .prm key (ParameterHandler.cpp:100-212) with the reference's meaning.
+ * Pointer members are borrowed (caller-owned) and may be NULL. */
+typedef struct {
+  int M;                         /* angle quadrature order (even) */
+  int G;                         /* energy groups */
+  int N;                         /* cells */
+  double efirst, elast;          /* log group grid (solver.cpp:6-19) when no bounds table */
+  double X;                      /* slab thickness; dx = X / N */
+  int bc_left_indicator;         /* 0 vacuum (falls through to source, solver.cpp:668), 1 source, 2 reflective */
+  int bc_right_indicator;        /* 0 vacuum, 1 source, 2 reflective (= vacuum in the reference) */
+  int use_mg_equilib;            /* psi_source from computeEquilibriumSources (solver.cpp:287-315) */
+  double rho, kappa_grey, T, V;
+  int use_correction;
+  int ts_method;                 /* 1 BE, 2 CN, 3 BDF2 (4 substeps per step) */
+  double dt;
+  int max_timesteps;
+  int include_validation;
+  const double *psi_source;      /* M*G, element (m, g) at m*G + g (ParameterHandler.cpp:126-132); NULL = zeros */
+  const double *group_bounds;    /* G+1 edges (have_group_bounds) or NULL */
+  const double *group_kappa;     /* G opacities (have_group_absorption_opacities) or NULL */
+} rt_params;
+
+typedef struct rt_solver rt_solver;
+
+/* ---- host-only configuration (no device calls) ------------------------- */
+
+/* ParameterHandler(filename) (ParameterHandler.cpp:12-17, 100-212): parses the
+ * .prm with the kaityo256/param semantics.  Tables are read from
+ * table_dir + name; table_dir NULL means the reference's "../prm/" relative
+ * to the working directory.  A missing .prm yields the defaults (as in the
+ * reference) and *prm_found = 0.  The returned arrays are owned by the
+ * library: release with rt_params_free. */
+rt_status rt_params_load(const char *prm_path, const char *table_dir, rt_params *out, int *prm_found);
+void rt_params_free(rt_params *p);
+void rt_params_default(rt_params *out); /* defaults of get_parameters, no arrays */
+
+/* Host physics the solver is built from (per-run constants; T is constant).
+ * GLQuad(M, 4 pi).mu()/wt() (GLQuad.cpp:4-44). */
+rt_status rt_quadrature(int M, double *mu, double *wt);
+/* Planck::get_Planck(T, edges) (Planck.cpp:50-77) times kcon -- the group
+ * emission B_g [jk/cm^2/sh] and dB/dT_g (correction.cpp:25-36). */
+rt_status rt_planck_groups(double T, int G, const double *e_edge, double *B, double *dBdT);
+
+/* ---- solver lifecycle --------------------------------------------------- */
+
+/* ParameterHandler(prm_path) + Solver ctor (solver.cpp:46-188): psi = B_g. */
+rt_status rt_create(const char *prm_path, const char *table_dir, int device, rt_solver **out);
+/* Same from an explicit configuration.  Only groups [g_lo, g_hi) get device
+ * state (energy groups are independent for the whole run because T is
+ * constant); all G groups' coefficients are still computed (the last Planck
+ * group is a remainder, Planck.cpp:73-76).  g_hi <= 0 means G. */
+rt_status rt_create_from_params(const rt_params *p, int g_lo, int g_hi, int device, rt_solver **out);
+void rt_destroy(rt_solver *s);
+
+/* Solver::solve (solver.cpp:590-823): max_timesteps full steps (x4 substeps
+ * for BDF2), preceded by computeEquilibriumSources when use_mg_equilib.
+ * Synchronous. */
+rt_status rt_solve(rt_solver *s);
+/* Asynchronous: enqueue nsteps full steps on the handle's stream. */
+rt_status rt_advance(rt_solver *s, int nsteps);
+rt_status rt_synchronize(rt_solver *s);
+/* hipStream_t of the handle, as void*. */
+void *rt_stream(rt_solver *s);
+
+/* ---- results (host buffers, reference layouts) ------------------------- */
+rt_status rt_get_dims(rt_solver *s, int *M, int *G_local, int *N, int *g_lo, int *g_hi);
+rt_status rt_get_psi(rt_solver *s, double *psi);                /* psi_mat_ref */
+rt_status rt_get_ends(rt_solver *s, double *ends);              /* Solver::ends */
+rt_status rt_set_ends(rt_solver *s, const double *ends);        /* test hook: load a state */
+/* compute_angle_integrated_intensity, compute_radiative_flux,
+ * compute_positive_angle_integrated_intensity (solver.cpp:191-237); any NULL skipped */
+rt_status rt_get_moments(rt_solver *s, double *phi, double *F, double *phi_plus);
+/* compute_group_ends + get_ends("left"/"right") (solver.cpp:826-864) */
+rt_status rt_get_group_ends(rt_solver *s, double *left, double *right);
+/* compute_balance + get_balance (solver.cpp:240-284) */
+rt_status rt_get_balance(rt_solver *s, double *balance);
+/* get_e_ave (solver.h:194): all G groups */
+rt_status rt_get_e_ave(rt_solver *s, double *e_ave);
+/* Group data of all G groups: e_edge (G+1), B, dBdT, kappa (G); any NULL skipped. */
+rt_status rt_get_group_data(rt_solver *s, double *e_edge, double *B, double *dBdT, double *kappa);
+rt_status rt_get_quadrature(rt_solver *s, double *mu, double *wt);
+/* Solver-owned psi_source (M*G, m*G+g) after construction / equilibrium sources. */
+rt_status rt_get_psi_source(rt_solver *s, double *psi_source);
+
+/* ---- device-side hooks (multi-GPU, measurement) ------------------------- */
+/* Group-summed absorption rate A(x_c) = sum_{g local} rho kappa_g phi_g(c),
+ * written to a DEVICE buffer of N doubles on the handle's stream: the per-rank
+ * partial of the group-sum all-reduce (north_star; the reference has no
+ * material-temperature update, so nothing consumes it in the solve). */
+rt_status rt_group_absorption_device(rt_solver *s, double *d_out);
+/* Per-launch timing of the sweep kernel with HIP events on the handle's
+ * stream (off by default). */
+rt_status rt_set_profiling(rt_solver *s, int on);
+rt_status rt_get_sweep_time(rt_solver *s, double *total_ms, long long *launches);
+/* Algorithmic HBM bytes of one sweep launch (one full step) and updates
+ * (cell x angle x group x substep) per full step, for the handle's groups. */
+rt_status rt_sweep_traffic(rt_solver *s, double *bytes_per_step, double *updates_per_step);
+/* Sweep geometry actually used: persistent workgroups, tiles per step. */
+rt_status rt_sweep_geometry(rt_solver *s, int *workgroups, long long *tiles);
+
+const char *rt_status_string(rt_status st);
+/* Last error message recorded on the handle (or the global one for s == NULL). */
+const char *rt_last_error(rt_solver *s);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RTSN_H */

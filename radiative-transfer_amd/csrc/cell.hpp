@@ -1,0 +1,157 @@
+// cell.hpp -- the per-cell algebra of the S_n sweep in the upwind frame.
+//
+// Shared by the sweep kernels (device) and the host-side setup that derives
+// each line's linear propagator (host), so both see one definition.
+//
+// Upwind frame: a (direction, group) "line" is stored with cell k = 0 at its
+// inflow boundary (physical cell N-1-k for mu < 0) and each cell's two nodes
+// as (e_in, e_out) = (upwind node, downwind node).  With m = |mu| the three
+// 2x2 cell systems of the reference are then sign-free:
+//   BE   solver.cpp:319-404   [[d, b/2], [-b/2, d]] u = (S + b x + dx/2 e_in, S + dx/2 e_out)
+//   CN   solver.cpp:407-490   rhs adds the explicit half of the step and A (x_prev + x_half)
+//   BDF  solver.cpp:493-587   BDF2 corrector from the half (H) and previous (P) states,
+//                             const_B built from the FULL dt (:501)
+// The source S = 1/2 c tau dx (sigma B_g + total_correction) with the v/c
+// correction (correction.cpp:393-395) linear in psi = (e_in + e_out)/2:
+//   S = Sc + Sl (e_in + e_out).
+// Each matrix is [[d, o], [-o, d]], whose inverse is [[i0, -i1], [i1, i0]]
+// with i0 = d/(d^2+o^2), i1 = o/(d^2+o^2): precomputed once per line.
+//
+// Fused step.  One full step is swept in ONE pass over the cells: BE (1
+// substep, X = x), CN (1 substep, X = (p_up, x_half)) or the 4-substep BDF2
+// cycle BE -> CN -> BE -> BDF (solver.cpp:721-753), carrying
+//   X = (p_up, x0, xh, x2, x3)
+// p_up = step-start downwind node of the upwind cell (prev_ends, :449/:483/
+// :542/:581), x0/xh/x2/x3 = the four substeps' upwind scalars.  Within the
+// step the half state H (solver.cpp:733) is the CN result for mu < 0 lines
+// and the BE-predictor result for mu > 0 lines.  X after a cell is an affine
+// function of X before it with a cell-independent linear part A -- the basis
+// of the cell-parallel scan (kernels.hip).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+namespace rtamd {
+
+enum LineConstIndex {
+  LC_SC = 0, LC_SL,
+  LC_BE_B, LC_BE_I0, LC_BE_I1,
+  LC_CN_A, LC_CN_K1, LC_CN_K2, LC_CN_I0, LC_CN_I1,
+  LC_BD_BC, LC_BD_Q1, LC_BD_Q2, LC_BD_Q3, LC_BD_Q4, LC_BD_I0, LC_BD_I1,
+  LC_COUNT
+};
+
+enum Scheme { SCHEME_BE = 1, SCHEME_CN = 2, SCHEME_BDF2 = 3 };
+
+template <int S> struct SchemeDim;
+template <> struct SchemeDim<SCHEME_BE> { static constexpr int K = 1; };
+template <> struct SchemeDim<SCHEME_CN> { static constexpr int K = 2; };
+template <> struct SchemeDim<SCHEME_BDF2> { static constexpr int K = 5; };
+
+struct LineConst {
+  double c[LC_COUNT];
+};
+
+__host__ __device__ __forceinline__ double src(const LineConst &L, double ein, double eout) {
+  return L.c[LC_SC] + L.c[LC_SL] * (ein + eout);
+}
+
+// Backward Euler cell (solver.cpp:319-404)
+__host__ __device__ __forceinline__ void cell_be(const LineConst &L, double hd, double ein, double eout, double x,
+                                                 double &uin, double &uout) {
+  const double S = src(L, ein, eout);
+  const double rin = S + L.c[LC_BE_B] * x + hd * ein;
+  const double rout = S + hd * eout;
+  uin = L.c[LC_BE_I0] * rin - L.c[LC_BE_I1] * rout;
+  uout = L.c[LC_BE_I1] * rin + L.c[LC_BE_I0] * rout;
+}
+
+// Crank-Nicolson cell (solver.cpp:407-490): xp = prev_ends of the upwind cell, xh = half_local_bdry
+__host__ __device__ __forceinline__ void cell_cn(const LineConst &L, double hd, double ein, double eout, double xp,
+                                                 double xh, double &uin, double &uout) {
+  const double S = src(L, ein, eout);
+  const double rin = S + L.c[LC_CN_K1] * ein - L.c[LC_CN_K2] * eout + L.c[LC_CN_A] * (xp + xh);
+  const double rout = S + L.c[LC_CN_K2] * ein + L.c[LC_CN_K1] * eout;
+  uin = L.c[LC_CN_I0] * rin - L.c[LC_CN_I1] * rout;
+  uout = L.c[LC_CN_I1] * rin + L.c[LC_CN_I0] * rout;
+}
+
+// BDF corrector cell (solver.cpp:493-587); (ein, eout) = state at substep start (source only)
+__host__ __device__ __forceinline__ void cell_bdf(const LineConst &L, double ein, double eout, double hin,
+                                                  double hout, double pin, double pout, double x, double xh,
+                                                  double xp, double &uin, double &uout) {
+  const double S = src(L, ein, eout);
+  const double rin = S + L.c[LC_BD_Q1] * hin - L.c[LC_BD_Q2] * hout - L.c[LC_BD_Q3] * pin - L.c[LC_BD_Q4] * pout +
+                     L.c[LC_BD_BC] * (x + 4.0 * xh + xp);
+  const double rout = S + L.c[LC_BD_Q2] * hin + L.c[LC_BD_Q1] * hout + L.c[LC_BD_Q4] * pin - L.c[LC_BD_Q3] * pout;
+  uin = L.c[LC_BD_I0] * rin - L.c[LC_BD_I1] * rout;
+  uout = L.c[LC_BD_I1] * rin + L.c[LC_BD_I0] * rout;
+}
+
+// One BDF2 full step of one cell with explicit upwind inputs.
+// x0/xh/x2/x3: the substeps' carried scalars; xp1/xp3: prev-state upwind node
+// seen by CN / BDF; hup: half-state upwind node seen by BDF.
+__host__ __device__ __forceinline__ void cell_bdf2_explicit(const LineConst &L, double hd, bool neg, double pin,
+                                                            double pout, double x0, double xh, double x2, double x3,
+                                                            double xp1, double xp3, double hup, double &e1out,
+                                                            double &e2out, double &e3out, double &oin,
+                                                            double &oout) {
+  double e1in, e2in, e3in;
+  cell_be(L, hd, pin, pout, x0, e1in, e1out);                    // substep 0: BE predictor
+  cell_cn(L, hd, e1in, e1out, xp1, xh, e2in, e2out);             // substep 1: CN corrector
+  const double hin = neg ? e2in : e1in, hout = neg ? e2out : e1out;  // half_ends (:733)
+  cell_be(L, hd, e2in, e2out, x2, e3in, e3out);                  // substep 2: BE predictor
+  cell_bdf(L, e3in, e3out, hin, hout, pin, pout, x3, hup, xp3, oin, oout);  // substep 3: BDF
+}
+
+// Generic interior cell: X -> X' for scheme S; (pin, pout) = step-start state,
+// (oin, oout) = step-end state.  neg selects the mu < 0 half-state rule.
+template <int S>
+__host__ __device__ __forceinline__ void cell_step(const LineConst &L, double hd, bool neg, double pin, double pout,
+                                                   double *X, double &oin, double &oout) {
+  if constexpr (S == SCHEME_BE) {
+    cell_be(L, hd, pin, pout, X[0], oin, oout);
+    X[0] = oout;
+  } else if constexpr (S == SCHEME_CN) {
+    cell_cn(L, hd, pin, pout, X[0], X[1], oin, oout);
+    X[0] = pout;
+    X[1] = oout;
+  } else {
+    double a, b, c;
+    const double hup = neg ? X[2] : X[1];
+    cell_bdf2_explicit(L, hd, neg, pin, pout, X[1], X[2], X[3], X[4], X[0], X[0], hup, a, b, c, oin, oout);
+    X[0] = pout;
+    X[1] = a;
+    X[2] = b;
+    X[3] = c;
+    X[4] = oout;
+  }
+}
+
+// First cell of a line (k = 0) with per-substep inflow values b[0..3]
+// (solver.cpp:695-697: local_bdry = half_local_bdry = local_bdry_prev_it = bdry_cond).
+template <int S>
+__host__ __device__ __forceinline__ void cell_first(const LineConst &L, double hd, bool neg, double pin, double pout,
+                                                    const double *b, double *X, double &oin, double &oout) {
+  if constexpr (S == SCHEME_BE) {
+    X[0] = b[0];
+    cell_step<S>(L, hd, neg, pin, pout, X, oin, oout);
+  } else if constexpr (S == SCHEME_CN) {
+    X[0] = b[0];
+    X[1] = b[0];
+    cell_step<S>(L, hd, neg, pin, pout, X, oin, oout);
+  } else {
+    double a, bb, c;
+    cell_bdf2_explicit(L, hd, neg, pin, pout, b[0], b[1], b[2], b[3], b[1], b[3], b[3], a, bb, c, oin, oout);
+    X[0] = pout;
+    X[1] = a;
+    X[2] = bb;
+    X[3] = c;
+    X[4] = oout;
+  }
+}
+
+// Index of (r, c), c <= r, in a packed lower triangle.
+__host__ __device__ __forceinline__ constexpr int tri(int r, int c) { return r * (r + 1) / 2 + c; }
+
+}  // namespace rtamd

@@ -1,0 +1,761 @@
+// rtsn_api.hip -- the C ABI (include/rtsn.h): solver lifecycle, device
+// state, per-line setup, launches and result reductions.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../../include/rtsn.h"
+#include "cell.hpp"
+#include "kernels.hpp"
+#include "physics.hpp"
+#include "prm.hpp"
+
+using namespace rtamd;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+struct DeviceBuf {
+  void *p = nullptr;
+  size_t bytes = 0;
+  ~DeviceBuf() {
+    if (p) (void)hipFree(p);
+  }
+};
+
+}  // namespace
+
+struct rt_solver {
+  // configuration (owned copies)
+  rt_params p{};
+  std::vector<double> prm_psi_source, prm_bounds, prm_kappa;
+  phys::GroupTable gt;
+  std::vector<double> mu, wt;
+  std::vector<double> psi_source;  // solver-owned, M*G
+  bool equilibrium_done = false;
+  int g_lo = 0, g_hi = 0, Gl = 0, H = 0, Lh = 0, Lpad = 0, Q = 0, J = 0;
+  int scheme = SCHEME_BDF2, K = 5;
+  long long tiles = 0;
+  int grid = 0;
+  int device = 0;
+  hipStream_t stream = nullptr;
+  // device state
+  DeviceBuf E, lc, Apow, bdry, outflow, outflow_flag, status, agg, pref, error, lineB, muwt, mom, rows, sigma;
+  // profiling
+  bool profiling = false;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  double sweep_ms = 0.0;
+  long long launches = 0;
+  std::string err;
+
+  ~rt_solver() {
+    if (ev0) (void)hipEventDestroy(ev0);
+    if (ev1) (void)hipEventDestroy(ev1);
+    if (stream) (void)hipStreamDestroy(stream);
+  }
+};
+
+static rt_status fail(rt_solver *s, rt_status st, const std::string &msg) {
+  if (s) s->err = msg;
+  g_last_error = msg;
+  return st;
+}
+
+#define HIP_TRY(s, expr)                                                                        \
+  do {                                                                                          \
+    hipError_t e_ = (expr);                                                                     \
+    if (e_ != hipSuccess) return fail((s), RT_ERR_DEVICE, std::string(#expr ": ") + hipGetErrorString(e_)); \
+  } while (0)
+
+static hipError_t dalloc(DeviceBuf &b, size_t bytes) {
+  b.bytes = bytes;
+  return hipMalloc(&b.p, bytes ? bytes : 16);
+}
+
+// ---------------------------------------------------------------------------
+// host-only configuration
+// ---------------------------------------------------------------------------
+extern "C" void rt_params_default(rt_params *out) {
+  if (!out) return;
+  *out = rt_params{};
+  out->M = 2;
+  out->G = 1;
+  out->N = 100;
+  out->efirst = .1;
+  out->elast = 10.;
+  out->X = 1.;
+  out->bc_left_indicator = 2;
+  out->bc_right_indicator = 1;
+  out->use_mg_equilib = 0;
+  out->rho = 1.;
+  out->kappa_grey = 1.;
+  out->T = 1.;
+  out->V = 0.;
+  out->use_correction = 0;
+  out->ts_method = 3;
+  out->dt = 0.00001;
+  out->max_timesteps = 1000;
+  out->include_validation = 1;
+}
+
+extern "C" rt_status rt_params_load(const char *prm_path, const char *table_dir, rt_params *out, int *prm_found) {
+  if (!prm_path || !out) return fail(nullptr, RT_ERR_ARG, "rt_params_load: NULL argument");
+  ParameterHandler ph(prm_path, table_dir ? table_dir : "");
+  if (prm_found) *prm_found = ph.prm_found();
+  if (ph.status() != RT_OK) return fail(nullptr, ph.status(), ph.error());
+  *out = ph.as_params();
+  auto dup = [](const std::vector<double> &v) -> double * {
+    if (v.empty()) return nullptr;
+    double *d = static_cast<double *>(std::malloc(sizeof(double) * v.size()));
+    std::memcpy(d, v.data(), sizeof(double) * v.size());
+    return d;
+  };
+  out->psi_source = dup(ph.psi_source());
+  out->group_bounds = ph.get_have_group_bounds() ? dup(ph.group_bounds()) : nullptr;
+  out->group_kappa = ph.get_have_group_absorption_opacities() ? dup(ph.group_kappa()) : nullptr;
+  return RT_OK;
+}
+
+extern "C" void rt_params_free(rt_params *p) {
+  if (!p) return;
+  std::free(const_cast<double *>(p->psi_source));
+  std::free(const_cast<double *>(p->group_bounds));
+  std::free(const_cast<double *>(p->group_kappa));
+  p->psi_source = p->group_bounds = p->group_kappa = nullptr;
+}
+
+extern "C" rt_status rt_quadrature(int M, double *mu, double *wt) {
+  if (M <= 0 || !mu || !wt) return fail(nullptr, RT_ERR_ARG, "rt_quadrature: bad argument");
+  phys::gauss_legendre(M, phys::kFourPi, mu, wt);
+  return RT_OK;
+}
+
+extern "C" rt_status rt_planck_groups(double T, int G, const double *e_edge, double *B, double *dBdT) {
+  if (G <= 0 || !e_edge || !B || !dBdT) return fail(nullptr, RT_ERR_ARG, "rt_planck_groups: bad argument");
+  std::vector<double> lo(e_edge, e_edge + G), hi(e_edge + 1, e_edge + G + 1);
+  std::fill(B, B + G, 0.0);
+  std::fill(dBdT, dBdT + G, 0.0);
+  phys::PlanckIntegrator().group_integrals(T, G, lo.data(), hi.data(), B, dBdT);
+  for (int g = 0; g < G; ++g) {
+    B[g] *= phys::kBoltzmannJPK;
+    dBdT[g] *= phys::kBoltzmannJPK;
+  }
+  return RT_OK;
+}
+
+// ---------------------------------------------------------------------------
+// per-line setup
+// ---------------------------------------------------------------------------
+// Line l of half h: direction i = H-1-i' (h = 0, mu < 0) or H+i' (h = 1),
+// local group gl, with l = i' + H*gl; both halves share (i', gl) numbering so
+// a reflective mu > 0 line and its mirror have the same l.
+static int line_direction(int H, int half, int ip) { return half == 0 ? H - 1 - ip : H + ip; }
+
+static LineConst line_constants(const rt_solver &s, int i, int g) {
+  const rt_params &p = s.p;
+  const double c = phys::kLight;
+  const double dx = p.X / p.N;
+  const double dt = p.dt;
+  const double tau = (p.ts_method == 3) ? dt / 2.0 : dt;
+  const double mu = s.mu[i], m = std::fabs(mu);
+  const double sigma = s.gt.rho[g] * s.gt.kappa[g];
+  LineConst L{};
+  const double half = 0.5 * c * tau * dx;
+  // S = 1/2 c tau dx (sigma B_g + total_correction), psi = (e_in + e_out)/2
+  L.c[LC_SC] = half * sigma * s.gt.B[g];
+  L.c[LC_SL] = 0.0;
+  if (p.use_correction) {
+    const double beta = p.V / c;
+    L.c[LC_SC] += half * ((s.gt.cor2[g] * mu) * beta - s.gt.cor3[g] * (mu * mu) * (beta * beta));
+    L.c[LC_SL] = half * s.gt.cor1[g] * mu * beta * 0.5;
+  }
+  auto inverse = [](double d, double o, double &i0, double &i1) {
+    const double det = d * d + o * o;
+    i0 = d / det;
+    i1 = o / det;
+  };
+  {  // BE(tau)
+    const double a = 1.0 + c * tau * sigma, b = c * tau * m;
+    L.c[LC_BE_B] = b;
+    inverse((a * dx + b) / 2.0, b / 2.0, L.c[LC_BE_I0], L.c[LC_BE_I1]);
+  }
+  {  // CN(tau)
+    const double t = 0.5 * c * tau * sigma, A = 0.5 * c * m * tau;
+    const double Bp = 1.0 + t, Cp = 1.0 - t;
+    L.c[LC_CN_A] = A;
+    L.c[LC_CN_K1] = 0.5 * (Cp * dx - A);
+    L.c[LC_CN_K2] = 0.5 * A;
+    inverse(0.5 * (A + Bp * dx), A / 2.0, L.c[LC_CN_I0], L.c[LC_CN_I1]);
+  }
+  {  // BDF(tau) with const_B from the full dt
+    const double t = c * sigma * tau / 6.0, Ab = 1.0 + t, Bc = c * m * dt / 6.0, Cb = 1.0 - 4.0 * t, D = t;
+    L.c[LC_BD_BC] = Bc;
+    L.c[LC_BD_Q1] = 0.5 * (Cb * dx - 4.0 * Bc);
+    L.c[LC_BD_Q2] = 2.0 * Bc;
+    L.c[LC_BD_Q3] = 0.5 * (Bc + D * dx);
+    L.c[LC_BD_Q4] = 0.5 * Bc;
+    inverse(0.5 * (Ab * dx + Bc), 0.5 * Bc, L.c[LC_BD_I0], L.c[LC_BD_I1]);
+  }
+  return L;
+}
+
+// Linear part A of the cell map X -> X' (cell.hpp), by evaluating the map
+// with the affine constants and the cell data set to zero.
+template <int S>
+static void propagator(const LineConst &Lin, double hd, bool neg, double *A /* K*K row-major */) {
+  constexpr int K = SchemeDim<S>::K;
+  LineConst L = Lin;
+  L.c[LC_SC] = 0.0;
+  for (int col = 0; col < K; ++col) {
+    double X[K] = {};
+    X[col] = 1.0;
+    double oi, oo;
+    cell_step<S>(L, hd, neg, 0.0, 0.0, X, oi, oo);
+    for (int r = 0; r < K; ++r) A[r * K + col] = X[r];
+  }
+}
+
+static void matmul(int K, const double *A, const double *B, double *C) {
+  for (int r = 0; r < K; ++r)
+    for (int c = 0; c < K; ++c) {
+      double acc = 0.0;
+      for (int m = 0; m < K; ++m) acc += A[r * K + m] * B[m * K + c];
+      C[r * K + c] = acc;
+    }
+}
+
+static rt_status upload(rt_solver *s, DeviceBuf &b, const void *src, size_t bytes) {
+  HIP_TRY(s, hipMemcpyAsync(b.p, src, bytes, hipMemcpyHostToDevice, s->stream));
+  return RT_OK;
+}
+
+// boundary inflow per line (solver.cpp:635-692) from the solver's psi_source
+static void line_inflow(const rt_solver &s, std::vector<double> &bd) {
+  const int M = s.p.M, G = s.p.G;
+  bd.assign(static_cast<size_t>(2) * s.Lpad, 0.0);
+  for (int half = 0; half < 2; ++half) {
+    const int bc = half == 0 ? s.p.bc_right_indicator : s.p.bc_left_indicator;
+    for (int gl = 0; gl < s.Gl; ++gl)
+      for (int ip = 0; ip < s.H; ++ip) {
+        const int i = line_direction(s.H, half, ip), g = s.g_lo + gl;
+        double v = 0.0;
+        if (half == 0 && bc == 1) v = s.psi_source[static_cast<size_t>(i) * G + g];
+        if (half == 1 && (bc == 0 || bc == 1)) v = s.psi_source[static_cast<size_t>(i) * G + g];
+        bd[static_cast<size_t>(half) * s.Lpad + ip + s.H * gl] = v;
+      }
+  }
+  (void)M;
+}
+
+static rt_status setup_lines(rt_solver *s) {
+  const int K = s->K, NT = K * (K + 1) / 2;
+  const double hd = 0.5 * (s->p.X / s->p.N);
+  std::vector<double> lc(static_cast<size_t>(2) * LC_COUNT * s->Lpad, 0.0);
+  std::vector<double> Ap(static_cast<size_t>(2) * 2 * NT * s->Lpad, 0.0);
+  std::vector<double> lineB(static_cast<size_t>(2) * s->Lpad, 0.0);
+  std::vector<double> A(K * K), T(K * K), P16(K * K), P64(K * K);
+  for (int half = 0; half < 2; ++half)
+    for (int gl = 0; gl < s->Gl; ++gl)
+      for (int ip = 0; ip < s->H; ++ip) {
+        const int i = line_direction(s->H, half, ip), g = s->g_lo + gl;
+        const int ell = ip + s->H * gl;
+        const LineConst L = line_constants(*s, i, g);
+        for (int n = 0; n < LC_COUNT; ++n) lc[(static_cast<size_t>(half) * LC_COUNT + n) * s->Lpad + ell] = L.c[n];
+        lineB[static_cast<size_t>(half) * s->Lpad + ell] = s->gt.B[g];
+        const bool neg = half == 0;
+        switch (s->scheme) {
+          case SCHEME_BE: propagator<SCHEME_BE>(L, hd, neg, A.data()); break;
+          case SCHEME_CN: propagator<SCHEME_CN>(L, hd, neg, A.data()); break;
+          default: propagator<SCHEME_BDF2>(L, hd, neg, A.data()); break;
+        }
+        P16 = A;  // A^16 by squaring
+        for (int sq = 0; sq < 4; ++sq) {
+          matmul(K, P16.data(), P16.data(), T.data());
+          P16 = T;
+        }
+        P64 = P16;  // A^64 = (A^16)^4
+        for (int sq = 0; sq < 2; ++sq) {
+          matmul(K, P64.data(), P64.data(), T.data());
+          P64 = T;
+        }
+        for (int r = 0; r < K; ++r)
+          for (int c = 0; c <= r; ++c) {
+            Ap[((static_cast<size_t>(half) * 2 + 0) * NT + tri(r, c)) * s->Lpad + ell] = P16[r * K + c];
+            Ap[((static_cast<size_t>(half) * 2 + 1) * NT + tri(r, c)) * s->Lpad + ell] = P64[r * K + c];
+          }
+      }
+  rt_status st;
+  if ((st = upload(s, s->lc, lc.data(), lc.size() * sizeof(double)))) return st;
+  if ((st = upload(s, s->Apow, Ap.data(), Ap.size() * sizeof(double)))) return st;
+  if ((st = upload(s, s->lineB, lineB.data(), lineB.size() * sizeof(double)))) return st;
+  std::vector<double> sig(s->Gl);
+  for (int gl = 0; gl < s->Gl; ++gl) sig[gl] = s->gt.rho[s->g_lo + gl] * s->gt.kappa[s->g_lo + gl];
+  if ((st = upload(s, s->sigma, sig.data(), sig.size() * sizeof(double)))) return st;
+  std::vector<double> muwt(2 * s->p.M);
+  std::copy(s->mu.begin(), s->mu.end(), muwt.begin());
+  std::copy(s->wt.begin(), s->wt.end(), muwt.begin() + s->p.M);
+  if ((st = upload(s, s->muwt, muwt.data(), muwt.size() * sizeof(double)))) return st;
+  HIP_TRY(s, hipStreamSynchronize(s->stream));  // host vectors die at return
+  return RT_OK;
+}
+
+static rt_status upload_inflow(rt_solver *s) {
+  std::vector<double> bd;
+  line_inflow(*s, bd);
+  rt_status st = upload(s, s->bdry, bd.data(), bd.size() * sizeof(double));
+  if (st) return st;
+  HIP_TRY(s, hipStreamSynchronize(s->stream));
+  return RT_OK;
+}
+
+static Geometry geometry(const rt_solver *s) { return Geometry{s->p.M, s->Gl, s->p.N, s->Lpad}; }
+
+// ---------------------------------------------------------------------------
+// lifecycle
+// ---------------------------------------------------------------------------
+extern "C" rt_status rt_create_from_params(const rt_params *pin, int g_lo, int g_hi, int device, rt_solver **out) {
+  if (!pin || !out) return fail(nullptr, RT_ERR_ARG, "rt_create_from_params: NULL argument");
+  *out = nullptr;
+  const rt_params &q = *pin;
+  if (q.M <= 0 || (q.M % 2) != 0) return fail(nullptr, RT_ERR_PARAM, "M must be positive and even (mu = 0 asserts, solver.cpp:402)");
+  if (q.G <= 0 || q.N <= 0) return fail(nullptr, RT_ERR_PARAM, "G and N must be positive");
+  if (q.ts_method < 1 || q.ts_method > 3) return fail(nullptr, RT_ERR_PARAM, "ts_method must be 1, 2 or 3 (solver.cpp:755)");
+  if (q.bc_left_indicator < 0 || q.bc_left_indicator > 2 || q.bc_right_indicator < 0 || q.bc_right_indicator > 2)
+    return fail(nullptr, RT_ERR_PARAM, "boundary indicators must be 0, 1 or 2 (solver.cpp:658-690)");
+  if (!(q.X > 0.0) || !(q.dt > 0.0)) return fail(nullptr, RT_ERR_PARAM, "X and dt must be positive");
+  if (g_hi <= 0) g_hi = q.G;
+  if (g_lo < 0 || g_lo >= g_hi || g_hi > q.G) return fail(nullptr, RT_ERR_PARAM, "bad group range");
+
+  std::unique_ptr<rt_solver> s(new rt_solver());
+  s->p = q;
+  const size_t MG = static_cast<size_t>(q.M) * q.G;
+  if (q.psi_source) s->prm_psi_source.assign(q.psi_source, q.psi_source + MG);
+  if (q.group_bounds) s->prm_bounds.assign(q.group_bounds, q.group_bounds + q.G + 1);
+  if (q.group_kappa) s->prm_kappa.assign(q.group_kappa, q.group_kappa + q.G);
+  s->p.psi_source = s->prm_psi_source.empty() ? nullptr : s->prm_psi_source.data();
+  s->p.group_bounds = s->prm_bounds.empty() ? nullptr : s->prm_bounds.data();
+  s->p.group_kappa = s->prm_kappa.empty() ? nullptr : s->prm_kappa.data();
+
+  rt_status st = phys::build_group_table(s->p, s->gt);
+  if (st) return fail(nullptr, st, "group table: group edges must increase");
+  s->mu.resize(q.M);
+  s->wt.resize(q.M);
+  phys::gauss_legendre(q.M, phys::kFourPi, s->mu.data(), s->wt.data());
+  phys::solver_psi_source(s->p, s->gt, s->mu.data(), s->psi_source);
+  if (q.use_mg_equilib) {  // only the ph copy until solve() (solver.cpp:601-604)
+    rt_params pre = s->p;
+    pre.use_mg_equilib = 0;
+    phys::solver_psi_source(pre, s->gt, s->mu.data(), s->psi_source);
+  }
+
+  s->g_lo = g_lo;
+  s->g_hi = g_hi;
+  s->Gl = g_hi - g_lo;
+  s->H = q.M / 2;
+  s->Lh = s->H * s->Gl;
+  s->Q = (s->Lh + 63) / 64;
+  s->Lpad = 64 * s->Q;
+  s->J = (q.N + kSweepTile - 1) / kSweepTile;
+  s->tiles = 2LL * s->J * s->Q;
+  s->scheme = q.ts_method;
+  s->K = q.ts_method == 1 ? 1 : (q.ts_method == 2 ? 2 : 5);
+  s->device = device;
+
+  rt_solver *h = s.get();
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= device || device < 0)
+    return fail(nullptr, RT_ERR_DEVICE, "no HIP device " + std::to_string(device));
+  HIP_TRY(h, hipSetDevice(device));
+  hipDeviceProp_t prop;
+  HIP_TRY(h, hipGetDeviceProperties(&prop, device));
+  if (std::string(prop.gcnArchName).find("gfx950") == std::string::npos)
+    return fail(nullptr, RT_ERR_DEVICE, std::string("librtsn is built for gfx950, device is ") + prop.gcnArchName);
+  HIP_TRY(h, hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
+
+  const size_t Lp = h->Lpad, N = q.N;
+  const int K = h->K, NT = K * (K + 1) / 2;
+  hipError_t e = hipSuccess;
+  if (!e) e = dalloc(h->E, sizeof(double2) * 2 * N * Lp);
+  if (!e) e = dalloc(h->lc, sizeof(double) * 2 * LC_COUNT * Lp);
+  if (!e) e = dalloc(h->Apow, sizeof(double) * 4 * NT * Lp);
+  if (!e) e = dalloc(h->bdry, sizeof(double) * 2 * Lp);
+  if (!e) e = dalloc(h->outflow, sizeof(double) * 4 * Lp);
+  if (!e) e = dalloc(h->outflow_flag, sizeof(unsigned) * h->Q);
+  if (!e) e = dalloc(h->status, sizeof(unsigned) * h->tiles);
+  if (!e) e = dalloc(h->agg, sizeof(double) * h->tiles * K * 64);
+  if (!e) e = dalloc(h->pref, sizeof(double) * h->tiles * K * 64);
+  if (!e) e = dalloc(h->error, 16);
+  if (!e) e = dalloc(h->lineB, sizeof(double) * 2 * Lp);
+  if (!e) e = dalloc(h->muwt, sizeof(double) * 2 * q.M);
+  if (!e) e = dalloc(h->mom, sizeof(double) * 3 * h->Gl * N);
+  if (!e) e = dalloc(h->rows, sizeof(double2) * 4 * Lp);
+  if (!e) e = dalloc(h->sigma, sizeof(double) * h->Gl);
+  if (e) return fail(nullptr, RT_ERR_NOMEM, std::string("device allocation: ") + hipGetErrorString(e));
+
+  if ((st = setup_lines(h))) return st;
+  if ((st = upload_inflow(h))) return st;
+  HIP_TRY(h, launch_init_state(static_cast<double2 *>(h->E.p), static_cast<const double *>(h->lineB.p), q.N, h->Lpad,
+                               h->stream));
+  HIP_TRY(h, hipMemsetAsync(h->outflow.p, 0, h->outflow.bytes, h->stream));
+
+  int per_cu = 0;
+  HIP_TRY(h, sweep_occupancy(h->scheme, &per_cu));
+  per_cu = std::max(1, std::min(per_cu, 8));
+  long long maxP = static_cast<long long>(prop.multiProcessorCount) * per_cu;
+  long long P = std::min<long long>(maxP, h->tiles);
+  if (P > h->Q && maxP >= h->Q) P = (P / h->Q) * h->Q;  // keep each workgroup on one line group
+  h->grid = static_cast<int>(std::max<long long>(1, P));
+  HIP_TRY(h, hipEventCreate(&h->ev0));
+  HIP_TRY(h, hipEventCreate(&h->ev1));
+  HIP_TRY(h, hipStreamSynchronize(h->stream));
+  *out = s.release();
+  return RT_OK;
+}
+
+extern "C" rt_status rt_create(const char *prm_path, const char *table_dir, int device, rt_solver **out) {
+  if (!prm_path || !out) return fail(nullptr, RT_ERR_ARG, "rt_create: NULL argument");
+  ParameterHandler ph(prm_path, table_dir ? table_dir : "");
+  if (ph.status() != RT_OK) return fail(nullptr, ph.status(), ph.error());
+  const rt_params p = ph.as_params();
+  return rt_create_from_params(&p, 0, 0, device, out);
+}
+
+extern "C" void rt_destroy(rt_solver *s) { delete s; }
+
+// ---------------------------------------------------------------------------
+// stepping
+// ---------------------------------------------------------------------------
+static rt_status check_validation(rt_solver *s) {
+  if (s->p.include_validation && !phys::validate_correction(s->p, s->gt))
+    return fail(s, RT_ERR_VALIDATION, "validate_correction() fails (correction.cpp:39-63,100-122)");
+  return RT_OK;
+}
+
+static rt_status ensure_equilibrium(rt_solver *s) {
+  if (!s->p.use_mg_equilib || s->equilibrium_done) return RT_OK;
+  rt_status st = check_validation(s);  // solver.cpp:290-293
+  if (st) return st;
+  phys::solver_psi_source(s->p, s->gt, s->mu.data(), s->psi_source);
+  s->equilibrium_done = true;
+  return upload_inflow(s);
+}
+
+static rt_status enqueue_steps(rt_solver *s, int nsteps) {
+  SweepArgs a{};
+  a.E = static_cast<double2 *>(s->E.p);
+  a.lc = static_cast<const double *>(s->lc.p);
+  a.Apow = static_cast<const double *>(s->Apow.p);
+  a.bdry = static_cast<const double *>(s->bdry.p);
+  a.outflow = static_cast<double *>(s->outflow.p);
+  a.outflow_flag = static_cast<unsigned *>(s->outflow_flag.p);
+  a.status = static_cast<unsigned *>(s->status.p);
+  a.agg = static_cast<double *>(s->agg.p);
+  a.pref = static_cast<double *>(s->pref.p);
+  a.error = static_cast<unsigned *>(s->error.p);
+  a.total_tiles = s->tiles;
+  a.N = s->p.N;
+  a.Lpad = s->Lpad;
+  a.Q = s->Q;
+  a.J = s->J;
+  a.reflective = s->p.bc_left_indicator == 2;
+  a.hd = 0.5 * (s->p.X / s->p.N);
+  for (int n = 0; n < nsteps; ++n) {
+    HIP_TRY(s, hipMemsetAsync(s->status.p, 0, s->status.bytes, s->stream));
+    HIP_TRY(s, hipMemsetAsync(s->outflow_flag.p, 0, s->outflow_flag.bytes, s->stream));
+    if (s->profiling) HIP_TRY(s, hipEventRecord(s->ev0, s->stream));
+    HIP_TRY(s, launch_sweep(s->scheme, a, s->grid, s->stream));
+    if (s->profiling) {
+      HIP_TRY(s, hipEventRecord(s->ev1, s->stream));
+      HIP_TRY(s, hipEventSynchronize(s->ev1));
+      float ms = 0.f;
+      HIP_TRY(s, hipEventElapsedTime(&ms, s->ev0, s->ev1));
+      s->sweep_ms += ms;
+    }
+    ++s->launches;
+  }
+  return RT_OK;
+}
+
+extern "C" rt_status rt_advance(rt_solver *s, int nsteps) {
+  if (!s || nsteps < 0) return fail(s, RT_ERR_ARG, "rt_advance: bad argument");
+  HIP_TRY(s, hipSetDevice(s->device));
+  rt_status st = check_validation(s);
+  if (st) return st;
+  if ((st = ensure_equilibrium(s))) return st;
+  return enqueue_steps(s, nsteps);
+}
+
+extern "C" rt_status rt_synchronize(rt_solver *s) {
+  if (!s) return fail(nullptr, RT_ERR_ARG, "rt_synchronize: NULL handle");
+  HIP_TRY(s, hipStreamSynchronize(s->stream));
+  unsigned err = 0;
+  HIP_TRY(s, hipMemcpy(&err, s->error.p, sizeof(unsigned), hipMemcpyDeviceToHost));
+  if (err) return fail(s, RT_ERR_TIMEOUT, "an inter-workgroup wait in the sweep timed out");
+  return RT_OK;
+}
+
+extern "C" rt_status rt_solve(rt_solver *s) {
+  if (!s) return fail(nullptr, RT_ERR_ARG, "rt_solve: NULL handle");
+  rt_status st = rt_advance(s, s->p.max_timesteps);
+  if (st) return st;
+  return rt_synchronize(s);
+}
+
+extern "C" void *rt_stream(rt_solver *s) { return s ? static_cast<void *>(s->stream) : nullptr; }
+
+// ---------------------------------------------------------------------------
+// results
+// ---------------------------------------------------------------------------
+extern "C" rt_status rt_get_dims(rt_solver *s, int *M, int *G_local, int *N, int *g_lo, int *g_hi) {
+  if (!s) return fail(nullptr, RT_ERR_ARG, "rt_get_dims: NULL handle");
+  if (M) *M = s->p.M;
+  if (G_local) *G_local = s->Gl;
+  if (N) *N = s->p.N;
+  if (g_lo) *g_lo = s->g_lo;
+  if (g_hi) *g_hi = s->g_hi;
+  return RT_OK;
+}
+
+template <typename F>
+static rt_status via_device(rt_solver *s, size_t count, double *host, F &&launch) {
+  double *d = nullptr;
+  HIP_TRY(s, hipMalloc(reinterpret_cast<void **>(&d), sizeof(double) * count));
+  hipError_t e = launch(d);
+  if (e == hipSuccess) e = hipMemcpyAsync(host, d, sizeof(double) * count, hipMemcpyDeviceToHost, s->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
+  (void)hipFree(d);
+  if (e != hipSuccess) return fail(s, RT_ERR_DEVICE, std::string("result transfer: ") + hipGetErrorString(e));
+  return RT_OK;
+}
+
+extern "C" rt_status rt_get_psi(rt_solver *s, double *psi) {
+  if (!s || !psi) return fail(s, RT_ERR_ARG, "rt_get_psi: bad argument");
+  HIP_TRY(s, hipSetDevice(s->device));
+  const Geometry g = geometry(s);
+  return via_device(s, static_cast<size_t>(g.M) * g.Gl * g.N, psi, [&](double *d) {
+    return launch_export_psi(static_cast<const double2 *>(s->E.p), d, g, s->stream);
+  });
+}
+
+extern "C" rt_status rt_get_ends(rt_solver *s, double *ends) {
+  if (!s || !ends) return fail(s, RT_ERR_ARG, "rt_get_ends: bad argument");
+  HIP_TRY(s, hipSetDevice(s->device));
+  const Geometry g = geometry(s);
+  return via_device(s, static_cast<size_t>(2) * g.M * g.Gl * g.N, ends, [&](double *d) {
+    return launch_export_ends(static_cast<const double2 *>(s->E.p), d, g, s->stream);
+  });
+}
+
+extern "C" rt_status rt_set_ends(rt_solver *s, const double *ends) {
+  if (!s || !ends) return fail(s, RT_ERR_ARG, "rt_set_ends: bad argument");
+  HIP_TRY(s, hipSetDevice(s->device));
+  const Geometry g = geometry(s);
+  const size_t n = static_cast<size_t>(2) * g.M * g.Gl * g.N;
+  double *d = nullptr;
+  HIP_TRY(s, hipMalloc(reinterpret_cast<void **>(&d), sizeof(double) * n));
+  hipError_t e = hipMemcpyAsync(d, ends, sizeof(double) * n, hipMemcpyHostToDevice, s->stream);
+  if (e == hipSuccess) e = launch_import_ends(static_cast<double2 *>(s->E.p), d, g, s->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
+  (void)hipFree(d);
+  if (e != hipSuccess) return fail(s, RT_ERR_DEVICE, std::string("rt_set_ends: ") + hipGetErrorString(e));
+  return RT_OK;
+}
+
+static rt_status compute_moments(rt_solver *s) {
+  const Geometry g = geometry(s);
+  const size_t GN = static_cast<size_t>(s->Gl) * s->p.N;
+  double *m = static_cast<double *>(s->mom.p);
+  const double *muwt = static_cast<const double *>(s->muwt.p);
+  HIP_TRY(s, launch_moments(static_cast<const double2 *>(s->E.p), muwt, muwt + s->p.M, m, m + GN, m + 2 * GN, g,
+                            s->stream));
+  return RT_OK;
+}
+
+extern "C" rt_status rt_get_moments(rt_solver *s, double *phi, double *F, double *phi_plus) {
+  if (!s) return fail(nullptr, RT_ERR_ARG, "rt_get_moments: NULL handle");
+  HIP_TRY(s, hipSetDevice(s->device));
+  rt_status st = compute_moments(s);
+  if (st) return st;
+  const size_t GN = static_cast<size_t>(s->Gl) * s->p.N;
+  const double *m = static_cast<const double *>(s->mom.p);
+  if (phi) HIP_TRY(s, hipMemcpyAsync(phi, m, sizeof(double) * GN, hipMemcpyDeviceToHost, s->stream));
+  if (F) HIP_TRY(s, hipMemcpyAsync(F, m + GN, sizeof(double) * GN, hipMemcpyDeviceToHost, s->stream));
+  if (phi_plus) HIP_TRY(s, hipMemcpyAsync(phi_plus, m + 2 * GN, sizeof(double) * GN, hipMemcpyDeviceToHost, s->stream));
+  HIP_TRY(s, hipStreamSynchronize(s->stream));
+  return RT_OK;
+}
+
+// boundary rows: [0] half0 k=0, [1] half0 k=N-1, [2] half1 k=0, [3] half1 k=N-1
+static rt_status fetch_rows(rt_solver *s, std::vector<double> &rows) {
+  const Geometry g = geometry(s);
+  rows.resize(static_cast<size_t>(8) * s->Lpad);
+  HIP_TRY(s, launch_boundary_rows(static_cast<const double2 *>(s->E.p), static_cast<double2 *>(s->rows.p), g,
+                                  s->stream));
+  HIP_TRY(s, hipMemcpyAsync(rows.data(), s->rows.p, sizeof(double) * rows.size(), hipMemcpyDeviceToHost, s->stream));
+  HIP_TRY(s, hipStreamSynchronize(s->stream));
+  return RT_OK;
+}
+
+// physical ends(i, g, c, node) for c in {0, N-1} from the boundary rows
+static double bnode(const rt_solver *s, const std::vector<double> &rows, int i, int gl, bool last_cell, int node) {
+  const int H = s->H;
+  if (i < H) {  // mu < 0: physical c = N-1-k; node 0 (left) = e_out
+    const int ell = (H - 1 - i) + H * gl;
+    const int which = last_cell ? 0 : 1;  // c = N-1 -> k = 0
+    const double *r = rows.data() + static_cast<size_t>(2) * (static_cast<size_t>(which) * s->Lpad + ell);
+    return node == 0 ? r[1] : r[0];
+  }
+  const int ell = (i - H) + H * gl;
+  const int which = last_cell ? 3 : 2;
+  const double *r = rows.data() + static_cast<size_t>(2) * (static_cast<size_t>(which) * s->Lpad + ell);
+  return node == 0 ? r[0] : r[1];
+}
+
+extern "C" rt_status rt_get_group_ends(rt_solver *s, double *left, double *right) {
+  if (!s) return fail(nullptr, RT_ERR_ARG, "rt_get_group_ends: NULL handle");
+  HIP_TRY(s, hipSetDevice(s->device));
+  std::vector<double> rows;
+  rt_status st = fetch_rows(s, rows);
+  if (st) return st;
+  for (int gl = 0; gl < s->Gl; ++gl) {  // solver.cpp:826-850
+    double l = 0., r = 0.;
+    for (int i = 0; i < s->p.M; ++i) {
+      if (s->mu[i] < 0.)
+        l += bnode(s, rows, i, gl, false, 0);
+      else
+        r += bnode(s, rows, i, gl, true, 1);
+    }
+    const double den = s->gt.de_ave[s->g_lo + gl] * phys::kLight;
+    if (left) left[gl] = l / den;
+    if (right) right[gl] = r / den;
+  }
+  return RT_OK;
+}
+
+extern "C" rt_status rt_get_balance(rt_solver *s, double *balance) {
+  if (!s || !balance) return fail(s, RT_ERR_ARG, "rt_get_balance: bad argument");
+  HIP_TRY(s, hipSetDevice(s->device));
+  const int N = s->p.N, Gl = s->Gl;
+  std::vector<double> phi(static_cast<size_t>(Gl) * N);
+  rt_status st = rt_get_moments(s, phi.data(), nullptr, nullptr);
+  if (st) return st;
+  std::vector<double> rows;
+  if ((st = fetch_rows(s, rows))) return st;
+  const double ac = phys::kRadA * phys::kLight, dx = s->p.X / N;
+  for (int gl = 0; gl < Gl; ++gl) {  // solver.cpp:240-284
+    const int g = s->g_lo + gl;
+    double jhm = 0., jhp = 0., jNm = 0., jNp = 0., ab = 0., sr = 0.;
+    for (int i = 0; i < s->p.M; ++i) {
+      const double mu = s->mu[i];
+      if (mu < 0.) {
+        jhm -= bnode(s, rows, i, gl, false, 0) * mu * s->wt[i];
+        jNm -= bnode(s, rows, i, gl, true, 0) * mu * s->wt[i];
+      } else {
+        jhp += bnode(s, rows, i, gl, false, 1) * mu * s->wt[i];
+        jNp += bnode(s, rows, i, gl, true, 1) * mu * s->wt[i];
+      }
+    }
+    const double rk = s->gt.rho[g] * s->gt.kappa[g];
+    for (int c = 0; c < N; ++c) {
+      ab += s->gt.rho[g] * s->gt.kappa[g] * phi[static_cast<size_t>(c) * Gl + gl] * dx;
+      sr += s->gt.rho[g] * s->gt.kappa[g] * ac * std::pow(s->p.T, 4) * dx;
+    }
+    (void)rk;
+    const double sources = jhp + jNm + sr, sinks = jNp + jhm + ab;
+    balance[gl] = std::fabs(sinks - sources) / sources;
+  }
+  return RT_OK;
+}
+
+extern "C" rt_status rt_get_e_ave(rt_solver *s, double *e_ave) {
+  if (!s || !e_ave) return fail(s, RT_ERR_ARG, "rt_get_e_ave: bad argument");
+  std::copy(s->gt.e_ave.begin(), s->gt.e_ave.end(), e_ave);
+  return RT_OK;
+}
+
+extern "C" rt_status rt_get_group_data(rt_solver *s, double *e_edge, double *B, double *dBdT, double *kappa) {
+  if (!s) return fail(nullptr, RT_ERR_ARG, "rt_get_group_data: NULL handle");
+  if (e_edge) std::copy(s->gt.e_edge.begin(), s->gt.e_edge.end(), e_edge);
+  if (B) std::copy(s->gt.B.begin(), s->gt.B.end(), B);
+  if (dBdT) std::copy(s->gt.dBdT.begin(), s->gt.dBdT.end(), dBdT);
+  if (kappa) std::copy(s->gt.kappa.begin(), s->gt.kappa.end(), kappa);
+  return RT_OK;
+}
+
+extern "C" rt_status rt_get_quadrature(rt_solver *s, double *mu, double *wt) {
+  if (!s) return fail(nullptr, RT_ERR_ARG, "rt_get_quadrature: NULL handle");
+  if (mu) std::copy(s->mu.begin(), s->mu.end(), mu);
+  if (wt) std::copy(s->wt.begin(), s->wt.end(), wt);
+  return RT_OK;
+}
+
+extern "C" rt_status rt_get_psi_source(rt_solver *s, double *out) {
+  if (!s || !out) return fail(s, RT_ERR_ARG, "rt_get_psi_source: bad argument");
+  std::copy(s->psi_source.begin(), s->psi_source.end(), out);
+  return RT_OK;
+}
+
+extern "C" rt_status rt_group_absorption_device(rt_solver *s, double *d_out) {
+  if (!s || !d_out) return fail(s, RT_ERR_ARG, "rt_group_absorption_device: bad argument");
+  HIP_TRY(s, hipSetDevice(s->device));
+  rt_status st = compute_moments(s);
+  if (st) return st;
+  HIP_TRY(s, launch_group_absorption(static_cast<const double *>(s->mom.p), static_cast<const double *>(s->sigma.p),
+                                     d_out, geometry(s), s->stream));
+  return RT_OK;
+}
+
+extern "C" rt_status rt_set_profiling(rt_solver *s, int on) {
+  if (!s) return fail(nullptr, RT_ERR_ARG, "rt_set_profiling: NULL handle");
+  s->profiling = on != 0;
+  s->sweep_ms = 0.0;
+  s->launches = 0;
+  return RT_OK;
+}
+
+extern "C" rt_status rt_get_sweep_time(rt_solver *s, double *total_ms, long long *launches) {
+  if (!s) return fail(nullptr, RT_ERR_ARG, "rt_get_sweep_time: NULL handle");
+  if (total_ms) *total_ms = s->sweep_ms;
+  if (launches) *launches = s->launches;
+  return RT_OK;
+}
+
+extern "C" rt_status rt_sweep_traffic(rt_solver *s, double *bytes_per_step, double *updates_per_step) {
+  if (!s) return fail(nullptr, RT_ERR_ARG, "rt_sweep_traffic: NULL handle");
+  const double lines_cells = static_cast<double>(s->p.M) * s->Gl * s->p.N;
+  // one pass: read (e_in, e_out) and write them back, per cell x line
+  if (bytes_per_step) *bytes_per_step = 32.0 * lines_cells;
+  if (updates_per_step) *updates_per_step = (s->p.ts_method == 3 ? 4.0 : 1.0) * lines_cells;
+  return RT_OK;
+}
+
+extern "C" rt_status rt_sweep_geometry(rt_solver *s, int *workgroups, long long *tiles) {
+  if (!s) return fail(nullptr, RT_ERR_ARG, "rt_sweep_geometry: NULL handle");
+  if (workgroups) *workgroups = s->grid;
+  if (tiles) *tiles = s->tiles;
+  return RT_OK;
+}
+
+extern "C" const char *rt_status_string(rt_status st) {
+  switch (st) {
+    case RT_OK: return "ok";
+    case RT_ERR_IO: return "io error";
+    case RT_ERR_PARSE: return "parse error";
+    case RT_ERR_PARAM: return "invalid parameter";
+    case RT_ERR_VALIDATION: return "correction validation failed";
+    case RT_ERR_NOMEM: return "out of memory";
+    case RT_ERR_DEVICE: return "device error";
+    case RT_ERR_TIMEOUT: return "in-kernel wait timed out";
+    case RT_ERR_ARG: return "bad argument";
+  }
+  return "unknown";
+}
+
+extern "C" const char *rt_last_error(rt_solver *s) { return s ? s->err.c_str() : g_last_error.c_str(); }

@@ -1,0 +1,54 @@
+// solver.hpp -- the reference's Solver class surface (include/solver.h:117-197)
+// over the C ABI (include/rtsn.h).  Caller-owned psi/phi/F buffers are
+// written through, as Solver writes through its Eigen references
+// (solver.cpp:50-53); here they are std::vector<double> in the reference's
+// ColMajor layouts (psi: i + M(g + G c); phi, F: g + G c).
+#pragma once
+
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/rtsn.h"
+#include "prm.hpp"
+
+namespace rt {
+
+class SolverError : public std::runtime_error {
+ public:
+  SolverError(rt_status st, const std::string &what) : std::runtime_error(what), status(st) {}
+  rt_status status;
+};
+
+class Solver {
+ public:
+  Solver(rtamd::ParameterHandler &parameter_handler, std::vector<double> &psi_mat, std::vector<double> &phi,
+         std::vector<double> &F, int device = 0);
+  ~Solver();
+  Solver(const Solver &) = delete;
+  Solver &operator=(const Solver &) = delete;
+
+  void solve();                                          // solver.cpp:590-823
+  void compute_angle_integrated_intensity();             // :191-204
+  void compute_positive_angle_integrated_intensity();    // :207-221
+  void compute_radiative_flux();                         // :224-237
+  void compute_balance();                                // :240-284
+  void compute_group_ends();                             // :826-850
+  void get_balance(std::vector<double> &balance) const { balance = balance_; }
+  void get_phi_plus(std::vector<double> &phi_plus) const { phi_plus = phi_plus_; }
+  void get_e_ave(std::vector<double> &e_ave) const;
+  void get_ends(const std::string &side, std::vector<double> &group_ends) const;  // :853-864
+
+  rt_solver *handle() { return h_; }
+
+ private:
+  void check(rt_status st, const char *what) const;
+  void refresh_psi();
+  rtamd::ParameterHandler &ph_;
+  std::vector<double> &psi_, &phi_, &F_;
+  std::vector<double> phi_plus_, balance_, left_ends_, right_ends_;
+  int M_, G_, N_;
+  rt_solver *h_ = nullptr;
+};
+
+}  // namespace rt

@@ -1,0 +1,351 @@
+"""ctypes binding of include/rtsn.h (see package docstring)."""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import re
+import subprocess
+from pathlib import Path
+from typing import Optional
+
+import numpy as np
+
+PKG_ROOT = Path(__file__).resolve().parent.parent          # radiative-transfer_amd/
+REPO_ROOT = PKG_ROOT.parent
+LIB_PATH = PKG_ROOT / "lib" / "librtsn.so"
+HEADER = REPO_ROOT / "include" / "rtsn.h"
+
+STATUS = {0: "ok", 1: "io error", 2: "parse error", 3: "invalid parameter", 4: "correction validation failed",
+          5: "out of memory", 6: "device error", 7: "in-kernel wait timed out", 8: "bad argument"}
+
+
+class RtError(RuntimeError):
+    def __init__(self, status: int, msg: str):
+        super().__init__(f"{msg}: {STATUS.get(status, status)}")
+        self.status = status
+
+
+class rt_params(C.Structure):
+    _fields_ = [
+        ("M", C.c_int), ("G", C.c_int), ("N", C.c_int),
+        ("efirst", C.c_double), ("elast", C.c_double), ("X", C.c_double),
+        ("bc_left_indicator", C.c_int), ("bc_right_indicator", C.c_int),
+        ("use_mg_equilib", C.c_int),
+        ("rho", C.c_double), ("kappa_grey", C.c_double), ("T", C.c_double), ("V", C.c_double),
+        ("use_correction", C.c_int), ("ts_method", C.c_int),
+        ("dt", C.c_double),
+        ("max_timesteps", C.c_int), ("include_validation", C.c_int),
+        ("psi_source", C.POINTER(C.c_double)),
+        ("group_bounds", C.POINTER(C.c_double)),
+        ("group_kappa", C.POINTER(C.c_double)),
+    ]
+
+
+_SCALARS = [f for f, _ in rt_params._fields_ if f not in ("psi_source", "group_bounds", "group_kappa")]
+
+
+def build(force: bool = False) -> Path:
+    """Compile librtsn.so (hipcc, gfx950) in-tree."""
+    if force or not LIB_PATH.exists():
+        subprocess.run(["make", "-C", str(PKG_ROOT), "-j8"], check=True)
+    return LIB_PATH
+
+
+_lib = None
+
+
+def lib():
+    """Load librtsn.so (raises if it has not been built)."""
+    global _lib
+    if _lib is None:
+        if not LIB_PATH.exists():
+            raise RtError(6, f"{LIB_PATH} is missing -- run build() / make -C radiative-transfer_amd")
+        L = C.CDLL(str(LIB_PATH))
+        dp = C.POINTER(C.c_double)
+        vp = C.c_void_p
+        L.rt_params_load.argtypes = [C.c_char_p, C.c_char_p, C.POINTER(rt_params), C.POINTER(C.c_int)]
+        L.rt_params_free.argtypes = [C.POINTER(rt_params)]
+        L.rt_params_free.restype = None
+        L.rt_params_default.argtypes = [C.POINTER(rt_params)]
+        L.rt_params_default.restype = None
+        L.rt_quadrature.argtypes = [C.c_int, dp, dp]
+        L.rt_planck_groups.argtypes = [C.c_double, C.c_int, dp, dp, dp]
+        L.rt_create.argtypes = [C.c_char_p, C.c_char_p, C.c_int, C.POINTER(vp)]
+        L.rt_create_from_params.argtypes = [C.POINTER(rt_params), C.c_int, C.c_int, C.c_int, C.POINTER(vp)]
+        L.rt_destroy.argtypes = [vp]
+        L.rt_destroy.restype = None
+        for name in ("rt_solve", "rt_synchronize"):
+            getattr(L, name).argtypes = [vp]
+        L.rt_advance.argtypes = [vp, C.c_int]
+        L.rt_stream.argtypes = [vp]
+        L.rt_stream.restype = vp
+        L.rt_get_dims.argtypes = [vp] + [C.POINTER(C.c_int)] * 5
+        for name in ("rt_get_psi", "rt_get_ends", "rt_get_balance", "rt_get_e_ave", "rt_get_psi_source",
+                     "rt_group_absorption_device"):
+            getattr(L, name).argtypes = [vp, dp]
+        L.rt_set_ends.argtypes = [vp, dp]
+        L.rt_get_moments.argtypes = [vp, dp, dp, dp]
+        L.rt_get_group_ends.argtypes = [vp, dp, dp]
+        L.rt_get_group_data.argtypes = [vp, dp, dp, dp, dp]
+        L.rt_get_quadrature.argtypes = [vp, dp, dp]
+        L.rt_set_profiling.argtypes = [vp, C.c_int]
+        L.rt_get_sweep_time.argtypes = [vp, dp, C.POINTER(C.c_longlong)]
+        L.rt_sweep_traffic.argtypes = [vp, dp, dp]
+        L.rt_sweep_geometry.argtypes = [vp, C.POINTER(C.c_int), C.POINTER(C.c_longlong)]
+        L.rt_status_string.argtypes = [C.c_int]
+        L.rt_status_string.restype = C.c_char_p
+        L.rt_last_error.argtypes = [vp]
+        L.rt_last_error.restype = C.c_char_p
+        _lib = L
+    return _lib
+
+
+def exported_symbols() -> list[str]:
+    """Function names declared in include/rtsn.h."""
+    text = HEADER.read_text()
+    return sorted(set(re.findall(r"\b(rt_[a-z_0-9]+)\s*\(", text)))
+
+
+def _dp(a: np.ndarray):
+    return a.ctypes.data_as(C.POINTER(C.c_double))
+
+
+def _check(st: int, what: str, handle=None):
+    if st != 0:
+        msg = lib().rt_last_error(handle).decode(errors="replace")
+        raise RtError(st, f"{what} ({msg})")
+
+
+def params_default() -> dict:
+    p = rt_params()
+    lib().rt_params_default(C.byref(p))
+    d = {f: getattr(p, f) for f in _SCALARS}
+    d.update(psi_source=None, group_bounds=None, group_kappa=None)
+    return d
+
+
+def quadrature(M: int):
+    mu, wt = np.empty(M), np.empty(M)
+    _check(lib().rt_quadrature(M, _dp(mu), _dp(wt)), "rt_quadrature")
+    return mu, wt
+
+
+def planck_groups(T: float, e_edge):
+    e = np.ascontiguousarray(e_edge, dtype=np.float64)
+    G = len(e) - 1
+    B, dB = np.empty(G), np.empty(G)
+    _check(lib().rt_planck_groups(T, G, _dp(e), _dp(B), _dp(dB)), "rt_planck_groups")
+    return B, dB
+
+
+class ParameterHandler:
+    """ParameterHandler(filename) (include/ParameterHandler.h:67): the .prm reader."""
+
+    def __init__(self, filename, table_dir: Optional[str] = None):
+        p = rt_params()
+        found = C.c_int(0)
+        td = None if table_dir is None else (str(table_dir).rstrip("/") + "/").encode()
+        _check(lib().rt_params_load(str(filename).encode(), td, C.byref(p), C.byref(found)), "rt_params_load")
+        self.prm_found = bool(found.value)
+        self.params = {f: getattr(p, f) for f in _SCALARS}
+        M, G = p.M, p.G
+        self.params["psi_source"] = (np.ctypeslib.as_array(p.psi_source, shape=(M * G,)).copy().reshape(M, G)
+                                     if p.psi_source else np.zeros((M, G)))
+        self.params["group_bounds"] = (np.ctypeslib.as_array(p.group_bounds, shape=(G + 1,)).copy()
+                                       if p.group_bounds else None)
+        self.params["group_kappa"] = (np.ctypeslib.as_array(p.group_kappa, shape=(G,)).copy()
+                                      if p.group_kappa else None)
+        lib().rt_params_free(C.byref(p))
+
+    def __getattr__(self, name):
+        # get_M(), get_G(), ... get_validation() as in ParameterHandler.h:73-98
+        if name.startswith("get_"):
+            key = {"get_validation": "include_validation",
+                   "get_bc_left_indicator": "bc_left_indicator", "get_bc_right_indicator": "bc_right_indicator",
+                   "get_have_group_bounds": "group_bounds",
+                   "get_have_group_absorption_opacities": "group_kappa"}.get(name, name[4:])
+            if key in ("group_bounds", "group_kappa"):
+                return lambda: self.params[key] is not None
+            if key == "dx":
+                return lambda: self.params["X"] / self.params["N"]
+            if key in self.params:
+                return lambda: self.params[key]
+        raise AttributeError(name)
+
+
+def _to_struct(params: dict, keep: list) -> rt_params:
+    p = rt_params()
+    for f in _SCALARS:
+        setattr(p, f, params[f])
+    M, G = params["M"], params["G"]
+    ps = params.get("psi_source")
+    if ps is not None:
+        a = np.ascontiguousarray(np.asarray(ps, dtype=np.float64).reshape(M * G))
+        keep.append(a)
+        p.psi_source = _dp(a)
+    for key in ("group_bounds", "group_kappa"):
+        v = params.get(key)
+        if v is not None:
+            a = np.ascontiguousarray(v, dtype=np.float64)
+            keep.append(a)
+            setattr(p, key, _dp(a))
+    return p
+
+
+class Solver:
+    """The reference's Solver (include/solver.h:117-197) on librtsn.
+
+    Solver(parameter_handler_or_params, device=0, g_lo=0, g_hi=0).  Results
+    are numpy arrays in the reference's index order: psi (M, G, N), phi / F /
+    phi_plus (G, N), ends (M, G, N, 2)."""
+
+    def __init__(self, ph, device: int = 0, g_lo: int = 0, g_hi: int = 0):
+        params = ph.params if isinstance(ph, ParameterHandler) else dict(ph)
+        for k, v in params_default().items():
+            params.setdefault(k, v)
+        keep: list = []
+        p = _to_struct(params, keep)
+        h = C.c_void_p()
+        _check(lib().rt_create_from_params(C.byref(p), g_lo, g_hi, device, C.byref(h)), "rt_create_from_params")
+        self._h = h
+        M, Gl, N, lo, hi = (C.c_int() for _ in range(5))
+        lib().rt_get_dims(h, C.byref(M), C.byref(Gl), C.byref(N), C.byref(lo), C.byref(hi))
+        self.M, self.G, self.N, self.g_lo, self.g_hi = M.value, Gl.value, N.value, lo.value, hi.value
+        self.G_total = params["G"]
+        self.params = params
+        self._phi_plus = None
+        self._balance = None
+        self._ends = None
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().rt_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # pragma: no cover
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    # ---- stepping ----
+    def solve(self):
+        _check(lib().rt_solve(self._h), "rt_solve", self._h)
+
+    def advance(self, nsteps: int):
+        _check(lib().rt_advance(self._h, int(nsteps)), "rt_advance", self._h)
+
+    def synchronize(self):
+        _check(lib().rt_synchronize(self._h), "rt_synchronize", self._h)
+
+    @property
+    def stream(self) -> int:
+        return lib().rt_stream(self._h) or 0
+
+    # ---- results ----
+    def psi(self) -> np.ndarray:
+        out = np.empty(self.M * self.G * self.N)
+        _check(lib().rt_get_psi(self._h, _dp(out)), "rt_get_psi", self._h)
+        return out.reshape(self.N, self.G, self.M).transpose(2, 1, 0).copy()
+
+    def ends(self) -> np.ndarray:
+        out = np.empty(2 * self.M * self.G * self.N)
+        _check(lib().rt_get_ends(self._h, _dp(out)), "rt_get_ends", self._h)
+        return out.reshape(2, self.N, self.G, self.M).transpose(3, 2, 1, 0).copy()
+
+    def set_ends(self, ends: np.ndarray):
+        flat = np.ascontiguousarray(np.asarray(ends, dtype=np.float64).transpose(3, 2, 1, 0)).ravel()
+        _check(lib().rt_set_ends(self._h, _dp(flat)), "rt_set_ends", self._h)
+
+    def moments(self):
+        n = self.G * self.N
+        phi, F, pp = np.empty(n), np.empty(n), np.empty(n)
+        _check(lib().rt_get_moments(self._h, _dp(phi), _dp(F), _dp(pp)), "rt_get_moments", self._h)
+        f = lambda a: a.reshape(self.N, self.G).T.copy()  # noqa: E731
+        return f(phi), f(F), f(pp)
+
+    def compute_angle_integrated_intensity(self) -> np.ndarray:
+        return self.moments()[0]
+
+    def compute_radiative_flux(self) -> np.ndarray:
+        return self.moments()[1]
+
+    def compute_positive_angle_integrated_intensity(self) -> np.ndarray:
+        self._phi_plus = self.moments()[2]
+        return self._phi_plus
+
+    def get_phi_plus(self) -> np.ndarray:
+        return self._phi_plus
+
+    def compute_balance(self) -> np.ndarray:
+        out = np.empty(self.G)
+        _check(lib().rt_get_balance(self._h, _dp(out)), "rt_get_balance", self._h)
+        self._balance = out
+        return out
+
+    def get_balance(self) -> np.ndarray:
+        return self._balance
+
+    def compute_group_ends(self):
+        left, right = np.empty(self.G), np.empty(self.G)
+        _check(lib().rt_get_group_ends(self._h, _dp(left), _dp(right)), "rt_get_group_ends", self._h)
+        self._ends = (left, right)
+        return self._ends
+
+    def get_ends(self, side: str) -> np.ndarray:
+        assert side in ("left", "right"), "Invalid option for 'side'."
+        return self._ends[0] if side == "left" else self._ends[1]
+
+    def get_e_ave(self) -> np.ndarray:
+        out = np.empty(self.G_total)
+        _check(lib().rt_get_e_ave(self._h, _dp(out)), "rt_get_e_ave", self._h)
+        return out
+
+    def groups(self) -> dict:
+        G = self.G_total
+        d = {"e_edge": np.empty(G + 1), "B": np.empty(G), "dBdT": np.empty(G), "kappa": np.empty(G)}
+        _check(lib().rt_get_group_data(self._h, _dp(d["e_edge"]), _dp(d["B"]), _dp(d["dBdT"]), _dp(d["kappa"])),
+               "rt_get_group_data", self._h)
+        return d
+
+    def quad(self):
+        mu, wt = np.empty(self.M), np.empty(self.M)
+        _check(lib().rt_get_quadrature(self._h, _dp(mu), _dp(wt)), "rt_get_quadrature", self._h)
+        return mu, wt
+
+    def psi_source(self) -> np.ndarray:
+        out = np.empty(self.M * self.G_total)
+        _check(lib().rt_get_psi_source(self._h, _dp(out)), "rt_get_psi_source", self._h)
+        return out.reshape(self.M, self.G_total)
+
+    def group_absorption_device(self, d_out_ptr: int):
+        _check(lib().rt_group_absorption_device(self._h, C.cast(C.c_void_p(d_out_ptr), C.POINTER(C.c_double))),
+               "rt_group_absorption_device", self._h)
+
+    # ---- measurement ----
+    def set_profiling(self, on: bool):
+        _check(lib().rt_set_profiling(self._h, int(on)), "rt_set_profiling", self._h)
+
+    def sweep_time(self):
+        ms = C.c_double()
+        n = C.c_longlong()
+        _check(lib().rt_get_sweep_time(self._h, C.byref(ms), C.byref(n)), "rt_get_sweep_time", self._h)
+        return ms.value, n.value
+
+    def sweep_traffic(self):
+        b = C.c_double()
+        u = C.c_double()
+        _check(lib().rt_sweep_traffic(self._h, C.byref(b), C.byref(u)), "rt_sweep_traffic", self._h)
+        return b.value, u.value
+
+    def sweep_geometry(self):
+        wg = C.c_int()
+        t = C.c_longlong()
+        _check(lib().rt_sweep_geometry(self._h, C.byref(wg), C.byref(t)), "rt_sweep_geometry", self._h)
+        return wg.value, t.value

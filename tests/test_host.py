@@ -1,0 +1,136 @@
+"""Host-side checks of librtsn.so that need no GPU: the library loads and
+exports every entry point of include/rtsn.h, and its host logic (the .prm
+reader with the kaityo256/param quirks, GLQuad, Planck) agrees with the
+oracle's restatement of the reference -- bitwise, since both run the
+reference's arithmetic on the same host."""
+import ctypes
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import PRM_DIR, REPO
+
+LIB = REPO / "radiative-transfer_amd" / "lib" / "librtsn.so"
+
+
+def test_library_exports_every_header_symbol(rtsn_mod):
+    assert LIB.exists(), "build librtsn.so first (__graft_entry__.build())"
+    out = subprocess.run(["nm", "-D", "--defined-only", str(LIB)], capture_output=True, text=True, check=True).stdout
+    exported = {line.split()[-1] for line in out.splitlines() if line.strip()}
+    declared = rtsn_mod.exported_symbols()
+    assert len(declared) >= 25
+    missing = [s for s in declared if s not in exported]
+    assert not missing, missing
+    ctypes.CDLL(str(LIB))  # loads (links against libamdhip64 only)
+
+
+def test_library_is_gfx950_code(rtsn_mod):
+    """The fat binary carries gfx950 code objects (and nothing else to fall back to)."""
+    blob = LIB.read_bytes()
+    assert b"gfx950" in blob
+    for other in (b"gfx942", b"gfx90a", b"sm_"):
+        assert other + b"\x00" not in blob or other == b"sm_"
+
+
+def _params_equal(ph, ref):
+    for k in ("M", "G", "N", "efirst", "elast", "X", "rho", "kappa_grey", "T", "V", "dt", "max_timesteps"):
+        assert ph.params[k] == ref[k], k
+    assert ph.params["bc_left_indicator"] == ref["bc_left"]
+    assert ph.params["bc_right_indicator"] == ref["bc_right"]
+    assert ph.params["use_mg_equilib"] == ref["use_mg_equilib"]
+    assert ph.params["use_correction"] == ref["use_correction"]
+    assert ph.params["ts_method"] == ref["ts_method"]
+    assert ph.params["include_validation"] == ref["include_validation"]
+    np.testing.assert_array_equal(ph.params["psi_source"], ref["psi_source"])
+    for a, b in (("group_bounds", "group_bounds"), ("group_kappa", "group_kappa")):
+        if ref[b] is None:
+            assert ph.params[a] is None
+        else:
+            np.testing.assert_array_equal(ph.params[a], ref[b])
+
+
+@pytest.mark.parametrize("name", ["single_group.prm", "multi_group_equilibrium.prm", "llnl_slab_test.prm",
+                                  "llnl_slab_test_uncapped.prm", "default.prm", "template.prm"])
+def test_prm_reader_matches_oracle(rtsn_mod, oracle_mod, name):
+    ph = rtsn_mod.ParameterHandler(PRM_DIR / name, table_dir=PRM_DIR)
+    ref = oracle_mod.parse_prm(PRM_DIR / name, table_dir=PRM_DIR)
+    _params_equal(ph, ref)
+
+
+def test_prm_quirks(rtsn_mod, tmp_path):
+    """param.h:62-75 / param.cpp:4-66 semantics."""
+    f = tmp_path / "q.prm"
+    f.write_text("\n".join([
+        "# comment line",
+        " # not a comment: key is ' # not a comment: key is ' -> ignored",
+        "M=4                    # trailing comment after a number is fine",
+        "M=8",                      # duplicate: first one wins
+        "G=2",
+        "use_correction=true   # trailing text -> false (exact match only)",
+        "include_validation=Yes",
+        "use_mg_equilib=TRUE",      # not one of yes/Yes/true/True
+        "N = 7",                    # key is 'N ' -> N stays at its default 100
+        "psi_source=1.5 2.5 3 4.25 7 8 9 10 # stops at '#'",
+        "dt=2.5e-3xyz",
+        "bc_left_indicator=1",
+    ]) + "\n")
+    ph = rtsn_mod.ParameterHandler(f, table_dir=tmp_path)
+    assert ph.get_M() == 4
+    assert ph.get_G() == 2
+    assert ph.get_N() == 100
+    assert ph.get_use_correction() == 0
+    assert ph.get_validation() == 1
+    assert ph.get_use_mg_equilib() == 0
+    assert ph.get_dt() == 2.5e-3
+    np.testing.assert_array_equal(ph.params["psi_source"], np.array([[1.5, 2.5], [3, 4.25], [7, 8], [9, 10]]))
+
+
+def test_prm_missing_file_gives_defaults(rtsn_mod, tmp_path):
+    ph = rtsn_mod.ParameterHandler(tmp_path / "nope.prm", table_dir=tmp_path)
+    assert not ph.prm_found
+    assert (ph.get_M(), ph.get_G(), ph.get_N(), ph.get_ts_method(), ph.get_max_timesteps()) == (2, 1, 100, 3, 1000)
+    assert ph.get_bc_left_indicator() == 2 and ph.get_bc_right_indicator() == 1
+
+
+def test_prm_errors(rtsn_mod, tmp_path):
+    f = tmp_path / "bad.prm"
+    f.write_text("M=abc\n")
+    with pytest.raises(rtsn_mod.RtError) as e:
+        rtsn_mod.ParameterHandler(f, table_dir=tmp_path)
+    assert e.value.status == 2  # RT_ERR_PARSE (std::stoi throws)
+    f.write_text("G=3\nhave_group_bounds=true\nfilename_group_bounds=missing.txt\n")
+    with pytest.raises(rtsn_mod.RtError) as e:
+        rtsn_mod.ParameterHandler(f, table_dir=tmp_path)
+    assert e.value.status == 1  # RT_ERR_IO (exit(1) in the reference)
+    (tmp_path / "b.txt").write_text("0.1 0.2\n")
+    f.write_text("G=3\nhave_group_bounds=true\nfilename_group_bounds=b.txt\n")
+    with pytest.raises(rtsn_mod.RtError) as e:
+        rtsn_mod.ParameterHandler(f, table_dir=tmp_path)
+    assert e.value.status == 3  # count assert
+
+
+@pytest.mark.parametrize("M", [2, 4, 16, 64, 128])
+def test_quadrature_bitwise(rtsn_mod, oracle_mod, M):
+    mu, wt = rtsn_mod.quadrature(M)
+    mo, wo = oracle_mod.glquad(M)
+    assert np.array_equal(mu, mo) and np.array_equal(wt, wo)
+
+
+@pytest.mark.parametrize("name", ["llnl_slab_test.prm", "multi_group_equilibrium.prm", "single_group.prm"])
+def test_planck_bitwise(rtsn_mod, oracle_mod, name):
+    p = oracle_mod.parse_prm(PRM_DIR / name, table_dir=PRM_DIR)
+    s = oracle_mod.OracleSolver(p)
+    g = s.groups()
+    B, dB = rtsn_mod.planck_groups(p["T"], g["e_edge"])
+    assert np.array_equal(B, g["B"])
+    assert np.array_equal(dB, g["dBdT"])
+
+
+def test_solver_without_gpu_fails_loudly(rtsn_mod):
+    from conftest import gpu_available
+    if gpu_available():
+        pytest.skip("a GPU is present")
+    with pytest.raises(rtsn_mod.RtError) as e:
+        rtsn_mod.Solver(rtsn_mod.params_default())
+    assert e.value.status == 6  # RT_ERR_DEVICE: no CPU fallback
