@@ -1,0 +1,207 @@
+#!/usr/bin/env python3
+"""Sweep throughput benchmark (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--variant v0|corr]
+                    [--scaling weak|strong] [--no-cpu-baseline]
+
+Workload (SURVEY.md §8(d) "SL"): 1D slab X = 0.4 cm, N = 1e6 cells, S64
+Gauss-Legendre (M = 64), 128 energy groups per GPU on a log grid 0.001-30 keV
+with kappa_g resampled from the LLNL capped table, rho = 1, T = 1 keV, BDF2
+(ts_method = 3), dt = 1e-3, vacuum boundaries; V = 0 (variant v0) or
+V = 5.994 with the v/c correction (variant corr).  A "step" is one full BDF2
+step (4 substeps) of every cell x angle x group of the GPU's groups, i.e.
+4 M G N cell-angle-group updates, computed in fp64 by the fused HIP sweep
+(one kernel launch per step).  State is resident in HBM before timing.
+
+Multi-GPU: one process per GPU (torch.distributed.run), groups sharded across
+ranks with no collective in the data path (groups are independent for the
+whole run: T is constant).  weak scaling (default): every rank owns 128 groups
+of a 128*N-group grid; strong: the 128 groups are split N ways.  Timing:
+barrier + device synchronise on both sides of the K timed steps, max over
+ranks.  After timing, the group-summed absorption rate is all-reduced over
+RCCL once (the north_star group-sum hook) and checked.
+
+roofline: algorithmic bytes of one sweep launch (16 B read + 16 B write per
+cell x line: the fused step moves the state once) / the sweep kernel's mean
+duration from HIP events recorded around each launch on the library's
+stream; peak 8.0 TB/s (MI355X_MICROARCH.md).  traffic: per-launch HBM bytes
+from rocprofv3 PMC passes recorded in profiles/pmc_<variant>.json
+(FETCH_SIZE x 2 + WRITE_SIZE, the gfx950 correction), null if absent.
+cpu_baseline: the C oracle (a single-threaded port of the reference's
+algorithm) on a bounded sample of the same workload.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+REPO = Path(__file__).resolve().parent
+sys.path.insert(0, str(REPO / "radiative-transfer_amd"))
+
+import numpy as np  # noqa: E402
+
+METRIC = "cell·angle·group updates/sec (Sn sweep) + BDF2 steps/sec, llnl_slab_test"
+HBM_PEAK = 8.0e12
+KAPPA_TABLE = REPO / "tests" / "golden" / "prm" / "llnl_slab_test_group_kappa_a.txt"
+
+
+def slab_params(G_total: int, variant: str, N: int = 1_000_000, M: int = 64) -> dict:
+    kap = np.loadtxt(KAPPA_TABLE)
+    return dict(M=M, G=G_total, N=N, X=0.4, efirst=0.001, elast=30.0,
+                bc_left_indicator=0, bc_right_indicator=0, use_mg_equilib=0,
+                rho=1.0, kappa_grey=1.0, T=1.0, V=(5.994 if variant == "corr" else 0.0),
+                use_correction=1, ts_method=3, dt=1e-3, max_timesteps=1, include_validation=0,
+                psi_source=np.zeros((M, G_total)), group_bounds=None,
+                group_kappa=kap[(np.arange(G_total) * len(kap)) // G_total])
+
+
+def cpu_baseline(variant: str) -> dict:
+    """The oracle on a bounded sample: all 64 angles of one group, 2.5e5 cells, 1 BDF2 step."""
+    sys.path.insert(0, str(REPO / "oracle"))
+    import oracle
+    oracle.build()
+    G, N, g = 128, 250_000, 64
+    p = slab_params(G, variant, N=N)
+    q = dict(p)
+    q.update(bc_left=p["bc_left_indicator"], bc_right=p["bc_right_indicator"], dx=p["X"] / N,
+             have_group_bounds=0, have_group_kappa=1, prm_found=1)
+    s = oracle.OracleSolver(q, g_lo=g, g_hi=g + 1)
+    t0 = time.perf_counter()
+    s.solve()
+    dt = time.perf_counter() - t0
+    upd = 4.0 * q["M"] * N
+    return {"value": upd / dt, "unit": "cell-angle-group updates/s", "cores": 1, "kind": "port",
+            "sample": f"oracle/rt_oracle.c (single-threaded restatement of solver.cpp), SL {variant}: "
+                      f"M=64, 1 of 128 groups (g={g}), N={N}, 1 BDF2 step = {upd:.3g} updates in {dt:.2f} s"}
+
+
+def load_traffic(variant: str):
+    f = REPO / "profiles" / f"pmc_{variant}.json"
+    if not f.exists():
+        return None
+    try:
+        return json.loads(f.read_text()).get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=4)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--variant", choices=["v0", "corr"], default="v0")
+    ap.add_argument("--scaling", choices=["weak", "strong"], default="weak")
+    ap.add_argument("--groups", type=int, default=128, help="groups per GPU (weak) or in total (strong)")
+    ap.add_argument("--cells", type=int, default=1_000_000)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    import rtsn
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    if args.scaling == "weak":
+        G_total = args.groups * world
+        g_lo, g_hi = rank * args.groups, (rank + 1) * args.groups
+    else:
+        G_total = args.groups
+        per = (G_total + world - 1) // world
+        g_lo, g_hi = rank * per, min(G_total, (rank + 1) * per)
+    p = slab_params(G_total, args.variant, N=args.cells)
+    solver = rtsn.Solver(p, device=local, g_lo=g_lo, g_hi=g_hi)
+    bytes_step, upd_step = solver.sweep_traffic()
+    wg, tiles = solver.sweep_geometry()
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    solver.advance(args.warmup)
+    solver.synchronize()
+    barrier()
+    solver.set_profiling(True)
+    t0 = time.perf_counter()
+    solver.advance(args.steps)
+    torch.cuda.synchronize()
+    solver.synchronize()
+    barrier()
+    wall = time.perf_counter() - t0
+    kern_ms, nlaunch = solver.sweep_time()
+    solver.set_profiling(False)
+
+    # group-summed absorption all-reduce (RCCL), outside the timed region
+    absorb = torch.zeros(p["N"], dtype=torch.float64, device=f"cuda:{local}")
+    solver.group_absorption_device(absorb.data_ptr())
+    solver.synchronize()
+    if world > 1:
+        dist.all_reduce(absorb)
+    finite = bool(torch.isfinite(absorb).all().item())
+
+    t = torch.tensor([wall, kern_ms / max(nlaunch, 1)], dtype=torch.float64, device=f"cuda:{local}")
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    wall_max, kern_avg_ms = float(t[0]), float(t[1])
+
+    total_updates = upd_step * args.steps * world
+    value = total_updates / wall_max
+    ms_per_step = 1e3 * wall_max / args.steps
+    achieved = bytes_step / (kern_avg_ms * 1e-3)
+    line = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "cell-angle-group updates/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_per_step,
+        "higher_is_better": True,
+        "scaling": args.scaling,
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic",
+        "bdf2_steps_per_s": 1e3 / ms_per_step,
+        "config": {
+            "workload": f"SL slab: N={p['N']} cells x S{p['M']} x {g_hi - g_lo} groups per GPU "
+                        f"({G_total} total), BDF2 dt=1e-3, V={p['V']}, use_correction=1, vacuum BCs",
+            "cells": p["N"], "angles": p["M"], "groups_per_gpu": g_hi - g_lo, "groups_total": G_total,
+            "time_scheme": "BDF2 (4 fused substeps per step)",
+            "parallelism": f"group shards x{world}, no data-path collective",
+            "sweep_workgroups": wg, "tiles_per_step": tiles,
+        },
+        "roofline": {
+            "bound": "hbm",
+            "achieved": achieved / 1e9,
+            "peak": HBM_PEAK / 1e9,
+            "unit": "GB/s",
+            "frac": achieved / HBM_PEAK,
+            "traffic": load_traffic(args.variant),
+            "kernel": "sweep_step_kernel<3>",
+            "kernel_ms": kern_avg_ms,
+            "algorithmic_bytes_per_launch": bytes_step,
+        },
+        "absorption_allreduce_finite": finite,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline(args.variant)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    solver.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

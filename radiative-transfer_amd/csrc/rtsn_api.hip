@@ -50,14 +50,14 @@ struct rt_solver {
   DeviceBuf E, lc, Apow, bdry, outflow, outflow_flag, status, agg, pref, error, lineB, muwt, mom, rows, sigma;
   // profiling
   bool profiling = false;
-  hipEvent_t ev0 = nullptr, ev1 = nullptr;
-  double sweep_ms = 0.0;
-  long long launches = 0;
+  std::vector<hipEvent_t> ev_pool;   // (start, stop) pairs of profiled launches
+  size_t ev_used = 0;
+  double sweep_ms = 0.0;             // folded-in time of earlier pairs
+  long long launches = 0, profiled = 0;
   std::string err;
 
   ~rt_solver() {
-    if (ev0) (void)hipEventDestroy(ev0);
-    if (ev1) (void)hipEventDestroy(ev1);
+    for (hipEvent_t e : ev_pool) (void)hipEventDestroy(e);
     if (stream) (void)hipStreamDestroy(stream);
   }
 };
@@ -404,6 +404,7 @@ extern "C" rt_status rt_create_from_params(const rt_params *pin, int g_lo, int g
   HIP_TRY(h, launch_init_state(static_cast<double2 *>(h->E.p), static_cast<const double *>(h->lineB.p), q.N, h->Lpad,
                                h->stream));
   HIP_TRY(h, hipMemsetAsync(h->outflow.p, 0, h->outflow.bytes, h->stream));
+  HIP_TRY(h, hipMemsetAsync(h->error.p, 0, h->error.bytes, h->stream));
 
   int per_cu = 0;
   HIP_TRY(h, sweep_occupancy(h->scheme, &per_cu));
@@ -412,8 +413,6 @@ extern "C" rt_status rt_create_from_params(const rt_params *pin, int g_lo, int g
   long long P = std::min<long long>(maxP, h->tiles);
   if (P > h->Q && maxP >= h->Q) P = (P / h->Q) * h->Q;  // keep each workgroup on one line group
   h->grid = static_cast<int>(std::max<long long>(1, P));
-  HIP_TRY(h, hipEventCreate(&h->ev0));
-  HIP_TRY(h, hipEventCreate(&h->ev1));
   HIP_TRY(h, hipStreamSynchronize(h->stream));
   *out = s.release();
   return RT_OK;
@@ -447,6 +446,18 @@ static rt_status ensure_equilibrium(rt_solver *s) {
   return upload_inflow(s);
 }
 
+// Sum the elapsed time of the recorded (start, stop) event pairs.
+static rt_status fold_events(rt_solver *s) {
+  for (size_t k = 0; k + 1 < s->ev_used; k += 2) {
+    HIP_TRY(s, hipEventSynchronize(s->ev_pool[k + 1]));
+    float ms = 0.f;
+    HIP_TRY(s, hipEventElapsedTime(&ms, s->ev_pool[k], s->ev_pool[k + 1]));
+    s->sweep_ms += ms;
+  }
+  s->ev_used = 0;
+  return RT_OK;
+}
+
 static rt_status enqueue_steps(rt_solver *s, int nsteps) {
   SweepArgs a{};
   a.E = static_cast<double2 *>(s->E.p);
@@ -469,14 +480,20 @@ static rt_status enqueue_steps(rt_solver *s, int nsteps) {
   for (int n = 0; n < nsteps; ++n) {
     HIP_TRY(s, hipMemsetAsync(s->status.p, 0, s->status.bytes, s->stream));
     HIP_TRY(s, hipMemsetAsync(s->outflow_flag.p, 0, s->outflow_flag.bytes, s->stream));
-    if (s->profiling) HIP_TRY(s, hipEventRecord(s->ev0, s->stream));
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (s->profiling) {
+      if (s->ev_used + 2 > s->ev_pool.size()) {
+        rt_status st = fold_events(s);  // drain the pool when it is full
+        if (st) return st;
+      }
+      e0 = s->ev_pool[s->ev_used++];
+      e1 = s->ev_pool[s->ev_used++];
+      HIP_TRY(s, hipEventRecord(e0, s->stream));
+    }
     HIP_TRY(s, launch_sweep(s->scheme, a, s->grid, s->stream));
     if (s->profiling) {
-      HIP_TRY(s, hipEventRecord(s->ev1, s->stream));
-      HIP_TRY(s, hipEventSynchronize(s->ev1));
-      float ms = 0.f;
-      HIP_TRY(s, hipEventElapsedTime(&ms, s->ev0, s->ev1));
-      s->sweep_ms += ms;
+      HIP_TRY(s, hipEventRecord(e1, s->stream));
+      ++s->profiled;
     }
     ++s->launches;
   }
@@ -714,16 +731,24 @@ extern "C" rt_status rt_group_absorption_device(rt_solver *s, double *d_out) {
 
 extern "C" rt_status rt_set_profiling(rt_solver *s, int on) {
   if (!s) return fail(nullptr, RT_ERR_ARG, "rt_set_profiling: NULL handle");
+  rt_status st = fold_events(s);
+  if (st) return st;
   s->profiling = on != 0;
   s->sweep_ms = 0.0;
-  s->launches = 0;
+  s->profiled = 0;
+  if (s->profiling && s->ev_pool.empty()) {
+    s->ev_pool.resize(256, nullptr);
+    for (hipEvent_t &e : s->ev_pool) HIP_TRY(s, hipEventCreate(&e));
+  }
   return RT_OK;
 }
 
 extern "C" rt_status rt_get_sweep_time(rt_solver *s, double *total_ms, long long *launches) {
   if (!s) return fail(nullptr, RT_ERR_ARG, "rt_get_sweep_time: NULL handle");
+  rt_status st = fold_events(s);
+  if (st) return st;
   if (total_ms) *total_ms = s->sweep_ms;
-  if (launches) *launches = s->launches;
+  if (launches) *launches = s->profiled;
   return RT_OK;
 }
 

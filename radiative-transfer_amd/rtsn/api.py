@@ -5,6 +5,7 @@ import ctypes as C
 import os
 import re
 import subprocess
+import sys
 from pathlib import Path
 from typing import Optional
 
@@ -58,6 +59,14 @@ def lib():
     """Load librtsn.so (raises if it has not been built)."""
     global _lib
     if _lib is None:
+        # PyTorch-ROCm bundles its own libamdhip64.so.7; load it first (if
+        # torch is installed) so that torch and librtsn share ONE HIP runtime
+        # in the process instead of two that race for the device.
+        if "torch" not in sys.modules:
+            try:
+                import torch  # noqa: F401
+            except ImportError:
+                pass
         if not LIB_PATH.exists():
             raise RtError(6, f"{LIB_PATH} is missing -- run build() / make -C radiative-transfer_amd")
         L = C.CDLL(str(LIB_PATH))

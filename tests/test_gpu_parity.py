@@ -134,6 +134,7 @@ def test_random_state_long_lines(rtsn_mod, oracle_mod):
     on 20k-cell lines: exercises the decoupled look-back across ~300 tiles."""
     p = load(oracle_mod, "llnl_slab_test.prm", N=20000, M=4, max_timesteps=1, use_correction=1, V=5.994)
     p["dx"] = p["X"] / p["N"]
+    p["psi_source"] = np.zeros((p["M"], p["G"]))
     lo, hi = 10, 26
     orc = oracle_mod.OracleSolver(p, g_lo=lo, g_hi=hi)
     B = orc.groups()["B"][lo:hi]
