@@ -151,6 +151,47 @@ __host__ __device__ __forceinline__ void cell_first(const LineConst &L, double h
   }
 }
 
+// Carried state entering the first cell of a line from per-substep inflow
+// values b[0..3] (solver.cpp:695-697: local_bdry = half_local_bdry =
+// local_bdry_prev_it = bdry_cond).
+template <int S>
+__host__ __device__ __forceinline__ void head_state(const double *b, double *X) {
+  if constexpr (S == SCHEME_BE) {
+    X[0] = b[0];
+  } else if constexpr (S == SCHEME_CN) {
+    X[0] = b[0];
+    X[1] = b[0];
+  } else {
+    X[0] = b[1];
+    X[1] = b[0];
+    X[2] = b[1];
+    X[3] = b[2];
+    X[4] = b[3];
+  }
+}
+
+// cell_step for a cell that may be a line head (head_state already applied):
+// in the BDF substep the head sees b[3] as both prev and half upwind node.
+// With equal inflows (non-reflective boundaries) this equals cell_step.
+template <int S>
+__host__ __device__ __forceinline__ void cell_step_maybe_head(const LineConst &L, double hd, bool neg, double pin,
+                                                              double pout, double *X, bool head, double b3,
+                                                              double &oin, double &oout) {
+  if constexpr (S == SCHEME_BDF2) {
+    double a, b, c;
+    const double hup = head ? b3 : (neg ? X[2] : X[1]);
+    const double xp3 = head ? b3 : X[0];
+    cell_bdf2_explicit(L, hd, neg, pin, pout, X[1], X[2], X[3], X[4], X[0], xp3, hup, a, b, c, oin, oout);
+    X[0] = pout;
+    X[1] = a;
+    X[2] = b;
+    X[3] = c;
+    X[4] = oout;
+  } else {
+    cell_step<S>(L, hd, neg, pin, pout, X, oin, oout);
+  }
+}
+
 // Index of (r, c), c <= r, in a packed lower triangle.
 __host__ __device__ __forceinline__ constexpr int tri(int r, int c) { return r * (r + 1) / 2 + c; }
 

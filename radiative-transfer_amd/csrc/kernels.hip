@@ -72,6 +72,21 @@ __device__ __forceinline__ unsigned wait_flag(const unsigned *flag, unsigned wan
   }
 }
 
+// A wave's 16 rows of one tile are addressed through a buffer descriptor built
+// from wave-uniform values: base (SGPR) + row offset (SGPR soffset) + lane*16
+// (one VGPR), instead of a 64-bit VGPR address per row.
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rows_rsrc(const double2 *base, int row_bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<double2 *>(base), 0, kSweepCells * row_bytes, 0x00020000);
+}
+__device__ __forceinline__ double2 row_load(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
+  return __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
+}
+__device__ __forceinline__ void row_store(__amdgpu_buffer_rsrc_t r, int voff, int soff, double x, double y) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, make_double2(x, y)), r, voff, soff, 0);
+}
+
 template <int K>
 __device__ __forceinline__ void matvec_lt(const double *Asm, int lane, const double *x, double *y) {
   // y = A x, A packed lower-triangular in LDS as [tri][64]
@@ -87,6 +102,39 @@ __device__ __forceinline__ void matvec_lt(const double *Asm, int lane, const dou
 // ------------------------------------------------------------------------
 // The sweep kernel
 // ------------------------------------------------------------------------
+// Phase-2 sweep of one wave's 16 cells: write the step-end state and
+// prefetch the same row of the workgroup's next tile into the registers just
+// consumed.  Rows are padded to whole tiles, so no access needs a bound check.
+// CAPTURE: also return the carried state after cell c_last (a mu < 0 line's
+// outflow, for reflective partners).
+template <int S, bool CAPTURE>
+__device__ __forceinline__ void sweep_phase2(const LineConst &L, double hd, bool neg, double (&ein)[kSweepCells],
+                                             double (&eout)[kSweepCells], double *X, bool head, double b3,
+                                             __amdgpu_buffer_rsrc_t Rw, __amdgpu_buffer_rsrc_t Rn, int voff,
+                                             int row_bytes, int c_last, double *Xcap) {
+  constexpr int K = SchemeDim<S>::K;
+#pragma unroll
+  for (int c = 0; c < kSweepCells; ++c) {
+    double oi, oo;
+    if (c == 0)
+      cell_step_maybe_head<S>(L, hd, neg, ein[0], eout[0], X, head, b3, oi, oo);
+    else
+      cell_step<S>(L, hd, neg, ein[c], eout[c], X, oi, oo);
+    row_store(Rw, voff, c * row_bytes, oi, oo);
+    const double2 v = row_load(Rn, voff, c * row_bytes);
+    ein[c] = v.x;
+    eout[c] = v.y;
+    // keep the prefetch in the registers it replaces: no hoisting across cells
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (CAPTURE) {
+      if (c == c_last) {
+#pragma unroll
+        for (int r = 0; r < K; ++r) Xcap[r] = X[r];
+      }
+    }
+  }
+}
+
 template <int S>
 __global__ __launch_bounds__(kSweepThreads) void sweep_step_kernel(SweepArgs a) {
   constexpr int K = SchemeDim<S>::K;
@@ -95,87 +143,103 @@ __global__ __launch_bounds__(kSweepThreads) void sweep_step_kernel(SweepArgs a) 
   __shared__ double sm_xin[K][64];
   __shared__ double sm_A16[NT * 64];
   __shared__ double sm_A64[NT * 64];
+  __shared__ double sm_lc[LC_COUNT * 64];  // this line group's constants
+  __shared__ double sm_bdry[64];           // and inflow values
 
   const int lane = threadIdx.x & 63;
-  const int w = threadIdx.x >> 6;
-  const long long tiles_per_half = static_cast<long long>(a.J) * a.Q;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform
+  const int tiles_per_half = a.J * a.Q;  // host guarantees 2 J Q < 2^31
+  const int total_tiles = static_cast<int>(a.total_tiles);
+  const size_t stride = static_cast<size_t>(a.Lpad);
   int cached_key = -1;
   LineConst L;
 
-  for (long long t = blockIdx.x; t < a.total_tiles; t += gridDim.x) {
-    const int half = static_cast<int>(t / tiles_per_half);
-    const long long rem = t - half * tiles_per_half;
-    const int j = static_cast<int>(rem / a.Q);
-    const int q = static_cast<int>(rem - static_cast<long long>(j) * a.Q);
-    const int ell = q * 64 + lane;
-    const bool neg = (half == 0);
-
-    const int key = half * a.Q + q;
-    if (key != cached_key) {
-      // line constants -> registers; propagator powers -> LDS
-      const double *lc = a.lc + static_cast<size_t>(half) * LC_COUNT * a.Lpad;
-#pragma unroll
-      for (int n = 0; n < LC_COUNT; ++n) L.c[n] = lc[static_cast<size_t>(n) * a.Lpad + ell];
-      __syncthreads();  // previous tile's LDS readers are done
-      const double *A16 = a.Apow + static_cast<size_t>(half * 2 + 0) * NT * a.Lpad;
-      const double *A64 = a.Apow + static_cast<size_t>(half * 2 + 1) * NT * a.Lpad;
-      for (int e = w; e < NT; e += kSweepWaves) {
-        sm_A16[e * 64 + lane] = A16[static_cast<size_t>(e) * a.Lpad + ell];
-        sm_A64[e * 64 + lane] = A64[static_cast<size_t>(e) * a.Lpad + ell];
-      }
-      cached_key = key;
-    }
-
+  // tile t -> (half, j, q) and the address of this wave's first row
+  auto decode = [&](int t, int &half, int &j, int &q) {
+    half = t >= tiles_per_half ? 1 : 0;
+    const int rem = t - half * tiles_per_half;
+    j = static_cast<int>(static_cast<unsigned>(rem) / static_cast<unsigned>(a.Q));
+    q = rem - j * a.Q;
+  };
+  const int row_bytes = a.Lpad * static_cast<int>(sizeof(double2));
+  const int voff = lane * static_cast<int>(sizeof(double2));
+  auto rows = [&](int half, int j, int q) {  // wave-uniform descriptor of this wave's 16 rows
     const int k0 = j * kSweepTile + w * kSweepCells;
-    const int nv = max(0, min(a.N - k0, kSweepCells));
-    const double2 *Eh = a.E + static_cast<size_t>(half) * a.N * a.Lpad;
-    double2 *Ehw = a.E + static_cast<size_t>(half) * a.N * a.Lpad;
+    return rows_rsrc(a.E + (static_cast<size_t>(half) * a.Nrow + k0) * stride + q * 64, row_bytes);
+  };
 
-    // ---- load this wave's cells (1 KiB per row, coalesced) ----
-    double ein[kSweepCells], eout[kSweepCells];
+  int t = blockIdx.x;
+  if (t >= total_tiles) return;
+  int half, j, q;
+  decode(t, half, j, q);
+  double ein[kSweepCells], eout[kSweepCells];
+  {  // prologue: this workgroup's first tile
+    const __amdgpu_buffer_rsrc_t R = rows(half, j, q);
 #pragma unroll
     for (int c = 0; c < kSweepCells; ++c) {
-      if (c < nv) {
-        const double2 v = Eh[static_cast<size_t>(k0 + c) * a.Lpad + ell];
-        ein[c] = v.x;
-        eout[c] = v.y;
-      } else {
-        ein[c] = 0.0;
-        eout[c] = 0.0;
-      }
+      const double2 v = row_load(R, voff, c * row_bytes);
+      ein[c] = v.x;
+      eout[c] = v.y;
     }
+  }
+
+  for (;;) {
+    const int ell = q * 64 + lane;
+    const bool neg = (half == 0);
+    const int key = half * a.Q + q;
+    if (key != cached_key) {
+      // a new line group: constants, inflows and propagator powers -> LDS.
+      // Every global load of this block is drained here, so the prefetched
+      // rows still in flight are never waited for on the common path.
+      __syncthreads();  // previous tile's LDS readers are done
+      const double *lc = a.lc + static_cast<size_t>(half) * LC_COUNT * stride;
+      const double *A16 = a.Apow + static_cast<size_t>(half * 2 + 0) * NT * stride;
+      const double *A64 = a.Apow + static_cast<size_t>(half * 2 + 1) * NT * stride;
+      for (int e = w; e < LC_COUNT; e += kSweepWaves) sm_lc[e * 64 + lane] = lc[e * stride + ell];
+      for (int e = w; e < NT; e += kSweepWaves) {
+        sm_A16[e * 64 + lane] = A16[e * stride + ell];
+        sm_A64[e * 64 + lane] = A64[e * stride + ell];
+      }
+      if (w == 0) sm_bdry[lane] = a.bdry[static_cast<size_t>(half) * stride + ell];
+      __builtin_amdgcn_s_waitcnt(0);  // vmcnt(0) expcnt(0) lgkmcnt(0)
+      __syncthreads();
+      cached_key = key;
+    }
+#pragma unroll
+    for (int n = 0; n < LC_COUNT; ++n) L.c[n] = sm_lc[n * 64 + lane];
 
     // ---- inflow values for the line head (tile 0, wave 0) ----
     const bool head = (j == 0 && w == 0);
-    double b[4] = {0.0, 0.0, 0.0, 0.0};
-    if (head) {
-      if (!neg && a.reflective) {
-        // solver.cpp:677-684: the mu > 0 line reads its mirror's outflow at cell 0,
-        // produced by the same substep of the mu < 0 sweep (earlier tiles)
-        wait_flag(a.outflow_flag + q, 1u, a.error);
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        const int nsub = (S == SCHEME_BDF2) ? 4 : 1;
-        for (int s = 0; s < nsub; ++s) b[s] = load_sc1(a.outflow + static_cast<size_t>(s) * a.Lpad + ell);
-      } else {
-        const double v = a.bdry[static_cast<size_t>(half) * a.Lpad + ell];
-        b[0] = b[1] = b[2] = b[3] = v;
-      }
+    double b[4];
+    {
+      const double v = sm_bdry[lane];
+      b[0] = b[1] = b[2] = b[3] = v;
+    }
+    if (head && !neg && a.reflective) {
+      // solver.cpp:677-684: the mu > 0 line reads its mirror's outflow at cell 0,
+      // produced by the same substep of the mu < 0 sweep (earlier tiles)
+      wait_flag(a.outflow_flag + q, 1u, a.error);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      const int nsub = (S == SCHEME_BDF2) ? 4 : 1;
+      for (int s = 0; s < nsub; ++s) b[s] = load_sc1(a.outflow + static_cast<size_t>(s) * stride + ell);
+      __builtin_amdgcn_s_waitcnt(0);
     }
 
     // ---- phase 1: aggregate from X = 0 (the head starts from its inflow) ----
     double X[K];
+    if (head) {
+      head_state<S>(b, X);
+    } else {
 #pragma unroll
-    for (int r = 0; r < K; ++r) X[r] = 0.0;
+      for (int r = 0; r < K; ++r) X[r] = 0.0;
+    }
     {
       double oi, oo;
+      cell_step_maybe_head<S>(L, a.hd, neg, ein[0], eout[0], X, head, b[3], oi, oo);
 #pragma unroll
-      for (int c = 0; c < kSweepCells; ++c) {
-        if (c < nv) {
-          if (head && c == 0)
-            cell_first<S>(L, a.hd, neg, ein[0], eout[0], b, X, oi, oo);
-          else
-            cell_step<S>(L, a.hd, neg, ein[c], eout[c], X, oi, oo);
-        }
+      for (int c = 1; c < kSweepCells; ++c) {
+        __builtin_amdgcn_sched_barrier(0);  // one cell at a time: bounded live ranges
+        cell_step<S>(L, a.hd, neg, ein[c], eout[c], X, oi, oo);
       }
     }
 #pragma unroll
@@ -183,8 +247,8 @@ __global__ __launch_bounds__(kSweepThreads) void sweep_step_kernel(SweepArgs a) 
     __syncthreads();
 
     // ---- wave 0: tile aggregate, publish, look-back, publish prefix ----
-    const size_t rec = static_cast<size_t>(t) * K * 64;
     if (w == 0) {
+      const size_t rec = static_cast<size_t>(t) * K * 64;
       double T[K], tmp[K];
 #pragma unroll
       for (int r = 0; r < K; ++r) T[r] = sm_agg[0][r][lane];
@@ -204,13 +268,12 @@ __global__ __launch_bounds__(kSweepThreads) void sweep_step_kernel(SweepArgs a) 
         for (int r = 0; r < K; ++r) store_sc1(a.agg + rec + r * 64 + lane, T[r]);
         drain_stores();
         if (lane == 0) store_flag(a.status + t, 1u);
-
         // decoupled look-back.  Pass 1 walks back over the predecessors of
         // this line group (t - Q, t - 2Q, ...) until one has published its
         // inclusive prefix; pass 2 folds forward from it:
         //   X_in = A64 (... (A64 pref[t - dQ] + agg[t - (d-1)Q]) ...) + agg[t - Q]
         // (published records are immutable, so pass 2 re-reads them safely).
-        long long s = t - a.Q;
+        int s = t - a.Q;
         for (;;) {
           const unsigned st = wait_flag(a.status + s, 1u, a.error);
           if (st >= 2u || st == 0u) break;
@@ -237,11 +300,22 @@ __global__ __launch_bounds__(kSweepThreads) void sweep_step_kernel(SweepArgs a) 
     }
     __syncthreads();
 
-    // ---- phase 2: this wave's true incoming X, re-sweep, stream out ----
-    if (nv > 0) {
+    // ---- phase 2: true incoming X, re-sweep, stream out; prefetch the next tile ----
+    // Re-derive every X-independent term from the data rather than keeping
+    // phase 1's copies live (register pressure / occupancy over FLOPs).
+#pragma unroll
+    for (int c = 0; c < kSweepCells; ++c) asm volatile("" : "+v"(ein[c]), "+v"(eout[c]));
+    const int tn = t + static_cast<int>(gridDim.x);
+    const bool more = tn < total_tiles;
+    int half_n = half, j_n = j, q_n = q;
+    if (more) decode(tn, half_n, j_n, q_n);
+    {
       double tmp[K];
       int first_wave;
-      if (j == 0) {
+      if (head) {
+        head_state<S>(b, X);
+        first_wave = 1;
+      } else if (j == 0) {
 #pragma unroll
         for (int r = 0; r < K; ++r) X[r] = sm_agg[0][r][lane];
         first_wave = 1;
@@ -255,29 +329,31 @@ __global__ __launch_bounds__(kSweepThreads) void sweep_step_kernel(SweepArgs a) 
 #pragma unroll
         for (int r = 0; r < K; ++r) X[r] = tmp[r] + sm_agg[ww][r][lane];
       }
-      double oi, oo;
-#pragma unroll
-      for (int c = 0; c < kSweepCells; ++c) {
-        if (c < nv) {
-          if (head && c == 0)
-            cell_first<S>(L, a.hd, neg, ein[0], eout[0], b, X, oi, oo);
-          else
-            cell_step<S>(L, a.hd, neg, ein[c], eout[c], X, oi, oo);
-          Ehw[static_cast<size_t>(k0 + c) * a.Lpad + ell] = make_double2(oi, oo);
-        }
-      }
-      // mu < 0 line ends: publish the per-substep outflows for reflective partners
-      if (neg && a.reflective && k0 + nv == a.N) {
-        if constexpr (S == SCHEME_BDF2) {
-#pragma unroll
-          for (int s = 0; s < 4; ++s) store_sc1(a.outflow + static_cast<size_t>(s) * a.Lpad + ell, X[1 + s]);
-        } else {
-          store_sc1(a.outflow + ell, X[K - 1]);
-        }
-        drain_stores();
-        if (lane == 0) store_flag(a.outflow_flag + q, 1u);
-      }
     }
+    const __amdgpu_buffer_rsrc_t Rw = rows(half, j, q);
+    const __amdgpu_buffer_rsrc_t Rn = rows(half_n, j_n, q_n);
+    const int k0 = j * kSweepTile + w * kSweepCells;
+    const int c_last = a.N - 1 - k0;  // this wave holds the line's last cell iff 0 <= c_last < 16
+    if (neg && a.reflective && c_last >= 0 && c_last < kSweepCells) {
+      double Xo[K];
+      sweep_phase2<S, true>(L, a.hd, neg, ein, eout, X, head, b[3], Rw, Rn, voff, row_bytes, c_last, Xo);
+      // publish the per-substep outflows for the reflective mu > 0 partners
+      if constexpr (S == SCHEME_BDF2) {
+#pragma unroll
+        for (int s = 0; s < 4; ++s) store_sc1(a.outflow + static_cast<size_t>(s) * stride + ell, Xo[1 + s]);
+      } else {
+        store_sc1(a.outflow + ell, Xo[K - 1]);
+      }
+      drain_stores();
+      if (lane == 0) store_flag(a.outflow_flag + q, 1u);
+    } else {
+      sweep_phase2<S, false>(L, a.hd, neg, ein, eout, X, head, b[3], Rw, Rn, voff, row_bytes, 0, nullptr);
+    }
+    if (!more) break;
+    t = tn;
+    half = half_n;
+    j = j_n;
+    q = q_n;
     __syncthreads();  // LDS (sm_agg, sm_xin) is reused by the next tile
   }
 }
@@ -285,19 +361,22 @@ __global__ __launch_bounds__(kSweepThreads) void sweep_step_kernel(SweepArgs a) 
 // ------------------------------------------------------------------------
 // Non-hot kernels: state initialisation, layout conversion, moments
 // ------------------------------------------------------------------------
-__global__ void init_state_kernel(double2 *E, const double *lineB, int N, int Lpad) {
-  const size_t total = static_cast<size_t>(2) * N * Lpad;
+// psi = ends = B_g (solver.cpp:165-181); padding rows k >= N are zero
+__global__ void init_state_kernel(double2 *E, const double *lineB, int N, int Nrow, int Lpad) {
+  const size_t total = static_cast<size_t>(2) * Nrow * Lpad;
   for (size_t idx = blockIdx.x * static_cast<size_t>(blockDim.x) + threadIdx.x; idx < total;
        idx += static_cast<size_t>(gridDim.x) * blockDim.x) {
-    const size_t half = idx / (static_cast<size_t>(N) * Lpad);
+    const size_t row = idx / Lpad;
+    const size_t half = row / Nrow;
+    const int k = static_cast<int>(row - half * Nrow);
     const int ell = static_cast<int>(idx % Lpad);
-    const double v = lineB[half * Lpad + ell];
+    const double v = k < N ? lineB[half * Lpad + ell] : 0.0;
     E[idx] = make_double2(v, v);
   }
 }
 
 struct LineMap {
-  int M, H, Gl, N, Lpad;
+  int M, H, Gl, N, Nrow, Lpad;
   // reference (i, g, c) -> (half, ell, k) and node swap for mu < 0
   __device__ __forceinline__ void map(int i, int g, int c, int &half, int &ell, int &k) const {
     if (i < H) {
@@ -311,7 +390,7 @@ struct LineMap {
     }
   }
   __device__ __forceinline__ size_t at(int half, int k, int ell) const {
-    return (static_cast<size_t>(half) * N + k) * Lpad + ell;
+    return (static_cast<size_t>(half) * Nrow + k) * Lpad + ell;
   }
 };
 
@@ -387,14 +466,14 @@ __global__ void moments_kernel(const double2 *E, const double *mu, const double 
 }
 
 // Boundary rows k = 0 and k = N-1 of both halves (for group ends / balance)
-__global__ void boundary_rows_kernel(const double2 *E, double2 *rows, int N, int Lpad) {
+__global__ void boundary_rows_kernel(const double2 *E, double2 *rows, int N, int Nrow, int Lpad) {
   const int total = 4 * Lpad;
   for (int o = blockIdx.x * blockDim.x + threadIdx.x; o < total; o += gridDim.x * blockDim.x) {
     const int which = o / Lpad;  // 0: half0 k=0, 1: half0 k=N-1, 2: half1 k=0, 3: half1 k=N-1
     const int ell = o % Lpad;
     const int half = which / 2;
     const int k = (which & 1) ? N - 1 : 0;
-    rows[o] = E[(static_cast<size_t>(half) * N + k) * Lpad + ell];
+    rows[o] = E[(static_cast<size_t>(half) * Nrow + k) * Lpad + ell];
   }
 }
 
@@ -443,13 +522,13 @@ static int grid_for(size_t total, int block) {
   return static_cast<int>(g);
 }
 
-hipError_t launch_init_state(double2 *E, const double *lineB, int N, int Lpad, hipStream_t st) {
-  hipLaunchKernelGGL(init_state_kernel, dim3(grid_for(static_cast<size_t>(2) * N * Lpad, 256)), dim3(256), 0, st, E,
-                     lineB, N, Lpad);
+hipError_t launch_init_state(double2 *E, const double *lineB, const Geometry &g, hipStream_t st) {
+  hipLaunchKernelGGL(init_state_kernel, dim3(grid_for(static_cast<size_t>(2) * g.Nrow * g.Lpad, 256)), dim3(256), 0, st,
+                     E, lineB, g.N, g.Nrow, g.Lpad);
   return hipGetLastError();
 }
 
-static LineMap make_map(const Geometry &g) { return LineMap{g.M, g.M / 2, g.Gl, g.N, g.Lpad}; }
+static LineMap make_map(const Geometry &g) { return LineMap{g.M, g.M / 2, g.Gl, g.N, g.Nrow, g.Lpad}; }
 
 hipError_t launch_export_psi(const double2 *E, double *psi, const Geometry &g, hipStream_t st) {
   hipLaunchKernelGGL(export_psi_kernel, dim3(grid_for(static_cast<size_t>(g.M) * g.Gl * g.N, 256)), dim3(256), 0, st,
@@ -478,7 +557,7 @@ hipError_t launch_moments(const double2 *E, const double *mu, const double *wt, 
 
 hipError_t launch_boundary_rows(const double2 *E, double2 *rows, const Geometry &g, hipStream_t st) {
   hipLaunchKernelGGL(boundary_rows_kernel, dim3(grid_for(static_cast<size_t>(4) * g.Lpad, 256)), dim3(256), 0, st, E,
-                     rows, g.N, g.Lpad);
+                     rows, g.N, g.Nrow, g.Lpad);
   return hipGetLastError();
 }
 

@@ -22,18 +22,18 @@ struct SweepArgs {
   double *pref;               // [total_tiles][K][64]
   unsigned *error;            // [1] timeout word
   long long total_tiles;      // 2 * J * Q
-  int N, Lpad, Q, J;
+  int N, Nrow, Lpad, Q, J;    // Nrow = 64 J rows per half (cells padded to whole tiles)
   int reflective;             // bc_left == 2
   double hd;                  // dx / 2
 };
 
 struct Geometry {
-  int M, Gl, N, Lpad;
+  int M, Gl, N, Nrow, Lpad;
 };
 
 hipError_t launch_sweep(int scheme, const SweepArgs &a, int grid, hipStream_t st);
 hipError_t sweep_occupancy(int scheme, int *blocks_per_cu);
-hipError_t launch_init_state(double2 *E, const double *lineB, int N, int Lpad, hipStream_t st);
+hipError_t launch_init_state(double2 *E, const double *lineB, const Geometry &g, hipStream_t st);
 hipError_t launch_export_psi(const double2 *E, double *psi, const Geometry &g, hipStream_t st);
 hipError_t launch_export_ends(const double2 *E, double *ends, const Geometry &g, hipStream_t st);
 hipError_t launch_import_ends(double2 *E, const double *ends, const Geometry &g, hipStream_t st);

@@ -315,7 +315,7 @@ static rt_status upload_inflow(rt_solver *s) {
   return RT_OK;
 }
 
-static Geometry geometry(const rt_solver *s) { return Geometry{s->p.M, s->Gl, s->p.N, s->Lpad}; }
+static Geometry geometry(const rt_solver *s) { return Geometry{s->p.M, s->Gl, s->p.N, s->J * kSweepTile, s->Lpad}; }
 
 // ---------------------------------------------------------------------------
 // lifecycle
@@ -364,6 +364,7 @@ extern "C" rt_status rt_create_from_params(const rt_params *pin, int g_lo, int g
   s->Lpad = 64 * s->Q;
   s->J = (q.N + kSweepTile - 1) / kSweepTile;
   s->tiles = 2LL * s->J * s->Q;
+  if (s->tiles >= (1LL << 31)) return fail(nullptr, RT_ERR_PARAM, "too many sweep tiles for one handle: shard the groups");
   s->scheme = q.ts_method;
   s->K = q.ts_method == 1 ? 1 : (q.ts_method == 2 ? 2 : 5);
   s->device = device;
@@ -382,7 +383,8 @@ extern "C" rt_status rt_create_from_params(const rt_params *pin, int g_lo, int g
   const size_t Lp = h->Lpad, N = q.N;
   const int K = h->K, NT = K * (K + 1) / 2;
   hipError_t e = hipSuccess;
-  if (!e) e = dalloc(h->E, sizeof(double2) * 2 * N * Lp);
+  const size_t Nrow = static_cast<size_t>(h->J) * kSweepTile;  // cells padded to whole tiles
+  if (!e) e = dalloc(h->E, sizeof(double2) * 2 * Nrow * Lp);
   if (!e) e = dalloc(h->lc, sizeof(double) * 2 * LC_COUNT * Lp);
   if (!e) e = dalloc(h->Apow, sizeof(double) * 4 * NT * Lp);
   if (!e) e = dalloc(h->bdry, sizeof(double) * 2 * Lp);
@@ -401,7 +403,7 @@ extern "C" rt_status rt_create_from_params(const rt_params *pin, int g_lo, int g
 
   if ((st = setup_lines(h))) return st;
   if ((st = upload_inflow(h))) return st;
-  HIP_TRY(h, launch_init_state(static_cast<double2 *>(h->E.p), static_cast<const double *>(h->lineB.p), q.N, h->Lpad,
+  HIP_TRY(h, launch_init_state(static_cast<double2 *>(h->E.p), static_cast<const double *>(h->lineB.p), geometry(h),
                                h->stream));
   HIP_TRY(h, hipMemsetAsync(h->outflow.p, 0, h->outflow.bytes, h->stream));
   HIP_TRY(h, hipMemsetAsync(h->error.p, 0, h->error.bytes, h->stream));
@@ -472,6 +474,7 @@ static rt_status enqueue_steps(rt_solver *s, int nsteps) {
   a.error = static_cast<unsigned *>(s->error.p);
   a.total_tiles = s->tiles;
   a.N = s->p.N;
+  a.Nrow = s->J * kSweepTile;
   a.Lpad = s->Lpad;
   a.Q = s->Q;
   a.J = s->J;
