@@ -116,6 +116,9 @@ __device__ __forceinline__ void sweep_phase2(const LineConst &L, double hd, bool
 #pragma unroll
   for (int c = 0; c < kSweepCells; ++c) {
     double oi, oo;
+#if RT_PIN_CELLS
+    asm volatile("" : "+v"(ein[c]), "+v"(eout[c]));
+#endif
     if (c == 0)
       cell_step_maybe_head<S>(L, hd, neg, ein[0], eout[0], X, head, b3, oi, oo);
     else
@@ -136,7 +139,7 @@ __device__ __forceinline__ void sweep_phase2(const LineConst &L, double hd, bool
 }
 
 template <int S>
-__global__ __launch_bounds__(kSweepThreads) void sweep_step_kernel(SweepArgs a) {
+__global__ __launch_bounds__(kSweepThreads, RT_SWEEP_MIN_WAVES) void sweep_step_kernel(SweepArgs a) {
   constexpr int K = SchemeDim<S>::K;
   constexpr int NT = K * (K + 1) / 2;
   __shared__ double sm_agg[kSweepWaves][K][64];
@@ -233,12 +236,16 @@ __global__ __launch_bounds__(kSweepThreads) void sweep_step_kernel(SweepArgs a) 
 #pragma unroll
       for (int r = 0; r < K; ++r) X[r] = 0.0;
     }
-    {
+    if (!(a.debug_flags & 2)) {
       double oi, oo;
       cell_step_maybe_head<S>(L, a.hd, neg, ein[0], eout[0], X, head, b[3], oi, oo);
 #pragma unroll
       for (int c = 1; c < kSweepCells; ++c) {
-        __builtin_amdgcn_sched_barrier(0);  // one cell at a time: bounded live ranges
+        // pin each cell's inputs to this point: no X-independent work of later
+        // cells is hoisted ahead (bounded live ranges -> occupancy)
+#if RT_PIN_CELLS
+        asm volatile("" : "+v"(ein[c]), "+v"(eout[c]));
+#endif
         cell_step<S>(L, a.hd, neg, ein[c], eout[c], X, oi, oo);
       }
     }
@@ -263,16 +270,73 @@ __global__ __launch_bounds__(kSweepThreads) void sweep_step_kernel(SweepArgs a) 
         for (int r = 0; r < K; ++r) store_sc1(a.pref + rec + r * 64 + lane, T[r]);
         drain_stores();
         if (lane == 0) store_flag(a.status + t, 2u);
+      } else if (a.debug_flags & 1) {
+#pragma unroll
+        for (int r = 0; r < K; ++r) sm_xin[r][lane] = 0.0;
       } else {
 #pragma unroll
         for (int r = 0; r < K; ++r) store_sc1(a.agg + rec + r * 64 + lane, T[r]);
         drain_stores();
         if (lane == 0) store_flag(a.status + t, 1u);
-        // decoupled look-back.  Pass 1 walks back over the predecessors of
-        // this line group (t - Q, t - 2Q, ...) until one has published its
-        // inclusive prefix; pass 2 folds forward from it:
+#if RT_LOOKBACK_PARALLEL
+        // decoupled look-back.  The 64 lanes poll the status words of the 64
+        // nearest predecessors of this line group (t - Q, t - 2Q, ...) in one
+        // go; the nearest one holding an inclusive prefix, with aggregates
+        // published by everything in between, closes the look-back:
         //   X_in = A64 (... (A64 pref[t - dQ] + agg[t - (d-1)Q]) ...) + agg[t - Q]
-        // (published records are immutable, so pass 2 re-reads them safely).
+        // (published records are immutable, so they are re-read safely).
+        const int window = min(j, 64);
+        int d = 0;
+        {
+          const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
+          for (;;) {
+            unsigned st = 0;
+            if (lane < window) st = load_flag(a.status + (t - (lane + 1) * a.Q));
+            const unsigned long long pm = __ballot(st >= 2u);
+            const unsigned long long rm = __ballot(st >= 1u);
+            if (pm) {
+              d = __builtin_ctzll(pm) + 1;  // distance of the nearest prefix
+              const unsigned long long need = (d == 64) ? ~0ull : ((1ull << d) - 1);
+              if ((rm & need) == need) break;
+            }
+            __builtin_amdgcn_s_sleep(2);
+            if (__builtin_amdgcn_s_memrealtime() - t_start > 2000000000ull) {  // 20 s
+              if (lane == 0) atomicOr(a.error, 1u);
+              d = 1;
+              break;
+            }
+          }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        double acc[K];
+        {
+          const double *pr = a.pref + static_cast<size_t>(t - d * a.Q) * K * 64 + lane;
+#pragma unroll
+          for (int r = 0; r < K; ++r) acc[r] = load_sc1(pr + r * 64);
+        }
+        for (int m = d - 1; m >= 1; m -= 2) {  // fold the aggregates, 2 records per batch
+          double v[2][K];
+#pragma unroll
+          for (int u = 0; u < 2; ++u)
+            if (m - u >= 1) {
+              const double *ag = a.agg + static_cast<size_t>(t - (m - u) * a.Q) * K * 64 + lane;
+#pragma unroll
+              for (int r = 0; r < K; ++r) v[u][r] = load_sc1(ag + r * 64);
+            }
+#pragma unroll
+          for (int u = 0; u < 2; ++u)
+            if (m - u >= 1) {
+              matvec_lt<K>(sm_A64, lane, acc, tmp);
+#pragma unroll
+              for (int r = 0; r < K; ++r) acc[r] = tmp[r] + v[u][r];
+            }
+        }
+#else
+        // decoupled look-back (serial): walk back over the predecessors of this
+        // line group (t - Q, t - 2Q, ...) until one has published its inclusive
+        // prefix, then fold forward from it:
+        //   X_in = A64 (... (A64 pref[t - dQ] + agg[t - (d-1)Q]) ...) + agg[t - Q]
+        // (published records are immutable, so they are re-read safely).
         int s = t - a.Q;
         for (;;) {
           const unsigned st = wait_flag(a.status + s, 1u, a.error);
@@ -288,6 +352,7 @@ __global__ __launch_bounds__(kSweepThreads) void sweep_step_kernel(SweepArgs a) 
 #pragma unroll
           for (int r = 0; r < K; ++r) acc[r] = tmp[r] + load_sc1(a.agg + static_cast<size_t>(s) * K * 64 + r * 64 + lane);
         }
+#endif
         // inclusive prefix = A64 X_in + T
         matvec_lt<K>(sm_A64, lane, acc, tmp);
 #pragma unroll
@@ -303,8 +368,10 @@ __global__ __launch_bounds__(kSweepThreads) void sweep_step_kernel(SweepArgs a) 
     // ---- phase 2: true incoming X, re-sweep, stream out; prefetch the next tile ----
     // Re-derive every X-independent term from the data rather than keeping
     // phase 1's copies live (register pressure / occupancy over FLOPs).
+#if RT_PHASE_BARRIER
 #pragma unroll
     for (int c = 0; c < kSweepCells; ++c) asm volatile("" : "+v"(ein[c]), "+v"(eout[c]));
+#endif
     const int tn = t + static_cast<int>(gridDim.x);
     const bool more = tn < total_tiles;
     int half_n = half, j_n = j, q_n = q;

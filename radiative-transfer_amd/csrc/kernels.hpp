@@ -5,9 +5,26 @@
 
 namespace rtamd {
 
+// Build-time tunables (defaults are the measured best).
+#ifndef RT_SWEEP_CELLS
+#define RT_SWEEP_CELLS 16     // cells per wave held in registers
+#endif
+#ifndef RT_PIN_CELLS
+#define RT_PIN_CELLS 0        // 1: asm-pin each cell's inputs (bounded live ranges)
+#endif
+#ifndef RT_PHASE_BARRIER
+#define RT_PHASE_BARRIER 1    // 1: phase 2 re-derives X-independent terms (no cross-phase CSE)
+#endif
+#ifndef RT_LOOKBACK_PARALLEL
+#define RT_LOOKBACK_PARALLEL 0  // 1: poll 64 predecessors at once
+#endif
+#ifndef RT_SWEEP_MIN_WAVES
+#define RT_SWEEP_MIN_WAVES 1  // __launch_bounds__ minimum waves per SIMD
+#endif
+
 constexpr int kSweepWaves = 4;                          // waves per workgroup
 constexpr int kSweepThreads = 64 * kSweepWaves;         // 256
-constexpr int kSweepCells = 16;                         // cells per wave (registers)
+constexpr int kSweepCells = RT_SWEEP_CELLS;             // cells per wave (registers)
 constexpr int kSweepTile = kSweepWaves * kSweepCells;   // 64 cells per tile
 
 struct SweepArgs {
@@ -24,6 +41,8 @@ struct SweepArgs {
   long long total_tiles;      // 2 * J * Q
   int N, Nrow, Lpad, Q, J;    // Nrow = 64 J rows per half (cells padded to whole tiles)
   int reflective;             // bc_left == 2
+  int debug_flags;            // timing experiments only (RTSN_DEBUG_FLAGS): 1 = skip the look-back
+                              // wait, 2 = skip phase 1; results are wrong when set
   double hd;                  // dx / 2
 };
 

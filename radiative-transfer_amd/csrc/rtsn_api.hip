@@ -5,6 +5,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <string>
@@ -479,6 +480,7 @@ static rt_status enqueue_steps(rt_solver *s, int nsteps) {
   a.Q = s->Q;
   a.J = s->J;
   a.reflective = s->p.bc_left_indicator == 2;
+  if (const char *dbg = std::getenv("RTSN_DEBUG_FLAGS")) a.debug_flags = std::atoi(dbg);
   a.hd = 0.5 * (s->p.X / s->p.N);
   for (int n = 0; n < nsteps; ++n) {
     HIP_TRY(s, hipMemsetAsync(s->status.p, 0, s->status.bytes, s->stream));
