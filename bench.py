@@ -188,7 +188,7 @@ def main():
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK,
             "traffic": load_traffic(args.variant),
-            "kernel": "sweep_step_kernel<3>",
+            "kernel": "sweep_segment_kernel<3,0>",
             "kernel_ms": kern_avg_ms,
             "algorithmic_bytes_per_launch": bytes_step,
         },

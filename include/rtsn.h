@@ -42,7 +42,7 @@ typedef enum {
   RT_ERR_VALIDATION = 4,  /* assert(validate_correction()) would fire (solver.cpp:609-612) */
   RT_ERR_NOMEM = 5,       /* host or device allocation failed */
   RT_ERR_DEVICE = 6,      /* HIP runtime error / no usable gfx950 device */
-  RT_ERR_TIMEOUT = 7,     /* an in-kernel inter-workgroup wait timed out (never expected) */
+  RT_ERR_TIMEOUT = 7,     /* reserved (no in-kernel waits in this version) */
   RT_ERR_ARG = 8          /* NULL handle / bad argument */
 } rt_status;
 
@@ -143,7 +143,8 @@ rt_status rt_get_sweep_time(rt_solver *s, double *total_ms, long long *launches)
 /* Algorithmic HBM bytes of one sweep launch (one full step) and updates
  * (cell x angle x group x substep) per full step, for the handle's groups. */
 rt_status rt_sweep_traffic(rt_solver *s, double *bytes_per_step, double *updates_per_step);
-/* Sweep geometry actually used: persistent workgroups, tiles per step. */
+/* Sweep geometry actually used: waves launched per step (one per line group
+ * and segment) and segments per line. */
 rt_status rt_sweep_geometry(rt_solver *s, int *workgroups, long long *tiles);
 
 const char *rt_status_string(rt_status st);

@@ -1,29 +1,33 @@
 // kernels.hip -- CDNA4 (gfx950) kernels of the S_n path.
 //
-// Hot path: sweep_step_kernel<S> -- one full time step (BE, CN or the fused
-// 4-substep BDF2 cycle) of every (direction, group) line, cell-parallel.
+// Hot path: sweep_segment_kernel<S, MODE> -- one full time step (BE, CN or the
+// fused 4-substep BDF2 cycle, cell.hpp) of every (direction, group) line.
 //
 // Layout in HBM:
 //   E[half][k][l]  double2 (e_in, e_out), half 0 = mu < 0 lines, half 1 = mu > 0,
-//                  k = cell in the line's upwind frame, l = line = i' + (M/2) g
-//                  padded to Lpad = 64 * Q.  One wave reads/writes a 1 KiB row.
+//                  k = cell in the line's upwind frame, l = line = i' + (M/2) g,
+//                  padded to Lpad = 64 Q lines and Nrow = 64 J rows.  A wave
+//                  moves one 1 KiB row per instruction.
 //
-// Parallelisation: a line is an affine recurrence X_{k+1} = A X_k + b_k over
-// its cells (cell.hpp).  A tile = 64 lines x 64 cells is owned by one
-// 256-thread workgroup; each of its 4 waves holds 16 cells x 64 lines in
-// registers.  Phase 1 sweeps each wave's cells from X = 0 (its aggregate);
-// the waves' aggregates are chained with A^16 through LDS; wave 0 publishes
-// the tile aggregate, resolves the tile's incoming X by a decoupled look-back
-// over its predecessors' records (A^64 powers), publishes the inclusive
-// prefix, and phase 2 re-sweeps the register-resident cells with the true X
-// and streams the step-end state out.  HBM traffic per cell x line x step:
-// 16 B read + 16 B write (+ 2 x 40 B of look-back records per 64 cells).
+// Parallelisation without in-step synchronisation.  Within a step, a line
+// is the affine recurrence X_{k+1} = A X_k + B d_k + c over its cells, and the
+// step-end state of cell k is R X_k + (data terms), with A, R constant per
+// line (cell.hpp).  Each line is cut into Sg segments of Ls cells; one wave
+// (64 lines) sweeps one segment in a single pass, streaming 16-row chunks
+// through registers with a rolling prefetch.  Segment 0 starts from the true
+// inflow; segment s > 0 starts from X = 0, so its stored state is
+// *provisional*: exact up to the term R A^(k - k_s) X_s, where X_s is the
+// segment's true incoming state.  Every wave publishes its final carried
+// state (its aggregate).  The next step -- or a finalize launch before any
+// read-out -- rebuilds X_s = fold of the previous segments' aggregates with
+// the segment propagator A^Ls and adds the correction while it loads the
+// rows.  No workgroup ever waits for another, so there is nothing to
+// deadlock and nothing to stall; the cost is ~20 FMA per cell for the
+// correction instead of a second compute pass.
 //
-// Scheduling: a persistent grid of P resident workgroups walks the tiles in
-// the static order t = b, b + P, ...; tiles are ordered [half][j][q] (q = line
-// group fastest), so a tile only ever waits on lower-numbered tiles, which
-// resident workgroups own: no deadlock for any dispatch order (every spin is
-// also bounded by a wall-clock timeout that sets an error word).
+// Reflective left boundary (solver.cpp:677-684): the mu > 0 heads need the
+// mu < 0 outflow of the SAME step, so the two halves go in two launches and
+// the mu > 0 head folds the mu < 0 aggregates of this step.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -33,48 +37,9 @@
 
 namespace rtamd {
 
-// ------------------------------------------------------------------------
-// inter-workgroup hand-off helpers (MI355X_MICROARCH.md "Valid forms":
-// 8-byte agent-scope atomic stores/loads both sides, drained before an
-// agent-scope flag store; relaxed polls)
-// ------------------------------------------------------------------------
-__device__ __forceinline__ void store_sc1(double *p, double v) {
-  __hip_atomic_store(reinterpret_cast<unsigned long long *>(p), static_cast<unsigned long long>(__double_as_longlong(v)),
-                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ double load_sc1(const double *p) {
-  const unsigned long long v = __hip_atomic_load(reinterpret_cast<const unsigned long long *>(p), __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_AGENT);
-  return __longlong_as_double(static_cast<long long>(v));
-}
-__device__ __forceinline__ void store_flag(unsigned *p, unsigned v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ unsigned load_flag(const unsigned *p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void drain_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
-
-// Poll *flag until it reaches >= want; returns the value, or 0 after the
-// timeout (error word set).  Wave-uniform: every lane polls the same word.
-__device__ __forceinline__ unsigned wait_flag(const unsigned *flag, unsigned want, unsigned *err) {
-  unsigned v = load_flag(flag);
-  if (v >= want) return v;
-  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();  // 100 MHz
-  for (;;) {
-    __builtin_amdgcn_s_sleep(2);
-    v = load_flag(flag);
-    if (v >= want) return v;
-    if (__builtin_amdgcn_s_memrealtime() - t0 > 2000000000ull) {  // 20 s
-      atomicOr(err, 1u);
-      return 0;
-    }
-  }
-}
-
-// A wave's 16 rows of one tile are addressed through a buffer descriptor built
-// from wave-uniform values: base (SGPR) + row offset (SGPR soffset) + lane*16
-// (one VGPR), instead of a 64-bit VGPR address per row.
+// A wave's 16 rows of one chunk are addressed through a buffer descriptor
+// built from wave-uniform values: base (SGPR) + row offset (SGPR soffset) +
+// lane*16 (one VGPR), instead of a 64-bit VGPR address per row.
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rows_rsrc(const double2 *base, int row_bytes) {
@@ -87,50 +52,81 @@ __device__ __forceinline__ void row_store(__amdgpu_buffer_rsrc_t r, int voff, in
   __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, make_double2(x, y)), r, voff, soff, 0);
 }
 
+// y = A x with A packed lower-triangular, one entry per stride in memory
 template <int K>
-__device__ __forceinline__ void matvec_lt(const double *Asm, int lane, const double *x, double *y) {
-  // y = A x, A packed lower-triangular in LDS as [tri][64]
+__device__ __forceinline__ void matvec_lt_g(const double *A, size_t stride, const double *x, double *y) {
 #pragma unroll
   for (int r = 0; r < K; ++r) {
     double acc = 0.0;
 #pragma unroll
-    for (int c = 0; c <= r; ++c) acc += Asm[tri(r, c) * 64 + lane] * x[c];
+    for (int c = 0; c <= r; ++c) acc += A[tri(r, c) * stride] * x[c];
     y[r] = acc;
   }
 }
 
-// ------------------------------------------------------------------------
-// The sweep kernel
-// ------------------------------------------------------------------------
-// Phase-2 sweep of one wave's 16 cells: write the step-end state and
-// prefetch the same row of the workgroup's next tile into the registers just
-// consumed.  Rows are padded to whole tiles, so no access needs a bound check.
-// CAPTURE: also return the carried state after cell c_last (a mu < 0 line's
-// outflow, for reflective partners).
-template <int S, bool CAPTURE>
-__device__ __forceinline__ void sweep_phase2(const LineConst &L, double hd, bool neg, double (&ein)[kSweepCells],
-                                             double (&eout)[kSweepCells], double *X, bool head, double b3,
-                                             __amdgpu_buffer_rsrc_t Rw, __amdgpu_buffer_rsrc_t Rn, int voff,
-                                             int row_bytes, int c_last, double *Xcap) {
+// X_s of segment s (its true incoming carried state) from the aggregates of
+// segments 0..s-1: X_1 = agg_0 (segment 0 starts from the true inflow),
+// X_{s'+1} = P_{s'} X_{s'} + agg_{s'}, with P = A^Ls, or A^Llast for the last
+// segment (last_short).
+template <int K>
+__device__ __forceinline__ void fold_segments(const double *agg, size_t seg_stride, size_t stride, int s,
+                                              const double *Aseg, const double *Alast, bool last_short,
+                                              double *X) {
+#pragma unroll
+  for (int r = 0; r < K; ++r) X[r] = agg[r * stride];
+  for (int sp = 1; sp < s; ++sp) {
+    double t[K];
+    const double *P = (last_short && sp == s - 1) ? Alast : Aseg;
+    matvec_lt_g<K>(P, stride, X, t);
+#pragma unroll
+    for (int r = 0; r < K; ++r) X[r] = t[r] + agg[sp * seg_stride + r * stride];
+  }
+}
+
+// One 16-row chunk: correct the loaded rows by the pending term R Y (Y <- A Y
+// per cell), sweep them (MODE 0), store, and prefetch the next chunk's rows
+// into the registers just consumed.  PARTIAL: only the first nv cells are
+// real; the carried state after cell nv-1 is returned in Xcap.
+template <int S, int MODE, bool PARTIAL>
+__device__ __forceinline__ void sweep_chunk(const LineConst &L, double hd, bool neg, double (&ein)[kSweepCells],
+                                            double (&eout)[kSweepCells], double *X, bool corr, double *Y,
+                                            const double *A1, const double *Rm, bool head, double b3,
+                                            __amdgpu_buffer_rsrc_t Rw, __amdgpu_buffer_rsrc_t Rn, int voff,
+                                            int row_bytes, int nv, double *Xcap) {
   constexpr int K = SchemeDim<S>::K;
 #pragma unroll
   for (int c = 0; c < kSweepCells; ++c) {
-    double oi, oo;
-#if RT_PIN_CELLS
-    asm volatile("" : "+v"(ein[c]), "+v"(eout[c]));
-#endif
-    if (c == 0)
-      cell_step_maybe_head<S>(L, hd, neg, ein[0], eout[0], X, head, b3, oi, oo);
-    else
-      cell_step<S>(L, hd, neg, ein[c], eout[c], X, oi, oo);
+    double pin = ein[c], pout = eout[c];
+    if (corr) {  // e += R Y ; Y <- A Y   (deferred cross-segment correction)
+#pragma unroll
+      for (int r = 0; r < K; ++r) {
+        pin += Rm[r] * Y[r];
+        pout += Rm[K + r] * Y[r];
+      }
+      double t[K];
+#pragma unroll
+      for (int r = 0; r < K; ++r) {
+        double acc = 0.0;
+#pragma unroll
+        for (int cc = 0; cc <= r; ++cc) acc += A1[tri(r, cc)] * Y[cc];
+        t[r] = acc;
+      }
+#pragma unroll
+      for (int r = 0; r < K; ++r) Y[r] = t[r];
+    }
+    double oi = pin, oo = pout;
+    if constexpr (MODE == 0) {
+      if (c == 0)
+        cell_step_maybe_head<S>(L, hd, neg, pin, pout, X, head, b3, oi, oo);
+      else
+        cell_step<S>(L, hd, neg, pin, pout, X, oi, oo);
+    }
     row_store(Rw, voff, c * row_bytes, oi, oo);
     const double2 v = row_load(Rn, voff, c * row_bytes);
     ein[c] = v.x;
     eout[c] = v.y;
-    // keep the prefetch in the registers it replaces: no hoisting across cells
-    __builtin_amdgcn_sched_barrier(0);
-    if constexpr (CAPTURE) {
-      if (c == c_last) {
+    if constexpr (PARTIAL) {
+      if (c == nv - 1) {
 #pragma unroll
         for (int r = 0; r < K; ++r) Xcap[r] = X[r];
       }
@@ -138,290 +134,119 @@ __device__ __forceinline__ void sweep_phase2(const LineConst &L, double hd, bool
   }
 }
 
-template <int S>
-__global__ __launch_bounds__(kSweepThreads, RT_SWEEP_MIN_WAVES) void sweep_step_kernel(SweepArgs a) {
+template <int S, int MODE>
+__global__ __launch_bounds__(64) void sweep_segment_kernel(SegArgs a) {
   constexpr int K = SchemeDim<S>::K;
   constexpr int NT = K * (K + 1) / 2;
-  __shared__ double sm_agg[kSweepWaves][K][64];
-  __shared__ double sm_xin[K][64];
-  __shared__ double sm_A16[NT * 64];
-  __shared__ double sm_A64[NT * 64];
-  __shared__ double sm_lc[LC_COUNT * 64];  // this line group's constants
-  __shared__ double sm_bdry[64];           // and inflow values
-
-  const int lane = threadIdx.x & 63;
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform
-  const int tiles_per_half = a.J * a.Q;  // host guarantees 2 J Q < 2^31
-  const int total_tiles = static_cast<int>(a.total_tiles);
+  const int lane = threadIdx.x;
   const size_t stride = static_cast<size_t>(a.Lpad);
-  int cached_key = -1;
-  LineConst L;
+  const int per_half = a.Q * a.Sg;
+  const int half = a.half0 + static_cast<int>(blockIdx.x) / per_half;
+  const int rem = static_cast<int>(blockIdx.x) % per_half;
+  const int s = rem / a.Q;  // segment (wave-uniform)
+  const int q = rem - s * a.Q;
+  const int ell = q * 64 + lane;
+  const bool neg = half == 0;
+  const int k_begin = s * a.Ls;
+  const int k_end = min(a.N, k_begin + a.Ls);
+  if (k_begin >= k_end) return;
+  const bool last_short = (a.N - (a.Sg - 1) * a.Ls) != a.Ls;
 
-  // tile t -> (half, j, q) and the address of this wave's first row
-  auto decode = [&](int t, int &half, int &j, int &q) {
-    half = t >= tiles_per_half ? 1 : 0;
-    const int rem = t - half * tiles_per_half;
-    j = static_cast<int>(static_cast<unsigned>(rem) / static_cast<unsigned>(a.Q));
-    q = rem - j * a.Q;
-  };
+  // per-line propagators: A1 (one cell), R (state -> step-end nodes), A^Ls, A^Llast
+  const double *pr = a.prop + static_cast<size_t>(half) * kPropCount<K> * stride + ell;
+  const double *pA1 = pr;
+  const double *pR = pr + NT * stride;
+  const double *pAseg = pr + (NT + 2 * K) * stride;
+  const double *pAlast = pr + (2 * NT + 2 * K) * stride;
+  const size_t seg_stride = static_cast<size_t>(K) * stride;
+
+  // ---- pending correction of the previous step: Y = true incoming state ----
+  const bool corr = a.pending && s > 0;
+  double Y[K], A1[NT], Rm[2 * K];
+#pragma unroll
+  for (int r = 0; r < K; ++r) Y[r] = 0.0;
+  if (corr) {
+    const double *ag = a.agg_prev + static_cast<size_t>(half) * a.Sg * seg_stride + ell;
+    fold_segments<K>(ag, seg_stride, stride, s, pAseg, pAlast, false, Y);
+  }
+#pragma unroll
+  for (int e = 0; e < NT; ++e) A1[e] = pA1[e * stride];
+#pragma unroll
+  for (int e = 0; e < 2 * K; ++e) Rm[e] = pR[e * stride];
+
+  // ---- line constants, inflow ----
+  LineConst L;
+#pragma unroll
+  for (int n = 0; n < LC_COUNT; ++n) L.c[n] = a.lc[(static_cast<size_t>(half) * LC_COUNT + n) * stride + ell];
+  double X[K];
+  double b[4];
+  const bool head_seg = (s == 0);
+  {
+    const double v = a.bdry[static_cast<size_t>(half) * stride + ell];
+    b[0] = b[1] = b[2] = b[3] = v;
+  }
+  if (MODE == 0 && head_seg && !neg && a.reflective) {
+    // solver.cpp:677-684: mu > 0 inflow = the mirror mu < 0 line's outflow of this
+    // step, folded from that line's segment aggregates (previous launch)
+    const double *ag = a.agg_cur + ell;  // half 0, same l
+    const double *pr0 = a.prop + ell;    // half 0 propagators
+    double Xo[K];
+    fold_segments<K>(ag, seg_stride, stride, a.Sg, pr0 + (NT + 2 * K) * stride,
+                     pr0 + (2 * NT + 2 * K) * stride, last_short, Xo);
+    if constexpr (S == SCHEME_BDF2) {
+      b[0] = Xo[1];
+      b[1] = Xo[2];
+      b[2] = Xo[3];
+      b[3] = Xo[4];
+    } else {
+      b[0] = b[1] = b[2] = b[3] = Xo[K - 1];
+    }
+  }
+  if (head_seg) {
+    head_state<S>(b, X);
+  } else {
+#pragma unroll
+    for (int r = 0; r < K; ++r) X[r] = 0.0;
+  }
+
+  // ---- stream the segment in 16-row chunks ----
   const int row_bytes = a.Lpad * static_cast<int>(sizeof(double2));
   const int voff = lane * static_cast<int>(sizeof(double2));
-  auto rows = [&](int half, int j, int q) {  // wave-uniform descriptor of this wave's 16 rows
-    const int k0 = j * kSweepTile + w * kSweepCells;
-    return rows_rsrc(a.E + (static_cast<size_t>(half) * a.Nrow + k0) * stride + q * 64, row_bytes);
-  };
-
-  int t = blockIdx.x;
-  if (t >= total_tiles) return;
-  int half, j, q;
-  decode(t, half, j, q);
+  const double2 *Eh = a.E + static_cast<size_t>(half) * a.Nrow * stride + q * 64;
+  auto rows = [&](int k0) { return rows_rsrc(Eh + static_cast<size_t>(k0) * stride, row_bytes); };
   double ein[kSweepCells], eout[kSweepCells];
-  {  // prologue: this workgroup's first tile
-    const __amdgpu_buffer_rsrc_t R = rows(half, j, q);
+  {
+    const __amdgpu_buffer_rsrc_t R0 = rows(k_begin);
 #pragma unroll
     for (int c = 0; c < kSweepCells; ++c) {
-      const double2 v = row_load(R, voff, c * row_bytes);
+      const double2 v = row_load(R0, voff, c * row_bytes);
       ein[c] = v.x;
       eout[c] = v.y;
     }
   }
-
-  for (;;) {
-    const int ell = q * 64 + lane;
-    const bool neg = (half == 0);
-    const int key = half * a.Q + q;
-    if (key != cached_key) {
-      // a new line group: constants, inflows and propagator powers -> LDS.
-      // Every global load of this block is drained here, so the prefetched
-      // rows still in flight are never waited for on the common path.
-      __syncthreads();  // previous tile's LDS readers are done
-      const double *lc = a.lc + static_cast<size_t>(half) * LC_COUNT * stride;
-      const double *A16 = a.Apow + static_cast<size_t>(half * 2 + 0) * NT * stride;
-      const double *A64 = a.Apow + static_cast<size_t>(half * 2 + 1) * NT * stride;
-      for (int e = w; e < LC_COUNT; e += kSweepWaves) sm_lc[e * 64 + lane] = lc[e * stride + ell];
-      for (int e = w; e < NT; e += kSweepWaves) {
-        sm_A16[e * 64 + lane] = A16[e * stride + ell];
-        sm_A64[e * 64 + lane] = A64[e * stride + ell];
-      }
-      if (w == 0) sm_bdry[lane] = a.bdry[static_cast<size_t>(half) * stride + ell];
-      __builtin_amdgcn_s_waitcnt(0);  // vmcnt(0) expcnt(0) lgkmcnt(0)
-      __syncthreads();
-      cached_key = key;
-    }
+  double Xcap[K];
+  int k0 = k_begin;
+  for (; k0 + kSweepCells < k_end; k0 += kSweepCells) {  // full chunks with a successor
+    sweep_chunk<S, MODE, false>(L, a.hd, neg, ein, eout, X, corr, Y, A1, Rm, head_seg && k0 == 0, b[3], rows(k0),
+                                rows(k0 + kSweepCells), voff, row_bytes, kSweepCells, Xcap);
+  }
+  {  // last chunk (possibly partial); its "prefetch" re-reads its own rows (harmless)
+    const int nv = k_end - k0;
+    const __amdgpu_buffer_rsrc_t Rl = rows(k0);
+    if (nv == kSweepCells) {
+      sweep_chunk<S, MODE, false>(L, a.hd, neg, ein, eout, X, corr, Y, A1, Rm, head_seg && k0 == 0, b[3], Rl, Rl,
+                                  voff, row_bytes, nv, Xcap);
 #pragma unroll
-    for (int n = 0; n < LC_COUNT; ++n) L.c[n] = sm_lc[n * 64 + lane];
-
-    // ---- inflow values for the line head (tile 0, wave 0) ----
-    const bool head = (j == 0 && w == 0);
-    double b[4];
-    {
-      const double v = sm_bdry[lane];
-      b[0] = b[1] = b[2] = b[3] = v;
-    }
-    if (head && !neg && a.reflective) {
-      // solver.cpp:677-684: the mu > 0 line reads its mirror's outflow at cell 0,
-      // produced by the same substep of the mu < 0 sweep (earlier tiles)
-      wait_flag(a.outflow_flag + q, 1u, a.error);
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      const int nsub = (S == SCHEME_BDF2) ? 4 : 1;
-      for (int s = 0; s < nsub; ++s) b[s] = load_sc1(a.outflow + static_cast<size_t>(s) * stride + ell);
-      __builtin_amdgcn_s_waitcnt(0);
-    }
-
-    // ---- phase 1: aggregate from X = 0 (the head starts from its inflow) ----
-    double X[K];
-    if (head) {
-      head_state<S>(b, X);
+      for (int r = 0; r < K; ++r) Xcap[r] = X[r];
     } else {
-#pragma unroll
-      for (int r = 0; r < K; ++r) X[r] = 0.0;
+      sweep_chunk<S, MODE, true>(L, a.hd, neg, ein, eout, X, corr, Y, A1, Rm, head_seg && k0 == 0, b[3], Rl, Rl,
+                                 voff, row_bytes, nv, Xcap);
     }
-    if (!(a.debug_flags & 2)) {
-      double oi, oo;
-      cell_step_maybe_head<S>(L, a.hd, neg, ein[0], eout[0], X, head, b[3], oi, oo);
+  }
+  if constexpr (MODE == 0) {
+    double *ag = a.agg_cur + static_cast<size_t>(half) * a.Sg * seg_stride + static_cast<size_t>(s) * seg_stride + ell;
 #pragma unroll
-      for (int c = 1; c < kSweepCells; ++c) {
-        // pin each cell's inputs to this point: no X-independent work of later
-        // cells is hoisted ahead (bounded live ranges -> occupancy)
-#if RT_PIN_CELLS
-        asm volatile("" : "+v"(ein[c]), "+v"(eout[c]));
-#endif
-        cell_step<S>(L, a.hd, neg, ein[c], eout[c], X, oi, oo);
-      }
-    }
-#pragma unroll
-    for (int r = 0; r < K; ++r) sm_agg[w][r][lane] = X[r];
-    __syncthreads();
-
-    // ---- wave 0: tile aggregate, publish, look-back, publish prefix ----
-    if (w == 0) {
-      const size_t rec = static_cast<size_t>(t) * K * 64;
-      double T[K], tmp[K];
-#pragma unroll
-      for (int r = 0; r < K; ++r) T[r] = sm_agg[0][r][lane];
-      for (int ww = 1; ww < kSweepWaves; ++ww) {
-        matvec_lt<K>(sm_A16, lane, T, tmp);
-#pragma unroll
-        for (int r = 0; r < K; ++r) T[r] = tmp[r] + sm_agg[ww][r][lane];
-      }
-      if (j == 0) {
-        // the head made this an inclusive prefix already
-#pragma unroll
-        for (int r = 0; r < K; ++r) store_sc1(a.pref + rec + r * 64 + lane, T[r]);
-        drain_stores();
-        if (lane == 0) store_flag(a.status + t, 2u);
-      } else if (a.debug_flags & 1) {
-#pragma unroll
-        for (int r = 0; r < K; ++r) sm_xin[r][lane] = 0.0;
-      } else {
-#pragma unroll
-        for (int r = 0; r < K; ++r) store_sc1(a.agg + rec + r * 64 + lane, T[r]);
-        drain_stores();
-        if (lane == 0) store_flag(a.status + t, 1u);
-#if RT_LOOKBACK_PARALLEL
-        // decoupled look-back.  The 64 lanes poll the status words of the 64
-        // nearest predecessors of this line group (t - Q, t - 2Q, ...) in one
-        // go; the nearest one holding an inclusive prefix, with aggregates
-        // published by everything in between, closes the look-back:
-        //   X_in = A64 (... (A64 pref[t - dQ] + agg[t - (d-1)Q]) ...) + agg[t - Q]
-        // (published records are immutable, so they are re-read safely).
-        const int window = min(j, 64);
-        int d = 0;
-        {
-          const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
-          for (;;) {
-            unsigned st = 0;
-            if (lane < window) st = load_flag(a.status + (t - (lane + 1) * a.Q));
-            const unsigned long long pm = __ballot(st >= 2u);
-            const unsigned long long rm = __ballot(st >= 1u);
-            if (pm) {
-              d = __builtin_ctzll(pm) + 1;  // distance of the nearest prefix
-              const unsigned long long need = (d == 64) ? ~0ull : ((1ull << d) - 1);
-              if ((rm & need) == need) break;
-            }
-            __builtin_amdgcn_s_sleep(2);
-            if (__builtin_amdgcn_s_memrealtime() - t_start > 2000000000ull) {  // 20 s
-              if (lane == 0) atomicOr(a.error, 1u);
-              d = 1;
-              break;
-            }
-          }
-        }
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        double acc[K];
-        {
-          const double *pr = a.pref + static_cast<size_t>(t - d * a.Q) * K * 64 + lane;
-#pragma unroll
-          for (int r = 0; r < K; ++r) acc[r] = load_sc1(pr + r * 64);
-        }
-        for (int m = d - 1; m >= 1; m -= 2) {  // fold the aggregates, 2 records per batch
-          double v[2][K];
-#pragma unroll
-          for (int u = 0; u < 2; ++u)
-            if (m - u >= 1) {
-              const double *ag = a.agg + static_cast<size_t>(t - (m - u) * a.Q) * K * 64 + lane;
-#pragma unroll
-              for (int r = 0; r < K; ++r) v[u][r] = load_sc1(ag + r * 64);
-            }
-#pragma unroll
-          for (int u = 0; u < 2; ++u)
-            if (m - u >= 1) {
-              matvec_lt<K>(sm_A64, lane, acc, tmp);
-#pragma unroll
-              for (int r = 0; r < K; ++r) acc[r] = tmp[r] + v[u][r];
-            }
-        }
-#else
-        // decoupled look-back (serial): walk back over the predecessors of this
-        // line group (t - Q, t - 2Q, ...) until one has published its inclusive
-        // prefix, then fold forward from it:
-        //   X_in = A64 (... (A64 pref[t - dQ] + agg[t - (d-1)Q]) ...) + agg[t - Q]
-        // (published records are immutable, so they are re-read safely).
-        int s = t - a.Q;
-        for (;;) {
-          const unsigned st = wait_flag(a.status + s, 1u, a.error);
-          if (st >= 2u || st == 0u) break;
-          s -= a.Q;
-        }
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        double acc[K];
-#pragma unroll
-        for (int r = 0; r < K; ++r) acc[r] = load_sc1(a.pref + static_cast<size_t>(s) * K * 64 + r * 64 + lane);
-        for (s += a.Q; s < t; s += a.Q) {
-          matvec_lt<K>(sm_A64, lane, acc, tmp);
-#pragma unroll
-          for (int r = 0; r < K; ++r) acc[r] = tmp[r] + load_sc1(a.agg + static_cast<size_t>(s) * K * 64 + r * 64 + lane);
-        }
-#endif
-        // inclusive prefix = A64 X_in + T
-        matvec_lt<K>(sm_A64, lane, acc, tmp);
-#pragma unroll
-        for (int r = 0; r < K; ++r) store_sc1(a.pref + rec + r * 64 + lane, tmp[r] + T[r]);
-        drain_stores();
-        if (lane == 0) store_flag(a.status + t, 2u);
-#pragma unroll
-        for (int r = 0; r < K; ++r) sm_xin[r][lane] = acc[r];
-      }
-    }
-    __syncthreads();
-
-    // ---- phase 2: true incoming X, re-sweep, stream out; prefetch the next tile ----
-    // Re-derive every X-independent term from the data rather than keeping
-    // phase 1's copies live (register pressure / occupancy over FLOPs).
-#if RT_PHASE_BARRIER
-#pragma unroll
-    for (int c = 0; c < kSweepCells; ++c) asm volatile("" : "+v"(ein[c]), "+v"(eout[c]));
-#endif
-    const int tn = t + static_cast<int>(gridDim.x);
-    const bool more = tn < total_tiles;
-    int half_n = half, j_n = j, q_n = q;
-    if (more) decode(tn, half_n, j_n, q_n);
-    {
-      double tmp[K];
-      int first_wave;
-      if (head) {
-        head_state<S>(b, X);
-        first_wave = 1;
-      } else if (j == 0) {
-#pragma unroll
-        for (int r = 0; r < K; ++r) X[r] = sm_agg[0][r][lane];
-        first_wave = 1;
-      } else {
-#pragma unroll
-        for (int r = 0; r < K; ++r) X[r] = sm_xin[r][lane];
-        first_wave = 0;
-      }
-      for (int ww = first_wave; ww < w; ++ww) {
-        matvec_lt<K>(sm_A16, lane, X, tmp);
-#pragma unroll
-        for (int r = 0; r < K; ++r) X[r] = tmp[r] + sm_agg[ww][r][lane];
-      }
-    }
-    const __amdgpu_buffer_rsrc_t Rw = rows(half, j, q);
-    const __amdgpu_buffer_rsrc_t Rn = rows(half_n, j_n, q_n);
-    const int k0 = j * kSweepTile + w * kSweepCells;
-    const int c_last = a.N - 1 - k0;  // this wave holds the line's last cell iff 0 <= c_last < 16
-    if (neg && a.reflective && c_last >= 0 && c_last < kSweepCells) {
-      double Xo[K];
-      sweep_phase2<S, true>(L, a.hd, neg, ein, eout, X, head, b[3], Rw, Rn, voff, row_bytes, c_last, Xo);
-      // publish the per-substep outflows for the reflective mu > 0 partners
-      if constexpr (S == SCHEME_BDF2) {
-#pragma unroll
-        for (int s = 0; s < 4; ++s) store_sc1(a.outflow + static_cast<size_t>(s) * stride + ell, Xo[1 + s]);
-      } else {
-        store_sc1(a.outflow + ell, Xo[K - 1]);
-      }
-      drain_stores();
-      if (lane == 0) store_flag(a.outflow_flag + q, 1u);
-    } else {
-      sweep_phase2<S, false>(L, a.hd, neg, ein, eout, X, head, b[3], Rw, Rn, voff, row_bytes, 0, nullptr);
-    }
-    if (!more) break;
-    t = tn;
-    half = half_n;
-    j = j_n;
-    q = q_n;
-    __syncthreads();  // LDS (sm_agg, sm_xin) is reused by the next tile
+    for (int r = 0; r < K; ++r) ag[r * stride] = Xcap[r];
   }
 }
 
@@ -556,29 +381,29 @@ __global__ void group_absorption_kernel(const double *phi, const double *sigma, 
 // ------------------------------------------------------------------------
 // launchers
 // ------------------------------------------------------------------------
-template <int S>
-static hipError_t launch_sweep_t(const SweepArgs &a, int grid, hipStream_t st) {
-  hipLaunchKernelGGL(sweep_step_kernel<S>, dim3(grid), dim3(kSweepThreads), 0, st, a);
+template <int S, int MODE>
+static hipError_t launch_seg_t(const SegArgs &a, int grid, hipStream_t st) {
+  hipLaunchKernelGGL((sweep_segment_kernel<S, MODE>), dim3(grid), dim3(64), 0, st, a);
   return hipGetLastError();
 }
 
-hipError_t launch_sweep(int scheme, const SweepArgs &a, int grid, hipStream_t st) {
+hipError_t launch_sweep(int scheme, bool finalize, const SegArgs &a, int grid, hipStream_t st) {
   switch (scheme) {
-    case SCHEME_BE: return launch_sweep_t<SCHEME_BE>(a, grid, st);
-    case SCHEME_CN: return launch_sweep_t<SCHEME_CN>(a, grid, st);
-    default: return launch_sweep_t<SCHEME_BDF2>(a, grid, st);
+    case SCHEME_BE: return finalize ? launch_seg_t<SCHEME_BE, 1>(a, grid, st) : launch_seg_t<SCHEME_BE, 0>(a, grid, st);
+    case SCHEME_CN: return finalize ? launch_seg_t<SCHEME_CN, 1>(a, grid, st) : launch_seg_t<SCHEME_CN, 0>(a, grid, st);
+    default:
+      return finalize ? launch_seg_t<SCHEME_BDF2, 1>(a, grid, st) : launch_seg_t<SCHEME_BDF2, 0>(a, grid, st);
   }
 }
 
-hipError_t sweep_occupancy(int scheme, int *blocks_per_cu) {
+hipError_t sweep_occupancy(int scheme, int *waves_per_cu) {
   switch (scheme) {
     case SCHEME_BE:
-      return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, sweep_step_kernel<SCHEME_BE>, kSweepThreads, 0);
+      return hipOccupancyMaxActiveBlocksPerMultiprocessor(waves_per_cu, sweep_segment_kernel<SCHEME_BE, 0>, 64, 0);
     case SCHEME_CN:
-      return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, sweep_step_kernel<SCHEME_CN>, kSweepThreads, 0);
+      return hipOccupancyMaxActiveBlocksPerMultiprocessor(waves_per_cu, sweep_segment_kernel<SCHEME_CN, 0>, 64, 0);
     default:
-      return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, sweep_step_kernel<SCHEME_BDF2>, kSweepThreads,
-                                                          0);
+      return hipOccupancyMaxActiveBlocksPerMultiprocessor(waves_per_cu, sweep_segment_kernel<SCHEME_BDF2, 0>, 64, 0);
   }
 }
 

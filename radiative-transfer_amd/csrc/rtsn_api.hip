@@ -43,12 +43,13 @@ struct rt_solver {
   bool equilibrium_done = false;
   int g_lo = 0, g_hi = 0, Gl = 0, H = 0, Lh = 0, Lpad = 0, Q = 0, J = 0;
   int scheme = SCHEME_BDF2, K = 5;
-  long long tiles = 0;
-  int grid = 0;
+  int Sg = 1, Ls = 16;           // segments per line and cells per segment
   int device = 0;
   hipStream_t stream = nullptr;
   // device state
-  DeviceBuf E, lc, Apow, bdry, outflow, outflow_flag, status, agg, pref, error, lineB, muwt, mom, rows, sigma;
+  DeviceBuf E, lc, prop, bdry, agg[2], lineB, muwt, mom, rows, sigma;
+  int agg_cur = 0;               // aggregates of the last step live in agg[agg_cur ^ 1]
+  bool pending = false;          // E holds provisional segments (correction outstanding)
   // profiling
   bool profiling = false;
   std::vector<hipEvent_t> ev_pool;   // (start, stop) pairs of profiled launches
@@ -207,10 +208,12 @@ static LineConst line_constants(const rt_solver &s, int i, int g) {
   return L;
 }
 
-// Linear part A of the cell map X -> X' (cell.hpp), by evaluating the map
-// with the affine constants and the cell data set to zero.
+// Linear parts of the cell map (cell.hpp): X' = A X + ..., step-end nodes
+// (oin, oout) = R X + ...; evaluated with the affine constants and the cell
+// data set to zero.  R is 2 x K (row 0: e_in, row 1: e_out).
 template <int S>
-static void propagator(const LineConst &Lin, double hd, bool neg, double *A /* K*K row-major */) {
+static void propagator(const LineConst &Lin, double hd, bool neg, double *A /* K*K row-major */,
+                       double *R /* 2*K */) {
   constexpr int K = SchemeDim<S>::K;
   LineConst L = Lin;
   L.c[LC_SC] = 0.0;
@@ -220,6 +223,8 @@ static void propagator(const LineConst &Lin, double hd, bool neg, double *A /* K
     double oi, oo;
     cell_step<S>(L, hd, neg, 0.0, 0.0, X, oi, oo);
     for (int r = 0; r < K; ++r) A[r * K + col] = X[r];
+    R[col] = oi;
+    R[K + col] = oo;
   }
 }
 
@@ -230,6 +235,24 @@ static void matmul(int K, const double *A, const double *B, double *C) {
       for (int m = 0; m < K; ++m) acc += A[r * K + m] * B[m * K + c];
       C[r * K + c] = acc;
     }
+}
+
+// A^n by binary exponentiation
+static void matpow(int K, const double *A, long long n, double *out) {
+  std::vector<double> base(A, A + K * K), acc(K * K, 0.0), tmp(K * K);
+  for (int r = 0; r < K; ++r) acc[r * K + r] = 1.0;
+  while (n > 0) {
+    if (n & 1) {
+      matmul(K, acc.data(), base.data(), tmp.data());
+      acc.swap(tmp);
+    }
+    n >>= 1;
+    if (n) {
+      matmul(K, base.data(), base.data(), tmp.data());
+      base.swap(tmp);
+    }
+  }
+  std::copy(acc.begin(), acc.end(), out);
 }
 
 static rt_status upload(rt_solver *s, DeviceBuf &b, const void *src, size_t bytes) {
@@ -256,12 +279,13 @@ static void line_inflow(const rt_solver &s, std::vector<double> &bd) {
 }
 
 static rt_status setup_lines(rt_solver *s) {
-  const int K = s->K, NT = K * (K + 1) / 2;
+  const int K = s->K, NT = K * (K + 1) / 2, NP = 3 * NT + 2 * K;
   const double hd = 0.5 * (s->p.X / s->p.N);
+  const long long L_last = s->p.N - static_cast<long long>(s->Sg - 1) * s->Ls;
   std::vector<double> lc(static_cast<size_t>(2) * LC_COUNT * s->Lpad, 0.0);
-  std::vector<double> Ap(static_cast<size_t>(2) * 2 * NT * s->Lpad, 0.0);
+  std::vector<double> pr(static_cast<size_t>(2) * NP * s->Lpad, 0.0);
   std::vector<double> lineB(static_cast<size_t>(2) * s->Lpad, 0.0);
-  std::vector<double> A(K * K), T(K * K), P16(K * K), P64(K * K);
+  std::vector<double> A(K * K), R(2 * K), Aseg(K * K), Alast(K * K);
   for (int half = 0; half < 2; ++half)
     for (int gl = 0; gl < s->Gl; ++gl)
       for (int ip = 0; ip < s->H; ++ip) {
@@ -272,29 +296,24 @@ static rt_status setup_lines(rt_solver *s) {
         lineB[static_cast<size_t>(half) * s->Lpad + ell] = s->gt.B[g];
         const bool neg = half == 0;
         switch (s->scheme) {
-          case SCHEME_BE: propagator<SCHEME_BE>(L, hd, neg, A.data()); break;
-          case SCHEME_CN: propagator<SCHEME_CN>(L, hd, neg, A.data()); break;
-          default: propagator<SCHEME_BDF2>(L, hd, neg, A.data()); break;
+          case SCHEME_BE: propagator<SCHEME_BE>(L, hd, neg, A.data(), R.data()); break;
+          case SCHEME_CN: propagator<SCHEME_CN>(L, hd, neg, A.data(), R.data()); break;
+          default: propagator<SCHEME_BDF2>(L, hd, neg, A.data(), R.data()); break;
         }
-        P16 = A;  // A^16 by squaring
-        for (int sq = 0; sq < 4; ++sq) {
-          matmul(K, P16.data(), P16.data(), T.data());
-          P16 = T;
-        }
-        P64 = P16;  // A^64 = (A^16)^4
-        for (int sq = 0; sq < 2; ++sq) {
-          matmul(K, P64.data(), P64.data(), T.data());
-          P64 = T;
-        }
+        matpow(K, A.data(), s->Ls, Aseg.data());
+        matpow(K, A.data(), L_last, Alast.data());
+        double *dst = pr.data() + static_cast<size_t>(half) * NP * s->Lpad + ell;
         for (int r = 0; r < K; ++r)
           for (int c = 0; c <= r; ++c) {
-            Ap[((static_cast<size_t>(half) * 2 + 0) * NT + tri(r, c)) * s->Lpad + ell] = P16[r * K + c];
-            Ap[((static_cast<size_t>(half) * 2 + 1) * NT + tri(r, c)) * s->Lpad + ell] = P64[r * K + c];
+            dst[static_cast<size_t>(tri(r, c)) * s->Lpad] = A[r * K + c];
+            dst[static_cast<size_t>(NT + 2 * K + tri(r, c)) * s->Lpad] = Aseg[r * K + c];
+            dst[static_cast<size_t>(2 * NT + 2 * K + tri(r, c)) * s->Lpad] = Alast[r * K + c];
           }
+        for (int e = 0; e < 2 * K; ++e) dst[static_cast<size_t>(NT + e) * s->Lpad] = R[e];
       }
   rt_status st;
   if ((st = upload(s, s->lc, lc.data(), lc.size() * sizeof(double)))) return st;
-  if ((st = upload(s, s->Apow, Ap.data(), Ap.size() * sizeof(double)))) return st;
+  if ((st = upload(s, s->prop, pr.data(), pr.size() * sizeof(double)))) return st;
   if ((st = upload(s, s->lineB, lineB.data(), lineB.size() * sizeof(double)))) return st;
   std::vector<double> sig(s->Gl);
   for (int gl = 0; gl < s->Gl; ++gl) sig[gl] = s->gt.rho[s->g_lo + gl] * s->gt.kappa[s->g_lo + gl];
@@ -364,8 +383,6 @@ extern "C" rt_status rt_create_from_params(const rt_params *pin, int g_lo, int g
   s->Q = (s->Lh + 63) / 64;
   s->Lpad = 64 * s->Q;
   s->J = (q.N + kSweepTile - 1) / kSweepTile;
-  s->tiles = 2LL * s->J * s->Q;
-  if (s->tiles >= (1LL << 31)) return fail(nullptr, RT_ERR_PARAM, "too many sweep tiles for one handle: shard the groups");
   s->scheme = q.ts_method;
   s->K = q.ts_method == 1 ? 1 : (q.ts_method == 2 ? 2 : 5);
   s->device = device;
@@ -381,23 +398,35 @@ extern "C" rt_status rt_create_from_params(const rt_params *pin, int g_lo, int g
     return fail(nullptr, RT_ERR_DEVICE, std::string("librtsn is built for gfx950, device is ") + prop.gcnArchName);
   HIP_TRY(h, hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
 
-  const size_t Lp = h->Lpad, N = q.N;
-  const int K = h->K, NT = K * (K + 1) / 2;
+  // segments: enough waves to fill the chip (occupancy x CUs), Ls a multiple of the chunk
+  int waves_per_cu = 0;
+  HIP_TRY(h, sweep_occupancy(h->scheme, &waves_per_cu));
+  waves_per_cu = std::max(1, std::min(waves_per_cu, 32));
+  {
+    const long long target = static_cast<long long>(prop.multiProcessorCount) * waves_per_cu;
+    long long sg = std::max<long long>(1, target / (2LL * h->Q));
+    const long long max_sg = (q.N + kSweepCells - 1) / kSweepCells;
+    sg = std::min(sg, max_sg);
+    long long ls = (q.N + sg - 1) / sg;
+    ls = ((ls + kSweepCells - 1) / kSweepCells) * kSweepCells;
+    h->Ls = static_cast<int>(ls);
+    h->Sg = static_cast<int>((q.N + ls - 1) / ls);
+  }
+  if (2LL * h->Q * h->Sg >= (1LL << 31)) return fail(nullptr, RT_ERR_PARAM, "too many lines for one handle: shard the groups");
+
+  const size_t Lp = h->Lpad;
+  const int K = h->K, NP = 3 * (K * (K + 1) / 2) + 2 * K;
   hipError_t e = hipSuccess;
   const size_t Nrow = static_cast<size_t>(h->J) * kSweepTile;  // cells padded to whole tiles
   if (!e) e = dalloc(h->E, sizeof(double2) * 2 * Nrow * Lp);
   if (!e) e = dalloc(h->lc, sizeof(double) * 2 * LC_COUNT * Lp);
-  if (!e) e = dalloc(h->Apow, sizeof(double) * 4 * NT * Lp);
+  if (!e) e = dalloc(h->prop, sizeof(double) * 2 * NP * Lp);
   if (!e) e = dalloc(h->bdry, sizeof(double) * 2 * Lp);
-  if (!e) e = dalloc(h->outflow, sizeof(double) * 4 * Lp);
-  if (!e) e = dalloc(h->outflow_flag, sizeof(unsigned) * h->Q);
-  if (!e) e = dalloc(h->status, sizeof(unsigned) * h->tiles);
-  if (!e) e = dalloc(h->agg, sizeof(double) * h->tiles * K * 64);
-  if (!e) e = dalloc(h->pref, sizeof(double) * h->tiles * K * 64);
-  if (!e) e = dalloc(h->error, 16);
+  if (!e) e = dalloc(h->agg[0], sizeof(double) * 2 * h->Sg * K * Lp);
+  if (!e) e = dalloc(h->agg[1], sizeof(double) * 2 * h->Sg * K * Lp);
   if (!e) e = dalloc(h->lineB, sizeof(double) * 2 * Lp);
   if (!e) e = dalloc(h->muwt, sizeof(double) * 2 * q.M);
-  if (!e) e = dalloc(h->mom, sizeof(double) * 3 * h->Gl * N);
+  if (!e) e = dalloc(h->mom, sizeof(double) * 3 * h->Gl * static_cast<size_t>(q.N));
   if (!e) e = dalloc(h->rows, sizeof(double2) * 4 * Lp);
   if (!e) e = dalloc(h->sigma, sizeof(double) * h->Gl);
   if (e) return fail(nullptr, RT_ERR_NOMEM, std::string("device allocation: ") + hipGetErrorString(e));
@@ -406,16 +435,9 @@ extern "C" rt_status rt_create_from_params(const rt_params *pin, int g_lo, int g
   if ((st = upload_inflow(h))) return st;
   HIP_TRY(h, launch_init_state(static_cast<double2 *>(h->E.p), static_cast<const double *>(h->lineB.p), geometry(h),
                                h->stream));
-  HIP_TRY(h, hipMemsetAsync(h->outflow.p, 0, h->outflow.bytes, h->stream));
-  HIP_TRY(h, hipMemsetAsync(h->error.p, 0, h->error.bytes, h->stream));
+  HIP_TRY(h, hipMemsetAsync(h->agg[0].p, 0, h->agg[0].bytes, h->stream));
+  HIP_TRY(h, hipMemsetAsync(h->agg[1].p, 0, h->agg[1].bytes, h->stream));
 
-  int per_cu = 0;
-  HIP_TRY(h, sweep_occupancy(h->scheme, &per_cu));
-  per_cu = std::max(1, std::min(per_cu, 8));
-  long long maxP = static_cast<long long>(prop.multiProcessorCount) * per_cu;
-  long long P = std::min<long long>(maxP, h->tiles);
-  if (P > h->Q && maxP >= h->Q) P = (P / h->Q) * h->Q;  // keep each workgroup on one line group
-  h->grid = static_cast<int>(std::max<long long>(1, P));
   HIP_TRY(h, hipStreamSynchronize(h->stream));
   *out = s.release();
   return RT_OK;
@@ -461,30 +483,31 @@ static rt_status fold_events(rt_solver *s) {
   return RT_OK;
 }
 
-static rt_status enqueue_steps(rt_solver *s, int nsteps) {
-  SweepArgs a{};
+static SegArgs seg_args(rt_solver *s) {
+  SegArgs a{};
   a.E = static_cast<double2 *>(s->E.p);
   a.lc = static_cast<const double *>(s->lc.p);
-  a.Apow = static_cast<const double *>(s->Apow.p);
+  a.prop = static_cast<const double *>(s->prop.p);
   a.bdry = static_cast<const double *>(s->bdry.p);
-  a.outflow = static_cast<double *>(s->outflow.p);
-  a.outflow_flag = static_cast<unsigned *>(s->outflow_flag.p);
-  a.status = static_cast<unsigned *>(s->status.p);
-  a.agg = static_cast<double *>(s->agg.p);
-  a.pref = static_cast<double *>(s->pref.p);
-  a.error = static_cast<unsigned *>(s->error.p);
-  a.total_tiles = s->tiles;
+  a.agg_prev = static_cast<const double *>(s->agg[s->agg_cur ^ 1].p);
+  a.agg_cur = static_cast<double *>(s->agg[s->agg_cur].p);
   a.N = s->p.N;
   a.Nrow = s->J * kSweepTile;
   a.Lpad = s->Lpad;
   a.Q = s->Q;
-  a.J = s->J;
+  a.Sg = s->Sg;
+  a.Ls = s->Ls;
+  a.half0 = 0;
   a.reflective = s->p.bc_left_indicator == 2;
-  if (const char *dbg = std::getenv("RTSN_DEBUG_FLAGS")) a.debug_flags = std::atoi(dbg);
+  a.pending = s->pending ? 1 : 0;
   a.hd = 0.5 * (s->p.X / s->p.N);
+  return a;
+}
+
+static rt_status enqueue_steps(rt_solver *s, int nsteps) {
+  const int per_half = s->Q * s->Sg;
   for (int n = 0; n < nsteps; ++n) {
-    HIP_TRY(s, hipMemsetAsync(s->status.p, 0, s->status.bytes, s->stream));
-    HIP_TRY(s, hipMemsetAsync(s->outflow_flag.p, 0, s->outflow_flag.bytes, s->stream));
+    SegArgs a = seg_args(s);
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (s->profiling) {
       if (s->ev_used + 2 > s->ev_pool.size()) {
@@ -495,13 +518,31 @@ static rt_status enqueue_steps(rt_solver *s, int nsteps) {
       e1 = s->ev_pool[s->ev_used++];
       HIP_TRY(s, hipEventRecord(e0, s->stream));
     }
-    HIP_TRY(s, launch_sweep(s->scheme, a, s->grid, s->stream));
+    if (a.reflective) {  // mu > 0 heads need this step's mu < 0 outflow: two launches
+      a.half0 = 0;
+      HIP_TRY(s, launch_sweep(s->scheme, false, a, per_half, s->stream));
+      a.half0 = 1;
+      HIP_TRY(s, launch_sweep(s->scheme, false, a, per_half, s->stream));
+    } else {
+      HIP_TRY(s, launch_sweep(s->scheme, false, a, 2 * per_half, s->stream));
+    }
     if (s->profiling) {
       HIP_TRY(s, hipEventRecord(e1, s->stream));
       ++s->profiled;
     }
     ++s->launches;
+    s->pending = s->Sg > 1;
+    s->agg_cur ^= 1;
   }
+  return RT_OK;
+}
+
+// Apply the outstanding cross-segment correction in place (before any read).
+static rt_status finalize(rt_solver *s) {
+  if (!s->pending) return RT_OK;
+  SegArgs a = seg_args(s);
+  HIP_TRY(s, launch_sweep(s->scheme, true, a, 2 * s->Q * s->Sg, s->stream));
+  s->pending = false;
   return RT_OK;
 }
 
@@ -517,9 +558,6 @@ extern "C" rt_status rt_advance(rt_solver *s, int nsteps) {
 extern "C" rt_status rt_synchronize(rt_solver *s) {
   if (!s) return fail(nullptr, RT_ERR_ARG, "rt_synchronize: NULL handle");
   HIP_TRY(s, hipStreamSynchronize(s->stream));
-  unsigned err = 0;
-  HIP_TRY(s, hipMemcpy(&err, s->error.p, sizeof(unsigned), hipMemcpyDeviceToHost));
-  if (err) return fail(s, RT_ERR_TIMEOUT, "an inter-workgroup wait in the sweep timed out");
   return RT_OK;
 }
 
@@ -560,6 +598,7 @@ static rt_status via_device(rt_solver *s, size_t count, double *host, F &&launch
 extern "C" rt_status rt_get_psi(rt_solver *s, double *psi) {
   if (!s || !psi) return fail(s, RT_ERR_ARG, "rt_get_psi: bad argument");
   HIP_TRY(s, hipSetDevice(s->device));
+  if (rt_status st = finalize(s)) return st;
   const Geometry g = geometry(s);
   return via_device(s, static_cast<size_t>(g.M) * g.Gl * g.N, psi, [&](double *d) {
     return launch_export_psi(static_cast<const double2 *>(s->E.p), d, g, s->stream);
@@ -569,6 +608,7 @@ extern "C" rt_status rt_get_psi(rt_solver *s, double *psi) {
 extern "C" rt_status rt_get_ends(rt_solver *s, double *ends) {
   if (!s || !ends) return fail(s, RT_ERR_ARG, "rt_get_ends: bad argument");
   HIP_TRY(s, hipSetDevice(s->device));
+  if (rt_status st = finalize(s)) return st;
   const Geometry g = geometry(s);
   return via_device(s, static_cast<size_t>(2) * g.M * g.Gl * g.N, ends, [&](double *d) {
     return launch_export_ends(static_cast<const double2 *>(s->E.p), d, g, s->stream);
@@ -584,6 +624,7 @@ extern "C" rt_status rt_set_ends(rt_solver *s, const double *ends) {
   HIP_TRY(s, hipMalloc(reinterpret_cast<void **>(&d), sizeof(double) * n));
   hipError_t e = hipMemcpyAsync(d, ends, sizeof(double) * n, hipMemcpyHostToDevice, s->stream);
   if (e == hipSuccess) e = launch_import_ends(static_cast<double2 *>(s->E.p), d, g, s->stream);
+  s->pending = false;  // the loaded state is exact
   if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
   (void)hipFree(d);
   if (e != hipSuccess) return fail(s, RT_ERR_DEVICE, std::string("rt_set_ends: ") + hipGetErrorString(e));
@@ -591,6 +632,7 @@ extern "C" rt_status rt_set_ends(rt_solver *s, const double *ends) {
 }
 
 static rt_status compute_moments(rt_solver *s) {
+  if (rt_status st = finalize(s)) return st;
   const Geometry g = geometry(s);
   const size_t GN = static_cast<size_t>(s->Gl) * s->p.N;
   double *m = static_cast<double *>(s->mom.p);
@@ -616,6 +658,7 @@ extern "C" rt_status rt_get_moments(rt_solver *s, double *phi, double *F, double
 
 // boundary rows: [0] half0 k=0, [1] half0 k=N-1, [2] half1 k=0, [3] half1 k=N-1
 static rt_status fetch_rows(rt_solver *s, std::vector<double> &rows) {
+  if (rt_status st = finalize(s)) return st;
   const Geometry g = geometry(s);
   rows.resize(static_cast<size_t>(8) * s->Lpad);
   HIP_TRY(s, launch_boundary_rows(static_cast<const double2 *>(s->E.p), static_cast<double2 *>(s->rows.p), g,
@@ -768,8 +811,8 @@ extern "C" rt_status rt_sweep_traffic(rt_solver *s, double *bytes_per_step, doub
 
 extern "C" rt_status rt_sweep_geometry(rt_solver *s, int *workgroups, long long *tiles) {
   if (!s) return fail(nullptr, RT_ERR_ARG, "rt_sweep_geometry: NULL handle");
-  if (workgroups) *workgroups = s->grid;
-  if (tiles) *tiles = s->tiles;
+  if (workgroups) *workgroups = 2 * s->Q * s->Sg;  // one 64-lane wave per (line group, segment)
+  if (tiles) *tiles = s->Sg;                        // segments per line
   return RT_OK;
 }
 
