@@ -1,0 +1,48 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 PMC passes of the sweep kernel into profiles/pmc_<variant>.json.
+
+usage: pmc_summary.py <variant> <fetch_dir> <write_dir> [<sq_dir> ...]
+
+HBM bytes per launch follow MI355X_MICROARCH.md §HBM: FETCH_SIZE and
+WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE reports half the bytes of a
+16-B-per-lane streaming read, so it is doubled.
+"""
+import csv
+import json
+import statistics
+import sys
+from pathlib import Path
+
+KERNEL = "sweep_segment_kernel"
+
+
+def counters(d):
+    out = {}
+    for f in Path(d).rglob("*counter_collection.csv"):
+        for r in csv.DictReader(open(f)):
+            if KERNEL in r["Kernel_Name"] and ", 1>" not in r["Kernel_Name"]:
+                out.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
+    return out
+
+
+def main():
+    variant, fdir, wdir, *rest = sys.argv[1:]
+    fetch = counters(fdir)["FETCH_SIZE"]
+    write = counters(wdir)["WRITE_SIZE"]
+    rd = statistics.median(fetch) * 1024 * 2
+    wr = statistics.median(write) * 1024
+    res = {"variant": variant, "kernel": KERNEL, "launches": len(fetch),
+           "fetch_size_kib_median": statistics.median(fetch), "write_size_kib_median": statistics.median(write),
+           "hbm_read_bytes_per_launch": rd, "hbm_write_bytes_per_launch": wr,
+           "hbm_bytes_per_launch": rd + wr,
+           "correction": "FETCH_SIZE x 2 (gfx950 half-count of 16 B/lane streaming reads), KiB -> bytes"}
+    for d in rest:
+        for k, v in counters(d).items():
+            res[k + "_median"] = statistics.median(v)
+    out = Path(__file__).resolve().parent.parent / "profiles" / f"pmc_{variant}.json"
+    out.write_text(json.dumps(res, indent=1) + "\n")
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()
