@@ -11,6 +11,6 @@ for pmc in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_
   timeout -k 10 300 rocprofv3 --pmc $pmc -d gpurun_out/pmc_${V}_$i -o run --output-format csv -- python3 bench.py --no-cpu-baseline --steps 2 --warmup 0 --variant $V > gpurun_out/pmc_${V}_$i.log 2>&1 || { tail -5 gpurun_out/pmc_${V}_$i.log; exit 1; }
 done
 python3 scripts/pmc_summary.py $V gpurun_out/pmc_${V}_1 gpurun_out/pmc_${V}_2 gpurun_out/pmc_${V}_3 gpurun_out/pmc_${V}_4
-cp gpurun_out/prof_kt_$V/run_kernel_stats.csv profiles/r01_${V}_kernel_stats.csv
+cp gpurun_out/prof_kt_$V/run_kernel_stats.csv gpurun_out/r01_${V}_kernel_stats.csv
 timeout -k 10 600 python bench.py --variant $V > gpurun_out/bench_$V.log 2>&1 || { tail -20 gpurun_out/bench_$V.log; exit 1; }
-tail -1 gpurun_out/bench_$V.log | tee profiles/r01_bench_$V.json
+tail -1 gpurun_out/bench_$V.log | tee gpurun_out/r01_bench_$V.json
