@@ -89,6 +89,106 @@ def load_traffic(variant: str):
         return None
 
 
+def shard(scaling: str, groups: int, world: int, rank: int):
+    """(G_total, g_lo, g_hi) of this rank.  weak: every rank owns `groups`
+    groups of a groups*world grid; strong: `groups` split into contiguous
+    ceil(groups/world) shards (the last may be short, or empty)."""
+    if scaling == "weak":
+        return groups * world, rank * groups, (rank + 1) * groups
+    per = (groups + world - 1) // world
+    lo = min(groups, rank * per)
+    return groups, lo, min(groups, lo + per)
+
+
+def run_rank(solver, p: dict, steps: int, warmup: int, world: int, device, shard_info, scaling: str):
+    """Warmup, K timed steps between barrier + device sync, max over ranks,
+    then the absorption all-reduce.  Collectives go through torch.distributed
+    on whatever backend is initialised (RCCL on the GPU box, gloo in the CPU
+    tests).  Returns the JSON line (all ranks compute it; rank 0 prints)."""
+    import torch
+    import torch.distributed as dist
+
+    G_total, g_lo, g_hi = shard_info
+    bytes_step, upd_step = solver.sweep_traffic()
+    wg, tiles = solver.sweep_geometry()
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        if device.type == "cuda":
+            torch.cuda.synchronize(device)
+
+    solver.advance(warmup)
+    solver.synchronize()
+    barrier()
+    solver.set_profiling(True)
+    t0 = time.perf_counter()
+    solver.advance(steps)
+    solver.synchronize()
+    barrier()
+    wall = time.perf_counter() - t0
+    kern_ms, nlaunch = solver.sweep_time()
+    solver.set_profiling(False)
+
+    # group-summed absorption all-reduce, outside the timed region
+    absorb = torch.zeros(p["N"], dtype=torch.float64, device=device)
+    solver.group_absorption(absorb)
+    solver.synchronize()
+    if world > 1:
+        dist.all_reduce(absorb)
+    finite = bool(torch.isfinite(absorb).all().item())
+
+    t = torch.tensor([wall, kern_ms / max(nlaunch, 1)], dtype=torch.float64, device=device)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    wall_max, kern_avg_ms = float(t[0]), float(t[1])
+    # whole-job updates: every rank's own count (shards may be ragged under strong scaling)
+    u = torch.tensor([upd_step * steps], dtype=torch.float64, device=device)
+    if world > 1:
+        dist.all_reduce(u)
+    total_updates = float(u[0])
+
+    value = total_updates / wall_max
+    ms_per_step = 1e3 * wall_max / steps
+    achieved = bytes_step / (kern_avg_ms * 1e-3) if kern_avg_ms > 0 else 0.0
+    line = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "cell-angle-group updates/s",
+        "n_gpus": world,
+        "steps": steps,
+        "warmup": warmup,
+        "ms_per_step": ms_per_step,
+        "higher_is_better": True,
+        "scaling": scaling,
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic",
+        "bdf2_steps_per_s": 1e3 / ms_per_step,
+        "config": {
+            "workload": f"SL slab: N={p['N']} cells x S{p['M']} x {g_hi - g_lo} groups per GPU "
+                        f"({G_total} total), BDF2 dt=1e-3, V={p['V']}, use_correction=1, vacuum BCs",
+            "cells": p["N"], "angles": p["M"], "groups_per_gpu": g_hi - g_lo, "groups_total": G_total,
+            "time_scheme": "BDF2 (4 fused substeps per step)",
+            "parallelism": f"group shards x{world}, no data-path collective",
+            "sweep_workgroups": wg, "tiles_per_step": tiles,
+        },
+        "roofline": {
+            "bound": "hbm",
+            "achieved": achieved / 1e9,
+            "peak": HBM_PEAK / 1e9,
+            "unit": "GB/s",
+            "frac": achieved / HBM_PEAK,
+            "traffic": None,
+            "kernel": "sweep_segment_kernel<3,0>",
+            "kernel_ms": kern_avg_ms,
+            "algorithmic_bytes_per_launch": bytes_step,
+        },
+        "absorption_allreduce_finite": finite,
+    }
+    return line, absorb
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -108,92 +208,16 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    device = torch.device("cuda", local)
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        dist.init_process_group("nccl", device_id=device)
 
-    if args.scaling == "weak":
-        G_total = args.groups * world
-        g_lo, g_hi = rank * args.groups, (rank + 1) * args.groups
-    else:
-        G_total = args.groups
-        per = (G_total + world - 1) // world
-        g_lo, g_hi = rank * per, min(G_total, (rank + 1) * per)
-    p = slab_params(G_total, args.variant, N=args.cells)
-    solver = rtsn.Solver(p, device=local, g_lo=g_lo, g_hi=g_hi)
-    bytes_step, upd_step = solver.sweep_traffic()
-    wg, tiles = solver.sweep_geometry()
-
-    def barrier():
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
-
-    solver.advance(args.warmup)
-    solver.synchronize()
-    barrier()
-    solver.set_profiling(True)
-    t0 = time.perf_counter()
-    solver.advance(args.steps)
-    torch.cuda.synchronize()
-    solver.synchronize()
-    barrier()
-    wall = time.perf_counter() - t0
-    kern_ms, nlaunch = solver.sweep_time()
-    solver.set_profiling(False)
-
-    # group-summed absorption all-reduce (RCCL), outside the timed region
-    absorb = torch.zeros(p["N"], dtype=torch.float64, device=f"cuda:{local}")
-    solver.group_absorption_device(absorb.data_ptr())
-    solver.synchronize()
-    if world > 1:
-        dist.all_reduce(absorb)
-    finite = bool(torch.isfinite(absorb).all().item())
-
-    t = torch.tensor([wall, kern_ms / max(nlaunch, 1)], dtype=torch.float64, device=f"cuda:{local}")
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    wall_max, kern_avg_ms = float(t[0]), float(t[1])
-
-    total_updates = upd_step * args.steps * world
-    value = total_updates / wall_max
-    ms_per_step = 1e3 * wall_max / args.steps
-    achieved = bytes_step / (kern_avg_ms * 1e-3)
-    line = {
-        "metric": METRIC,
-        "value": value,
-        "unit": "cell-angle-group updates/s",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": ms_per_step,
-        "higher_is_better": True,
-        "scaling": args.scaling,
-        "vs_baseline": None,
-        "dtype": "f64",
-        "data": "synthetic",
-        "bdf2_steps_per_s": 1e3 / ms_per_step,
-        "config": {
-            "workload": f"SL slab: N={p['N']} cells x S{p['M']} x {g_hi - g_lo} groups per GPU "
-                        f"({G_total} total), BDF2 dt=1e-3, V={p['V']}, use_correction=1, vacuum BCs",
-            "cells": p["N"], "angles": p["M"], "groups_per_gpu": g_hi - g_lo, "groups_total": G_total,
-            "time_scheme": "BDF2 (4 fused substeps per step)",
-            "parallelism": f"group shards x{world}, no data-path collective",
-            "sweep_workgroups": wg, "tiles_per_step": tiles,
-        },
-        "roofline": {
-            "bound": "hbm",
-            "achieved": achieved / 1e9,
-            "peak": HBM_PEAK / 1e9,
-            "unit": "GB/s",
-            "frac": achieved / HBM_PEAK,
-            "traffic": load_traffic(args.variant),
-            "kernel": "sweep_segment_kernel<3,0>",
-            "kernel_ms": kern_avg_ms,
-            "algorithmic_bytes_per_launch": bytes_step,
-        },
-        "absorption_allreduce_finite": finite,
-    }
+    info = shard(args.scaling, args.groups, world, rank)
+    p = slab_params(info[0], args.variant, N=args.cells)
+    solver = rtsn.Solver(p, device=local, g_lo=info[1], g_hi=info[2])
+    line, _ = run_rank(solver, p, args.steps, args.warmup, world, device, info, args.scaling)
+    line["roofline"]["traffic"] = load_traffic(args.variant)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(args.variant)
     if rank == 0:

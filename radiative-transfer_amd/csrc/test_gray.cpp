@@ -1,5 +1,5 @@
 // test_gray -- the reference's GrayTest (tests/test_gray.cpp:47-101) on the
-// MI355X solver: prm/single_group.prm, pass iff |max_c F| < 1e-6 (the signed
+// MI355X solver: $TRANSFER_DIR/prm/single_group.prm, pass iff |max_c F| < 1e-6 (the signed
 // maximum, as written at :89).
 #include <cmath>
 #include <cstdlib>
@@ -10,9 +10,10 @@
 #include "eigen_text.hpp"
 #include "prm.hpp"
 #include "solver.hpp"
+#include "transfer_dir.hpp"
 
 int main(int argc, char **argv) {
-  const std::string filename = argc > 1 ? argv[1] : "prm/single_group.prm";
+  const std::string filename = argc > 1 ? argv[1] : rtamd::transfer_dir() + "prm/single_group.prm";
   rtamd::ParameterHandler parameter_handler(filename);
   if (parameter_handler.status() != RT_OK) {
     std::cerr << parameter_handler.error() << std::endl;

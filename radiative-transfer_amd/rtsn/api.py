@@ -337,6 +337,15 @@ class Solver:
         _check(lib().rt_group_absorption_device(self._h, C.cast(C.c_void_p(d_out_ptr), C.POINTER(C.c_double))),
                "rt_group_absorption_device", self._h)
 
+    def group_absorption(self, out):
+        """Group-summed absorption into a contiguous float64 torch tensor of N
+        elements on this solver's GPU (ordered on the solver's stream)."""
+        import torch
+        if not (isinstance(out, torch.Tensor) and out.is_cuda and out.dtype == torch.float64
+                and out.is_contiguous() and out.numel() == self.N):
+            raise ValueError("group_absorption: need a contiguous float64 CUDA tensor of N elements")
+        self.group_absorption_device(out.data_ptr())
+
     # ---- measurement ----
     def set_profiling(self, on: bool):
         _check(lib().rt_set_profiling(self._h, int(on)), "rt_set_profiling", self._h)

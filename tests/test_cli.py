@@ -1,0 +1,144 @@
+"""The reference's executables on the MI355X path: bin/transfer (src/main.cc)
+and bin/test_gray (tests/test_gray.cpp).
+
+CSV text: main.cc:37-57 writes `file << mat << endl` with Eigen's default
+IOFormat (Eigen/src/Core/IO.h print_matrix, Eigen 3.3/3.4 -- Eigen is absent
+from this image, so the format is restated below from its published
+algorithm): stream precision 6 (printf "%.6g"), every coefficient
+right-aligned to the widest one, " " between coefficients, "\n" between rows;
+a rank-3 Tensor prints as its dim0 x (rest) ColMajor matrix (Eigen
+TensorIO.h).  `eigen_text` is that restatement; the CPU test pins the C++
+writer (csrc/eigen_text.hpp) to it on edge values, the GPU test compares the
+eight CSV files of a run with the oracle's numbers byte for byte.
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+from conftest import REPO, PRM_DIR
+
+PKG = REPO / "radiative-transfer_amd"
+
+
+def eigen_text(a: np.ndarray) -> str:
+    """`os << m << std::endl` for a 2-D array under Eigen's default IOFormat."""
+    a = np.atleast_2d(np.asarray(a, dtype=np.float64))
+    s = [["%.6g" % v for v in row] for row in a]
+    w = max(len(x) for row in s for x in row)
+    return "\n".join(" ".join(x.rjust(w) for x in row) for row in s) + "\n"
+
+
+def tensor_text(psi: np.ndarray) -> str:
+    """Eigen::Tensor<double,3>(M,G,N): dim0 x (G*N) ColMajor view."""
+    M, G, N = psi.shape
+    return eigen_text(psi.transpose(0, 2, 1).reshape(M, N * G))
+
+
+DRIVER = r"""
+#include "eigen_text.hpp"
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+int main(int argc, char **argv) {
+  // argv: out rows cols v0 v1 ... (ColMajor)
+  const size_t r = std::atol(argv[2]), c = std::atol(argv[3]);
+  std::vector<double> v;
+  for (int k = 4; k < argc; ++k) v.push_back(std::strtod(argv[k], nullptr));
+  return rtamd::write_eigen_text(argv[1], v, r, c) ? 0 : 1;
+}
+"""
+
+
+@pytest.fixture(scope="module")
+def text_driver(tmp_path_factory):
+    d = tmp_path_factory.mktemp("eigen_text")
+    src = d / "drv.cpp"
+    src.write_text(DRIVER)
+    exe = d / "drv"
+    subprocess.run(["g++", "-std=c++17", "-O1", f"-I{PKG / 'csrc'}", str(src), "-o", str(exe)], check=True)
+    return exe
+
+
+@pytest.mark.parametrize("rows,cols,vals", [
+    (1, 1, [0.5]),
+    (2, 3, [1.0, -2.5, 1e-300, 123456789.0, -0.0, 3.14159265358979]),
+    (3, 1, [1e20, -1e-5, 7.0]),
+    (1, 4, [0.1, 0.25, -1234567.0, 5e-324]),
+    (2, 2, [999999.5, 1e6, 0.000123456789, -0.0001]),
+])
+def test_eigen_text_format(text_driver, tmp_path, rows, cols, vals):
+    out = tmp_path / "m.csv"
+    subprocess.run([str(text_driver), str(out), str(rows), str(cols)] + [repr(v) for v in vals], check=True)
+    a = np.array(vals).reshape(cols, rows).T  # ColMajor input
+    assert out.read_text() == eigen_text(a)
+
+
+def test_tensor_text_layout():
+    psi = np.arange(2 * 3 * 4, dtype=float).reshape(2, 3, 4)
+    lines = tensor_text(psi).splitlines()
+    assert len(lines) == 2 and len(lines[0].split()) == 12
+    # column j = g + G*c holds psi(i, g, c)
+    assert float(lines[1].split()[1 + 3 * 2]) == psi[1, 1, 2]
+
+
+def _bin(name: str) -> Path:
+    exe = PKG / "bin" / name
+    if not exe.exists():
+        pytest.skip(f"{exe} not built")
+    return exe
+
+
+def _run_tree(tmp_path: Path) -> Path:
+    """build/ next to prm/, as the reference is run (tables from ../prm/)."""
+    shutil.copytree(PRM_DIR, tmp_path / "prm")
+    run = tmp_path / "build"
+    run.mkdir()
+    return run
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["llnl_slab_test", "single_group"])
+def test_transfer_csv_files(oracle_mod, tmp_path, name):
+    run = _run_tree(tmp_path)
+    prm = f"../prm/{name}.prm"
+    r = subprocess.run([str(_bin("transfer")), prm], cwd=run, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.startswith(f"filename: {prm}\n")
+
+    q = oracle_mod.parse_prm(str(run / prm), table_dir=str(tmp_path / "prm") + "/")
+    s = oracle_mod.OracleSolver(q)
+    s.solve()
+    phi, F, phi_plus = s.moments()
+    left, right = s.group_ends()
+    N = q["N"]
+    x = (np.arange(N) + 0.5) * q["dx"]
+    expect = {
+        "phi.csv": eigen_text(phi), "phi_plus.csv": eigen_text(phi_plus), "F.csv": eigen_text(F),
+        "psi.csv": tensor_text(s.psi()), "x.csv": eigen_text(x[:, None]),
+        "e_ave.csv": eigen_text(s.groups()["e_ave"][:, None]),
+        "left_ends.csv": eigen_text(left[:, None]), "right_ends.csv": eigen_text(right[:, None]),
+    }
+    for fname, text in expect.items():
+        got = (run / fname).read_text()
+        if fname == "F.csv":
+            # F cancels to ~1e-17 in equilibrium: its digits are rounding noise, so
+            # compare the layout and the values to the scale of the summands
+            g = np.loadtxt(run / fname, ndmin=2)
+            assert g.shape == F.shape
+            np.testing.assert_allclose(g, F, rtol=1e-5, atol=1e-10 * np.abs(phi).max())
+        else:
+            assert got == text, fname
+
+
+@pytest.mark.gpu
+def test_gray_binary(tmp_path):
+    run = _run_tree(tmp_path)
+    env = dict(os.environ, TRANSFER_DIR=str(tmp_path) + "/")
+    r = subprocess.run([str(_bin("test_gray"))], cwd=run, capture_output=True, text=True, timeout=600, env=env)
+    assert r.returncode == 0, r.stdout + r.stderr

@@ -1,0 +1,163 @@
+"""Multi-rank path of bench.py on CPU: world_size 2 over gloo.
+
+bench.py shards energy groups across ranks: no collective in
+the data path, barrier + max-over-ranks timing, one all-reduce of the
+group-summed absorption A(x) = sum_g rho kappa_g phi_g(x) after timing.  Here
+each rank drives bench.run_rank() with a CPU stand-in solver built on the
+oracle over its group shard (the stand-in is the test's, never the product's),
+and the all-reduced A(x) must equal the single-process oracle over all groups
+-- the check that the shard boundaries, the per-rank group tables (the last
+Planck group is a remainder of ALL groups) and the reductions are right.
+"""
+from __future__ import annotations
+
+import json
+import os
+import socket
+import sys
+import time
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from conftest import REPO
+
+sys.path.insert(0, str(REPO))
+sys.path.insert(0, str(REPO / "oracle"))
+
+import bench  # noqa: E402
+import oracle  # noqa: E402
+
+oracle.build()
+
+
+def small_params(G_total: int, variant: str = "corr") -> dict:
+    p = bench.slab_params(G_total, variant, N=48, M=8)
+    return p
+
+
+def oracle_dict(p: dict) -> dict:
+    q = dict(p)
+    q.update(bc_left=p["bc_left_indicator"], bc_right=p["bc_right_indicator"], dx=p["X"] / p["N"],
+             have_group_bounds=0, have_group_kappa=1, prm_found=1)
+    return q
+
+
+class OracleShard:
+    """CPU stand-in with the rtsn.Solver methods run_rank uses."""
+
+    def __init__(self, p: dict, g_lo: int, g_hi: int):
+        self.p = p
+        self.s = oracle.OracleSolver(oracle_dict(p), g_lo=g_lo, g_hi=g_hi)
+        self.g_lo, self.g_hi = g_lo, g_hi
+        self.it = 0
+        self.prof = False
+        self.ms = 0.0
+        self.n = 0
+
+    def sweep_traffic(self):
+        Gl = self.g_hi - self.g_lo
+        return 32.0 * self.p["M"] * Gl * self.p["N"], 4.0 * self.p["M"] * Gl * self.p["N"]
+
+    def sweep_geometry(self):
+        return 1, 1
+
+    def advance(self, n):
+        for _ in range(n):
+            t0 = time.perf_counter()
+            self.s.run_substeps(self.it, 4)
+            self.it += 4
+            if self.prof:
+                self.ms += 1e3 * (time.perf_counter() - t0)
+                self.n += 1
+
+    def synchronize(self):
+        pass
+
+    def set_profiling(self, on):
+        self.prof = bool(on)
+        if on:
+            self.ms, self.n = 0.0, 0
+
+    def sweep_time(self):
+        return self.ms, self.n
+
+    def group_absorption(self, out):
+        phi, _, _ = self.s.moments()
+        kap = self.s.groups()["kappa"][self.g_lo:self.g_hi]
+        a = (self.p["rho"] * kap[:, None] * phi).sum(axis=0) if len(kap) else np.zeros(self.p["N"])
+        out.copy_(torch.from_numpy(a))
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, scaling, groups, steps, outdir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        info = bench.shard(scaling, groups, world, rank)
+        p = small_params(info[0])
+        solver = OracleShard(p, info[1], info[2])
+        line, absorb = bench.run_rank(solver, p, steps, 1, world, torch.device("cpu"), info, scaling)
+        np.save(os.path.join(outdir, f"absorb{rank}.npy"), absorb.numpy())
+        with open(os.path.join(outdir, f"line{rank}.json"), "w") as f:
+            json.dump({"line": line, "info": list(info), "wall_ms": solver.ms}, f)
+    finally:
+        dist.destroy_process_group()
+
+
+def _run(tmp_path, scaling, groups, steps=2, world=2):
+    mp.start_processes(_worker, args=(world, _free_port(), scaling, groups, steps, str(tmp_path)),
+                       nprocs=world, join=True, start_method="spawn")
+    lines = [json.load(open(tmp_path / f"line{r}.json")) for r in range(world)]
+    absorbs = [np.load(tmp_path / f"absorb{r}.npy") for r in range(world)]
+    return lines, absorbs
+
+
+def full_absorption(G_total: int, steps: int) -> np.ndarray:
+    p = small_params(G_total)
+    s = oracle.OracleSolver(oracle_dict(p))
+    s.run_substeps(0, 4 * (steps + 1))  # warmup 1 + timed steps
+    phi, _, _ = s.moments()
+    kap = s.groups()["kappa"]
+    return (p["rho"] * kap[:, None] * phi).sum(axis=0)
+
+
+@pytest.mark.parametrize("scaling,groups", [("weak", 3), ("strong", 5)])
+def test_two_rank_group_shards(tmp_path, scaling, groups):
+    steps = 2
+    lines, absorbs = _run(tmp_path, scaling, groups, steps)
+    G_total = groups * 2 if scaling == "weak" else groups
+    # shards tile [0, G_total) without overlap
+    spans = sorted(tuple(l["info"][1:]) for l in lines)
+    assert spans[0][0] == 0 and spans[-1][1] == G_total and spans[0][1] == spans[1][0]
+    # all-reduced absorption == single-process oracle over all groups
+    ref = full_absorption(G_total, steps)
+    for a in absorbs:
+        np.testing.assert_array_equal(a, absorbs[0])
+        np.testing.assert_allclose(a, ref, rtol=1e-13, atol=0)
+    # the JSON line: whole-job updates over the max-over-ranks wall time
+    line = lines[0]["line"]
+    for k in ("value", "ms_per_step", "n_gpus", "absorption_allreduce_finite"):
+        assert line[k] == lines[1]["line"][k]  # reduced over ranks
+    assert line["roofline"]["kernel_ms"] == lines[1]["line"]["roofline"]["kernel_ms"]
+    total = sum(4.0 * 8 * (l["info"][2] - l["info"][1]) * 48 * steps for l in lines)
+    assert line["n_gpus"] == 2 and line["scaling"] == scaling
+    assert line["value"] == pytest.approx(total / (line["ms_per_step"] * 1e-3 * steps), rel=1e-12)
+    assert line["config"]["groups_total"] == G_total
+    assert line["absorption_allreduce_finite"] is True
+    assert line["roofline"]["kernel_ms"] >= max(l["wall_ms"] for l in lines) / steps * (1 - 1e-9)
+
+
+def test_shard_table():
+    assert bench.shard("weak", 128, 8, 3) == (1024, 384, 512)
+    assert bench.shard("strong", 128, 3, 2) == (128, 86, 128)
+    spans = [bench.shard("strong", 10, 4, r)[1:] for r in range(4)]
+    assert spans == [(0, 3), (3, 6), (6, 9), (9, 10)]
