@@ -79,13 +79,15 @@ def cpu_baseline(variant: str) -> dict:
                       f"M=64, 1 of 128 groups (g={g}), N={N}, 1 BDF2 step = {upd:.3g} updates in {dt:.2f} s"}
 
 
-def load_traffic(variant: str):
-    f = REPO / "profiles" / f"pmc_{variant}.json"
+def load_traffic(variant: str, tb: int):
+    """Measured HBM bytes per sweep launch (rocprofv3 PMC, scripts/gpu_profile.sh) for
+    this variant and time block, or None."""
+    f = REPO / "profiles" / f"pmc_{variant}_t{tb}.json"
     if not f.exists():
         return None
     try:
         return json.loads(f.read_text()).get("hbm_bytes_per_launch")
-    except Exception:
+    except (OSError, ValueError):
         return None
 
 
@@ -109,7 +111,8 @@ def run_rank(solver, p: dict, steps: int, warmup: int, world: int, device, shard
     import torch.distributed as dist
 
     G_total, g_lo, g_hi = shard_info
-    bytes_step, upd_step = solver.sweep_traffic()
+    bytes_launch, upd_step = solver.sweep_traffic()  # per pass (T fused steps), per full step
+    tb = getattr(solver, "time_block", 1)
     wg, tiles = solver.sweep_geometry()
 
     def barrier():
@@ -150,7 +153,7 @@ def run_rank(solver, p: dict, steps: int, warmup: int, world: int, device, shard
 
     value = total_updates / wall_max
     ms_per_step = 1e3 * wall_max / steps
-    achieved = bytes_step / (kern_avg_ms * 1e-3) if kern_avg_ms > 0 else 0.0
+    achieved = bytes_launch / (kern_avg_ms * 1e-3) if kern_avg_ms > 0 else 0.0
     line = {
         "metric": METRIC,
         "value": value,
@@ -170,6 +173,7 @@ def run_rank(solver, p: dict, steps: int, warmup: int, world: int, device, shard
                         f"({G_total} total), BDF2 dt=1e-3, V={p['V']}, use_correction=1, vacuum BCs",
             "cells": p["N"], "angles": p["M"], "groups_per_gpu": g_hi - g_lo, "groups_total": G_total,
             "time_scheme": "BDF2 (4 fused substeps per step)",
+            "steps_per_pass": tb,
             "parallelism": f"group shards x{world}, no data-path collective",
             "sweep_workgroups": wg, "tiles_per_step": tiles,
         },
@@ -180,9 +184,9 @@ def run_rank(solver, p: dict, steps: int, warmup: int, world: int, device, shard
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK,
             "traffic": None,
-            "kernel": "sweep_segment_kernel<3,0>",
+            "kernel": f"sweep_block_kernel<3, {tb}, 0>",
             "kernel_ms": kern_avg_ms,
-            "algorithmic_bytes_per_launch": bytes_step,
+            "algorithmic_bytes_per_launch": bytes_launch,
         },
         "absorption_allreduce_finite": finite,
     }
@@ -198,6 +202,8 @@ def main():
     ap.add_argument("--scaling", choices=["weak", "strong"], default="weak")
     ap.add_argument("--groups", type=int, default=128, help="groups per GPU (weak) or in total (strong)")
     ap.add_argument("--cells", type=int, default=1_000_000)
+    ap.add_argument("--time-block", type=int, default=0,
+                    help="full steps fused per HBM pass (0: the library default)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
@@ -216,8 +222,10 @@ def main():
     info = shard(args.scaling, args.groups, world, rank)
     p = slab_params(info[0], args.variant, N=args.cells)
     solver = rtsn.Solver(p, device=local, g_lo=info[1], g_hi=info[2])
+    if args.time_block:
+        solver.time_block = args.time_block
     line, _ = run_rank(solver, p, args.steps, args.warmup, world, device, info, args.scaling)
-    line["roofline"]["traffic"] = load_traffic(args.variant)
+    line["roofline"]["traffic"] = load_traffic(args.variant, solver.time_block)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(args.variant)
     if rank == 0:

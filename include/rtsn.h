@@ -140,9 +140,15 @@ rt_status rt_group_absorption_device(rt_solver *s, double *d_out);
  * stream (off by default). */
 rt_status rt_set_profiling(rt_solver *s, int on);
 rt_status rt_get_sweep_time(rt_solver *s, double *total_ms, long long *launches);
-/* Algorithmic HBM bytes of one sweep launch (one full step) and updates
- * (cell x angle x group x substep) per full step, for the handle's groups. */
-rt_status rt_sweep_traffic(rt_solver *s, double *bytes_per_step, double *updates_per_step);
+/* Algorithmic HBM bytes of one sweep pass (one profiled launch: T full steps,
+ * the state is read and written once) and updates (cell x angle x group x
+ * substep) per full step, for the handle's groups. */
+rt_status rt_sweep_traffic(rt_solver *s, double *bytes_per_launch, double *updates_per_step);
+/* Time blocking: full steps advanced per pass over HBM (1..4).  Results do
+ * not depend on it beyond rounding; rt_advance(n) runs n / T passes of T
+ * steps and one pass of n % T. */
+rt_status rt_set_time_block(rt_solver *s, int steps_per_pass);
+rt_status rt_get_time_block(rt_solver *s, int *steps_per_pass);
 /* Sweep geometry actually used: waves launched per step (one per line group
  * and segment) and segments per line. */
 rt_status rt_sweep_geometry(rt_solver *s, int *workgroups, long long *tiles);

@@ -195,4 +195,92 @@ __host__ __device__ __forceinline__ void cell_step_maybe_head(const LineConst &L
 // Index of (r, c), c <= r, in a packed lower triangle.
 __host__ __device__ __forceinline__ constexpr int tri(int r, int c) { return r * (r + 1) / 2 + c; }
 
+// ---------------------------------------------------------------------------
+// The cell step as a per-line affine map.
+//
+// Because sigma, B_g and the correction constants do not vary along a line
+// (T and rho are constant, solver.cpp:157), one full step of one cell is an
+// affine map with line-constant coefficients from the inputs
+//   u = (X[0..K-1], pin, pout)            (carried state, step-start nodes)
+// to the outputs
+//   row r < K : X'[r]      row K : oin      (oout == X'[K-1] for every scheme).
+// The coefficients are derived on the host by evaluating cell_step<S> above
+// (the reference's algebra) on unit inputs, so the map is the same
+// arithmetic up to rounding.  Rows keep only their structural non-zeros:
+//   BE   X=(x)                     X'0=oout: x,pin,pout      oin: x,pin,pout
+//   CN   X=(p_up,xh)               X'0=pout (copy)           X'1=oout, oin: all
+//   BDF2 X=(p_up,x0,xh,x2,x3)      X'0=pout (copy)  X'1=e1out: x0,pin,pout
+//        X'2=e2out: p_up,x0,xh,pin,pout   X'3=e3out: + x2   X'4=oout, oin: all
+// (the host checks every other coefficient is exactly zero).
+// ---------------------------------------------------------------------------
+template <int S>
+__host__ __device__ constexpr bool map_copy_row0() {
+  return S != SCHEME_BE;
+}
+
+// does output row r (0..K) depend on input c (0..K+1)?
+template <int S>
+__host__ __device__ constexpr bool map_dep(int r, int c) {
+  constexpr int K = SchemeDim<S>::K;
+  if (map_copy_row0<S>() && r == 0) return false;
+  if (c >= K) return true;  // pin, pout feed every computed row
+  if constexpr (S == SCHEME_BDF2) {
+    if (r == 1) return c == 1;
+    if (r == 2) return c <= 2;
+    if (r == 3) return c <= 3;
+    return true;
+  }
+  return true;
+}
+
+// slot of coefficient (r, c) in the packed map; the constant of row r follows its coefficients
+template <int S>
+__host__ __device__ constexpr int map_slot(int r, int c) {
+  constexpr int K = SchemeDim<S>::K;
+  int n = 0;
+  for (int rr = 0; rr <= K; ++rr) {
+    if (map_copy_row0<S>() && rr == 0) continue;
+    for (int cc = 0; cc < K + 2; ++cc) {
+      if (!map_dep<S>(rr, cc)) continue;
+      if (rr == r && cc == c) return n;
+      ++n;
+    }
+    if (rr == r && c == K + 2) return n;  // constant
+    ++n;
+  }
+  return -1;
+}
+
+template <int S>
+__host__ __device__ constexpr int map_count() {
+  constexpr int K = SchemeDim<S>::K;
+  return map_slot<S>(K, K + 2) + 1;
+}
+
+// Apply the map (CONST: with the affine constants; otherwise its linear part).
+template <int S, bool CONST>
+__host__ __device__ __forceinline__ void map_apply(const double *W, const double *X, double din, double dout,
+                                                   double *Xn, double &oin, double &oout) {
+  constexpr int K = SchemeDim<S>::K;
+#pragma unroll
+  for (int r = 0; r <= K; ++r) {
+    if (map_copy_row0<S>() && r == 0) {
+      Xn[0] = dout;
+      continue;
+    }
+    double acc = CONST ? W[map_slot<S>(r, K + 2)] : 0.0;
+#pragma unroll
+    for (int c = 0; c < K + 2; ++c) {
+      if (!map_dep<S>(r, c)) continue;
+      const double u = c < K ? X[c] : (c == K ? din : dout);
+      acc = fma(W[map_slot<S>(r, c)], u, acc);
+    }
+    if (r < K)
+      Xn[r] = acc;
+    else
+      oin = acc;
+  }
+  oout = Xn[K - 1];
+}
+
 }  // namespace rtamd

@@ -42,8 +42,9 @@ namespace rtamd {
 // lane*16 (one VGPR), instead of a 64-bit VGPR address per row.
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
+template <int C>
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rows_rsrc(const double2 *base, int row_bytes) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<double2 *>(base), 0, kSweepCells * row_bytes, 0x00020000);
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<double2 *>(base), 0, C * row_bytes, 0x00020000);
 }
 __device__ __forceinline__ double2 row_load(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
   return __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
@@ -52,92 +53,134 @@ __device__ __forceinline__ void row_store(__amdgpu_buffer_rsrc_t r, int voff, in
   __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, make_double2(x, y)), r, voff, soff, 0);
 }
 
-// y = A x with A packed lower-triangular, one entry per stride in memory
-template <int K>
-__device__ __forceinline__ void matvec_lt_g(const double *A, size_t stride, const double *x, double *y) {
+// True incoming carried state of every segment from the aggregates of one
+// pass (each segment swept from X = 0):  Y_1 = agg_0,
+// Y_{s+1} = P_s Y_s + agg_s with P = A^Ls, or A^Llast for the last segment;
+// Y_Sg is the state after the whole line (the reflective outflow).  One
+// thread per (half, line); only_last: write Y_Sg alone, to y[KC][Lpad].
+template <int KC>
+__global__ void fold_kernel(FoldArgs f) {
+  constexpr int NTC = KC * (KC + 1) / 2;
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= f.nhalf * f.Lpad) return;
+  const int half = f.half0 + idx / f.Lpad, ell = idx % f.Lpad;
+  const size_t stride = f.Lpad, seg_stride = static_cast<size_t>(KC) * stride;
+  const double *ag = f.agg + static_cast<size_t>(half) * f.Sg * seg_stride + ell;
+  const double *pr = f.prop + static_cast<size_t>(half) * f.prop_half * stride + ell;
+  double *y = f.y + static_cast<size_t>(half) * (f.Sg + 1) * seg_stride + ell;
+  double X[KC];
 #pragma unroll
-  for (int r = 0; r < K; ++r) {
-    double acc = 0.0;
+  for (int r = 0; r < KC; ++r) X[r] = ag[r * stride];
+  for (int s = 1; s <= f.Sg; ++s) {
+    if (!f.only_last) {
 #pragma unroll
-    for (int c = 0; c <= r; ++c) acc += A[tri(r, c) * stride] * x[c];
-    y[r] = acc;
+      for (int r = 0; r < KC; ++r) y[(s * KC + r) * stride] = X[r];
+    }
+    if (s == f.Sg) break;
+    const double *P = (f.last_short && s == f.Sg - 1) ? pr + NTC * stride : pr;
+    double t[KC];
+#pragma unroll
+    for (int r = 0; r < KC; ++r) {
+      double acc = ag[(static_cast<size_t>(s) * KC + r) * stride];
+#pragma unroll
+      for (int c = 0; c <= r; ++c) acc += P[tri(r, c) * stride] * X[c];
+      t[r] = acc;
+    }
+#pragma unroll
+    for (int r = 0; r < KC; ++r) X[r] = t[r];
+  }
+  if (f.only_last) {
+#pragma unroll
+    for (int r = 0; r < KC; ++r) f.y[r * stride + ell] = X[r];
   }
 }
 
-// X_s of segment s (its true incoming carried state) from the aggregates of
-// segments 0..s-1: X_1 = agg_0 (segment 0 starts from the true inflow),
-// X_{s'+1} = P_{s'} X_{s'} + agg_{s'}, with P = A^Ls, or A^Llast for the last
-// segment (last_short).
-template <int K>
-__device__ __forceinline__ void fold_segments(const double *agg, size_t seg_stride, size_t stride, int s,
-                                              const double *Aseg, const double *Alast, bool last_short,
-                                              double *X) {
+// Reflective mu > 0 head cell (cell 0 of segment 0) with distinct per-substep
+// inflows: the reference's algebra with cell_step_maybe_head (cell.hpp),
+// level by level.  Rare (one cell per line per pass): line constants are
+// read from memory here instead of being kept in registers.
+template <int S, int T>
+__device__ __forceinline__ void head_cell(const double *lcp, size_t stride, double hd,
+                                                    const double (&b)[T][4], double (&X)[T][SchemeDim<S>::K],
+                                                    double &oi, double &oo) {
+  LineConst L;
 #pragma unroll
-  for (int r = 0; r < K; ++r) X[r] = agg[r * stride];
-  for (int sp = 1; sp < s; ++sp) {
-    double t[K];
-    const double *P = (last_short && sp == s - 1) ? Alast : Aseg;
-    matvec_lt_g<K>(P, stride, X, t);
+  for (int n = 0; n < LC_COUNT; ++n) L.c[n] = lcp[n * stride];
 #pragma unroll
-    for (int r = 0; r < K; ++r) X[r] = t[r] + agg[sp * seg_stride + r * stride];
+  for (int t = 0; t < T; ++t) {
+    double a, c;
+    cell_step_maybe_head<S>(L, hd, false, oi, oo, X[t], true, b[t][3], a, c);
+    oi = a;
+    oo = c;
   }
 }
 
-// One 16-row chunk: correct the loaded rows by the pending term R Y (Y <- A Y
-// per cell), sweep them (MODE 0), store, and prefetch the next chunk's rows
-// into the registers just consumed.  PARTIAL: only the first nv cells are
-// real; the carried state after cell nv-1 is returned in Xcap.
-template <int S, int MODE, bool PARTIAL>
-__device__ __forceinline__ void sweep_chunk(const LineConst &L, double hd, bool neg, double (&ein)[kSweepCells],
-                                            double (&eout)[kSweepCells], double *X, bool corr, double *Y,
-                                            const double *A1, const double *Rm, bool head, double b3,
+// One chunk of C rows of a T-step pass: correct the loaded rows by the
+// pending term of the previous pass (the linear part of the T-level map run
+// on the correction state Z), advance every cell through T full steps with
+// the per-line affine map W (level t's outputs are level t+1's inputs),
+// store, and prefetch the next chunk's rows into the registers just
+// consumed.  LAST: the segment's final chunk -- no prefetch, and only its
+// first nv cells are real (X is left after cell nv-1).
+template <int S, int T, int MODE, int C, bool LAST>
+__device__ __forceinline__ void sweep_chunk(const double *W, double (&ein)[C], double (&eout)[C],
+                                            double (&X)[T][SchemeDim<S>::K], bool corr,
+                                            double (&Z)[T][SchemeDim<S>::K], bool head, double h_oi, double h_oo,
                                             __amdgpu_buffer_rsrc_t Rw, __amdgpu_buffer_rsrc_t Rn, int voff,
-                                            int row_bytes, int nv, double *Xcap) {
+                                            int row_bytes, int nv) {
   constexpr int K = SchemeDim<S>::K;
 #pragma unroll
-  for (int c = 0; c < kSweepCells; ++c) {
+  for (int c = 0; c < C; ++c) {
+    if (LAST && c >= nv) continue;  // wave-uniform: past the end of the segment
     double pin = ein[c], pout = eout[c];
-    if (corr) {  // e += R Y ; Y <- A Y   (deferred cross-segment correction)
+    if (corr) {  // e += (R' A'^k Y): the linear T-level chain on Z, zero data delta at level 0
+      double di = 0.0, dd = 0.0;
 #pragma unroll
-      for (int r = 0; r < K; ++r) {
-        pin += Rm[r] * Y[r];
-        pout += Rm[K + r] * Y[r];
+      for (int t = 0; t < T; ++t) {
+        double Zn[K], a, e;
+        map_apply<S, false>(W, Z[t], di, dd, Zn, a, e);
+#pragma unroll
+        for (int r = 0; r < K; ++r) Z[t][r] = Zn[r];
+        di = a;
+        dd = e;
       }
-      double t[K];
-#pragma unroll
-      for (int r = 0; r < K; ++r) {
-        double acc = 0.0;
-#pragma unroll
-        for (int cc = 0; cc <= r; ++cc) acc += A1[tri(r, cc)] * Y[cc];
-        t[r] = acc;
-      }
-#pragma unroll
-      for (int r = 0; r < K; ++r) Y[r] = t[r];
+      pin += di;
+      pout += dd;
     }
     double oi = pin, oo = pout;
     if constexpr (MODE == 0) {
-      if (c == 0)
-        cell_step_maybe_head<S>(L, hd, neg, pin, pout, X, head, b3, oi, oo);
-      else
-        cell_step<S>(L, hd, neg, pin, pout, X, oi, oo);
+      if (c == 0 && head) {  // reflective head cell, computed in the prologue
+        oi = h_oi;
+        oo = h_oo;
+      } else {
+#pragma unroll
+        for (int t = 0; t < T; ++t) {
+          double Xn[K], a, e;
+          map_apply<S, true>(W, X[t], oi, oo, Xn, a, e);
+#pragma unroll
+          for (int r = 0; r < K; ++r) X[t][r] = Xn[r];
+          oi = a;
+          oo = e;
+        }
+      }
     }
     row_store(Rw, voff, c * row_bytes, oi, oo);
-    const double2 v = row_load(Rn, voff, c * row_bytes);
-    ein[c] = v.x;
-    eout[c] = v.y;
-    if constexpr (PARTIAL) {
-      if (c == nv - 1) {
-#pragma unroll
-        for (int r = 0; r < K; ++r) Xcap[r] = X[r];
-      }
+    if constexpr (!LAST) {
+      const double2 v = row_load(Rn, voff, c * row_bytes);
+      ein[c] = v.x;
+      eout[c] = v.y;
     }
   }
 }
 
-template <int S, int MODE>
-__global__ __launch_bounds__(64) void sweep_segment_kernel(SegArgs a) {
+// One pass of T full steps over every line (MODE 0), or only the pending
+// correction of a T-step pass (MODE 1, finalize before a read-out).
+template <int S, int T, int MODE>
+__global__ __launch_bounds__(64) void sweep_block_kernel(SegArgs a) {
   constexpr int K = SchemeDim<S>::K;
-  constexpr int NT = K * (K + 1) / 2;
+  constexpr int KC = T * K;
+  constexpr int WN = map_count<S>();
+  constexpr int C = chunk_cells(S, T);
   const int lane = threadIdx.x;
   const size_t stride = static_cast<size_t>(a.Lpad);
   const int per_half = a.Q * a.Sg;
@@ -150,103 +193,104 @@ __global__ __launch_bounds__(64) void sweep_segment_kernel(SegArgs a) {
   const int k_begin = s * a.Ls;
   const int k_end = min(a.N, k_begin + a.Ls);
   if (k_begin >= k_end) return;
-  const bool last_short = (a.N - (a.Sg - 1) * a.Ls) != a.Ls;
+  if (MODE == 1 && s == 0) return;  // segment 0 is never provisional
+  const size_t seg_stride = static_cast<size_t>(KC) * stride;
 
-  // per-line propagators: A1 (one cell), R (state -> step-end nodes), A^Ls, A^Llast
-  const double *pr = a.prop + static_cast<size_t>(half) * kPropCount<K> * stride + ell;
-  const double *pA1 = pr;
-  const double *pR = pr + NT * stride;
-  const double *pAseg = pr + (NT + 2 * K) * stride;
-  const double *pAlast = pr + (2 * NT + 2 * K) * stride;
-  const size_t seg_stride = static_cast<size_t>(K) * stride;
-
-  // ---- pending correction of the previous step: Y = true incoming state ----
+  // ---- pending correction of the previous pass: Z = true incoming state ----
   const bool corr = a.pending && s > 0;
-  double Y[K], A1[NT], Rm[2 * K];
+  double Z[T][K];
 #pragma unroll
-  for (int r = 0; r < K; ++r) Y[r] = 0.0;
-  if (corr) {
-    const double *ag = a.agg_prev + static_cast<size_t>(half) * a.Sg * seg_stride + ell;
-    fold_segments<K>(ag, seg_stride, stride, s, pAseg, pAlast, false, Y);
+  for (int t = 0; t < T; ++t)
+#pragma unroll
+    for (int r = 0; r < K; ++r) Z[t][r] = 0.0;
+  if (corr) {  // folded by fold_kernel from the previous pass's aggregates
+    const double *y = a.yseg + (static_cast<size_t>(half) * (a.Sg + 1) + s) * seg_stride + ell;
+#pragma unroll
+    for (int t = 0; t < T; ++t)
+#pragma unroll
+      for (int r = 0; r < K; ++r) Z[t][r] = y[(t * K + r) * stride];
   }
-#pragma unroll
-  for (int e = 0; e < NT; ++e) A1[e] = pA1[e * stride];
-#pragma unroll
-  for (int e = 0; e < 2 * K; ++e) Rm[e] = pR[e * stride];
 
-  // ---- line constants, inflow ----
-  LineConst L;
-#pragma unroll
-  for (int n = 0; n < LC_COUNT; ++n) L.c[n] = a.lc[(static_cast<size_t>(half) * LC_COUNT + n) * stride + ell];
-  double X[K];
-  double b[4];
+  // ---- inflow and carried state ----
   const bool head_seg = (s == 0);
+  double b[T][4];
   {
     const double v = a.bdry[static_cast<size_t>(half) * stride + ell];
-    b[0] = b[1] = b[2] = b[3] = v;
+#pragma unroll
+    for (int t = 0; t < T; ++t) b[t][0] = b[t][1] = b[t][2] = b[t][3] = v;
   }
-  if (MODE == 0 && head_seg && !neg && a.reflective) {
-    // solver.cpp:677-684: mu > 0 inflow = the mirror mu < 0 line's outflow of this
-    // step, folded from that line's segment aggregates (previous launch)
-    const double *ag = a.agg_cur + ell;  // half 0, same l
-    const double *pr0 = a.prop + ell;    // half 0 propagators
-    double Xo[K];
-    fold_segments<K>(ag, seg_stride, stride, a.Sg, pr0 + (NT + 2 * K) * stride,
-                     pr0 + (2 * NT + 2 * K) * stride, last_short, Xo);
-    if constexpr (S == SCHEME_BDF2) {
-      b[0] = Xo[1];
-      b[1] = Xo[2];
-      b[2] = Xo[3];
-      b[3] = Xo[4];
-    } else {
-      b[0] = b[1] = b[2] = b[3] = Xo[K - 1];
+  const bool refl_head = MODE == 0 && head_seg && !neg && a.reflective;
+  if (refl_head) {
+    // solver.cpp:677-684: mu > 0 inflow = the mirror mu < 0 line's outflow of the
+    // same step, folded by fold_kernel from that line's aggregates of this pass
+    double Xo[KC];
+#pragma unroll
+    for (int r = 0; r < KC; ++r) Xo[r] = a.yrefl[r * stride + ell];
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+      if constexpr (S == SCHEME_BDF2) {
+        b[t][0] = Xo[t * K + 1];
+        b[t][1] = Xo[t * K + 2];
+        b[t][2] = Xo[t * K + 3];
+        b[t][3] = Xo[t * K + 4];
+      } else {
+        b[t][0] = b[t][1] = b[t][2] = b[t][3] = Xo[t * K + K - 1];
+      }
     }
   }
-  if (head_seg) {
-    head_state<S>(b, X);
-  } else {
+  double X[T][K];
 #pragma unroll
-    for (int r = 0; r < K; ++r) X[r] = 0.0;
+  for (int t = 0; t < T; ++t) {
+    if (head_seg) {
+      head_state<S>(b[t], X[t]);
+    } else {
+#pragma unroll
+      for (int r = 0; r < K; ++r) X[t][r] = 0.0;
+    }
   }
+  const double *lcp = a.lc + static_cast<size_t>(half) * LC_COUNT * stride + ell;
 
   // ---- stream the segment in 16-row chunks ----
   const int row_bytes = a.Lpad * static_cast<int>(sizeof(double2));
   const int voff = lane * static_cast<int>(sizeof(double2));
   const double2 *Eh = a.E + static_cast<size_t>(half) * a.Nrow * stride + q * 64;
-  auto rows = [&](int k0) { return rows_rsrc(Eh + static_cast<size_t>(k0) * stride, row_bytes); };
-  double ein[kSweepCells], eout[kSweepCells];
+  auto rows = [&](int k0) { return rows_rsrc<C>(Eh + static_cast<size_t>(k0) * stride, row_bytes); };
+  double ein[C], eout[C];
   {
     const __amdgpu_buffer_rsrc_t R0 = rows(k_begin);
 #pragma unroll
-    for (int c = 0; c < kSweepCells; ++c) {
+    for (int c = 0; c < C; ++c) {
       const double2 v = row_load(R0, voff, c * row_bytes);
       ein[c] = v.x;
       eout[c] = v.y;
     }
   }
-  double Xcap[K];
-  int k0 = k_begin;
-  for (; k0 + kSweepCells < k_end; k0 += kSweepCells) {  // full chunks with a successor
-    sweep_chunk<S, MODE, false>(L, a.hd, neg, ein, eout, X, corr, Y, A1, Rm, head_seg && k0 == 0, b[3], rows(k0),
-                                rows(k0 + kSweepCells), voff, row_bytes, kSweepCells, Xcap);
+  // reflective head cell (cell 0 of segment 0, distinct per-substep inflows)
+  double h_oi = 0.0, h_oo = 0.0;
+  if (refl_head) {
+    h_oi = ein[0];
+    h_oo = eout[0];
+    head_cell<S, T>(lcp, stride, a.hd, b, X, h_oi, h_oo);
   }
-  {  // last chunk (possibly partial); its "prefetch" re-reads its own rows (harmless)
-    const int nv = k_end - k0;
-    const __amdgpu_buffer_rsrc_t Rl = rows(k0);
-    if (nv == kSweepCells) {
-      sweep_chunk<S, MODE, false>(L, a.hd, neg, ein, eout, X, corr, Y, A1, Rm, head_seg && k0 == 0, b[3], Rl, Rl,
-                                  voff, row_bytes, nv, Xcap);
+
+  // ---- the line's cell map ----
+  double W[WN];
 #pragma unroll
-      for (int r = 0; r < K; ++r) Xcap[r] = X[r];
-    } else {
-      sweep_chunk<S, MODE, true>(L, a.hd, neg, ein, eout, X, corr, Y, A1, Rm, head_seg && k0 == 0, b[3], Rl, Rl,
-                                 voff, row_bytes, nv, Xcap);
-    }
+  for (int n = 0; n < WN; ++n) W[n] = a.map[(static_cast<size_t>(half) * WN + n) * stride + ell];
+
+  int k0 = k_begin;
+  for (; k0 + C < k_end; k0 += C) {  // full chunks with a successor
+    sweep_chunk<S, T, MODE, C, false>(W, ein, eout, X, corr, Z, refl_head && k0 == 0, h_oi, h_oo, rows(k0),
+                                      rows(k0 + C), voff, row_bytes, C);
   }
+  sweep_chunk<S, T, MODE, C, true>(W, ein, eout, X, corr, Z, refl_head && k0 == 0, h_oi, h_oo, rows(k0), rows(k0),
+                                   voff, row_bytes, k_end - k0);
   if constexpr (MODE == 0) {
     double *ag = a.agg_cur + static_cast<size_t>(half) * a.Sg * seg_stride + static_cast<size_t>(s) * seg_stride + ell;
 #pragma unroll
-    for (int r = 0; r < K; ++r) ag[r * stride] = Xcap[r];
+    for (int t = 0; t < T; ++t)
+#pragma unroll
+      for (int r = 0; r < K; ++r) ag[(t * K + r) * stride] = X[t][r];
   }
 }
 
@@ -333,27 +377,66 @@ __global__ void import_ends_kernel(double2 *E, const double *ends, LineMap m) {
 
 // phi, F, phi_plus (Gl, N) ColMajor: sequential sums over i in the
 // reference's order (solver.cpp:191-237), no FMA contraction.
+// A task is (cell c, chunk of gpc groups): the block reads the chunk's rows
+// of both halves coalesced (row k = N-1-c of half 0, k = c of half 1), stages
+// psi in LDS with one padding slot per group (conflict-free strided reads),
+// then 3 * gpc threads run the three sums, one per (group, moment).  The
+// weights live in LDS too (WL) unless M is too large for that.
+template <bool WL>
 __global__ void moments_kernel(const double2 *E, const double *mu, const double *wt, double *phi, double *F,
-                               double *phi_plus, LineMap m) {
+                               double *phi_plus, LineMap m, int gpc) {
 #pragma clang fp contract(off)
-  const size_t total = static_cast<size_t>(m.Gl) * m.N;
-  for (size_t o = blockIdx.x * static_cast<size_t>(blockDim.x) + threadIdx.x; o < total;
-       o += static_cast<size_t>(gridDim.x) * blockDim.x) {
-    const int g = static_cast<int>(o % m.Gl);
-    const int c = static_cast<int>(o / m.Gl);
-    double a = 0.0, f = 0.0, p = 0.0;
-    for (int i = 0; i < m.M; ++i) {
-      int half, ell, k;
-      m.map(i, g, c, half, ell, k);
-      const double2 v = E[m.at(half, k, ell)];
-      const double psi = 0.5 * (v.x + v.y);
-      a += wt[i] * psi;
-      f += mu[i] * wt[i] * psi;
-      if (i >= m.M / 2) p += wt[i] * psi;
+  extern __shared__ double mom_lds[];
+  const int H = m.H, HP = H + 1;
+  double *s0 = mom_lds, *s1 = mom_lds + gpc * HP;
+  const double *w = wt, *x = mu;
+  if constexpr (WL) {
+    double *lw = s1 + gpc * HP, *lx = lw + m.M;
+    for (int i = threadIdx.x; i < m.M; i += blockDim.x) {
+      lw[i] = wt[i];
+      lx[i] = mu[i];
     }
-    phi[o] = a;
-    F[o] = f;
-    phi_plus[o] = p;
+    w = lw;
+    x = lx;
+  }
+  const int nchunks = (m.Gl + gpc - 1) / gpc;
+  const size_t tasks = static_cast<size_t>(m.N) * nchunks;
+  for (size_t task = blockIdx.x; task < tasks; task += gridDim.x) {
+    const int c = static_cast<int>(task / nchunks);
+    const int g0 = static_cast<int>(task % nchunks) * gpc;
+    const int ng = min(gpc, m.Gl - g0);
+    const double2 *r0 = E + m.at(0, m.N - 1 - c, H * g0);
+    const double2 *r1 = E + m.at(1, c, H * g0);
+    for (int t = threadIdx.x; t < ng * H; t += blockDim.x) {
+      const int slot = (t / H) * HP + t % H;
+      const double2 a = r0[t], b = r1[t];
+      s0[slot] = 0.5 * (a.x + a.y);
+      s1[slot] = 0.5 * (b.x + b.y);
+    }
+    __syncthreads();
+    const int which = threadIdx.x / gpc, gl = threadIdx.x % gpc;
+    if (which < 3 && gl < ng) {
+      const double *p0 = s0 + gl * HP, *p1 = s1 + gl * HP;
+      double acc = 0.0;
+      if (which == 0) {
+#pragma unroll 8
+        for (int i = 0; i < H; ++i) acc += w[i] * p0[H - 1 - i];
+#pragma unroll 8
+        for (int i = H; i < m.M; ++i) acc += w[i] * p1[i - H];
+        phi[static_cast<size_t>(c) * m.Gl + g0 + gl] = acc;
+      } else if (which == 1) {
+#pragma unroll 8
+        for (int i = 0; i < H; ++i) acc += x[i] * w[i] * p0[H - 1 - i];
+#pragma unroll 8
+        for (int i = H; i < m.M; ++i) acc += x[i] * w[i] * p1[i - H];
+        F[static_cast<size_t>(c) * m.Gl + g0 + gl] = acc;
+      } else {
+#pragma unroll 8
+        for (int i = H; i < m.M; ++i) acc += w[i] * p1[i - H];
+        phi_plus[static_cast<size_t>(c) * m.Gl + g0 + gl] = acc;
+      }
+    }
+    __syncthreads();
   }
 }
 
@@ -381,29 +464,63 @@ __global__ void group_absorption_kernel(const double *phi, const double *sigma, 
 // ------------------------------------------------------------------------
 // launchers
 // ------------------------------------------------------------------------
-template <int S, int MODE>
-static hipError_t launch_seg_t(const SegArgs &a, int grid, hipStream_t st) {
-  hipLaunchKernelGGL((sweep_segment_kernel<S, MODE>), dim3(grid), dim3(64), 0, st, a);
+template <int S, int T>
+static hipError_t launch_t(bool finalize, const SegArgs &a, int grid, hipStream_t st) {
+  if (finalize)
+    hipLaunchKernelGGL((sweep_block_kernel<S, T, 1>), dim3(grid), dim3(64), 0, st, a);
+  else
+    hipLaunchKernelGGL((sweep_block_kernel<S, T, 0>), dim3(grid), dim3(64), 0, st, a);
   return hipGetLastError();
 }
 
-hipError_t launch_sweep(int scheme, bool finalize, const SegArgs &a, int grid, hipStream_t st) {
-  switch (scheme) {
-    case SCHEME_BE: return finalize ? launch_seg_t<SCHEME_BE, 1>(a, grid, st) : launch_seg_t<SCHEME_BE, 0>(a, grid, st);
-    case SCHEME_CN: return finalize ? launch_seg_t<SCHEME_CN, 1>(a, grid, st) : launch_seg_t<SCHEME_CN, 0>(a, grid, st);
-    default:
-      return finalize ? launch_seg_t<SCHEME_BDF2, 1>(a, grid, st) : launch_seg_t<SCHEME_BDF2, 0>(a, grid, st);
+template <int S>
+static hipError_t launch_s(int T, bool finalize, const SegArgs &a, int grid, hipStream_t st) {
+  switch (T) {
+    case 1: return launch_t<S, 1>(finalize, a, grid, st);
+    case 2: return launch_t<S, 2>(finalize, a, grid, st);
+    case 3: return launch_t<S, 3>(finalize, a, grid, st);
+    case 4: return launch_t<S, 4>(finalize, a, grid, st);
+    default: return hipErrorInvalidValue;
   }
 }
 
-hipError_t sweep_occupancy(int scheme, int *waves_per_cu) {
+hipError_t launch_sweep(int scheme, int T, bool finalize, const SegArgs &a, int grid, hipStream_t st) {
   switch (scheme) {
-    case SCHEME_BE:
-      return hipOccupancyMaxActiveBlocksPerMultiprocessor(waves_per_cu, sweep_segment_kernel<SCHEME_BE, 0>, 64, 0);
-    case SCHEME_CN:
-      return hipOccupancyMaxActiveBlocksPerMultiprocessor(waves_per_cu, sweep_segment_kernel<SCHEME_CN, 0>, 64, 0);
-    default:
-      return hipOccupancyMaxActiveBlocksPerMultiprocessor(waves_per_cu, sweep_segment_kernel<SCHEME_BDF2, 0>, 64, 0);
+    case SCHEME_BE: return launch_s<SCHEME_BE>(T, finalize, a, grid, st);
+    case SCHEME_CN: return launch_s<SCHEME_CN>(T, finalize, a, grid, st);
+    default: return launch_s<SCHEME_BDF2>(T, finalize, a, grid, st);
+  }
+}
+
+hipError_t launch_fold(int KC, const FoldArgs &f, hipStream_t st) {
+  const dim3 grid((f.nhalf * f.Lpad + 255) / 256), block(256);
+  switch (KC) {
+#define RT_FOLD_CASE(n) \
+  case n: hipLaunchKernelGGL(fold_kernel<n>, grid, block, 0, st, f); break;
+    RT_FOLD_CASE(1) RT_FOLD_CASE(2) RT_FOLD_CASE(3) RT_FOLD_CASE(4) RT_FOLD_CASE(5) RT_FOLD_CASE(6)
+    RT_FOLD_CASE(8) RT_FOLD_CASE(10) RT_FOLD_CASE(15) RT_FOLD_CASE(20)
+#undef RT_FOLD_CASE
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+template <int S>
+static hipError_t occupancy_s(int T, int *w) {
+  switch (T) {
+    case 1: return hipOccupancyMaxActiveBlocksPerMultiprocessor(w, sweep_block_kernel<S, 1, 0>, 64, 0);
+    case 2: return hipOccupancyMaxActiveBlocksPerMultiprocessor(w, sweep_block_kernel<S, 2, 0>, 64, 0);
+    case 3: return hipOccupancyMaxActiveBlocksPerMultiprocessor(w, sweep_block_kernel<S, 3, 0>, 64, 0);
+    case 4: return hipOccupancyMaxActiveBlocksPerMultiprocessor(w, sweep_block_kernel<S, 4, 0>, 64, 0);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+hipError_t sweep_occupancy(int scheme, int T, int *waves_per_cu) {
+  switch (scheme) {
+    case SCHEME_BE: return occupancy_s<SCHEME_BE>(T, waves_per_cu);
+    case SCHEME_CN: return occupancy_s<SCHEME_CN>(T, waves_per_cu);
+    default: return occupancy_s<SCHEME_BDF2>(T, waves_per_cu);
   }
 }
 
@@ -442,8 +559,18 @@ hipError_t launch_import_ends(double2 *E, const double *ends, const Geometry &g,
 
 hipError_t launch_moments(const double2 *E, const double *mu, const double *wt, double *phi, double *F,
                           double *phi_plus, const Geometry &g, hipStream_t st) {
-  hipLaunchKernelGGL(moments_kernel, dim3(grid_for(static_cast<size_t>(g.Gl) * g.N, 256)), dim3(256), 0, st, E, mu, wt,
-                     phi, F, phi_plus, make_map(g));
+  const LineMap m = make_map(g);
+  // groups per task: ~512 lines, at most 85 so that 3 sums per group fit 256 threads
+  const int gpc = max(1, min(85, 512 / m.H));
+  const size_t lds = static_cast<size_t>(2) * gpc * (m.H + 1) * sizeof(double);
+  const size_t ldsw = lds + static_cast<size_t>(2) * m.M * sizeof(double);
+  if (lds > 65536) return hipErrorInvalidValue;  // M > ~8000
+  const size_t tasks = static_cast<size_t>(g.N) * ((g.Gl + gpc - 1) / gpc);
+  const dim3 grid(static_cast<unsigned>(tasks < 8192 ? tasks : 8192));
+  if (ldsw <= 65536)
+    hipLaunchKernelGGL(moments_kernel<true>, grid, dim3(256), ldsw, st, E, mu, wt, phi, F, phi_plus, m, gpc);
+  else
+    hipLaunchKernelGGL(moments_kernel<false>, grid, dim3(256), lds, st, E, mu, wt, phi, F, phi_plus, m, gpc);
   return hipGetLastError();
 }
 

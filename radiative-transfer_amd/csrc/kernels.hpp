@@ -10,21 +10,30 @@ namespace rtamd {
 #define RT_SWEEP_CELLS 16     // cells per wave held in registers
 #endif
 
-constexpr int kSweepCells = RT_SWEEP_CELLS;             // rows per chunk held in registers
+constexpr int kSweepCells = RT_SWEEP_CELLS;             // segment lengths are multiples of this
+// rows per chunk held in registers (prefetch depth) for scheme S fusing T steps:
+// the longer T, the more compute per row and the fewer registers to spare
+#ifndef RT_CHUNK_BDF2_T2
+#define RT_CHUNK_BDF2_T2 8
+#endif
+constexpr int chunk_cells(int S, int T) { return (S == 3 && T >= 2) ? RT_CHUNK_BDF2_T2 : RT_SWEEP_CELLS; }
 constexpr int kSweepTile = 64;                          // cells are padded to whole tiles of 64 rows
 
-// Per-line propagator block: A (one cell, packed lower-triangular), R (2 x K,
-// state -> step-end nodes), A^Ls and A^Llast (segment propagators).
-template <int K>
-constexpr int kPropCount = 3 * (K * (K + 1) / 2) + 2 * K;
+constexpr int kMaxTimeBlock = 4;                        // full steps fused per pass (template range)
+
+// Segment propagators of the T-level combined state (KC = T K, packed lower
+// triangle of NTC = KC (KC + 1) / 2 entries each): A_T^Ls, A_T^Llast.
+constexpr int prop_count(int K, int T) { return (T * K) * (T * K + 1); }
 
 struct SegArgs {
   double2 *E;                 // [2][Nrow][Lpad] (e_in, e_out)
-  const double *lc;           // [2][LC_COUNT][Lpad] line constants
-  const double *prop;         // [2][kPropCount<K>][Lpad] propagators
+  const double *map;          // [2][map_count<S>][Lpad] per-line affine cell map (cell.hpp)
+  const double *lc;           // [2][LC_COUNT][Lpad] line constants (reflective head cell only)
+  const double *prop;         // [2][prop_count(K, T)][Lpad] segment propagators for this T
   const double *bdry;         // [2][Lpad] inflow value per line (non-reflective)
-  const double *agg_prev;     // [2][Sg][K][Lpad] segment aggregates of the previous step
-  double *agg_cur;            // [2][Sg][K][Lpad] segment aggregates of this step
+  const double *yseg;         // [2][Sg+1][T K][Lpad] true incoming state per segment (fold_kernel)
+  const double *yrefl;        // [T K][Lpad] this pass's mu < 0 line outflow state (reflective)
+  double *agg_cur;            // [2][Sg][T K][Lpad] segment aggregates of this pass
   int N, Nrow, Lpad, Q;
   int Sg, Ls;                 // segments per line, cells per segment (multiple of 16)
   int half0;                  // first half swept by this launch (grid covers 1 or 2 halves)
@@ -33,12 +42,21 @@ struct SegArgs {
   double hd;                  // dx / 2
 };
 
+struct FoldArgs {
+  const double *agg;          // [2][Sg][KC][Lpad]
+  const double *prop;         // [2][prop_half][Lpad]: A^Ls then A^Llast (packed)
+  double *y;                  // [2][Sg+1][KC][Lpad], or [KC][Lpad] when only_last
+  int prop_half, Sg, Lpad, half0, nhalf, last_short, only_last;
+};
+
 struct Geometry {
   int M, Gl, N, Nrow, Lpad;
 };
 
-hipError_t launch_sweep(int scheme, bool finalize, const SegArgs &a, int grid, hipStream_t st);
-hipError_t sweep_occupancy(int scheme, int *waves_per_cu);
+// One pass of T full steps (finalize: only the pending correction of a T-step pass).
+hipError_t launch_sweep(int scheme, int T, bool finalize, const SegArgs &a, int grid, hipStream_t st);
+hipError_t sweep_occupancy(int scheme, int T, int *waves_per_cu);
+hipError_t launch_fold(int KC, const FoldArgs &f, hipStream_t st);
 hipError_t launch_init_state(double2 *E, const double *lineB, const Geometry &g, hipStream_t st);
 hipError_t launch_export_psi(const double2 *E, double *psi, const Geometry &g, hipStream_t st);
 hipError_t launch_export_ends(const double2 *E, double *ends, const Geometry &g, hipStream_t st);

@@ -43,12 +43,14 @@ struct rt_solver {
   bool equilibrium_done = false;
   int g_lo = 0, g_hi = 0, Gl = 0, H = 0, Lh = 0, Lpad = 0, Q = 0, J = 0;
   int scheme = SCHEME_BDF2, K = 5;
+  int T = 1;                     // full steps fused per pass (time block)
+  int Tp = 0;                    // steps of the pass whose correction is pending
   int Sg = 1, Ls = 16;           // segments per line and cells per segment
   int device = 0;
   hipStream_t stream = nullptr;
   // device state
-  DeviceBuf E, lc, prop, bdry, agg[2], lineB, muwt, mom, rows, sigma;
-  int agg_cur = 0;               // aggregates of the last step live in agg[agg_cur ^ 1]
+  DeviceBuf E, map, lc, prop[kMaxTimeBlock + 1], bdry, agg[2], yseg, yrefl, lineB, muwt, mom, rows, sigma;
+  int agg_cur = 0;               // aggregates of the last pass live in agg[agg_cur ^ 1]
   bool pending = false;          // E holds provisional segments (correction outstanding)
   // profiling
   bool profiling = false;
@@ -75,6 +77,19 @@ static rt_status fail(rt_solver *s, rt_status st, const std::string &msg) {
     hipError_t e_ = (expr);                                                                     \
     if (e_ != hipSuccess) return fail((s), RT_ERR_DEVICE, std::string(#expr ": ") + hipGetErrorString(e_)); \
   } while (0)
+
+// Full steps fused per HBM pass by default (rt_set_time_block changes it).
+// Measured on SL (profiles/): BDF2 43.9 / 25.0 / 23.3 / 19.8 ms per step at
+// T = 1 / 2 / 3 / 4 -- one pass is HBM-bound at T = 1 and FP64-bound beyond.
+static int default_time_block(int) { return kMaxTimeBlock; }
+
+static int map_count_of(int scheme) {
+  switch (scheme) {
+    case SCHEME_BE: return map_count<SCHEME_BE>();
+    case SCHEME_CN: return map_count<SCHEME_CN>();
+    default: return map_count<SCHEME_BDF2>();
+  }
+}
 
 static hipError_t dalloc(DeviceBuf &b, size_t bytes) {
   b.bytes = bytes;
@@ -208,23 +223,57 @@ static LineConst line_constants(const rt_solver &s, int i, int g) {
   return L;
 }
 
-// Linear parts of the cell map (cell.hpp): X' = A X + ..., step-end nodes
-// (oin, oout) = R X + ...; evaluated with the affine constants and the cell
-// data set to zero.  R is 2 x K (row 0: e_in, row 1: e_out).
+// The per-line affine cell map (cell.hpp, map_apply): coefficients from
+// cell_step<S> on unit inputs (constants and data zeroed), constants from
+// cell_step<S> on zero inputs.  Every coefficient outside the structural
+// pattern must come out exactly zero; false otherwise.
 template <int S>
-static void propagator(const LineConst &Lin, double hd, bool neg, double *A /* K*K row-major */,
-                       double *R /* 2*K */) {
+static bool cell_map(const LineConst &Lin, double hd, bool neg, double *W) {
   constexpr int K = SchemeDim<S>::K;
-  LineConst L = Lin;
-  L.c[LC_SC] = 0.0;
-  for (int col = 0; col < K; ++col) {
+  double dense[K + 1][K + 3];  // [row][input 0..K+1, constant K+2]
+  for (int col = 0; col <= K + 2; ++col) {
+    LineConst L = Lin;
+    if (col != K + 2) L.c[LC_SC] = 0.0;
     double X[K] = {};
-    X[col] = 1.0;
+    double pin = 0.0, pout = 0.0;
+    if (col < K) X[col] = 1.0;
+    if (col == K) pin = 1.0;
+    if (col == K + 1) pout = 1.0;
     double oi, oo;
-    cell_step<S>(L, hd, neg, 0.0, 0.0, X, oi, oo);
-    for (int r = 0; r < K; ++r) A[r * K + col] = X[r];
-    R[col] = oi;
-    R[K + col] = oo;
+    cell_step<S>(L, hd, neg, pin, pout, X, oi, oo);
+    for (int r = 0; r < K; ++r) dense[r][col] = X[r];
+    dense[K][col] = oi;
+    if (X[K - 1] != oo) return false;  // oout is X'[K-1]
+  }
+  for (int r = 0; r <= K; ++r)
+    for (int col = 0; col <= K + 2; ++col) {
+      const bool copy = map_copy_row0<S>() && r == 0;
+      const bool used = !copy && (col == K + 2 || map_dep<S>(r, col));
+      if (used) {
+        W[map_slot<S>(r, col)] = dense[r][col];
+      } else if (dense[r][col] != (copy && col == K + 1 ? 1.0 : 0.0)) {
+        return false;
+      }
+    }
+  return true;
+}
+
+// Linear part of the T-level combined map on the carried state (X_0..X_{T-1}):
+// level t's outputs are level t+1's data (KC x KC row-major, lower triangular).
+template <int S>
+static void combined_linear(const double *W, int T, double *A) {
+  constexpr int K = SchemeDim<S>::K;
+  const int KC = T * K;
+  for (int col = 0; col < KC; ++col) {
+    double di = 0.0, dd = 0.0;
+    for (int t = 0; t < T; ++t) {
+      double X[K] = {}, Xn[K], a, e;
+      if (col / K == t) X[col % K] = 1.0;
+      map_apply<S, false>(W, X, di, dd, Xn, a, e);
+      for (int r = 0; r < K; ++r) A[(t * K + r) * KC + col] = Xn[r];
+      di = a;
+      dd = e;
+    }
   }
 }
 
@@ -278,42 +327,49 @@ static void line_inflow(const rt_solver &s, std::vector<double> &bd) {
   (void)M;
 }
 
-static rt_status setup_lines(rt_solver *s) {
-  const int K = s->K, NT = K * (K + 1) / 2, NP = 3 * NT + 2 * K;
+template <int S>
+static rt_status setup_lines_s(rt_solver *s) {
+  constexpr int K = SchemeDim<S>::K, WN = map_count<S>();
   const double hd = 0.5 * (s->p.X / s->p.N);
   const long long L_last = s->p.N - static_cast<long long>(s->Sg - 1) * s->Ls;
-  std::vector<double> lc(static_cast<size_t>(2) * LC_COUNT * s->Lpad, 0.0);
-  std::vector<double> pr(static_cast<size_t>(2) * NP * s->Lpad, 0.0);
-  std::vector<double> lineB(static_cast<size_t>(2) * s->Lpad, 0.0);
-  std::vector<double> A(K * K), R(2 * K), Aseg(K * K), Alast(K * K);
+  const size_t Lp = s->Lpad;
+  std::vector<double> lc(2 * LC_COUNT * Lp, 0.0), map(2 * WN * Lp, 0.0), lineB(2 * Lp, 0.0);
+  std::vector<std::vector<double>> pr(kMaxTimeBlock + 1);
+  for (int T = 1; T <= kMaxTimeBlock; ++T) pr[T].assign(2 * prop_count(K, T) * Lp, 0.0);
+  std::vector<double> A, Aseg, Alast;
+  double W[WN];
   for (int half = 0; half < 2; ++half)
     for (int gl = 0; gl < s->Gl; ++gl)
       for (int ip = 0; ip < s->H; ++ip) {
         const int i = line_direction(s->H, half, ip), g = s->g_lo + gl;
-        const int ell = ip + s->H * gl;
+        const size_t ell = ip + static_cast<size_t>(s->H) * gl;
         const LineConst L = line_constants(*s, i, g);
-        for (int n = 0; n < LC_COUNT; ++n) lc[(static_cast<size_t>(half) * LC_COUNT + n) * s->Lpad + ell] = L.c[n];
-        lineB[static_cast<size_t>(half) * s->Lpad + ell] = s->gt.B[g];
-        const bool neg = half == 0;
-        switch (s->scheme) {
-          case SCHEME_BE: propagator<SCHEME_BE>(L, hd, neg, A.data(), R.data()); break;
-          case SCHEME_CN: propagator<SCHEME_CN>(L, hd, neg, A.data(), R.data()); break;
-          default: propagator<SCHEME_BDF2>(L, hd, neg, A.data(), R.data()); break;
+        for (int n = 0; n < LC_COUNT; ++n) lc[(half * LC_COUNT + n) * Lp + ell] = L.c[n];
+        lineB[half * Lp + ell] = s->gt.B[g];
+        if (!cell_map<S>(L, hd, half == 0, W))
+          return fail(s, RT_ERR_PARAM, "cell map: a structurally zero coefficient is not zero");
+        for (int n = 0; n < WN; ++n) map[(half * WN + n) * Lp + ell] = W[n];
+        for (int T = 1; T <= kMaxTimeBlock; ++T) {
+          const int KC = T * K, NTC = KC * (KC + 1) / 2;
+          A.assign(KC * KC, 0.0);
+          Aseg.resize(KC * KC);
+          Alast.resize(KC * KC);
+          combined_linear<S>(W, T, A.data());
+          matpow(KC, A.data(), s->Ls, Aseg.data());
+          matpow(KC, A.data(), L_last, Alast.data());
+          double *dst = pr[T].data() + half * prop_count(K, T) * Lp + ell;
+          for (int r = 0; r < KC; ++r)
+            for (int c = 0; c <= r; ++c) {
+              dst[tri(r, c) * Lp] = Aseg[r * KC + c];
+              dst[(NTC + tri(r, c)) * Lp] = Alast[r * KC + c];
+            }
         }
-        matpow(K, A.data(), s->Ls, Aseg.data());
-        matpow(K, A.data(), L_last, Alast.data());
-        double *dst = pr.data() + static_cast<size_t>(half) * NP * s->Lpad + ell;
-        for (int r = 0; r < K; ++r)
-          for (int c = 0; c <= r; ++c) {
-            dst[static_cast<size_t>(tri(r, c)) * s->Lpad] = A[r * K + c];
-            dst[static_cast<size_t>(NT + 2 * K + tri(r, c)) * s->Lpad] = Aseg[r * K + c];
-            dst[static_cast<size_t>(2 * NT + 2 * K + tri(r, c)) * s->Lpad] = Alast[r * K + c];
-          }
-        for (int e = 0; e < 2 * K; ++e) dst[static_cast<size_t>(NT + e) * s->Lpad] = R[e];
       }
   rt_status st;
   if ((st = upload(s, s->lc, lc.data(), lc.size() * sizeof(double)))) return st;
-  if ((st = upload(s, s->prop, pr.data(), pr.size() * sizeof(double)))) return st;
+  if ((st = upload(s, s->map, map.data(), map.size() * sizeof(double)))) return st;
+  for (int T = 1; T <= kMaxTimeBlock; ++T)
+    if ((st = upload(s, s->prop[T], pr[T].data(), pr[T].size() * sizeof(double)))) return st;
   if ((st = upload(s, s->lineB, lineB.data(), lineB.size() * sizeof(double)))) return st;
   std::vector<double> sig(s->Gl);
   for (int gl = 0; gl < s->Gl; ++gl) sig[gl] = s->gt.rho[s->g_lo + gl] * s->gt.kappa[s->g_lo + gl];
@@ -324,6 +380,14 @@ static rt_status setup_lines(rt_solver *s) {
   if ((st = upload(s, s->muwt, muwt.data(), muwt.size() * sizeof(double)))) return st;
   HIP_TRY(s, hipStreamSynchronize(s->stream));  // host vectors die at return
   return RT_OK;
+}
+
+static rt_status setup_lines(rt_solver *s) {
+  switch (s->scheme) {
+    case SCHEME_BE: return setup_lines_s<SCHEME_BE>(s);
+    case SCHEME_CN: return setup_lines_s<SCHEME_CN>(s);
+    default: return setup_lines_s<SCHEME_BDF2>(s);
+  }
 }
 
 static rt_status upload_inflow(rt_solver *s) {
@@ -400,7 +464,8 @@ extern "C" rt_status rt_create_from_params(const rt_params *pin, int g_lo, int g
 
   // segments: enough waves to fill the chip (occupancy x CUs), Ls a multiple of the chunk
   int waves_per_cu = 0;
-  HIP_TRY(h, sweep_occupancy(h->scheme, &waves_per_cu));
+  h->T = default_time_block(h->scheme);
+  HIP_TRY(h, sweep_occupancy(h->scheme, h->T, &waves_per_cu));
   waves_per_cu = std::max(1, std::min(waves_per_cu, 32));
   {
     const long long target = static_cast<long long>(prop.multiProcessorCount) * waves_per_cu;
@@ -415,15 +480,19 @@ extern "C" rt_status rt_create_from_params(const rt_params *pin, int g_lo, int g
   if (2LL * h->Q * h->Sg >= (1LL << 31)) return fail(nullptr, RT_ERR_PARAM, "too many lines for one handle: shard the groups");
 
   const size_t Lp = h->Lpad;
-  const int K = h->K, NP = 3 * (K * (K + 1) / 2) + 2 * K;
+  const int K = h->K;
   hipError_t e = hipSuccess;
   const size_t Nrow = static_cast<size_t>(h->J) * kSweepTile;  // cells padded to whole tiles
   if (!e) e = dalloc(h->E, sizeof(double2) * 2 * Nrow * Lp);
   if (!e) e = dalloc(h->lc, sizeof(double) * 2 * LC_COUNT * Lp);
-  if (!e) e = dalloc(h->prop, sizeof(double) * 2 * NP * Lp);
+  if (!e) e = dalloc(h->map, sizeof(double) * 2 * map_count_of(h->scheme) * Lp);
+  for (int T = 1; T <= kMaxTimeBlock; ++T)
+    if (!e) e = dalloc(h->prop[T], sizeof(double) * 2 * prop_count(K, T) * Lp);
   if (!e) e = dalloc(h->bdry, sizeof(double) * 2 * Lp);
-  if (!e) e = dalloc(h->agg[0], sizeof(double) * 2 * h->Sg * K * Lp);
-  if (!e) e = dalloc(h->agg[1], sizeof(double) * 2 * h->Sg * K * Lp);
+  if (!e) e = dalloc(h->agg[0], sizeof(double) * 2 * h->Sg * kMaxTimeBlock * K * Lp);
+  if (!e) e = dalloc(h->agg[1], sizeof(double) * 2 * h->Sg * kMaxTimeBlock * K * Lp);
+  if (!e) e = dalloc(h->yseg, sizeof(double) * 2 * (h->Sg + 1) * kMaxTimeBlock * K * Lp);
+  if (!e) e = dalloc(h->yrefl, sizeof(double) * kMaxTimeBlock * K * Lp);
   if (!e) e = dalloc(h->lineB, sizeof(double) * 2 * Lp);
   if (!e) e = dalloc(h->muwt, sizeof(double) * 2 * q.M);
   if (!e) e = dalloc(h->mom, sizeof(double) * 3 * h->Gl * static_cast<size_t>(q.N));
@@ -483,13 +552,15 @@ static rt_status fold_events(rt_solver *s) {
   return RT_OK;
 }
 
-static SegArgs seg_args(rt_solver *s) {
+static SegArgs seg_args(rt_solver *s, int T) {
   SegArgs a{};
   a.E = static_cast<double2 *>(s->E.p);
+  a.map = static_cast<const double *>(s->map.p);
   a.lc = static_cast<const double *>(s->lc.p);
-  a.prop = static_cast<const double *>(s->prop.p);
+  a.prop = static_cast<const double *>(s->prop[T].p);
   a.bdry = static_cast<const double *>(s->bdry.p);
-  a.agg_prev = static_cast<const double *>(s->agg[s->agg_cur ^ 1].p);
+  a.yseg = static_cast<const double *>(s->yseg.p);
+  a.yrefl = static_cast<const double *>(s->yrefl.p);
   a.agg_cur = static_cast<double *>(s->agg[s->agg_cur].p);
   a.N = s->p.N;
   a.Nrow = s->J * kSweepTile;
@@ -504,45 +575,88 @@ static SegArgs seg_args(rt_solver *s) {
   return a;
 }
 
-static rt_status enqueue_steps(rt_solver *s, int nsteps) {
-  const int per_half = s->Q * s->Sg;
-  for (int n = 0; n < nsteps; ++n) {
-    SegArgs a = seg_args(s);
-    hipEvent_t e0 = nullptr, e1 = nullptr;
-    if (s->profiling) {
-      if (s->ev_used + 2 > s->ev_pool.size()) {
-        rt_status st = fold_events(s);  // drain the pool when it is full
-        if (st) return st;
-      }
-      e0 = s->ev_pool[s->ev_used++];
-      e1 = s->ev_pool[s->ev_used++];
-      HIP_TRY(s, hipEventRecord(e0, s->stream));
-    }
-    if (a.reflective) {  // mu > 0 heads need this step's mu < 0 outflow: two launches
-      a.half0 = 0;
-      HIP_TRY(s, launch_sweep(s->scheme, false, a, per_half, s->stream));
-      a.half0 = 1;
-      HIP_TRY(s, launch_sweep(s->scheme, false, a, per_half, s->stream));
-    } else {
-      HIP_TRY(s, launch_sweep(s->scheme, false, a, 2 * per_half, s->stream));
-    }
-    if (s->profiling) {
-      HIP_TRY(s, hipEventRecord(e1, s->stream));
-      ++s->profiled;
-    }
-    ++s->launches;
-    s->pending = s->Sg > 1;
-    s->agg_cur ^= 1;
-  }
+// Fold segment aggregates of a T-step pass into true incoming states:
+// previous pass (agg_prev) -> yseg for the pending correction, or this pass's
+// mu < 0 half (agg_cur) -> yrefl for the reflective mu > 0 heads.
+static rt_status enqueue_fold(rt_solver *s, int T, bool reflective_outflow) {
+  FoldArgs f{};
+  const int slot = reflective_outflow ? s->agg_cur : (s->agg_cur ^ 1);
+  f.agg = static_cast<const double *>(s->agg[slot].p);
+  f.prop = static_cast<const double *>(s->prop[T].p);
+  f.y = static_cast<double *>(reflective_outflow ? s->yrefl.p : s->yseg.p);
+  f.prop_half = prop_count(s->K, T);
+  f.Sg = s->Sg;
+  f.Lpad = s->Lpad;
+  f.half0 = 0;
+  f.nhalf = reflective_outflow ? 1 : 2;
+  f.last_short = (s->p.N - (s->Sg - 1) * s->Ls) != s->Ls;
+  f.only_last = reflective_outflow ? 1 : 0;
+  HIP_TRY(s, launch_fold(T * s->K, f, s->stream));
   return RT_OK;
 }
 
-// Apply the outstanding cross-segment correction in place (before any read).
+// Apply the outstanding cross-segment correction in place (before any read,
+// or before a pass with a different time block).
 static rt_status finalize(rt_solver *s) {
   if (!s->pending) return RT_OK;
-  SegArgs a = seg_args(s);
-  HIP_TRY(s, launch_sweep(s->scheme, true, a, 2 * s->Q * s->Sg, s->stream));
+  rt_status st = enqueue_fold(s, s->Tp, false);
+  if (st) return st;
+  SegArgs a = seg_args(s, s->Tp);
+  HIP_TRY(s, launch_sweep(s->scheme, s->Tp, true, a, 2 * s->Q * s->Sg, s->stream));
   s->pending = false;
+  return RT_OK;
+}
+
+// One pass of T full steps.
+static rt_status enqueue_pass(rt_solver *s, int T) {
+  if (s->pending && s->Tp != T) {
+    rt_status st = finalize(s);
+    if (st) return st;
+  }
+  const int per_half = s->Q * s->Sg;
+  SegArgs a = seg_args(s, T);
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  if (s->profiling) {
+    if (s->ev_used + 2 > s->ev_pool.size()) {
+      rt_status st = fold_events(s);  // drain the pool when it is full
+      if (st) return st;
+    }
+    e0 = s->ev_pool[s->ev_used++];
+    e1 = s->ev_pool[s->ev_used++];
+    HIP_TRY(s, hipEventRecord(e0, s->stream));
+  }
+  if (s->pending) {
+    rt_status st = enqueue_fold(s, T, false);
+    if (st) return st;
+  }
+  if (a.reflective) {  // mu > 0 heads need this pass's mu < 0 outflow: two launches
+    a.half0 = 0;
+    HIP_TRY(s, launch_sweep(s->scheme, T, false, a, per_half, s->stream));
+    rt_status st = enqueue_fold(s, T, true);
+    if (st) return st;
+    a.half0 = 1;
+    HIP_TRY(s, launch_sweep(s->scheme, T, false, a, per_half, s->stream));
+  } else {
+    HIP_TRY(s, launch_sweep(s->scheme, T, false, a, 2 * per_half, s->stream));
+  }
+  if (s->profiling) {
+    HIP_TRY(s, hipEventRecord(e1, s->stream));
+    ++s->profiled;
+  }
+  ++s->launches;
+  s->pending = s->Sg > 1;
+  s->Tp = T;
+  s->agg_cur ^= 1;
+  return RT_OK;
+}
+
+// nsteps full steps: passes of T steps, then one pass of the remainder.
+static rt_status enqueue_steps(rt_solver *s, int nsteps) {
+  for (int n = 0; n + s->T <= nsteps; n += s->T) {
+    rt_status st = enqueue_pass(s, s->T);
+    if (st) return st;
+  }
+  if (nsteps % s->T) return enqueue_pass(s, nsteps % s->T);
   return RT_OK;
 }
 
@@ -800,12 +914,26 @@ extern "C" rt_status rt_get_sweep_time(rt_solver *s, double *total_ms, long long
   return RT_OK;
 }
 
-extern "C" rt_status rt_sweep_traffic(rt_solver *s, double *bytes_per_step, double *updates_per_step) {
+extern "C" rt_status rt_sweep_traffic(rt_solver *s, double *bytes_per_launch, double *updates_per_step) {
   if (!s) return fail(nullptr, RT_ERR_ARG, "rt_sweep_traffic: NULL handle");
   const double lines_cells = static_cast<double>(s->p.M) * s->Gl * s->p.N;
-  // one pass: read (e_in, e_out) and write them back, per cell x line
-  if (bytes_per_step) *bytes_per_step = 32.0 * lines_cells;
+  // one pass (of T steps): read (e_in, e_out) and write them back, per cell x line
+  if (bytes_per_launch) *bytes_per_launch = 32.0 * lines_cells;
   if (updates_per_step) *updates_per_step = (s->p.ts_method == 3 ? 4.0 : 1.0) * lines_cells;
+  return RT_OK;
+}
+
+extern "C" rt_status rt_set_time_block(rt_solver *s, int steps_per_pass) {
+  if (!s) return fail(nullptr, RT_ERR_ARG, "rt_set_time_block: NULL handle");
+  if (steps_per_pass < 1 || steps_per_pass > kMaxTimeBlock)
+    return fail(s, RT_ERR_ARG, "rt_set_time_block: steps per pass must be 1.." + std::to_string(kMaxTimeBlock));
+  s->T = steps_per_pass;
+  return RT_OK;
+}
+
+extern "C" rt_status rt_get_time_block(rt_solver *s, int *steps_per_pass) {
+  if (!s || !steps_per_pass) return fail(s, RT_ERR_ARG, "rt_get_time_block: bad argument");
+  *steps_per_pass = s->T;
   return RT_OK;
 }
 

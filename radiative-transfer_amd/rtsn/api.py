@@ -101,6 +101,8 @@ def lib():
         L.rt_get_sweep_time.argtypes = [vp, dp, C.POINTER(C.c_longlong)]
         L.rt_sweep_traffic.argtypes = [vp, dp, dp]
         L.rt_sweep_geometry.argtypes = [vp, C.POINTER(C.c_int), C.POINTER(C.c_longlong)]
+        L.rt_set_time_block.argtypes = [vp, C.c_int]
+        L.rt_get_time_block.argtypes = [vp, C.POINTER(C.c_int)]
         L.rt_status_string.argtypes = [C.c_int]
         L.rt_status_string.restype = C.c_char_p
         L.rt_last_error.argtypes = [vp]
@@ -356,10 +358,22 @@ class Solver:
         _check(lib().rt_get_sweep_time(self._h, C.byref(ms), C.byref(n)), "rt_get_sweep_time", self._h)
         return ms.value, n.value
 
+    @property
+    def time_block(self) -> int:
+        """Full steps advanced per pass over HBM (rt_set_time_block)."""
+        t = C.c_int()
+        _check(lib().rt_get_time_block(self._h, C.byref(t)), "rt_get_time_block", self._h)
+        return t.value
+
+    @time_block.setter
+    def time_block(self, steps_per_pass: int):
+        _check(lib().rt_set_time_block(self._h, int(steps_per_pass)), "rt_set_time_block", self._h)
+
     def sweep_traffic(self):
         b = C.c_double()
         u = C.c_double()
         _check(lib().rt_sweep_traffic(self._h, C.byref(b), C.byref(u)), "rt_sweep_traffic", self._h)
+        # (algorithmic bytes per pass = per profiled launch, updates per full step)
         return b.value, u.value
 
     def sweep_geometry(self):

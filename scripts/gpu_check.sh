@@ -1,9 +1,14 @@
+# Full GPU check (run from the repo root on the GPU box): every -m gpu test,
+# smoke(), a kernel-trace profile of the bench and the bench line itself.
 set -o pipefail
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 600 python -m pytest tests/test_gpu_parity.py -q -m gpu > gpurun_out/gpu_tests.log 2>&1 || { tail -30 gpurun_out/gpu_tests.log; exit 1; }
+TAG=${TAG:-r01}
+timeout -k 10 900 python -m pytest tests -q -m gpu > gpurun_out/gpu_tests.log 2>&1 || { tail -40 gpurun_out/gpu_tests.log; exit 1; }
 tail -3 gpurun_out/gpu_tests.log
-timeout -k 10 300 python bench.py --cells 100000 --no-cpu-baseline > gpurun_out/bench_small.log 2>&1 || { tail -20 gpurun_out/bench_small.log; exit 1; }
-tail -2 gpurun_out/bench_small.log
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { tail -20 gpurun_out/smoke.log; exit 1; }
+tail -2 gpurun_out/smoke.log
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_kt -o run --output-format csv -- python3 bench.py --no-cpu-baseline > gpurun_out/prof_kt.log 2>&1 || { tail -20 gpurun_out/prof_kt.log; exit 1; }
+cp gpurun_out/prof_kt/run_kernel_stats.csv gpurun_out/${TAG}_kernel_stats.csv
 timeout -k 10 600 python bench.py > gpurun_out/bench_full.log 2>&1 || { tail -20 gpurun_out/bench_full.log; exit 1; }
-tail -2 gpurun_out/bench_full.log
+tail -1 gpurun_out/bench_full.log | tee gpurun_out/${TAG}_bench.json

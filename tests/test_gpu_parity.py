@@ -90,9 +90,12 @@ def test_gray_test_on_gpu(rtsn_mod):
         assert abs(F.max()) < 1e-6
 
 
+@pytest.mark.parametrize("tb", [1, 3, 4])
 @pytest.mark.parametrize("ts", [1, 2, 3])
 @pytest.mark.parametrize("bc_left,bc_right", [(0, 0), (1, 1), (2, 1), (2, 0), (1, 2), (0, 1)])
-def test_schemes_and_boundaries(rtsn_mod, oracle_mod, ts, bc_left, bc_right):
+def test_schemes_and_boundaries(rtsn_mod, oracle_mod, ts, bc_left, bc_right, tb):
+    """4 steps with tb full steps per pass: tb = 3 runs a 3-step pass, a
+    finalize and a 1-step pass."""
     p = load(oracle_mod, "template.prm", ts_method=ts, bc_left=bc_left, bc_right=bc_right, max_timesteps=4,
              M=6, N=150, V=2.0)
     p["dx"] = p["X"] / p["N"]
@@ -100,18 +103,21 @@ def test_schemes_and_boundaries(rtsn_mod, oracle_mod, ts, bc_left, bc_right):
     orc = oracle_mod.OracleSolver(p)
     orc.solve()
     with rtsn_mod.Solver(to_rt(p)) as gpu:
+        gpu.time_block = tb
         gpu.solve()
         compare_all(gpu, orc)
 
 
+@pytest.mark.parametrize("tb", [1, 3])
 @pytest.mark.parametrize("N", [1, 2, 15, 16, 17, 63, 64, 65, 128, 777, 4096 + 5])
-def test_ragged_cell_counts(rtsn_mod, oracle_mod, N):
+def test_ragged_cell_counts(rtsn_mod, oracle_mod, N, tb):
     """Tiles are 64 cells (4 waves x 16): partial waves, partial tiles, multi-tile lines."""
-    p = load(oracle_mod, "multi_group_equilibrium.prm", N=N, max_timesteps=2, bc_left=2)
+    p = load(oracle_mod, "multi_group_equilibrium.prm", N=N, max_timesteps=2 * tb, bc_left=2)
     p["dx"] = p["X"] / N
     orc = oracle_mod.OracleSolver(p)
     orc.solve()
     with rtsn_mod.Solver(to_rt(p)) as gpu:
+        gpu.time_block = tb
         gpu.solve()
         compare_all(gpu, orc)
 
@@ -129,10 +135,13 @@ def test_line_counts(rtsn_mod, oracle_mod, M, G):
         compare_all(gpu, orc)
 
 
-def test_random_state_long_lines(rtsn_mod, oracle_mod):
-    """One BDF2 step from a random state (seed 20261015, psi0 = B U[0.5,1.5))
-    on 20k-cell lines: exercises the decoupled look-back across ~300 tiles."""
-    p = load(oracle_mod, "llnl_slab_test.prm", N=20000, M=4, max_timesteps=1, use_correction=1, V=5.994)
+@pytest.mark.parametrize("tb,steps", [(1, 1), (1, 3), (2, 4), (3, 3), (3, 5), (4, 4)])
+def test_random_state_long_lines(rtsn_mod, oracle_mod, tb, steps):
+    """BDF2 steps from a random state (seed 20261015, psi0 = B U[0.5,1.5))
+    on 20k-cell lines cut into many segments: the deferred cross-segment
+    correction across passes of tb fused steps (and the finalize between a
+    tb-step pass and a shorter remainder pass)."""
+    p = load(oracle_mod, "llnl_slab_test.prm", N=20000, M=4, max_timesteps=steps, use_correction=1, V=5.994)
     p["dx"] = p["X"] / p["N"]
     p["psi_source"] = np.zeros((p["M"], p["G"]))
     lo, hi = 10, 26
@@ -143,9 +152,39 @@ def test_random_state_long_lines(rtsn_mod, oracle_mod):
     orc.set_ends(ends)
     orc.solve()
     with rtsn_mod.Solver(to_rt(p), g_lo=lo, g_hi=hi) as gpu:
+        gpu.time_block = tb
         gpu.set_ends(ends)
         gpu.solve()
         compare_all(gpu, orc)
+
+
+def test_time_block_switching(rtsn_mod, oracle_mod):
+    """advance() calls with changing time blocks and read-outs in between
+    equal one oracle run of the same total number of steps."""
+    p = load(oracle_mod, "llnl_slab_test.prm", N=3000, M=8, use_correction=1, V=5.994, bc_left=2)
+    p["dx"] = p["X"] / p["N"]
+    p["psi_source"] = np.full((p["M"], p["G"]), 0.25)
+    plan = [(3, 2), (2, 3), (4, 4), (1, 1), (3, 6)]  # (time block, steps)
+    p["max_timesteps"] = sum(n for _, n in plan)
+    orc = oracle_mod.OracleSolver(p)
+    orc.solve()
+    with rtsn_mod.Solver(to_rt(p)) as gpu:
+        for k, (tb, n) in enumerate(plan):
+            gpu.time_block = tb
+            gpu.advance(n)
+            if k == 2:
+                gpu.psi()  # a read-out in the middle finalizes the pending correction
+        gpu.synchronize()
+        compare_all(gpu, orc)
+
+
+def test_time_block_range(rtsn_mod):
+    d = rtsn_mod.params_default()
+    with rtsn_mod.Solver(d) as s:
+        for bad in (0, 5, -1):
+            with pytest.raises(rtsn_mod.RtError) as e:
+                s.time_block = bad
+            assert e.value.status == 8
 
 
 def test_group_shards_equal_full_run(rtsn_mod, oracle_mod):
