@@ -2,7 +2,7 @@
 """Sweep throughput benchmark (BASELINE.json metric).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--variant v0|corr]
-                    [--scaling weak|strong] [--no-cpu-baseline]
+                    [--scaling weak|strong] [--time-block T] [--no-cpu-baseline]
 
 Workload (SURVEY.md §8(d) "SL"): 1D slab X = 0.4 cm, N = 1e6 cells, S64
 Gauss-Legendre (M = 64), 128 energy groups per GPU on a log grid 0.001-30 keV
@@ -10,8 +10,8 @@ with kappa_g resampled from the LLNL capped table, rho = 1, T = 1 keV, BDF2
 (ts_method = 3), dt = 1e-3, vacuum boundaries; V = 0 (variant v0) or
 V = 5.994 with the v/c correction (variant corr).  A "step" is one full BDF2
 step (4 substeps) of every cell x angle x group of the GPU's groups, i.e.
-4 M G N cell-angle-group updates, computed in fp64 by the fused HIP sweep
-(one kernel launch per step).  State is resident in HBM before timing.
+4 M G N cell-angle-group updates, computed in fp64 by the fused HIP sweep.
+State is resident in HBM before timing.
 
 Multi-GPU: one process per GPU (torch.distributed.run), groups sharded across
 ranks with no collective in the data path (groups are independent for the
@@ -21,12 +21,18 @@ barrier + device synchronise on both sides of the K timed steps, max over
 ranks.  After timing, the group-summed absorption rate is all-reduced over
 RCCL once (the north_star group-sum hook) and checked.
 
-roofline: algorithmic bytes of one sweep launch (16 B read + 16 B write per
-cell x line: the fused step moves the state once) / the sweep kernel's mean
-duration from HIP events recorded around each launch on the library's
-stream; peak 8.0 TB/s (MI355X_MICROARCH.md).  traffic: per-launch HBM bytes
-from rocprofv3 PMC passes recorded in profiles/pmc_<variant>.json
-(FETCH_SIZE x 2 + WRITE_SIZE, the gfx950 correction), null if absent.
+Time blocking: one sweep launch (a "pass") advances T full steps (default
+T = 4, --time-block), reading and writing the state once.
+
+roofline: per pass, the algorithmic HBM bytes (16 B read + 16 B write per
+cell x line) and the algorithmic FP64 flops (2 per coefficient of the
+per-line affine cell map, 28 FMAs per cell x line x BDF2 step, times T) over
+the sweep kernel's mean duration from HIP events recorded around each
+launch on the library's stream.  At T = 1 the pass is HBM-bound (peak
+8.0 TB/s, MI355X_MICROARCH.md); at T > 1 it is FP64-bound (peak 78.6
+TFLOP/s spec).  traffic: per-launch HBM bytes from rocprofv3 PMC passes
+recorded in profiles/pmc_<variant>_t<T>.json (FETCH_SIZE x 2 + WRITE_SIZE,
+the gfx950 correction), null if absent.
 cpu_baseline: the C oracle (a single-threaded port of the reference's
 algorithm) on a bounded sample of the same workload.
 """
@@ -46,6 +52,7 @@ import numpy as np  # noqa: E402
 
 METRIC = "cell·angle·group updates/sec (Sn sweep) + BDF2 steps/sec, llnl_slab_test"
 HBM_PEAK = 8.0e12
+FP64_PEAK = 78.6e12  # MI355X FP64 vector spec (256 CU x 4 SIMD x 16 FMA lanes x 2 x 2.4 GHz); measured 71 TF: profiles/r01_fp64_peak.txt
 KAPPA_TABLE = REPO / "tests" / "golden" / "prm" / "llnl_slab_test_group_kappa_a.txt"
 
 
@@ -112,6 +119,7 @@ def run_rank(solver, p: dict, steps: int, warmup: int, world: int, device, shard
 
     G_total, g_lo, g_hi = shard_info
     bytes_launch, upd_step = solver.sweep_traffic()  # per pass (T fused steps), per full step
+    flops_launch = solver.sweep_flops()               # algorithmic FP64 flops per pass
     tb = getattr(solver, "time_block", 1)
     wg, tiles = solver.sweep_geometry()
 
@@ -153,7 +161,9 @@ def run_rank(solver, p: dict, steps: int, warmup: int, world: int, device, shard
 
     value = total_updates / wall_max
     ms_per_step = 1e3 * wall_max / steps
-    achieved = bytes_launch / (kern_avg_ms * 1e-3) if kern_avg_ms > 0 else 0.0
+    kern_s = kern_avg_ms * 1e-3
+    achieved = bytes_launch / kern_s if kern_s > 0 else 0.0
+    achieved_fl = flops_launch / kern_s if kern_s > 0 else 0.0
     line = {
         "metric": METRIC,
         "value": value,
@@ -177,16 +187,24 @@ def run_rank(solver, p: dict, steps: int, warmup: int, world: int, device, shard
             "parallelism": f"group shards x{world}, no data-path collective",
             "sweep_workgroups": wg, "tiles_per_step": tiles,
         },
+        # One pass moves the state once (HBM-bound at T = 1) and runs T steps of
+        # the cell map (FP64-bound at T > 1): the bound is the
+        # roofline the pass sits on; both are reported.
         "roofline": {
-            "bound": "hbm",
-            "achieved": achieved / 1e9,
-            "peak": HBM_PEAK / 1e9,
-            "unit": "GB/s",
-            "frac": achieved / HBM_PEAK,
+            "bound": "fp64" if tb > 1 else "hbm",
+            "achieved": achieved_fl / 1e12 if tb > 1 else achieved / 1e9,
+            "peak": FP64_PEAK / 1e12 if tb > 1 else HBM_PEAK / 1e9,
+            "unit": "TFLOP/s" if tb > 1 else "GB/s",
+            "frac": achieved_fl / FP64_PEAK if tb > 1 else achieved / HBM_PEAK,
             "traffic": None,
             "kernel": f"sweep_block_kernel<3, {tb}, 0>",
             "kernel_ms": kern_avg_ms,
+            "algorithmic_flops_per_launch": flops_launch,
             "algorithmic_bytes_per_launch": bytes_launch,
+            "hbm": {"achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+                    "frac": achieved / HBM_PEAK},
+            "fp64": {"achieved": achieved_fl / 1e12, "peak": FP64_PEAK / 1e12, "unit": "TFLOP/s",
+                     "frac": achieved_fl / FP64_PEAK},
         },
         "absorption_allreduce_finite": finite,
     }
@@ -196,8 +214,10 @@ def run_rank(solver, p: dict, steps: int, warmup: int, world: int, device, shard
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=4)
-    ap.add_argument("--warmup", type=int, default=1)
+    # defaults are whole passes of the default time block (4 steps per pass), so that the
+    # timed region is 2 steady-state passes (each applying the previous pass's correction)
+    ap.add_argument("--steps", type=int, default=8)
+    ap.add_argument("--warmup", type=int, default=4)
     ap.add_argument("--variant", choices=["v0", "corr"], default="v0")
     ap.add_argument("--scaling", choices=["weak", "strong"], default="weak")
     ap.add_argument("--groups", type=int, default=128, help="groups per GPU (weak) or in total (strong)")

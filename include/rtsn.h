@@ -144,6 +144,10 @@ rt_status rt_get_sweep_time(rt_solver *s, double *total_ms, long long *launches)
  * the state is read and written once) and updates (cell x angle x group x
  * substep) per full step, for the handle's groups. */
 rt_status rt_sweep_traffic(rt_solver *s, double *bytes_per_launch, double *updates_per_step);
+/* Algorithmic FP64 flops of one pass: 2 per coefficient of the per-line
+ * affine cell map (BDF2 28, CN 8, BE 6 FMAs per cell x line x step) times T
+ * steps; the cross-segment correction is parallelisation overhead, not counted. */
+rt_status rt_sweep_flops(rt_solver *s, double *flops_per_launch);
 /* Time blocking: full steps advanced per pass over HBM (1..4).  Results do
  * not depend on it beyond rounding; rt_advance(n) runs n / T passes of T
  * steps and one pass of n % T. */

@@ -923,6 +923,16 @@ extern "C" rt_status rt_sweep_traffic(rt_solver *s, double *bytes_per_launch, do
   return RT_OK;
 }
 
+extern "C" rt_status rt_sweep_flops(rt_solver *s, double *flops_per_launch) {
+  if (!s || !flops_per_launch) return fail(s, RT_ERR_ARG, "rt_sweep_flops: bad argument");
+  // one FMA per structural coefficient of the cell map (cell.hpp): the
+  // affine constants are the accumulators' initial values, not extra ops
+  const int rows = s->K + 1 - (s->scheme == SCHEME_BE ? 0 : 1);
+  const double fma = static_cast<double>(map_count_of(s->scheme) - rows);
+  *flops_per_launch = 2.0 * fma * s->T * static_cast<double>(s->p.M) * s->Gl * s->p.N;
+  return RT_OK;
+}
+
 extern "C" rt_status rt_set_time_block(rt_solver *s, int steps_per_pass) {
   if (!s) return fail(nullptr, RT_ERR_ARG, "rt_set_time_block: NULL handle");
   if (steps_per_pass < 1 || steps_per_pass > kMaxTimeBlock)

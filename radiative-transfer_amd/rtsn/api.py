@@ -101,6 +101,7 @@ def lib():
         L.rt_get_sweep_time.argtypes = [vp, dp, C.POINTER(C.c_longlong)]
         L.rt_sweep_traffic.argtypes = [vp, dp, dp]
         L.rt_sweep_geometry.argtypes = [vp, C.POINTER(C.c_int), C.POINTER(C.c_longlong)]
+        L.rt_sweep_flops.argtypes = [vp, dp]
         L.rt_set_time_block.argtypes = [vp, C.c_int]
         L.rt_get_time_block.argtypes = [vp, C.POINTER(C.c_int)]
         L.rt_status_string.argtypes = [C.c_int]
@@ -375,6 +376,12 @@ class Solver:
         _check(lib().rt_sweep_traffic(self._h, C.byref(b), C.byref(u)), "rt_sweep_traffic", self._h)
         # (algorithmic bytes per pass = per profiled launch, updates per full step)
         return b.value, u.value
+
+    def sweep_flops(self) -> float:
+        """Algorithmic FP64 flops of one pass (rt_sweep_flops)."""
+        f = C.c_double()
+        _check(lib().rt_sweep_flops(self._h, C.byref(f)), "rt_sweep_flops", self._h)
+        return f.value
 
     def sweep_geometry(self):
         wg = C.c_int()

@@ -62,6 +62,9 @@ class OracleShard:
         Gl = self.g_hi - self.g_lo
         return 32.0 * self.p["M"] * Gl * self.p["N"], 4.0 * self.p["M"] * Gl * self.p["N"]
 
+    def sweep_flops(self):
+        return 56.0 * self.p["M"] * (self.g_hi - self.g_lo) * self.p["N"]
+
     def sweep_geometry(self):
         return 1, 1
 
