@@ -129,6 +129,7 @@ def run_rank(solver, p: dict, steps: int, warmup: int, world: int, device, shard
         if device.type == "cuda":
             torch.cuda.synchronize(device)
 
+    t_start = time.perf_counter()
     solver.advance(warmup)
     solver.synchronize()
     barrier()
@@ -140,6 +141,12 @@ def run_rank(solver, p: dict, steps: int, warmup: int, world: int, device, shard
     wall = time.perf_counter() - t0
     kern_ms, nlaunch = solver.sweep_time()
     solver.set_profiling(False)
+    # outside the timed region: finish every queued step (pipeline drain / correction)
+    t1 = time.perf_counter()
+    solver.finish()
+    solver.synchronize()
+    barrier()
+    t_end = time.perf_counter()
 
     # group-summed absorption all-reduce, outside the timed region
     absorb = torch.zeros(p["N"], dtype=torch.float64, device=device)
@@ -147,7 +154,7 @@ def run_rank(solver, p: dict, steps: int, warmup: int, world: int, device, shard
     solver.synchronize()
     if world > 1:
         dist.all_reduce(absorb)
-    finite = bool(torch.isfinite(absorb).all().item())
+    finite = bool(torch.isfinite(absorb).all().item())  # see DESIGN.md §5: the reference's BDF2 grows ~10^3 per step on SL
 
     t = torch.tensor([wall, kern_ms / max(nlaunch, 1)], dtype=torch.float64, device=device)
     if world > 1:
@@ -178,6 +185,10 @@ def run_rank(solver, p: dict, steps: int, warmup: int, world: int, device, shard
         "dtype": "f64",
         "data": "synthetic",
         "bdf2_steps_per_s": 1e3 / ms_per_step,
+        "schedule": {"pipelined": bool(getattr(solver, "pipeline", False)), "steps_per_pass": tb,
+                     "warmup_steps": warmup, "drain_ms": 1e3 * (t_end - t1),
+                     "end_to_end_ms": 1e3 * (t_end - t_start),
+                     "end_to_end_updates_per_s": upd_step * (warmup + steps) / (t_end - t_start)},
         "config": {
             "workload": f"SL slab: N={p['N']} cells x S{p['M']} x {g_hi - g_lo} groups per GPU "
                         f"({G_total} total), BDF2 dt=1e-3, V={p['V']}, use_correction=1, vacuum BCs",
@@ -206,7 +217,7 @@ def run_rank(solver, p: dict, steps: int, warmup: int, world: int, device, shard
             "fp64": {"achieved": achieved_fl / 1e12, "peak": FP64_PEAK / 1e12, "unit": "TFLOP/s",
                      "frac": achieved_fl / FP64_PEAK},
         },
-        "absorption_allreduce_finite": finite,
+        "state_finite": finite,
     }
     return line, absorb
 
@@ -217,13 +228,16 @@ def main():
     # defaults are whole passes of the default time block (4 steps per pass), so that the
     # timed region is 2 steady-state passes (each applying the previous pass's correction)
     ap.add_argument("--steps", type=int, default=8)
-    ap.add_argument("--warmup", type=int, default=4)
+    ap.add_argument("--warmup", type=int, default=-1,
+                    help="untimed steps before timing (default: fill the pipeline plus one pass)")
     ap.add_argument("--variant", choices=["v0", "corr"], default="v0")
     ap.add_argument("--scaling", choices=["weak", "strong"], default="weak")
     ap.add_argument("--groups", type=int, default=128, help="groups per GPU (weak) or in total (strong)")
     ap.add_argument("--cells", type=int, default=1_000_000)
     ap.add_argument("--time-block", type=int, default=0,
                     help="full steps fused per HBM pass (0: the library default)")
+    ap.add_argument("--schedule", choices=["pipelined", "aligned"], default="pipelined",
+                    help="staggered segments (exact starts) or aligned segments with deferred correction")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
@@ -244,7 +258,16 @@ def main():
     solver = rtsn.Solver(p, device=local, g_lo=info[1], g_hi=info[2])
     if args.time_block:
         solver.time_block = args.time_block
-    line, _ = run_rank(solver, p, args.steps, args.warmup, world, device, info, args.scaling)
+    solver.pipeline = args.schedule == "pipelined"
+    tb = solver.time_block
+    warmup = args.warmup
+    if warmup < 0:  # pipeline depth (segments per line) passes: fill + one steady pass
+        warmup = solver.sweep_geometry()[1] * tb if solver.pipeline else tb
+    # whole passes only: steps are launched in passes of tb (a remainder would be
+    # queued until the next read-out, outside the timed region)
+    steps = -(-args.steps // tb) * tb
+    warmup = -(-warmup // tb) * tb
+    line, _ = run_rank(solver, p, steps, warmup, world, device, info, args.scaling)
     line["roofline"]["traffic"] = load_traffic(args.variant, solver.time_block)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(args.variant)

@@ -104,8 +104,14 @@ void rt_destroy(rt_solver *s);
  * for BDF2), preceded by computeEquilibriumSources when use_mg_equilib.
  * Synchronous. */
 rt_status rt_solve(rt_solver *s);
-/* Asynchronous: enqueue nsteps full steps on the handle's stream. */
+/* Asynchronous: enqueue nsteps full steps on the handle's stream (with the
+ * pipelined schedule, whole passes are launched now and a remainder of fewer
+ * than T steps when the state is next read). */
 rt_status rt_advance(rt_solver *s, int nsteps);
+/* Enqueue what brings the stored state exactly to the requested time --
+ * pipeline drain, queued remainder steps, pending correction.  Every
+ * read-out does this implicitly; asynchronous. */
+rt_status rt_finish(rt_solver *s);
 rt_status rt_synchronize(rt_solver *s);
 /* hipStream_t of the handle, as void*. */
 void *rt_stream(rt_solver *s);
@@ -152,6 +158,14 @@ rt_status rt_sweep_flops(rt_solver *s, double *flops_per_launch);
  * not depend on it beyond rounding; rt_advance(n) runs n / T passes of T
  * steps and one pass of n % T. */
 rt_status rt_set_time_block(rt_solver *s, int steps_per_pass);
+/* Pipelined schedule (default on): the segments of a line run at staggered
+ * time levels, one pass apart, so each starts from its upwind neighbour's
+ * exact exit state -- no cross-segment correction.  Steps are queued and
+ * launched as whole passes; the pipeline fills over the first launches and
+ * drains when a result is read (or rt_solve returns).  Off: every pass moves
+ * all segments together and corrects them in the next pass. */
+rt_status rt_set_pipeline(rt_solver *s, int on);
+rt_status rt_get_pipeline(rt_solver *s, int *on);
 rt_status rt_get_time_block(rt_solver *s, int *steps_per_pass);
 /* Sweep geometry actually used: waves launched per step (one per line group
  * and segment) and segments per line. */

@@ -148,7 +148,7 @@ __device__ __forceinline__ void sweep_chunk(const double *W, double (&ein)[C], d
       pout += dd;
     }
     double oi = pin, oo = pout;
-    if constexpr (MODE == 0) {
+    if constexpr (MODE != 1) {
       if (c == 0 && head) {  // reflective head cell, computed in the prologue
         oi = h_oi;
         oo = h_oo;
@@ -173,8 +173,12 @@ __device__ __forceinline__ void sweep_chunk(const double *W, double (&ein)[C], d
   }
 }
 
-// One pass of T full steps over every line (MODE 0), or only the pending
-// correction of a T-step pass (MODE 1, finalize before a read-out).
+// One pass of T full steps over every line (MODE 0), only the pending
+// correction of a T-step pass (MODE 1, finalize before a read-out), or one
+// launch of the pipelined schedule (MODE 2): segments at staggered time
+// levels, each one pass behind its upwind neighbour, so every segment starts
+// from the exact incoming state that neighbour published in the previous
+// launch -- no provisional state, no correction.
 template <int S, int T, int MODE>
 __global__ __launch_bounds__(64) void sweep_block_kernel(SegArgs a) {
   constexpr int K = SchemeDim<S>::K;
@@ -183,11 +187,32 @@ __global__ __launch_bounds__(64) void sweep_block_kernel(SegArgs a) {
   constexpr int C = chunk_cells(S, T);
   const int lane = threadIdx.x;
   const size_t stride = static_cast<size_t>(a.Lpad);
-  const int per_half = a.Q * a.Sg;
-  const int half = a.half0 + static_cast<int>(blockIdx.x) / per_half;
-  const int rem = static_cast<int>(blockIdx.x) % per_half;
-  const int s = rem / a.Q;  // segment (wave-uniform)
-  const int q = rem - s * a.Q;
+  int half, s, q, slot = 0;
+  if constexpr (MODE == 2) {
+    // active chain positions [pos_lo, pos_lo + npos): two chains of Sg segments
+    // (one per half), or one chain of 2 Sg (half 0 then half 1) when reflective
+    int pos;
+    if (a.reflective) {
+      pos = a.pos_lo + static_cast<int>(blockIdx.x) / a.Q;
+      q = static_cast<int>(blockIdx.x) % a.Q;
+      half = pos / a.Sg;
+      s = pos % a.Sg;
+    } else {
+      const int per_half = a.Q * a.npos;
+      half = static_cast<int>(blockIdx.x) / per_half;
+      const int rem = static_cast<int>(blockIdx.x) % per_half;
+      pos = a.pos_lo + rem / a.Q;
+      q = rem % a.Q;
+      s = pos;
+    }
+    slot = (a.pass_lo - (pos - a.pos_lo)) & 1;  // aggregates of pass p live in slot p & 1
+  } else {
+    const int per_half = a.Q * a.Sg;
+    half = a.half0 + static_cast<int>(blockIdx.x) / per_half;
+    const int rem = static_cast<int>(blockIdx.x) % per_half;
+    s = rem / a.Q;  // segment (wave-uniform)
+    q = rem - s * a.Q;
+  }
   const int ell = q * 64 + lane;
   const bool neg = half == 0;
   const int k_begin = s * a.Ls;
@@ -195,9 +220,10 @@ __global__ __launch_bounds__(64) void sweep_block_kernel(SegArgs a) {
   if (k_begin >= k_end) return;
   if (MODE == 1 && s == 0) return;  // segment 0 is never provisional
   const size_t seg_stride = static_cast<size_t>(KC) * stride;
+  const size_t half_stride = static_cast<size_t>(a.Sg) * seg_stride;
 
   // ---- pending correction of the previous pass: Z = true incoming state ----
-  const bool corr = a.pending && s > 0;
+  const bool corr = MODE != 2 && a.pending && s > 0;
   double Z[T][K];
 #pragma unroll
   for (int t = 0; t < T; ++t)
@@ -219,13 +245,15 @@ __global__ __launch_bounds__(64) void sweep_block_kernel(SegArgs a) {
 #pragma unroll
     for (int t = 0; t < T; ++t) b[t][0] = b[t][1] = b[t][2] = b[t][3] = v;
   }
-  const bool refl_head = MODE == 0 && head_seg && !neg && a.reflective;
+  const bool refl_head = MODE != 1 && head_seg && !neg && a.reflective;
   if (refl_head) {
     // solver.cpp:677-684: mu > 0 inflow = the mirror mu < 0 line's outflow of the
-    // same step, folded by fold_kernel from that line's aggregates of this pass
+    // same steps: folded by fold_kernel from that line's aggregates of this pass
+    // (MODE 0), or the aggregate its last segment published (MODE 2)
+    const double *src = MODE == 2 ? a.aggs[slot] + (a.Sg - 1) * seg_stride + ell : a.yrefl + ell;
     double Xo[KC];
 #pragma unroll
-    for (int r = 0; r < KC; ++r) Xo[r] = a.yrefl[r * stride + ell];
+    for (int r = 0; r < KC; ++r) Xo[r] = src[r * stride];
 #pragma unroll
     for (int t = 0; t < T; ++t) {
       if constexpr (S == SCHEME_BDF2) {
@@ -239,14 +267,20 @@ __global__ __launch_bounds__(64) void sweep_block_kernel(SegArgs a) {
     }
   }
   double X[T][K];
+  if (head_seg) {
 #pragma unroll
-  for (int t = 0; t < T; ++t) {
-    if (head_seg) {
-      head_state<S>(b[t], X[t]);
-    } else {
+    for (int t = 0; t < T; ++t) head_state<S>(b[t], X[t]);
+  } else if (MODE == 2) {  // exact: the upwind segment's exit state, published last launch
+    const double *up = a.aggs[slot] + half * half_stride + (s - 1) * seg_stride + ell;
+#pragma unroll
+    for (int t = 0; t < T; ++t)
+#pragma unroll
+      for (int r = 0; r < K; ++r) X[t][r] = up[(t * K + r) * stride];
+  } else {
+#pragma unroll
+    for (int t = 0; t < T; ++t)
 #pragma unroll
       for (int r = 0; r < K; ++r) X[t][r] = 0.0;
-    }
   }
   const double *lcp = a.lc + static_cast<size_t>(half) * LC_COUNT * stride + ell;
 
@@ -285,8 +319,8 @@ __global__ __launch_bounds__(64) void sweep_block_kernel(SegArgs a) {
   }
   sweep_chunk<S, T, MODE, C, true>(W, ein, eout, X, corr, Z, refl_head && k0 == 0, h_oi, h_oo, rows(k0), rows(k0),
                                    voff, row_bytes, k_end - k0);
-  if constexpr (MODE == 0) {
-    double *ag = a.agg_cur + static_cast<size_t>(half) * a.Sg * seg_stride + static_cast<size_t>(s) * seg_stride + ell;
+  if constexpr (MODE != 1) {
+    double *ag = (MODE == 2 ? a.aggs[slot] : a.agg_cur) + half * half_stride + static_cast<size_t>(s) * seg_stride + ell;
 #pragma unroll
     for (int t = 0; t < T; ++t)
 #pragma unroll
@@ -465,30 +499,32 @@ __global__ void group_absorption_kernel(const double *phi, const double *sigma, 
 // launchers
 // ------------------------------------------------------------------------
 template <int S, int T>
-static hipError_t launch_t(bool finalize, const SegArgs &a, int grid, hipStream_t st) {
-  if (finalize)
-    hipLaunchKernelGGL((sweep_block_kernel<S, T, 1>), dim3(grid), dim3(64), 0, st, a);
-  else
-    hipLaunchKernelGGL((sweep_block_kernel<S, T, 0>), dim3(grid), dim3(64), 0, st, a);
+static hipError_t launch_t(int mode, const SegArgs &a, int grid, hipStream_t st) {
+  switch (mode) {
+    case SWEEP_PASS: hipLaunchKernelGGL((sweep_block_kernel<S, T, 0>), dim3(grid), dim3(64), 0, st, a); break;
+    case SWEEP_FINALIZE: hipLaunchKernelGGL((sweep_block_kernel<S, T, 1>), dim3(grid), dim3(64), 0, st, a); break;
+    case SWEEP_PIPELINED: hipLaunchKernelGGL((sweep_block_kernel<S, T, 2>), dim3(grid), dim3(64), 0, st, a); break;
+    default: return hipErrorInvalidValue;
+  }
   return hipGetLastError();
 }
 
 template <int S>
-static hipError_t launch_s(int T, bool finalize, const SegArgs &a, int grid, hipStream_t st) {
+static hipError_t launch_s(int T, int mode, const SegArgs &a, int grid, hipStream_t st) {
   switch (T) {
-    case 1: return launch_t<S, 1>(finalize, a, grid, st);
-    case 2: return launch_t<S, 2>(finalize, a, grid, st);
-    case 3: return launch_t<S, 3>(finalize, a, grid, st);
-    case 4: return launch_t<S, 4>(finalize, a, grid, st);
+    case 1: return launch_t<S, 1>(mode, a, grid, st);
+    case 2: return launch_t<S, 2>(mode, a, grid, st);
+    case 3: return launch_t<S, 3>(mode, a, grid, st);
+    case 4: return launch_t<S, 4>(mode, a, grid, st);
     default: return hipErrorInvalidValue;
   }
 }
 
-hipError_t launch_sweep(int scheme, int T, bool finalize, const SegArgs &a, int grid, hipStream_t st) {
+hipError_t launch_sweep(int scheme, int T, int mode, const SegArgs &a, int grid, hipStream_t st) {
   switch (scheme) {
-    case SCHEME_BE: return launch_s<SCHEME_BE>(T, finalize, a, grid, st);
-    case SCHEME_CN: return launch_s<SCHEME_CN>(T, finalize, a, grid, st);
-    default: return launch_s<SCHEME_BDF2>(T, finalize, a, grid, st);
+    case SCHEME_BE: return launch_s<SCHEME_BE>(T, mode, a, grid, st);
+    case SCHEME_CN: return launch_s<SCHEME_CN>(T, mode, a, grid, st);
+    default: return launch_s<SCHEME_BDF2>(T, mode, a, grid, st);
   }
 }
 

@@ -34,11 +34,13 @@ struct SegArgs {
   const double *yseg;         // [2][Sg+1][T K][Lpad] true incoming state per segment (fold_kernel)
   const double *yrefl;        // [T K][Lpad] this pass's mu < 0 line outflow state (reflective)
   double *agg_cur;            // [2][Sg][T K][Lpad] segment aggregates of this pass
+  double *aggs[2];            // pipelined: aggregates of pass p in aggs[p & 1], [2][Sg][T K][Lpad]
   int N, Nrow, Lpad, Q;
   int Sg, Ls;                 // segments per line, cells per segment (multiple of 16)
   int half0;                  // first half swept by this launch (grid covers 1 or 2 halves)
   int reflective;             // bc_left == 2
   int pending;                // the stored state is provisional: apply the correction
+  int pos_lo, npos, pass_lo;  // pipelined: active chain positions and the pass of the first
   double hd;                  // dx / 2
 };
 
@@ -53,8 +55,12 @@ struct Geometry {
   int M, Gl, N, Nrow, Lpad;
 };
 
-// One pass of T full steps (finalize: only the pending correction of a T-step pass).
-hipError_t launch_sweep(int scheme, int T, bool finalize, const SegArgs &a, int grid, hipStream_t st);
+enum SweepMode {
+  SWEEP_PASS = 0,       // one pass of T full steps, every segment at the same time level
+  SWEEP_FINALIZE = 1,   // only the pending correction of a T-step pass
+  SWEEP_PIPELINED = 2   // one launch of the staggered (pipelined) schedule
+};
+hipError_t launch_sweep(int scheme, int T, int mode, const SegArgs &a, int grid, hipStream_t st);
 hipError_t sweep_occupancy(int scheme, int T, int *waves_per_cu);
 hipError_t launch_fold(int KC, const FoldArgs &f, hipStream_t st);
 hipError_t launch_init_state(double2 *E, const double *lineB, const Geometry &g, hipStream_t st);

@@ -52,6 +52,14 @@ struct rt_solver {
   DeviceBuf E, map, lc, prop[kMaxTimeBlock + 1], bdry, agg[2], yseg, yrefl, lineB, muwt, mom, rows, sigma;
   int agg_cur = 0;               // aggregates of the last pass live in agg[agg_cur ^ 1]
   bool pending = false;          // E holds provisional segments (correction outstanding)
+  // pipelined schedule (rt_set_pipeline): chain positions (segments; half 0 then
+  // half 1 when the left boundary is reflective) at staggered time levels
+  bool pipe = true;
+  std::vector<long long> tau;    // full steps completed per chain position
+  long long target = 0;          // full steps every position must reach
+  long long pipe_base = 0;       // tau of every position when the pipeline started
+  int queued = 0;                // requested steps not yet enqueued (< T)
+  int Tpipe = 0;                 // time block of the running pipeline (0: positions aligned)
   // profiling
   bool profiling = false;
   std::vector<hipEvent_t> ev_pool;   // (start, stop) pairs of profiled launches
@@ -65,6 +73,12 @@ struct rt_solver {
     if (stream) (void)hipStreamDestroy(stream);
   }
 };
+
+// Chain positions of the pipelined schedule: the Sg segments of a line (both
+// halves in step), or 2 Sg when the mu > 0 lines continue the mu < 0 ones.
+static int chain_positions(const rt_solver *s) {
+  return s->p.bc_left_indicator == 2 ? 2 * s->Sg : s->Sg;
+}
 
 static rt_status fail(rt_solver *s, rt_status st, const std::string &msg) {
   if (s) s->err = msg;
@@ -466,6 +480,8 @@ extern "C" rt_status rt_create_from_params(const rt_params *pin, int g_lo, int g
   int waves_per_cu = 0;
   h->T = default_time_block(h->scheme);
   HIP_TRY(h, sweep_occupancy(h->scheme, h->T, &waves_per_cu));
+  // tuning knob for experiments: target resident waves per CU (segments per line follow)
+  if (const char *w = std::getenv("RTSN_WAVES_PER_CU")) waves_per_cu = std::atoi(w);
   waves_per_cu = std::max(1, std::min(waves_per_cu, 32));
   {
     const long long target = static_cast<long long>(prop.multiProcessorCount) * waves_per_cu;
@@ -500,6 +516,7 @@ extern "C" rt_status rt_create_from_params(const rt_params *pin, int g_lo, int g
   if (!e) e = dalloc(h->sigma, sizeof(double) * h->Gl);
   if (e) return fail(nullptr, RT_ERR_NOMEM, std::string("device allocation: ") + hipGetErrorString(e));
 
+  h->tau.assign(chain_positions(h), 0);
   if ((st = setup_lines(h))) return st;
   if ((st = upload_inflow(h))) return st;
   HIP_TRY(h, launch_init_state(static_cast<double2 *>(h->E.p), static_cast<const double *>(h->lineB.p), geometry(h),
@@ -597,56 +614,65 @@ static rt_status enqueue_fold(rt_solver *s, int T, bool reflective_outflow) {
 
 // Apply the outstanding cross-segment correction in place (before any read,
 // or before a pass with a different time block).
-static rt_status finalize(rt_solver *s) {
+static rt_status apply_correction(rt_solver *s) {
   if (!s->pending) return RT_OK;
   rt_status st = enqueue_fold(s, s->Tp, false);
   if (st) return st;
   SegArgs a = seg_args(s, s->Tp);
-  HIP_TRY(s, launch_sweep(s->scheme, s->Tp, true, a, 2 * s->Q * s->Sg, s->stream));
+  HIP_TRY(s, launch_sweep(s->scheme, s->Tp, SWEEP_FINALIZE, a, 2 * s->Q * s->Sg, s->stream));
   s->pending = false;
   return RT_OK;
 }
 
-// One pass of T full steps.
-static rt_status enqueue_pass(rt_solver *s, int T) {
-  if (s->pending && s->Tp != T) {
-    rt_status st = finalize(s);
+static rt_status event_begin(rt_solver *s, hipEvent_t *e1) {
+  *e1 = nullptr;
+  if (!s->profiling) return RT_OK;
+  if (s->ev_used + 2 > s->ev_pool.size()) {
+    rt_status st = fold_events(s);  // drain the pool when it is full
     if (st) return st;
   }
-  const int per_half = s->Q * s->Sg;
-  SegArgs a = seg_args(s, T);
-  hipEvent_t e0 = nullptr, e1 = nullptr;
-  if (s->profiling) {
-    if (s->ev_used + 2 > s->ev_pool.size()) {
-      rt_status st = fold_events(s);  // drain the pool when it is full
-      if (st) return st;
-    }
-    e0 = s->ev_pool[s->ev_used++];
-    e1 = s->ev_pool[s->ev_used++];
-    HIP_TRY(s, hipEventRecord(e0, s->stream));
-  }
-  if (s->pending) {
-    rt_status st = enqueue_fold(s, T, false);
-    if (st) return st;
-  }
-  if (a.reflective) {  // mu > 0 heads need this pass's mu < 0 outflow: two launches
-    a.half0 = 0;
-    HIP_TRY(s, launch_sweep(s->scheme, T, false, a, per_half, s->stream));
-    rt_status st = enqueue_fold(s, T, true);
-    if (st) return st;
-    a.half0 = 1;
-    HIP_TRY(s, launch_sweep(s->scheme, T, false, a, per_half, s->stream));
-  } else {
-    HIP_TRY(s, launch_sweep(s->scheme, T, false, a, 2 * per_half, s->stream));
-  }
-  if (s->profiling) {
+  hipEvent_t e0 = s->ev_pool[s->ev_used++];
+  *e1 = s->ev_pool[s->ev_used++];
+  HIP_TRY(s, hipEventRecord(e0, s->stream));
+  return RT_OK;
+}
+
+static rt_status event_end(rt_solver *s, hipEvent_t e1) {
+  if (e1) {
     HIP_TRY(s, hipEventRecord(e1, s->stream));
     ++s->profiled;
   }
   ++s->launches;
+  return RT_OK;
+}
+
+// One pass of T full steps, every segment at the same time level.
+static rt_status enqueue_pass(rt_solver *s, int T) {
+  if (s->pending && s->Tp != T) {
+    rt_status st = apply_correction(s);
+    if (st) return st;
+  }
+  const int per_half = s->Q * s->Sg;
+  SegArgs a = seg_args(s, T);
+  hipEvent_t e1;
+  rt_status st = event_begin(s, &e1);
+  if (st) return st;
+  if (s->pending && (st = enqueue_fold(s, T, false))) return st;
+  if (a.reflective) {  // mu > 0 heads need this pass's mu < 0 outflow: two launches
+    a.half0 = 0;
+    HIP_TRY(s, launch_sweep(s->scheme, T, SWEEP_PASS, a, per_half, s->stream));
+    if ((st = enqueue_fold(s, T, true))) return st;
+    a.half0 = 1;
+    HIP_TRY(s, launch_sweep(s->scheme, T, SWEEP_PASS, a, per_half, s->stream));
+  } else {
+    HIP_TRY(s, launch_sweep(s->scheme, T, SWEEP_PASS, a, 2 * per_half, s->stream));
+  }
+  if ((st = event_end(s, e1))) return st;
   s->pending = s->Sg > 1;
   s->Tp = T;
   s->agg_cur ^= 1;
+  for (long long &t : s->tau) t += T;
+  s->target += T;
   return RT_OK;
 }
 
@@ -660,13 +686,108 @@ static rt_status enqueue_steps(rt_solver *s, int nsteps) {
   return RT_OK;
 }
 
+// ---------------------------------------------------------------------------
+// Pipelined schedule.  Chain position c (segment s of half 0, or of half 1:
+// c = s for both halves, or c = Sg + s when the mu > 0 heads take the mu < 0
+// outflow) runs one pass behind position c-1: in every launch each position
+// that can advance T steps does, starting from the exit state position c-1
+// published in the previous launch for exactly those steps.  Every segment
+// starts exact, so no provisional state and no correction.  The first
+// launches fill the pipeline (position c starts in launch c), the last ones
+// drain it; both happen once per run of advances, and the drain only when a
+// read-out needs the state (finalize).
+// ---------------------------------------------------------------------------
+static rt_status pipe_launch(rt_solver *s) {
+  const int P = chain_positions(s), T = s->Tpipe;
+  int lo = -1, hi = -1;
+  for (int c = 0; c < P; ++c) {
+    const bool ready = s->tau[c] < s->target && (c == 0 || s->tau[c - 1] >= s->tau[c] + T);
+    if (!ready) continue;
+    if (lo < 0) lo = c;
+    if (hi >= 0 && hi != c - 1) return fail(s, RT_ERR_PARAM, "pipeline: active positions not contiguous");
+    hi = c;
+  }
+  if (lo < 0) return RT_OK;
+  for (int c = lo; c <= hi; ++c)
+    if (s->tau[c] != s->tau[lo] - static_cast<long long>(c - lo) * T)
+      return fail(s, RT_ERR_PARAM, "pipeline: positions out of step");
+  SegArgs a = seg_args(s, T);
+  a.aggs[0] = static_cast<double *>(s->agg[0].p);
+  a.aggs[1] = static_cast<double *>(s->agg[1].p);
+  a.pending = 0;
+  a.pos_lo = lo;
+  a.npos = hi - lo + 1;
+  a.pass_lo = static_cast<int>(((s->tau[lo] - s->pipe_base) / T) & 1);
+  const int grid = (a.reflective ? 1 : 2) * a.npos * s->Q;
+  hipEvent_t e1;
+  rt_status st = event_begin(s, &e1);
+  if (st) return st;
+  HIP_TRY(s, launch_sweep(s->scheme, T, SWEEP_PIPELINED, a, grid, s->stream));
+  if ((st = event_end(s, e1))) return st;
+  for (int c = lo; c <= hi; ++c) s->tau[c] += T;
+  return RT_OK;
+}
+
+// Queue nsteps; launch whole passes while the chain head is behind.
+static rt_status pipe_advance(rt_solver *s, int nsteps) {
+  s->queued += nsteps;
+  const int T = s->T;
+  rt_status st;
+  if (s->Tpipe && s->Tpipe != T) {  // a lagged pipeline of another block size: let it drain
+    while (s->tau.back() < s->target)
+      if ((st = pipe_launch(s))) return st;
+    s->Tpipe = 0;
+  }
+  const long long passes = s->queued / T;
+  if (passes == 0) return RT_OK;
+  if (!s->Tpipe) {  // start from aligned positions with an exact state
+    if ((st = apply_correction(s))) return st;
+    s->Tpipe = T;
+    s->pipe_base = s->tau[0];
+  }
+  s->queued -= static_cast<int>(passes * T);
+  s->target += passes * T;
+  while (s->tau[0] < s->target)
+    if ((st = pipe_launch(s))) return st;
+  return RT_OK;
+}
+
+// Bring every position to the target (drain) and run the queued remainder.
+static rt_status complete(rt_solver *s) {
+  rt_status st;
+  if (s->Tpipe) {
+    while (s->tau.back() < s->target)
+      if ((st = pipe_launch(s))) return st;
+    s->Tpipe = 0;
+  }
+  if (s->queued) {
+    const int r = s->queued;
+    s->queued = 0;
+    if ((st = enqueue_pass(s, r))) return st;
+  }
+  return RT_OK;
+}
+
+// The state at the requested time, exact: before any read-out.
+static rt_status finalize(rt_solver *s) {
+  rt_status st = complete(s);
+  if (st) return st;
+  return apply_correction(s);
+}
+
 extern "C" rt_status rt_advance(rt_solver *s, int nsteps) {
   if (!s || nsteps < 0) return fail(s, RT_ERR_ARG, "rt_advance: bad argument");
   HIP_TRY(s, hipSetDevice(s->device));
   rt_status st = check_validation(s);
   if (st) return st;
   if ((st = ensure_equilibrium(s))) return st;
-  return enqueue_steps(s, nsteps);
+  return s->pipe ? pipe_advance(s, nsteps) : enqueue_steps(s, nsteps);
+}
+
+extern "C" rt_status rt_finish(rt_solver *s) {
+  if (!s) return fail(nullptr, RT_ERR_ARG, "rt_finish: NULL handle");
+  HIP_TRY(s, hipSetDevice(s->device));
+  return finalize(s);
 }
 
 extern "C" rt_status rt_synchronize(rt_solver *s) {
@@ -679,6 +800,7 @@ extern "C" rt_status rt_solve(rt_solver *s) {
   if (!s) return fail(nullptr, RT_ERR_ARG, "rt_solve: NULL handle");
   rt_status st = rt_advance(s, s->p.max_timesteps);
   if (st) return st;
+  if ((st = complete(s))) return st;
   return rt_synchronize(s);
 }
 
@@ -732,6 +854,7 @@ extern "C" rt_status rt_get_ends(rt_solver *s, double *ends) {
 extern "C" rt_status rt_set_ends(rt_solver *s, const double *ends) {
   if (!s || !ends) return fail(s, RT_ERR_ARG, "rt_set_ends: bad argument");
   HIP_TRY(s, hipSetDevice(s->device));
+  if (rt_status st = complete(s)) return st;  // requested steps happen before the state is replaced
   const Geometry g = geometry(s);
   const size_t n = static_cast<size_t>(2) * g.M * g.Gl * g.N;
   double *d = nullptr;
@@ -930,6 +1053,22 @@ extern "C" rt_status rt_sweep_flops(rt_solver *s, double *flops_per_launch) {
   const int rows = s->K + 1 - (s->scheme == SCHEME_BE ? 0 : 1);
   const double fma = static_cast<double>(map_count_of(s->scheme) - rows);
   *flops_per_launch = 2.0 * fma * s->T * static_cast<double>(s->p.M) * s->Gl * s->p.N;
+  return RT_OK;
+}
+
+extern "C" rt_status rt_set_pipeline(rt_solver *s, int on) {
+  if (!s) return fail(nullptr, RT_ERR_ARG, "rt_set_pipeline: NULL handle");
+  HIP_TRY(s, hipSetDevice(s->device));
+  if (!on && s->pipe) {
+    if (rt_status st = complete(s)) return st;  // leave the positions aligned
+  }
+  s->pipe = on != 0;
+  return RT_OK;
+}
+
+extern "C" rt_status rt_get_pipeline(rt_solver *s, int *on) {
+  if (!s || !on) return fail(s, RT_ERR_ARG, "rt_get_pipeline: bad argument");
+  *on = s->pipe ? 1 : 0;
   return RT_OK;
 }
 

@@ -83,7 +83,7 @@ def lib():
         L.rt_create_from_params.argtypes = [C.POINTER(rt_params), C.c_int, C.c_int, C.c_int, C.POINTER(vp)]
         L.rt_destroy.argtypes = [vp]
         L.rt_destroy.restype = None
-        for name in ("rt_solve", "rt_synchronize"):
+        for name in ("rt_solve", "rt_synchronize", "rt_finish"):
             getattr(L, name).argtypes = [vp]
         L.rt_advance.argtypes = [vp, C.c_int]
         L.rt_stream.argtypes = [vp]
@@ -103,6 +103,8 @@ def lib():
         L.rt_sweep_geometry.argtypes = [vp, C.POINTER(C.c_int), C.POINTER(C.c_longlong)]
         L.rt_sweep_flops.argtypes = [vp, dp]
         L.rt_set_time_block.argtypes = [vp, C.c_int]
+        L.rt_set_pipeline.argtypes = [vp, C.c_int]
+        L.rt_get_pipeline.argtypes = [vp, C.POINTER(C.c_int)]
         L.rt_get_time_block.argtypes = [vp, C.POINTER(C.c_int)]
         L.rt_status_string.argtypes = [C.c_int]
         L.rt_status_string.restype = C.c_char_p
@@ -253,6 +255,10 @@ class Solver:
     def advance(self, nsteps: int):
         _check(lib().rt_advance(self._h, int(nsteps)), "rt_advance", self._h)
 
+    def finish(self):
+        """Enqueue the pipeline drain / remainder / pending correction (rt_finish)."""
+        _check(lib().rt_finish(self._h), "rt_finish", self._h)
+
     def synchronize(self):
         _check(lib().rt_synchronize(self._h), "rt_synchronize", self._h)
 
@@ -369,6 +375,17 @@ class Solver:
     @time_block.setter
     def time_block(self, steps_per_pass: int):
         _check(lib().rt_set_time_block(self._h, int(steps_per_pass)), "rt_set_time_block", self._h)
+
+    @property
+    def pipeline(self) -> bool:
+        """Pipelined (staggered-segment) schedule on/off (rt_set_pipeline)."""
+        v = C.c_int()
+        _check(lib().rt_get_pipeline(self._h, C.byref(v)), "rt_get_pipeline", self._h)
+        return bool(v.value)
+
+    @pipeline.setter
+    def pipeline(self, on: bool):
+        _check(lib().rt_set_pipeline(self._h, int(bool(on))), "rt_set_pipeline", self._h)
 
     def sweep_traffic(self):
         b = C.c_double()

@@ -10,7 +10,6 @@ WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE reports half the bytes of a
 """
 import csv
 import json
-import statistics
 import sys
 from pathlib import Path
 
@@ -22,25 +21,27 @@ def counters(d):
     for f in Path(d).rglob("*counter_collection.csv"):
         for r in csv.DictReader(open(f)):
             name = r["Kernel_Name"]
-            if KERNEL in name and name.replace(" ", "").split("(")[0].endswith(",0>"):  # MODE 0: a pass
+            mode = name.replace(" ", "").split("(")[0]
+            if KERNEL in name and (mode.endswith(",0>") or mode.endswith(",2>")):  # a pass (aligned or pipelined)
                 out.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
     return out
 
 
 def main():
     variant, fdir, wdir, *rest = sys.argv[1:]
+    # the largest launch is a full pass (pipeline fill/drain launches cover fewer segments)
     fetch = counters(fdir)["FETCH_SIZE"]
     write = counters(wdir)["WRITE_SIZE"]
-    rd = statistics.median(fetch) * 1024 * 2
-    wr = statistics.median(write) * 1024
+    rd = max(fetch) * 1024 * 2
+    wr = max(write) * 1024
     res = {"variant": variant, "kernel": KERNEL, "launches": len(fetch),
-           "fetch_size_kib_median": statistics.median(fetch), "write_size_kib_median": statistics.median(write),
+           "fetch_size_kib_max": max(fetch), "write_size_kib_max": max(write),
            "hbm_read_bytes_per_launch": rd, "hbm_write_bytes_per_launch": wr,
            "hbm_bytes_per_launch": rd + wr,
            "correction": "FETCH_SIZE x 2 (gfx950 half-count of 16 B/lane streaming reads), KiB -> bytes"}
     for d in rest:
         for k, v in counters(d).items():
-            res[k + "_median"] = statistics.median(v)
+            res[k + "_max"] = max(v)
     out = Path(__file__).resolve().parent.parent / "profiles" / f"pmc_{variant}.json"
     out.write_text(json.dumps(res, indent=1) + "\n")
     print(json.dumps(res))

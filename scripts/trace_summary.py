@@ -1,0 +1,37 @@
+#!/usr/bin/env python3
+"""Per-dispatch view of a rocprofv3 --kernel-trace run of bench.py.
+
+usage: trace_summary.py <run_kernel_trace.csv> <out.json>
+
+The pipelined schedule's first and last launches (fill / drain) cover fewer
+segments than a steady-state pass, so the kernel's plain average over all
+dispatches is not the per-pass time bench.py reports.  Dispatches are
+grouped by (kernel, grid size); for each group: count, mean and median
+duration.  The full-grid group of the sweep kernel is the steady-state pass.
+"""
+import csv
+import json
+import statistics
+import sys
+from collections import defaultdict
+
+
+def main():
+    src, out = sys.argv[1:3]
+    groups = defaultdict(list)
+    for r in csv.DictReader(open(src)):
+        dur_ms = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
+        groups[(r["Kernel_Name"], int(r["Grid_Size_X"]))].append(dur_ms)
+    rows = []
+    for (name, grid), d in sorted(groups.items(), key=lambda kv: -sum(kv[1])):
+        rows.append({"kernel": name, "grid_threads": grid, "dispatches": len(d), "total_ms": sum(d),
+                     "mean_ms": statistics.mean(d), "median_ms": statistics.median(d)})
+    sweep = [r for r in rows if "sweep_block_kernel" in r["kernel"]]
+    full = max(sweep, key=lambda r: r["grid_threads"]) if sweep else None
+    res = {"steady_state_pass": full, "groups": rows}
+    open(out, "w").write(json.dumps(res, indent=1) + "\n")
+    print(json.dumps(full))
+
+
+if __name__ == "__main__":
+    main()

@@ -80,6 +80,9 @@ class OracleShard:
     def synchronize(self):
         pass
 
+    def finish(self):
+        pass
+
     def set_profiling(self, on):
         self.prof = bool(on)
         if on:
@@ -148,14 +151,14 @@ def test_two_rank_group_shards(tmp_path, scaling, groups):
         np.testing.assert_allclose(a, ref, rtol=1e-13, atol=0)
     # the JSON line: whole-job updates over the max-over-ranks wall time
     line = lines[0]["line"]
-    for k in ("value", "ms_per_step", "n_gpus", "absorption_allreduce_finite"):
+    for k in ("value", "ms_per_step", "n_gpus", "state_finite"):
         assert line[k] == lines[1]["line"][k]  # reduced over ranks
     assert line["roofline"]["kernel_ms"] == lines[1]["line"]["roofline"]["kernel_ms"]
     total = sum(4.0 * 8 * (l["info"][2] - l["info"][1]) * 48 * steps for l in lines)
     assert line["n_gpus"] == 2 and line["scaling"] == scaling
     assert line["value"] == pytest.approx(total / (line["ms_per_step"] * 1e-3 * steps), rel=1e-12)
     assert line["config"]["groups_total"] == G_total
-    assert line["absorption_allreduce_finite"] is True
+    assert line["state_finite"] is True
     assert line["roofline"]["kernel_ms"] >= max(l["wall_ms"] for l in lines) / steps * (1 - 1e-9)
 
 

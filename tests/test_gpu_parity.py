@@ -36,7 +36,12 @@ def to_rt(p: dict) -> dict:
     return q
 
 
-def compare_all(gpu, orc, tol=TOL):
+def compare_all(gpu, orc, tol=TOL, plus_vs_group=False):
+    """plus_vs_group: measure phi_plus against the group's intensity scale
+    (max|psi| x sum of mu > 0 weights) instead of max|phi_plus| -- for runs in
+    which the reference's BDF2 instability leaves the mu > 0
+    intensities ~1e-7 of the mu < 0 ones, so that phi_plus inherits the
+    rounding of values 1e7 times larger."""
     mu, wt = orc.quad()
     psi_o = orc.psi()
     err = {"psi": per_group_rel(gpu.psi(), psi_o, 1),
@@ -44,7 +49,11 @@ def compare_all(gpu, orc, tol=TOL):
     phi_g, F_g, pp_g = gpu.moments()
     phi_o, F_o, pp_o = orc.moments()
     err["phi"] = per_group_rel(phi_g, phi_o, 0)
-    err["phi_plus"] = per_group_rel(pp_g, pp_o, 0)
+    if plus_vs_group:
+        scale = np.abs(psi_o).max(axis=(0, 2)) * wt[mu > 0].sum()
+        err["phi_plus"] = float((np.abs(pp_g - pp_o).max(axis=1) / scale).max())
+    else:
+        err["phi_plus"] = per_group_rel(pp_g, pp_o, 0)
     err["F"] = flux_rel(F_g, F_o, psi_o, mu, wt)
     l_g, r_g = gpu.compute_group_ends()
     l_o, r_o = orc.group_ends()
@@ -90,12 +99,13 @@ def test_gray_test_on_gpu(rtsn_mod):
         assert abs(F.max()) < 1e-6
 
 
+@pytest.mark.parametrize("pipe", [True, False])
 @pytest.mark.parametrize("tb", [1, 3, 4])
 @pytest.mark.parametrize("ts", [1, 2, 3])
 @pytest.mark.parametrize("bc_left,bc_right", [(0, 0), (1, 1), (2, 1), (2, 0), (1, 2), (0, 1)])
-def test_schemes_and_boundaries(rtsn_mod, oracle_mod, ts, bc_left, bc_right, tb):
-    """4 steps with tb full steps per pass: tb = 3 runs a 3-step pass, a
-    finalize and a 1-step pass."""
+def test_schemes_and_boundaries(rtsn_mod, oracle_mod, ts, bc_left, bc_right, tb, pipe):
+    """4 steps with tb full steps per pass, pipelined or aligned schedule:
+    tb = 3 runs one 3-step pass and a 1-step remainder pass."""
     p = load(oracle_mod, "template.prm", ts_method=ts, bc_left=bc_left, bc_right=bc_right, max_timesteps=4,
              M=6, N=150, V=2.0)
     p["dx"] = p["X"] / p["N"]
@@ -104,6 +114,7 @@ def test_schemes_and_boundaries(rtsn_mod, oracle_mod, ts, bc_left, bc_right, tb)
     orc.solve()
     with rtsn_mod.Solver(to_rt(p)) as gpu:
         gpu.time_block = tb
+        gpu.pipeline = pipe
         gpu.solve()
         compare_all(gpu, orc)
 
@@ -135,8 +146,9 @@ def test_line_counts(rtsn_mod, oracle_mod, M, G):
         compare_all(gpu, orc)
 
 
-@pytest.mark.parametrize("tb,steps", [(1, 1), (1, 3), (2, 4), (3, 3), (3, 5), (4, 4)])
-def test_random_state_long_lines(rtsn_mod, oracle_mod, tb, steps):
+@pytest.mark.parametrize("pipe", [True, False])
+@pytest.mark.parametrize("tb,steps", [(1, 1), (1, 3), (2, 4), (3, 3), (3, 5), (4, 4), (4, 9)])
+def test_random_state_long_lines(rtsn_mod, oracle_mod, tb, steps, pipe):
     """BDF2 steps from a random state (seed 20261015, psi0 = B U[0.5,1.5))
     on 20k-cell lines cut into many segments: the deferred cross-segment
     correction across passes of tb fused steps (and the finalize between a
@@ -153,13 +165,16 @@ def test_random_state_long_lines(rtsn_mod, oracle_mod, tb, steps):
     orc.solve()
     with rtsn_mod.Solver(to_rt(p), g_lo=lo, g_hi=hi) as gpu:
         gpu.time_block = tb
+        gpu.pipeline = pipe
         gpu.set_ends(ends)
         gpu.solve()
         compare_all(gpu, orc)
 
 
-def test_time_block_switching(rtsn_mod, oracle_mod):
-    """advance() calls with changing time blocks and read-outs in between
+@pytest.mark.parametrize("toggle", [False, True])
+def test_time_block_switching(rtsn_mod, oracle_mod, toggle):
+    """advance() calls with changing time blocks (and, with toggle, switching
+    between the pipelined and aligned schedules) and a read-out in between
     equal one oracle run of the same total number of steps."""
     p = load(oracle_mod, "llnl_slab_test.prm", N=3000, M=8, use_correction=1, V=5.994, bc_left=2)
     p["dx"] = p["X"] / p["N"]
@@ -171,11 +186,30 @@ def test_time_block_switching(rtsn_mod, oracle_mod):
     with rtsn_mod.Solver(to_rt(p)) as gpu:
         for k, (tb, n) in enumerate(plan):
             gpu.time_block = tb
+            if toggle:
+                gpu.pipeline = k % 2 == 0
             gpu.advance(n)
             if k == 2:
                 gpu.psi()  # a read-out in the middle finalizes the pending correction
         gpu.synchronize()
         compare_all(gpu, orc)
+
+
+@pytest.mark.parametrize("ts", [1, 2, 3])
+def test_pipeline_long_run_many_segments(rtsn_mod, oracle_mod, ts):
+    """Enough passes to fill, run and drain the pipeline (reflective: one chain
+    of 2 Sg positions), split over several advance() calls."""
+    p = load(oracle_mod, "multi_group_equilibrium.prm", N=3000, M=4, max_timesteps=45, bc_left=2, ts_method=ts)
+    p["dx"] = p["X"] / p["N"]
+    p["psi_source"] = np.ones((p["M"], p["G"]))
+    orc = oracle_mod.OracleSolver(p)
+    orc.solve()
+    with rtsn_mod.Solver(to_rt(p)) as gpu:
+        _, segs = gpu.sweep_geometry()
+        assert segs > 4
+        for n in (5, 17, 8, 15):
+            gpu.advance(n)
+        compare_all(gpu, orc, plus_vs_group=ts == 3)
 
 
 def test_time_block_range(rtsn_mod):
