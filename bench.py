@@ -208,7 +208,7 @@ def run_rank(solver, p: dict, steps: int, warmup: int, world: int, device, shard
             "unit": "TFLOP/s" if tb > 1 else "GB/s",
             "frac": achieved_fl / FP64_PEAK if tb > 1 else achieved / HBM_PEAK,
             "traffic": None,
-            "kernel": f"sweep_block_kernel<3, {tb}, 0>",
+            "kernel": f"sweep_block_kernel<3, {tb}, {2 if getattr(solver, 'pipeline', False) else 0}>",
             "kernel_ms": kern_avg_ms,
             "algorithmic_flops_per_launch": flops_launch,
             "algorithmic_bytes_per_launch": bytes_launch,
