@@ -185,7 +185,7 @@ def run_rank(solver, p: dict, steps: int, warmup: int, world: int, device, shard
         "dtype": "f64",
         "data": "synthetic",
         "bdf2_steps_per_s": 1e3 / ms_per_step,
-        "schedule": {"pipelined": bool(getattr(solver, "pipeline", False)), "steps_per_pass": tb,
+        "schedule": {"pipeline_mode": int(getattr(solver, "pipeline", 0)), "steps_per_pass": tb,
                      "warmup_steps": warmup, "drain_ms": 1e3 * (t_end - t1),
                      "end_to_end_ms": 1e3 * (t_end - t_start),
                      "end_to_end_updates_per_s": upd_step * (warmup + steps) / (t_end - t_start)},
@@ -258,7 +258,7 @@ def main():
     solver = rtsn.Solver(p, device=local, g_lo=info[1], g_hi=info[2])
     if args.time_block:
         solver.time_block = args.time_block
-    solver.pipeline = args.schedule == "pipelined"
+    solver.pipeline = 1 if args.schedule == "pipelined" else 0  # 1: pipelined when the run fills it
     tb = solver.time_block
     warmup = args.warmup
     if warmup < 0:  # pipeline depth (segments per line) passes: fill + one steady pass

@@ -154,16 +154,18 @@ rt_status rt_sweep_traffic(rt_solver *s, double *bytes_per_launch, double *updat
  * affine cell map (BDF2 28, CN 8, BE 6 FMAs per cell x line x step) times T
  * steps; the cross-segment correction is parallelisation overhead, not counted. */
 rt_status rt_sweep_flops(rt_solver *s, double *flops_per_launch);
-/* Time blocking: full steps advanced per pass over HBM (1..4).  Results do
- * not depend on it beyond rounding; rt_advance(n) runs n / T passes of T
- * steps and one pass of n % T. */
+/* Time blocking: full steps advanced per pass over HBM: 1..8, 12 or 16
+ * (default 16; aligned passes take at most 4).  Results do not depend on it
+ * beyond rounding. */
 rt_status rt_set_time_block(rt_solver *s, int steps_per_pass);
-/* Pipelined schedule (default on): the segments of a line run at staggered
- * time levels, one pass apart, so each starts from its upwind neighbour's
- * exact exit state -- no cross-segment correction.  Steps are queued and
- * launched as whole passes; the pipeline fills over the first launches and
- * drains when a result is read (or rt_solve returns).  Off: every pass moves
- * all segments together and corrects them in the next pass. */
+/* Pipelined schedule: the segments of a line run at staggered time levels,
+ * one pass apart, so each starts from its upwind neighbour's exact exit state
+ * -- no cross-segment correction.  Steps are queued and launched as whole
+ * passes; the pipeline fills over the first launches (one per segment) and
+ * drains when a result is read (or rt_solve returns).  0: off -- every pass
+ * moves all segments together (at most 4 steps) and corrects them in the
+ * next pass; 1 (default): pipelined when an advance brings at least as many
+ * passes as the pipeline is deep, else aligned; 2: always pipelined. */
 rt_status rt_set_pipeline(rt_solver *s, int on);
 rt_status rt_get_pipeline(rt_solver *s, int *on);
 rt_status rt_get_time_block(rt_solver *s, int *steps_per_pass);

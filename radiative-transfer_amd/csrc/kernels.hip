@@ -500,13 +500,20 @@ __global__ void group_absorption_kernel(const double *phi, const double *sigma, 
 // ------------------------------------------------------------------------
 template <int S, int T>
 static hipError_t launch_t(int mode, const SegArgs &a, int grid, hipStream_t st) {
-  switch (mode) {
-    case SWEEP_PASS: hipLaunchKernelGGL((sweep_block_kernel<S, T, 0>), dim3(grid), dim3(64), 0, st, a); break;
-    case SWEEP_FINALIZE: hipLaunchKernelGGL((sweep_block_kernel<S, T, 1>), dim3(grid), dim3(64), 0, st, a); break;
-    case SWEEP_PIPELINED: hipLaunchKernelGGL((sweep_block_kernel<S, T, 2>), dim3(grid), dim3(64), 0, st, a); break;
-    default: return hipErrorInvalidValue;
+  if (mode == SWEEP_PIPELINED) {
+    hipLaunchKernelGGL((sweep_block_kernel<S, T, 2>), dim3(grid), dim3(64), 0, st, a);
+    return hipGetLastError();
   }
-  return hipGetLastError();
+  if constexpr (T <= kMaxAlignedBlock) {
+    if (mode == SWEEP_PASS)
+      hipLaunchKernelGGL((sweep_block_kernel<S, T, 0>), dim3(grid), dim3(64), 0, st, a);
+    else if (mode == SWEEP_FINALIZE)
+      hipLaunchKernelGGL((sweep_block_kernel<S, T, 1>), dim3(grid), dim3(64), 0, st, a);
+    else
+      return hipErrorInvalidValue;
+    return hipGetLastError();
+  }
+  return hipErrorInvalidValue;
 }
 
 template <int S>
@@ -516,6 +523,12 @@ static hipError_t launch_s(int T, int mode, const SegArgs &a, int grid, hipStrea
     case 2: return launch_t<S, 2>(mode, a, grid, st);
     case 3: return launch_t<S, 3>(mode, a, grid, st);
     case 4: return launch_t<S, 4>(mode, a, grid, st);
+    case 5: return launch_t<S, 5>(mode, a, grid, st);
+    case 6: return launch_t<S, 6>(mode, a, grid, st);
+    case 7: return launch_t<S, 7>(mode, a, grid, st);
+    case 8: return launch_t<S, 8>(mode, a, grid, st);
+    case 12: return launch_t<S, 12>(mode, a, grid, st);
+    case 16: return launch_t<S, 16>(mode, a, grid, st);
     default: return hipErrorInvalidValue;
   }
 }
@@ -548,6 +561,12 @@ static hipError_t occupancy_s(int T, int *w) {
     case 2: return hipOccupancyMaxActiveBlocksPerMultiprocessor(w, sweep_block_kernel<S, 2, 0>, 64, 0);
     case 3: return hipOccupancyMaxActiveBlocksPerMultiprocessor(w, sweep_block_kernel<S, 3, 0>, 64, 0);
     case 4: return hipOccupancyMaxActiveBlocksPerMultiprocessor(w, sweep_block_kernel<S, 4, 0>, 64, 0);
+    case 5: return hipOccupancyMaxActiveBlocksPerMultiprocessor(w, sweep_block_kernel<S, 5, 2>, 64, 0);
+    case 6: return hipOccupancyMaxActiveBlocksPerMultiprocessor(w, sweep_block_kernel<S, 6, 2>, 64, 0);
+    case 7: return hipOccupancyMaxActiveBlocksPerMultiprocessor(w, sweep_block_kernel<S, 7, 2>, 64, 0);
+    case 8: return hipOccupancyMaxActiveBlocksPerMultiprocessor(w, sweep_block_kernel<S, 8, 2>, 64, 0);
+    case 12: return hipOccupancyMaxActiveBlocksPerMultiprocessor(w, sweep_block_kernel<S, 12, 2>, 64, 0);
+    case 16: return hipOccupancyMaxActiveBlocksPerMultiprocessor(w, sweep_block_kernel<S, 16, 2>, 64, 0);
     default: return hipErrorInvalidValue;
   }
 }

@@ -19,7 +19,8 @@ constexpr int kSweepCells = RT_SWEEP_CELLS;             // segment lengths are m
 constexpr int chunk_cells(int S, int T) { return (S == 3 && T >= 2) ? RT_CHUNK_BDF2_T2 : RT_SWEEP_CELLS; }
 constexpr int kSweepTile = 64;                          // cells are padded to whole tiles of 64 rows
 
-constexpr int kMaxTimeBlock = 4;                        // full steps fused per pass (template range)
+constexpr int kMaxTimeBlock = 16;                       // full steps fused per pipelined pass (template range)
+constexpr int kMaxAlignedBlock = 4;                     // ... per aligned pass (carries a T K correction state)
 
 // Segment propagators of the T-level combined state (KC = T K, packed lower
 // triangle of NTC = KC (KC + 1) / 2 entries each): A_T^Ls, A_T^Llast.

@@ -49,12 +49,12 @@ struct rt_solver {
   int device = 0;
   hipStream_t stream = nullptr;
   // device state
-  DeviceBuf E, map, lc, prop[kMaxTimeBlock + 1], bdry, agg[2], yseg, yrefl, lineB, muwt, mom, rows, sigma;
+  DeviceBuf E, map, lc, prop[kMaxAlignedBlock + 1], bdry, agg[2], yseg, yrefl, lineB, muwt, mom, rows, sigma;
   int agg_cur = 0;               // aggregates of the last pass live in agg[agg_cur ^ 1]
   bool pending = false;          // E holds provisional segments (correction outstanding)
   // pipelined schedule (rt_set_pipeline): chain positions (segments; half 0 then
   // half 1 when the left boundary is reflective) at staggered time levels
-  bool pipe = true;
+  int pipe = 1;                  // 0 off, 1 auto (runs long enough to fill), 2 always
   std::vector<long long> tau;    // full steps completed per chain position
   long long target = 0;          // full steps every position must reach
   long long pipe_base = 0;       // tau of every position when the pipeline started
@@ -93,9 +93,9 @@ static rt_status fail(rt_solver *s, rt_status st, const std::string &msg) {
   } while (0)
 
 // Full steps fused per HBM pass by default (rt_set_time_block changes it).
-// Measured on SL (profiles/): BDF2 43.9 / 25.0 / 23.3 / 19.8 ms per step at
-// T = 1 / 2 / 3 / 4 -- one pass is HBM-bound at T = 1 and FP64-bound beyond.
-static int default_time_block(int) { return kMaxTimeBlock; }
+// Measured on SL (pipelined schedule, profiles/): BDF2 43.0 / 21.7 / 14.5 / 12.3 /
+// 9.5 / 9.0 / 8.4 ms per step at T = 1 / 2 / 3 / 4 / 8 / 12 / 16.
+static int default_time_block(int) { return 16; }
 
 static int map_count_of(int scheme) {
   switch (scheme) {
@@ -348,8 +348,8 @@ static rt_status setup_lines_s(rt_solver *s) {
   const long long L_last = s->p.N - static_cast<long long>(s->Sg - 1) * s->Ls;
   const size_t Lp = s->Lpad;
   std::vector<double> lc(2 * LC_COUNT * Lp, 0.0), map(2 * WN * Lp, 0.0), lineB(2 * Lp, 0.0);
-  std::vector<std::vector<double>> pr(kMaxTimeBlock + 1);
-  for (int T = 1; T <= kMaxTimeBlock; ++T) pr[T].assign(2 * prop_count(K, T) * Lp, 0.0);
+  std::vector<std::vector<double>> pr(kMaxAlignedBlock + 1);
+  for (int T = 1; T <= kMaxAlignedBlock; ++T) pr[T].assign(2 * prop_count(K, T) * Lp, 0.0);
   std::vector<double> A, Aseg, Alast;
   double W[WN];
   for (int half = 0; half < 2; ++half)
@@ -363,7 +363,7 @@ static rt_status setup_lines_s(rt_solver *s) {
         if (!cell_map<S>(L, hd, half == 0, W))
           return fail(s, RT_ERR_PARAM, "cell map: a structurally zero coefficient is not zero");
         for (int n = 0; n < WN; ++n) map[(half * WN + n) * Lp + ell] = W[n];
-        for (int T = 1; T <= kMaxTimeBlock; ++T) {
+        for (int T = 1; T <= kMaxAlignedBlock; ++T) {
           const int KC = T * K, NTC = KC * (KC + 1) / 2;
           A.assign(KC * KC, 0.0);
           Aseg.resize(KC * KC);
@@ -382,7 +382,7 @@ static rt_status setup_lines_s(rt_solver *s) {
   rt_status st;
   if ((st = upload(s, s->lc, lc.data(), lc.size() * sizeof(double)))) return st;
   if ((st = upload(s, s->map, map.data(), map.size() * sizeof(double)))) return st;
-  for (int T = 1; T <= kMaxTimeBlock; ++T)
+  for (int T = 1; T <= kMaxAlignedBlock; ++T)
     if ((st = upload(s, s->prop[T], pr[T].data(), pr[T].size() * sizeof(double)))) return st;
   if ((st = upload(s, s->lineB, lineB.data(), lineB.size() * sizeof(double)))) return st;
   std::vector<double> sig(s->Gl);
@@ -479,6 +479,7 @@ extern "C" rt_status rt_create_from_params(const rt_params *pin, int g_lo, int g
   // segments: enough waves to fill the chip (occupancy x CUs), Ls a multiple of the chunk
   int waves_per_cu = 0;
   h->T = default_time_block(h->scheme);
+  if (const char *t = std::getenv("RTSN_TIME_BLOCK")) h->T = std::atoi(t);  // experiments: segment count follows
   HIP_TRY(h, sweep_occupancy(h->scheme, h->T, &waves_per_cu));
   // tuning knob for experiments: target resident waves per CU (segments per line follow)
   if (const char *w = std::getenv("RTSN_WAVES_PER_CU")) waves_per_cu = std::atoi(w);
@@ -502,13 +503,13 @@ extern "C" rt_status rt_create_from_params(const rt_params *pin, int g_lo, int g
   if (!e) e = dalloc(h->E, sizeof(double2) * 2 * Nrow * Lp);
   if (!e) e = dalloc(h->lc, sizeof(double) * 2 * LC_COUNT * Lp);
   if (!e) e = dalloc(h->map, sizeof(double) * 2 * map_count_of(h->scheme) * Lp);
-  for (int T = 1; T <= kMaxTimeBlock; ++T)
+  for (int T = 1; T <= kMaxAlignedBlock; ++T)
     if (!e) e = dalloc(h->prop[T], sizeof(double) * 2 * prop_count(K, T) * Lp);
   if (!e) e = dalloc(h->bdry, sizeof(double) * 2 * Lp);
   if (!e) e = dalloc(h->agg[0], sizeof(double) * 2 * h->Sg * kMaxTimeBlock * K * Lp);
   if (!e) e = dalloc(h->agg[1], sizeof(double) * 2 * h->Sg * kMaxTimeBlock * K * Lp);
-  if (!e) e = dalloc(h->yseg, sizeof(double) * 2 * (h->Sg + 1) * kMaxTimeBlock * K * Lp);
-  if (!e) e = dalloc(h->yrefl, sizeof(double) * kMaxTimeBlock * K * Lp);
+  if (!e) e = dalloc(h->yseg, sizeof(double) * 2 * (h->Sg + 1) * kMaxAlignedBlock * K * Lp);
+  if (!e) e = dalloc(h->yrefl, sizeof(double) * kMaxAlignedBlock * K * Lp);
   if (!e) e = dalloc(h->lineB, sizeof(double) * 2 * Lp);
   if (!e) e = dalloc(h->muwt, sizeof(double) * 2 * q.M);
   if (!e) e = dalloc(h->mom, sizeof(double) * 3 * h->Gl * static_cast<size_t>(q.N));
@@ -676,13 +677,15 @@ static rt_status enqueue_pass(rt_solver *s, int T) {
   return RT_OK;
 }
 
-// nsteps full steps: passes of T steps, then one pass of the remainder.
+// nsteps full steps in aligned passes of at most T (and kMaxAlignedBlock) steps.
 static rt_status enqueue_steps(rt_solver *s, int nsteps) {
-  for (int n = 0; n + s->T <= nsteps; n += s->T) {
-    rt_status st = enqueue_pass(s, s->T);
+  const int T = std::min(s->T, kMaxAlignedBlock);
+  while (nsteps > 0) {
+    const int n = std::min(T, nsteps);
+    rt_status st = enqueue_pass(s, n);
     if (st) return st;
+    nsteps -= n;
   }
-  if (nsteps % s->T) return enqueue_pass(s, nsteps % s->T);
   return RT_OK;
 }
 
@@ -740,7 +743,14 @@ static rt_status pipe_advance(rt_solver *s, int nsteps) {
   }
   const long long passes = s->queued / T;
   if (passes == 0) return RT_OK;
-  if (!s->Tpipe) {  // start from aligned positions with an exact state
+  if (!s->Tpipe) {
+    if (s->pipe == 1 && passes < chain_positions(s)) {
+      // too few passes to fill the pipeline (it would run its segments nearly one
+      // at a time): aligned passes of at most kMaxAlignedBlock steps instead
+      s->queued -= static_cast<int>(passes * T);
+      return enqueue_steps(s, static_cast<int>(passes * T));
+    }
+    // start from aligned positions with an exact state
     if ((st = apply_correction(s))) return st;
     s->Tpipe = T;
     s->pipe_base = s->tau[0];
@@ -763,7 +773,7 @@ static rt_status complete(rt_solver *s) {
   if (s->queued) {
     const int r = s->queued;
     s->queued = 0;
-    if ((st = enqueue_pass(s, r))) return st;
+    if ((st = enqueue_steps(s, r))) return st;
   }
   return RT_OK;
 }
@@ -1059,22 +1069,24 @@ extern "C" rt_status rt_sweep_flops(rt_solver *s, double *flops_per_launch) {
 extern "C" rt_status rt_set_pipeline(rt_solver *s, int on) {
   if (!s) return fail(nullptr, RT_ERR_ARG, "rt_set_pipeline: NULL handle");
   HIP_TRY(s, hipSetDevice(s->device));
+  if (on < 0 || on > 2) return fail(s, RT_ERR_ARG, "rt_set_pipeline: 0 (off), 1 (auto) or 2 (always)");
   if (!on && s->pipe) {
     if (rt_status st = complete(s)) return st;  // leave the positions aligned
   }
-  s->pipe = on != 0;
+  s->pipe = on;
   return RT_OK;
 }
 
 extern "C" rt_status rt_get_pipeline(rt_solver *s, int *on) {
   if (!s || !on) return fail(s, RT_ERR_ARG, "rt_get_pipeline: bad argument");
-  *on = s->pipe ? 1 : 0;
+  *on = s->pipe;
   return RT_OK;
 }
 
 extern "C" rt_status rt_set_time_block(rt_solver *s, int steps_per_pass) {
   if (!s) return fail(nullptr, RT_ERR_ARG, "rt_set_time_block: NULL handle");
-  if (steps_per_pass < 1 || steps_per_pass > kMaxTimeBlock)
+  if (steps_per_pass < 1 || steps_per_pass > kMaxTimeBlock ||
+      (steps_per_pass > 8 && steps_per_pass != 12 && steps_per_pass != 16))
     return fail(s, RT_ERR_ARG, "rt_set_time_block: steps per pass must be 1.." + std::to_string(kMaxTimeBlock));
   s->T = steps_per_pass;
   return RT_OK;

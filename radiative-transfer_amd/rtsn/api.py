@@ -377,15 +377,15 @@ class Solver:
         _check(lib().rt_set_time_block(self._h, int(steps_per_pass)), "rt_set_time_block", self._h)
 
     @property
-    def pipeline(self) -> bool:
-        """Pipelined (staggered-segment) schedule on/off (rt_set_pipeline)."""
+    def pipeline(self) -> int:
+        """Pipelined (staggered-segment) schedule: 0 off, 1 auto, 2 always (rt_set_pipeline)."""
         v = C.c_int()
         _check(lib().rt_get_pipeline(self._h, C.byref(v)), "rt_get_pipeline", self._h)
-        return bool(v.value)
+        return v.value
 
     @pipeline.setter
-    def pipeline(self, on: bool):
-        _check(lib().rt_set_pipeline(self._h, int(bool(on))), "rt_set_pipeline", self._h)
+    def pipeline(self, mode):
+        _check(lib().rt_set_pipeline(self._h, int(mode)), "rt_set_pipeline", self._h)
 
     def sweep_traffic(self):
         b = C.c_double()

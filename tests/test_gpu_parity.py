@@ -114,7 +114,7 @@ def test_schemes_and_boundaries(rtsn_mod, oracle_mod, ts, bc_left, bc_right, tb,
     orc.solve()
     with rtsn_mod.Solver(to_rt(p)) as gpu:
         gpu.time_block = tb
-        gpu.pipeline = pipe
+        gpu.pipeline = 2 if pipe else 0
         gpu.solve()
         compare_all(gpu, orc)
 
@@ -147,7 +147,7 @@ def test_line_counts(rtsn_mod, oracle_mod, M, G):
 
 
 @pytest.mark.parametrize("pipe", [True, False])
-@pytest.mark.parametrize("tb,steps", [(1, 1), (1, 3), (2, 4), (3, 3), (3, 5), (4, 4), (4, 9)])
+@pytest.mark.parametrize("tb,steps", [(1, 1), (1, 3), (2, 4), (3, 3), (3, 5), (4, 4), (4, 9), (6, 13), (8, 17)])
 def test_random_state_long_lines(rtsn_mod, oracle_mod, tb, steps, pipe):
     """BDF2 steps from a random state (seed 20261015, psi0 = B U[0.5,1.5))
     on 20k-cell lines cut into many segments: the deferred cross-segment
@@ -165,10 +165,34 @@ def test_random_state_long_lines(rtsn_mod, oracle_mod, tb, steps, pipe):
     orc.solve()
     with rtsn_mod.Solver(to_rt(p), g_lo=lo, g_hi=hi) as gpu:
         gpu.time_block = tb
-        gpu.pipeline = pipe
+        gpu.pipeline = 2 if pipe else 0
         gpu.set_ends(ends)
         gpu.solve()
         compare_all(gpu, orc)
+
+
+@pytest.mark.parametrize("ts,tb,steps", [(3, 12, 13), (3, 16, 17), (3, 8, 16), (2, 16, 40), (1, 16, 40),
+                                         (2, 12, 30), (1, 5, 11)])
+def test_large_time_blocks(rtsn_mod, oracle_mod, ts, tb, steps):
+    """Pipelined passes of up to 16 fused steps (and their aligned remainder)
+    on many-segment lines with a random start state."""
+    p = load(oracle_mod, "llnl_slab_test.prm", N=6000, M=4, max_timesteps=steps, use_correction=1, V=5.994,
+             ts_method=ts, bc_left=2)
+    p["dx"] = p["X"] / p["N"]
+    p["psi_source"] = np.full((p["M"], p["G"]), 0.5)
+    lo, hi = 40, 56
+    orc = oracle_mod.OracleSolver(p, g_lo=lo, g_hi=hi)
+    B = orc.groups()["B"][lo:hi]
+    rng = np.random.default_rng(SEED + tb)
+    ends = B[None, :, None, None] * rng.uniform(0.5, 1.5, size=(p["M"], hi - lo, p["N"], 2))
+    orc.set_ends(ends)
+    orc.solve()
+    with rtsn_mod.Solver(to_rt(p), g_lo=lo, g_hi=hi) as gpu:
+        gpu.time_block = tb
+        gpu.pipeline = 2
+        gpu.set_ends(ends)
+        gpu.solve()
+        compare_all(gpu, orc, plus_vs_group=ts == 3)
 
 
 @pytest.mark.parametrize("toggle", [False, True])
@@ -179,7 +203,7 @@ def test_time_block_switching(rtsn_mod, oracle_mod, toggle):
     p = load(oracle_mod, "llnl_slab_test.prm", N=3000, M=8, use_correction=1, V=5.994, bc_left=2)
     p["dx"] = p["X"] / p["N"]
     p["psi_source"] = np.full((p["M"], p["G"]), 0.25)
-    plan = [(3, 2), (2, 3), (4, 4), (1, 1), (3, 6)]  # (time block, steps)
+    plan = [(3, 2), (2, 3), (4, 4), (1, 1), (7, 7), (5, 2)]  # (time block, steps)
     p["max_timesteps"] = sum(n for _, n in plan)
     orc = oracle_mod.OracleSolver(p)
     orc.solve()
@@ -187,7 +211,7 @@ def test_time_block_switching(rtsn_mod, oracle_mod, toggle):
         for k, (tb, n) in enumerate(plan):
             gpu.time_block = tb
             if toggle:
-                gpu.pipeline = k % 2 == 0
+                gpu.pipeline = 2 if k % 2 == 0 else 0
             gpu.advance(n)
             if k == 2:
                 gpu.psi()  # a read-out in the middle finalizes the pending correction
@@ -205,6 +229,8 @@ def test_pipeline_long_run_many_segments(rtsn_mod, oracle_mod, ts):
     orc = oracle_mod.OracleSolver(p)
     orc.solve()
     with rtsn_mod.Solver(to_rt(p)) as gpu:
+        gpu.pipeline = 2
+        gpu.time_block = 4
         _, segs = gpu.sweep_geometry()
         assert segs > 4
         for n in (5, 17, 8, 15):
@@ -215,7 +241,10 @@ def test_pipeline_long_run_many_segments(rtsn_mod, oracle_mod, ts):
 def test_time_block_range(rtsn_mod):
     d = rtsn_mod.params_default()
     with rtsn_mod.Solver(d) as s:
-        for bad in (0, 5, -1):
+        for ok in (1, 4, 8, 12, 16):
+            s.time_block = ok
+            assert s.time_block == ok
+        for bad in (0, 9, 13, 17, -1):
             with pytest.raises(rtsn_mod.RtError) as e:
                 s.time_block = bad
             assert e.value.status == 8
