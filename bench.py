@@ -225,9 +225,8 @@ def run_rank(solver, p: dict, steps: int, warmup: int, world: int, device, shard
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    # defaults are whole passes of the default time block (4 steps per pass), so that the
-    # timed region is 2 steady-state passes (each applying the previous pass's correction)
-    ap.add_argument("--steps", type=int, default=8)
+    # defaults: the timed region is 2 steady-state passes (steps are rounded up to whole passes)
+    ap.add_argument("--steps", type=int, default=0, help="timed steps (default: two passes)")
     ap.add_argument("--warmup", type=int, default=-1,
                     help="untimed steps before timing (default: fill the pipeline plus one pass)")
     ap.add_argument("--variant", choices=["v0", "corr"], default="v0")
@@ -265,7 +264,7 @@ def main():
         warmup = solver.sweep_geometry()[1] * tb if solver.pipeline else tb
     # whole passes only: steps are launched in passes of tb (a remainder would be
     # queued until the next read-out, outside the timed region)
-    steps = -(-args.steps // tb) * tb
+    steps = -(-args.steps // tb) * tb if args.steps > 0 else 2 * tb
     warmup = -(-warmup // tb) * tb
     line, _ = run_rank(solver, p, steps, warmup, world, device, info, args.scaling)
     line["roofline"]["traffic"] = load_traffic(args.variant, solver.time_block)

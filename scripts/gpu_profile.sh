@@ -13,7 +13,7 @@ T=$(python3 -c "import json;print([json.loads(l) for l in open('gpurun_out/prof_
 i=0
 for pmc in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU" "GRBM_GUI_ACTIVE SQ_INSTS_SALU SQ_INSTS_VMEM SQ_INSTS_LDS"; do
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --pmc $pmc -d gpurun_out/pmc_${V}_$i -o run --output-format csv -- python3 $B --steps $((2*T)) > gpurun_out/pmc_${V}_$i.log 2>&1 || { tail -5 gpurun_out/pmc_${V}_$i.log; exit 1; }
+  timeout -k 10 300 rocprofv3 --pmc $pmc -d gpurun_out/pmc_${V}_$i -o run --output-format csv -- python3 $B > gpurun_out/pmc_${V}_$i.log 2>&1 || { tail -5 gpurun_out/pmc_${V}_$i.log; exit 1; }
 done
 python3 scripts/pmc_summary.py ${V}_t$T gpurun_out/pmc_${V}_1 gpurun_out/pmc_${V}_2 gpurun_out/pmc_${V}_3 gpurun_out/pmc_${V}_4
 cp profiles/pmc_${V}_t$T.json gpurun_out/
