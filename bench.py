@@ -109,7 +109,41 @@ def shard(scaling: str, groups: int, world: int, rank: int):
     return groups, lo, min(groups, lo + per)
 
 
-def run_rank(solver, p: dict, steps: int, warmup: int, world: int, device, shard_info, scaling: str):
+def gather_results(solver, N: int, world: int, shard_info, shards, device):
+    """All-gather of the per-rank result blocks (RCCL on the GPU box, gloo in
+    the CPU tests): returns {"phi", "F", "phi_plus"} as (N, G_total) tensors and
+    {"left", "right", "balance"} as (G_total,) tensors."""
+    import torch
+    import torch.distributed as dist
+
+    G_total, g_lo, g_hi = shard_info
+    shards = shards or [(g_lo, g_hi)]
+    Gl = g_hi - g_lo
+    Gmax = max(hi - lo for lo, hi in shards)
+    block = torch.zeros(3, N, Gmax, dtype=torch.float64, device=device)
+    mom = torch.empty(3, N * Gl, dtype=torch.float64, device=device)
+    solver.moments_device(mom[0], mom[1], mom[2])
+    left, right = solver.compute_group_ends()
+    bal = solver.compute_balance()
+    solver.synchronize()
+    block[:, :, :Gl] = mom.view(3, N, Gl)
+    small = torch.zeros(3, Gmax, dtype=torch.float64, device=device)
+    small[:, :Gl] = torch.as_tensor(np.stack([left, right, bal]), device=device)
+    if world > 1:
+        big = [torch.empty_like(block) for _ in range(world)]
+        dist.all_gather(big, block)
+        sm = [torch.empty_like(small) for _ in range(world)]
+        dist.all_gather(sm, small)
+    else:
+        big, sm = [block], [small]
+    fields = torch.cat([big[r][:, :, :hi - lo] for r, (lo, hi) in enumerate(shards)], dim=2)
+    scal = torch.cat([sm[r][:, :hi - lo] for r, (lo, hi) in enumerate(shards)], dim=1)
+    return {"phi": fields[0], "F": fields[1], "phi_plus": fields[2],
+            "left": scal[0], "right": scal[1], "balance": scal[2]}
+
+
+def run_rank(solver, p: dict, steps: int, warmup: int, world: int, device, shard_info, scaling: str,
+             scaling_shards=None):
     """Warmup, K timed steps between barrier + device sync, max over ranks,
     then the absorption all-reduce.  Collectives go through torch.distributed
     on whatever backend is initialised (RCCL on the GPU box, gloo in the CPU
@@ -155,6 +189,13 @@ def run_rank(solver, p: dict, steps: int, warmup: int, world: int, device, shard
     if world > 1:
         dist.all_reduce(absorb)
     finite = bool(torch.isfinite(absorb).all().item())  # see DESIGN.md §5: the reference's BDF2 grows ~10^3 per step on SL
+
+    # end-of-run gather: every rank's phi, F, phi_plus (N x G_local, g
+    # fastest) and its group ends and balance, assembled into the reference's (N, G)
+    # / (G) arrays on every rank; ragged shards are padded to the largest
+    t2 = time.perf_counter()
+    gathered = gather_results(solver, p["N"], world, shard_info, scaling_shards, device)
+    gather_ms = 1e3 * (time.perf_counter() - t2)
 
     t = torch.tensor([wall, kern_ms / max(nlaunch, 1)], dtype=torch.float64, device=device)
     if world > 1:
@@ -218,8 +259,10 @@ def run_rank(solver, p: dict, steps: int, warmup: int, world: int, device, shard
                      "frac": achieved_fl / FP64_PEAK},
         },
         "state_finite": finite,
+        "gather": {"fields": "phi, F, phi_plus (N x G) + left/right ends, balance (G)",
+                   "bytes_per_rank": 8 * 3 * p["N"] * (g_hi - g_lo), "ms": gather_ms},
     }
-    return line, absorb
+    return line, absorb, gathered
 
 
 def main():
@@ -266,7 +309,8 @@ def main():
     # queued until the next read-out, outside the timed region)
     steps = -(-args.steps // tb) * tb if args.steps > 0 else 2 * tb
     warmup = -(-warmup // tb) * tb
-    line, _ = run_rank(solver, p, steps, warmup, world, device, info, args.scaling)
+    shards = [shard(args.scaling, args.groups, world, r)[1:] for r in range(world)]
+    line, _, _ = run_rank(solver, p, steps, warmup, world, device, info, args.scaling, shards)
     line["roofline"]["traffic"] = load_traffic(args.variant, solver.time_block)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(args.variant)

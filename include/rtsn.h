@@ -137,6 +137,10 @@ rt_status rt_get_quadrature(rt_solver *s, double *mu, double *wt);
 rt_status rt_get_psi_source(rt_solver *s, double *psi_source);
 
 /* ---- device-side hooks (multi-GPU, measurement) ------------------------- */
+/* rt_get_moments into DEVICE buffers of G_local*N doubles (g + G_local*c), on
+ * the handle's stream, asynchronous: the per-rank blocks of the end-of-run
+ * gather; any NULL skipped. */
+rt_status rt_get_moments_device(rt_solver *s, double *d_phi, double *d_F, double *d_phi_plus);
 /* Group-summed absorption rate A(x_c) = sum_{g local} rho kappa_g phi_g(c),
  * written to a DEVICE buffer of N doubles on the handle's stream: the per-rank
  * partial of the group-sum all-reduce (north_star; the reference has no

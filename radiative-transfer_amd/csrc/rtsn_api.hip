@@ -903,6 +903,19 @@ extern "C" rt_status rt_get_moments(rt_solver *s, double *phi, double *F, double
   return RT_OK;
 }
 
+extern "C" rt_status rt_get_moments_device(rt_solver *s, double *d_phi, double *d_F, double *d_phi_plus) {
+  if (!s) return fail(nullptr, RT_ERR_ARG, "rt_get_moments_device: NULL handle");
+  HIP_TRY(s, hipSetDevice(s->device));
+  rt_status st = compute_moments(s);
+  if (st) return st;
+  const size_t GN = static_cast<size_t>(s->Gl) * s->p.N;
+  const double *m = static_cast<const double *>(s->mom.p);
+  double *dst[3] = {d_phi, d_F, d_phi_plus};
+  for (int k = 0; k < 3; ++k)
+    if (dst[k]) HIP_TRY(s, hipMemcpyAsync(dst[k], m + k * GN, sizeof(double) * GN, hipMemcpyDeviceToDevice, s->stream));
+  return RT_OK;
+}
+
 // boundary rows: [0] half0 k=0, [1] half0 k=N-1, [2] half1 k=0, [3] half1 k=N-1
 static rt_status fetch_rows(rt_solver *s, std::vector<double> &rows) {
   if (rt_status st = finalize(s)) return st;

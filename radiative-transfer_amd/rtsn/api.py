@@ -94,6 +94,7 @@ def lib():
             getattr(L, name).argtypes = [vp, dp]
         L.rt_set_ends.argtypes = [vp, dp]
         L.rt_get_moments.argtypes = [vp, dp, dp, dp]
+        L.rt_get_moments_device.argtypes = [vp, vp, vp, vp]
         L.rt_get_group_ends.argtypes = [vp, dp, dp]
         L.rt_get_group_data.argtypes = [vp, dp, dp, dp, dp]
         L.rt_get_quadrature.argtypes = [vp, dp, dp]
@@ -345,6 +346,21 @@ class Solver:
     def group_absorption_device(self, d_out_ptr: int):
         _check(lib().rt_group_absorption_device(self._h, C.cast(C.c_void_p(d_out_ptr), C.POINTER(C.c_double))),
                "rt_group_absorption_device", self._h)
+
+    def moments_device(self, phi, F=None, phi_plus=None):
+        """rt_get_moments_device into contiguous float64 CUDA tensors of N*G_local
+        elements (layout g + G_local*c), on the solver's stream."""
+        import torch
+        ptrs = []
+        for t in (phi, F, phi_plus):
+            if t is None:
+                ptrs.append(None)
+                continue
+            if not (isinstance(t, torch.Tensor) and t.is_cuda and t.dtype == torch.float64
+                    and t.is_contiguous() and t.numel() == self.N * self.G):
+                raise ValueError("moments_device: need contiguous float64 CUDA tensors of N*G_local elements")
+            ptrs.append(t.data_ptr())
+        _check(lib().rt_get_moments_device(self._h, *ptrs), "rt_get_moments_device", self._h)
 
     def group_absorption(self, out):
         """Group-summed absorption into a contiguous float64 torch tensor of N

@@ -91,6 +91,18 @@ class OracleShard:
     def sweep_time(self):
         return self.ms, self.n
 
+    def moments_device(self, phi, F=None, phi_plus=None):
+        ph, f, pp = self.s.moments()  # (G_local, N) -> N x G_local, g fastest
+        for t, a in ((phi, ph), (F, f), (phi_plus, pp)):
+            if t is not None:
+                t.copy_(torch.from_numpy(np.ascontiguousarray(a.T).ravel()))
+
+    def compute_group_ends(self):
+        return self.s.group_ends()
+
+    def compute_balance(self):
+        return self.s.balance()
+
     def group_absorption(self, out):
         phi, _, _ = self.s.moments()
         kap = self.s.groups()["kappa"][self.g_lo:self.g_hi]
@@ -111,8 +123,11 @@ def _worker(rank, world, port, scaling, groups, steps, outdir):
         info = bench.shard(scaling, groups, world, rank)
         p = small_params(info[0])
         solver = OracleShard(p, info[1], info[2])
-        line, absorb = bench.run_rank(solver, p, steps, 1, world, torch.device("cpu"), info, scaling)
+        shards = [bench.shard(scaling, groups, world, r)[1:] for r in range(world)]
+        line, absorb, gathered = bench.run_rank(solver, p, steps, 1, world, torch.device("cpu"), info, scaling,
+                                                shards)
         np.save(os.path.join(outdir, f"absorb{rank}.npy"), absorb.numpy())
+        np.savez(os.path.join(outdir, f"gathered{rank}.npz"), **{k: v.numpy() for k, v in gathered.items()})
         with open(os.path.join(outdir, f"line{rank}.json"), "w") as f:
             json.dump({"line": line, "info": list(info), "wall_ms": solver.ms}, f)
     finally:
@@ -124,31 +139,40 @@ def _run(tmp_path, scaling, groups, steps=2, world=2):
                        nprocs=world, join=True, start_method="spawn")
     lines = [json.load(open(tmp_path / f"line{r}.json")) for r in range(world)]
     absorbs = [np.load(tmp_path / f"absorb{r}.npy") for r in range(world)]
-    return lines, absorbs
+    gathered = [dict(np.load(tmp_path / f"gathered{r}.npz")) for r in range(world)]
+    return lines, absorbs, gathered
 
 
-def full_absorption(G_total: int, steps: int) -> np.ndarray:
+def full_run(G_total: int, steps: int):
+    """Single-process oracle over all groups: absorption and the gathered fields."""
     p = small_params(G_total)
     s = oracle.OracleSolver(oracle_dict(p))
     s.run_substeps(0, 4 * (steps + 1))  # warmup 1 + timed steps
-    phi, _, _ = s.moments()
+    phi, F, pp = s.moments()
     kap = s.groups()["kappa"]
-    return (p["rho"] * kap[:, None] * phi).sum(axis=0)
+    left, right = s.group_ends()
+    ref = {"phi": phi.T, "F": F.T, "phi_plus": pp.T, "left": left, "right": right, "balance": s.balance()}
+    return (p["rho"] * kap[:, None] * phi).sum(axis=0), ref
 
 
 @pytest.mark.parametrize("scaling,groups", [("weak", 3), ("strong", 5)])
 def test_two_rank_group_shards(tmp_path, scaling, groups):
     steps = 2
-    lines, absorbs = _run(tmp_path, scaling, groups, steps)
+    lines, absorbs, gathered = _run(tmp_path, scaling, groups, steps)
     G_total = groups * 2 if scaling == "weak" else groups
     # shards tile [0, G_total) without overlap
     spans = sorted(tuple(l["info"][1:]) for l in lines)
     assert spans[0][0] == 0 and spans[-1][1] == G_total and spans[0][1] == spans[1][0]
     # all-reduced absorption == single-process oracle over all groups
-    ref = full_absorption(G_total, steps)
+    ref, fields = full_run(G_total, steps)
     for a in absorbs:
         np.testing.assert_array_equal(a, absorbs[0])
         np.testing.assert_allclose(a, ref, rtol=1e-13, atol=0)
+    # end-of-run all-gather: every rank holds the full (N, G) fields and (G) vectors,
+    # equal (bitwise: same per-group arithmetic) to the single-process oracle
+    for g in gathered:
+        for k, v in fields.items():
+            np.testing.assert_array_equal(g[k], v, err_msg=k)
     # the JSON line: whole-job updates over the max-over-ranks wall time
     line = lines[0]["line"]
     for k in ("value", "ms_per_step", "n_gpus", "state_finite"):

@@ -304,3 +304,17 @@ def test_group_absorption(rtsn_mod, oracle_mod):
         phi = s.moments()[0]
         sig = p["rho"] * p["group_kappa"]
         np.testing.assert_allclose(out.cpu().numpy(), (sig[:, None] * phi).sum(axis=0), rtol=1e-12)
+
+
+def test_moments_device(rtsn_mod, oracle_mod):
+    """rt_get_moments_device (the gather's per-rank block) equals rt_get_moments."""
+    import torch
+    p = to_rt(load(oracle_mod, "llnl_slab_test.prm"))
+    with rtsn_mod.Solver(p, g_lo=7, g_hi=70) as s:
+        s.solve()
+        t = torch.empty(3, s.N * s.G, dtype=torch.float64, device="cuda")
+        s.moments_device(t[0], t[1], t[2])
+        s.synchronize()
+        host = s.moments()
+        for k in range(3):
+            np.testing.assert_array_equal(t[k].cpu().numpy().reshape(s.N, s.G).T, host[k])
