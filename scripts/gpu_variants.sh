@@ -4,6 +4,6 @@ export TMPDIR=/tmp
 mkdir -p gpurun_out
 for v in base $VARIANTS; do
   if [ "$v" = base ]; then lib=radiative-transfer_amd/lib/librtsn.so; else lib=radiative-transfer_amd/variants/$v/librtsn.so; fi
-  RTSN_LIB=$PWD/$lib timeout -k 10 300 python bench.py --no-cpu-baseline --steps 3 > gpurun_out/var_$v.log 2>&1 || { tail -5 gpurun_out/var_$v.log; exit 1; }
-  echo "$v $(python3 -c "import json;d=json.loads(open('gpurun_out/var_$v.log').read().strip().splitlines()[-1]);print(round(d['ms_per_step'],2),'ms', d['config']['sweep_workgroups'],'wg', round(d['roofline']['frac'],3))")"
+  RTSN_LIB=$PWD/$lib timeout -k 10 300 python bench.py --no-cpu-baseline > gpurun_out/var_$v.log 2>&1 || { tail -5 gpurun_out/var_$v.log; exit 1; }
+  echo "$v $(python3 -c "import json;d=[json.loads(x) for x in open('gpurun_out/var_$v.log') if x.startswith('{')][-1];print(round(d['ms_per_step'],2),'ms', d['config']['sweep_workgroups'],'wg', round(d['roofline']['frac'],3))")"
 done
