@@ -67,23 +67,34 @@ def slab_params(G_total: int, variant: str, N: int = 1_000_000, M: int = 64) -> 
 
 
 def cpu_baseline(variant: str) -> dict:
-    """The oracle on a bounded sample: all 64 angles of one group, 2.5e5 cells, 1 BDF2 step."""
+    """The C oracle (the reference's algorithm restated, solver.cpp loop order) on bounded
+    samples of the SL workload: all 64 angles, N = 250000 cells, 1 BDF2 step, for 1 group
+    on 1 thread and for one group per thread with OpenMP over the lines of each direction
+    on up to 16 host cores (the GPU box's CPU share)."""
     sys.path.insert(0, str(REPO / "oracle"))
     import oracle
     oracle.build()
-    G, N, g = 128, 250_000, 64
+    G, N = 128, 250_000
     p = slab_params(G, variant, N=N)
     q = dict(p)
     q.update(bc_left=p["bc_left_indicator"], bc_right=p["bc_right_indicator"], dx=p["X"] / N,
              have_group_bounds=0, have_group_kappa=1, prm_found=1)
-    s = oracle.OracleSolver(q, g_lo=g, g_hi=g + 1)
-    t0 = time.perf_counter()
-    s.solve()
-    dt = time.perf_counter() - t0
-    upd = 4.0 * q["M"] * N
-    return {"value": upd / dt, "unit": "cell-angle-group updates/s", "cores": 1, "kind": "port",
-            "sample": f"oracle/rt_oracle.c (single-threaded restatement of solver.cpp), SL {variant}: "
-                      f"M=64, 1 of 128 groups (g={g}), N={N}, 1 BDF2 step = {upd:.3g} updates in {dt:.2f} s"}
+
+    def timed(g_lo, g_hi, threads):
+        s = oracle.OracleSolver(q, g_lo=g_lo, g_hi=g_hi)
+        s.set_threads(threads)
+        t0 = time.perf_counter()
+        s.solve()
+        return 4.0 * q["M"] * N * (g_hi - g_lo), time.perf_counter() - t0
+
+    u1, t1 = timed(64, 65, 1)
+    cores = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", "16")), len(os.sched_getaffinity(0))))
+    un, tn = timed(64 - cores // 2, 64 - cores // 2 + cores, cores)
+    return {"value": un / tn, "unit": "cell-angle-group updates/s", "cores": cores, "kind": "port",
+            "single_thread_value": u1 / t1,
+            "sample": f"oracle/rt_oracle.c (restatement of solver.cpp, gcc -O2), SL {variant}: M=64, N={N}, "
+                      f"1 BDF2 step; {cores} groups on {cores} OpenMP threads = {un:.3g} updates in {tn:.2f} s; "
+                      f"1 group on 1 thread = {u1:.3g} updates in {t1:.2f} s"}
 
 
 def load_traffic(variant: str, tb: int):

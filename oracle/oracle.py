@@ -62,6 +62,8 @@ def lib():
         L.orc_destroy.argtypes = [C.c_void_p]
         L.orc_solve.argtypes = [C.c_void_p]
         L.orc_run_substeps.argtypes = [C.c_void_p, C.c_int, C.c_int]
+        L.orc_set_threads.argtypes = [C.c_void_p, C.c_int]
+        L.orc_set_threads.restype = None
         L.orc_num_groups_local.argtypes = [C.c_void_p]
         for name in ("orc_get_psi", "orc_get_ends", "orc_set_ends", "orc_get_psi_source"):
             getattr(L, name).argtypes = [C.c_void_p, dp]
@@ -159,6 +161,10 @@ class OracleSolver:
         if h:
             lib().orc_destroy(h)
             self._h = None
+
+    def set_threads(self, n: int):
+        """OpenMP threads over the lines of a direction (results do not depend on it)."""
+        lib().orc_set_threads(self._h, int(n))
 
     def solve(self):
         st = lib().orc_solve(self._h)

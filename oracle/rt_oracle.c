@@ -511,6 +511,7 @@ struct orc_solver {
   int M, G, N, g_lo, Gl;
   double dx, dt;
   int literal_half;
+  int threads;        /* OpenMP threads over the lines of a direction (orc_set_threads); 1 = serial */
   double ac;          /* RADIATION_CONSTANT_A * c (solver.h:128, correction.h:25) */
   double *mu, *wt;
   double *e_edge, *e_ave, *de_ave;
@@ -605,9 +606,10 @@ static void corr_compute(orc_solver *s) {
   corr_components(s);
   corr_terms(s);
   double beta = s->p.V / C_LIGHT;
+#pragma omp parallel for collapse(2) schedule(static) num_threads(s->threads) if (s->threads > 1)
   for (int i = 0; i < s->M; ++i) {
-    double mu = s->mu[i];
     for (int gl = 0; gl < s->Gl; ++gl) {
+      double mu = s->mu[i];
       int g = s->g_lo + gl;
       for (int c = 0; c < s->N; ++c) {
         double val = (s->cor1[g] * PSI(s, i, gl, c) + s->cor2[g]) * mu * beta;
@@ -641,6 +643,8 @@ static void *xcalloc(size_t n, size_t sz, int *ok) {
 }
 
 /* Solver::Solver (solver.cpp:46-188) */
+void orc_set_threads(orc_solver *s, int threads) { s->threads = threads > 0 ? threads : 1; }
+
 orc_solver *orc_create(const orc_params *pin, int half_copy_literal, int g_lo, int g_hi, int *status) {
   *status = ORC_OK;
   if (pin->M <= 0 || (pin->M % 2) != 0 || pin->G <= 0 || pin->N <= 0 ||
@@ -652,6 +656,7 @@ orc_solver *orc_create(const orc_params *pin, int half_copy_literal, int g_lo, i
   if (g_hi <= 0) g_hi = pin->G;
   if (g_lo < 0 || g_lo >= g_hi || g_hi > pin->G) { *status = ORC_ERR_PARAM; return NULL; }
   orc_solver *s = (orc_solver *)calloc(1, sizeof(orc_solver));
+  if (s) s->threads = 1;
   int ok = 1;
   s->p = *pin;
   int M = pin->M, G = pin->G, N = pin->N;
@@ -900,9 +905,61 @@ static int equilibrium_sources(orc_solver *s) {
 static size_t ends_bytes(const orc_solver *s) { return sizeof(double) * 2 * (size_t)s->M * s->Gl * s->N; }
 
 /* One iteration _it of Solver::solve's time loop (solver.cpp:606-819) */
-static int solve_iteration(orc_solver *s, int it) {
+/* One line (i, g) of one substep: boundary value (solver.cpp:635-697) and the
+ * cell sweep (:699-816).  *half_pending: a mu<0 CN cell ran (lazy :733 copy). */
+static int sweep_line(orc_solver *s, int it, int i, int gl, int *half_pending) {
   const int M = s->M, N = s->N, ts = s->p.ts_method;
-  const double dt = s->dt;
+  const double dt = s->dt, mu = s->mu[i];
+  const int g = s->g_lo + gl;
+  double bdry = 0.;
+  if (mu < 0.) {
+    switch (s->p.bc_right) {
+      case 0: bdry = 0.; break;
+      case 2: bdry = 0.; break; /* TODO in the reference */
+      case 1: bdry = s->psi_source[i * s->G + g]; break;
+      default: return ORC_ERR_PARAM;
+    }
+  } else {
+    switch (s->p.bc_left) {
+      case 0: /* falls through to source (:668-676) */
+      case 1: bdry = s->psi_source[i * s->G + g]; break;
+      case 2: {
+        int diff = i - (M / 2);
+        int m_neg = (M / 2) - 1 - diff;
+        bdry = E4(s->ends, s, m_neg, gl, 0, 0);
+        break;
+      }
+      default: return ORC_ERR_PARAM;
+    }
+  }
+  sweep_t w = {bdry, bdry, bdry};
+  for (int j = 0; j < N; ++j) {
+    int cell = mu < 0 ? N - j - 1 : j;
+    switch (ts) {
+      case 1: cell_be(s, &w, cell, i, gl, dt, mu); break;
+      case 2: cell_cn(s, &w, cell, i, gl, dt, mu); break;
+      case 3:
+        switch (it % 4) {
+          case 0: cell_be(s, &w, cell, i, gl, dt / 2., mu); break;
+          case 1:
+            cell_cn(s, &w, cell, i, gl, dt / 2., mu);
+            if (mu < 0) {
+              if (s->literal_half) memcpy(s->half_ends, s->ends, ends_bytes(s));
+              else *half_pending = 1;
+            }
+            break;
+          case 2: cell_be(s, &w, cell, i, gl, dt / 2., mu); break;
+          case 3: cell_bdf(s, &w, cell, i, gl, dt / 2., mu); break;
+        }
+        break;
+      default: return ORC_ERR_PARAM;
+    }
+  }
+  return ORC_OK;
+}
+
+static int solve_iteration(orc_solver *s, int it) {
+  const int M = s->M, ts = s->p.ts_method;
   corr_compute(s);                                           /* :608 */
   if (s->p.include_validation && !corr_validate(s)) return ORC_ERR_VALIDATION; /* :609-612 */
   memcpy(s->B, s->cB, sizeof(double) * s->G);                /* :614 */
@@ -916,53 +973,16 @@ static int solve_iteration(orc_solver *s, int it) {
       memcpy(s->half_ends, s->ends, ends_bytes(s));
       half_copy_pending = 0;
     }
+    int err = 0, pend = 0;
+    /* lines (i, g) of one direction are independent (groups never couple, T constant) */
+#pragma omp parallel for schedule(static) num_threads(s->threads) reduction(| : err, pend) if (s->threads > 1 && !s->literal_half)
     for (int gl = 0; gl < s->Gl; ++gl) {
-      int g = s->g_lo + gl;
-      double bdry = 0.;
-      if (mu < 0.) {
-        switch (s->p.bc_right) {
-          case 0: bdry = 0.; break;
-          case 2: bdry = 0.; break; /* TODO in the reference */
-          case 1: bdry = s->psi_source[i * s->G + g]; break;
-          default: return ORC_ERR_PARAM;
-        }
-      } else {
-        switch (s->p.bc_left) {
-          case 0: /* falls through to source (:668-676) */
-          case 1: bdry = s->psi_source[i * s->G + g]; break;
-          case 2: {
-            int diff = i - (M / 2);
-            int m_neg = (M / 2) - 1 - diff;
-            bdry = E4(s->ends, s, m_neg, gl, 0, 0);
-            break;
-          }
-          default: return ORC_ERR_PARAM;
-        }
-      }
-      sweep_t w = {bdry, bdry, bdry};
-      for (int j = 0; j < N; ++j) {
-        int cell = mu < 0 ? N - j - 1 : j;
-        switch (ts) {
-          case 1: cell_be(s, &w, cell, i, gl, dt, mu); break;
-          case 2: cell_cn(s, &w, cell, i, gl, dt, mu); break;
-          case 3:
-            switch (it % 4) {
-              case 0: cell_be(s, &w, cell, i, gl, dt / 2., mu); break;
-              case 1:
-                cell_cn(s, &w, cell, i, gl, dt / 2., mu);
-                if (mu < 0) {
-                  if (s->literal_half) memcpy(s->half_ends, s->ends, ends_bytes(s));
-                  else half_copy_pending = 1;
-                }
-                break;
-              case 2: cell_be(s, &w, cell, i, gl, dt / 2., mu); break;
-              case 3: cell_bdf(s, &w, cell, i, gl, dt / 2., mu); break;
-            }
-            break;
-          default: return ORC_ERR_PARAM;
-        }
-      }
+      int hp = 0;
+      err |= sweep_line(s, it, i, gl, &hp);
+      pend |= hp;
     }
+    if (err) return ORC_ERR_PARAM;
+    if (pend) half_copy_pending = 1;
   }
   if (half_copy_pending) memcpy(s->half_ends, s->ends, ends_bytes(s));
   return ORC_OK;

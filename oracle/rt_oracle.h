@@ -65,6 +65,8 @@ typedef struct orc_solver orc_solver;
  * Groups [g_lo, g_hi) are swept; all G groups' coefficients are computed.
  * g_hi <= 0 means G. */
 orc_solver *orc_create(const orc_params *p, int half_copy_literal, int g_lo, int g_hi, int *status);
+/* OpenMP threads over the lines of one direction (default 1; results do not depend on it) */
+void orc_set_threads(orc_solver *s, int threads);
 void orc_destroy(orc_solver *s);
 /* Solver::solve (solver.cpp:590-823). Returns ORC_ERR_VALIDATION where the
  * reference would hit assert(validate_correction()). */

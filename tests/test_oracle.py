@@ -146,3 +146,19 @@ def test_group_subset_is_independent(oracle_mod):
     part = oracle_mod.OracleSolver(p, g_lo=30, g_hi=70)
     part.solve()
     assert np.array_equal(part.ends(), full.ends()[:, 30:70])
+
+
+def test_threaded_oracle_bitwise(oracle_mod):
+    """orc_set_threads (the multi-core CPU baseline) does not change any bit."""
+    p = oracle_mod.parse_prm(PRM_DIR / "llnl_slab_test.prm", table_dir=PRM_DIR)
+    p.update(M=8, N=200, V=5.994, bc_left=2, max_timesteps=3)
+    p["psi_source"] = np.ones((8, p["G"]))
+    p["dx"] = p["X"] / p["N"]
+    outs = []
+    for threads in (1, 4):
+        s = oracle_mod.OracleSolver(p)
+        s.set_threads(threads)
+        s.solve()
+        outs.append((s.ends(), s.psi()))
+    np.testing.assert_array_equal(outs[0][0], outs[1][0])
+    np.testing.assert_array_equal(outs[0][1], outs[1][1])
