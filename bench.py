@@ -97,6 +97,35 @@ def cpu_baseline(variant: str) -> dict:
                       f"1 group on 1 thread = {u1:.3g} updates in {t1:.2f} s"}
 
 
+def reference_config_timings() -> dict:
+    """the reference's own llnl_slab_test (M2 G124 N50, 2 BDF2 steps) end to
+    end -- create + solve + moments on the GPU, and the oracle on one core, in the
+    reference's loop order with the per-cell half_ends copy done lazily and literally
+    (solver.cpp:733, quadratic in the state size)."""
+    import rtsn
+    sys.path.insert(0, str(REPO / "oracle"))
+    import oracle
+    oracle.build()
+    prm = REPO / "tests" / "golden" / "prm" / "llnl_slab_test.prm"
+    tdir = str(prm.parent) + "/"
+    out = {"config": "llnl_slab_test.prm (M=2, G=124, N=50, 2 BDF2 steps)"}
+    ph = rtsn.ParameterHandler(prm, table_dir=tdir)
+    for _ in range(2):  # second round timed (first pays module/kernel loading)
+        t0 = time.perf_counter()
+        with rtsn.Solver(ph) as s:
+            s.solve()
+            s.moments()
+        out["gpu_end_to_end_ms"] = 1e3 * (time.perf_counter() - t0)
+    q = oracle.parse_prm(prm, table_dir=tdir)
+    for literal in (False, True):
+        o = oracle.OracleSolver(q, half_copy_literal=literal)
+        t0 = time.perf_counter()
+        o.solve()
+        o.moments()
+        out["cpu_literal_half_copy_ms" if literal else "cpu_ms"] = 1e3 * (time.perf_counter() - t0)
+    return out
+
+
 def load_traffic(variant: str, tb: int):
     """Measured HBM bytes per sweep launch (rocprofv3 PMC, scripts/gpu_profile.sh) for
     this variant and time block, or None."""
@@ -325,6 +354,7 @@ def main():
     line["roofline"]["traffic"] = load_traffic(args.variant, solver.time_block)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(args.variant)
+        line["reference_config"] = reference_config_timings()
     if rank == 0:
         print(json.dumps(line), flush=True)
     solver.close()
