@@ -128,6 +128,9 @@ rt_status rt_get_moments(rt_solver *s, double *phi, double *F, double *phi_plus)
 rt_status rt_get_group_ends(rt_solver *s, double *left, double *right);
 /* compute_balance + get_balance (solver.cpp:240-284) */
 rt_status rt_get_balance(rt_solver *s, double *balance);
+/* ... with the sources and sinks it is built from (printed by the reference,
+ * solver.cpp:278-279); any NULL skipped */
+rt_status rt_get_balance_terms(rt_solver *s, double *balance, double *sources, double *sinks);
 /* get_e_ave (solver.h:194): all G groups */
 rt_status rt_get_e_ave(rt_solver *s, double *e_ave);
 /* Group data of all G groups: e_edge (G+1), B, dBdT, kappa (G); any NULL skipped. */

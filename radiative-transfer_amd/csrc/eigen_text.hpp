@@ -13,25 +13,30 @@
 
 namespace rtamd {
 
-// data is ColMajor rows x cols; writes the matrix followed by std::endl
-inline bool write_eigen_text(const std::string &path, const double *data, size_t rows, size_t cols) {
-  std::ofstream file(path);
-  if (!file.is_open()) return false;
+// `os << matrix` for data ColMajor rows x cols (no trailing newline)
+inline void write_eigen_text(std::ostream &os, const double *data, size_t rows, size_t cols) {
   size_t width = 0;
   for (size_t k = 0; k < rows * cols; ++k) {
     std::stringstream ss;
-    ss.copyfmt(file);
+    ss.copyfmt(os);
     ss << data[k];
     width = std::max(width, ss.str().size());
   }
   for (size_t i = 0; i < rows; ++i) {
-    if (i) file << "\n";
+    if (i) os << "\n";
     for (size_t j = 0; j < cols; ++j) {
-      if (j) file << " ";
-      file.width(static_cast<std::streamsize>(width));
-      file << data[i + rows * j];
+      if (j) os << " ";
+      os.width(static_cast<std::streamsize>(width));
+      os << data[i + rows * j];
     }
   }
+}
+
+// print_to_file (main.cc:37-57): the matrix followed by std::endl
+inline bool write_eigen_text(const std::string &path, const double *data, size_t rows, size_t cols) {
+  std::ofstream file(path);
+  if (!file.is_open()) return false;
+  write_eigen_text(file, data, rows, cols);
   file << std::endl;
   return true;
 }

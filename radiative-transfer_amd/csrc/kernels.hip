@@ -1,7 +1,8 @@
 // kernels.hip -- CDNA4 (gfx950) kernels of the S_n path.
 //
-// Hot path: sweep_segment_kernel<S, MODE> -- one full time step (BE, CN or the
-// fused 4-substep BDF2 cycle, cell.hpp) of every (direction, group) line.
+// Hot path: sweep_block_kernel<S, T, MODE> -- T full time steps (BE, CN or the
+// fused 4-substep BDF2 cycle) of every (direction, group) line in one pass
+// over HBM, each cell step evaluated as the line's affine map (cell.hpp).
 //
 // Layout in HBM:
 //   E[half][k][l]  double2 (e_in, e_out), half 0 = mu < 0 lines, half 1 = mu > 0,
@@ -9,25 +10,24 @@
 //                  padded to Lpad = 64 Q lines and Nrow = 64 J rows.  A wave
 //                  moves one 1 KiB row per instruction.
 //
-// Parallelisation without in-step synchronisation.  Within a step, a line
-// is the affine recurrence X_{k+1} = A X_k + B d_k + c over its cells, and the
-// step-end state of cell k is R X_k + (data terms), with A, R constant per
-// line (cell.hpp).  Each line is cut into Sg segments of Ls cells; one wave
-// (64 lines) sweeps one segment in a single pass, streaming 16-row chunks
-// through registers with a rolling prefetch.  Segment 0 starts from the true
-// inflow; segment s > 0 starts from X = 0, so its stored state is
-// *provisional*: exact up to the term R A^(k - k_s) X_s, where X_s is the
-// segment's true incoming state.  Every wave publishes its final carried
-// state (its aggregate).  The next step -- or a finalize launch before any
-// read-out -- rebuilds X_s = fold of the previous segments' aggregates with
-// the segment propagator A^Ls and adds the correction while it loads the
-// rows.  No workgroup ever waits for another, so there is nothing to
-// deadlock and nothing to stall; the cost is ~20 FMA per cell for the
-// correction instead of a second compute pass.
+// Parallelisation over cells.  Each line is cut into Sg segments of Ls cells;
+// one wave (64 lines) sweeps one segment, streaming C-row chunks through
+// registers with a rolling prefetch, carrying T states (one per fused step;
+// level t's step-end nodes are level t+1's data).  The state entering
+// segment s > 0 comes from one of two schedules, neither with any
+// inter-workgroup wait:
+//   MODE 2 (pipelined): segments run at staggered time levels, one pass
+//     apart; segment s starts from the exit state segment s-1 published in
+//     the previous launch -- exact, nothing to correct.
+//   MODE 0 (aligned): segment s starts from X = 0, so its stored state is
+//     provisional, exact up to R_T A_T^(k - k_s) Y_s (Y_s its true incoming
+//     state).  fold_kernel rebuilds Y_s from the segments' exit states; the
+//     next pass (or MODE 1, finalize) adds the correction while it loads the
+//     rows, by running the linear part of the map on Y.
 //
 // Reflective left boundary (solver.cpp:677-684): the mu > 0 heads need the
-// mu < 0 outflow of the SAME step, so the two halves go in two launches and
-// the mu > 0 head folds the mu < 0 aggregates of this step.
+// mu < 0 outflow of the same steps: the next chain position (MODE 2), or a
+// second launch after a fold of the mu < 0 exit states (MODE 0).
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -37,7 +37,7 @@
 
 namespace rtamd {
 
-// A wave's 16 rows of one chunk are addressed through a buffer descriptor
+// A wave's C rows of one chunk are addressed through a buffer descriptor
 // built from wave-uniform values: base (SGPR) + row offset (SGPR soffset) +
 // lane*16 (one VGPR), instead of a 64-bit VGPR address per row.
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
@@ -284,7 +284,7 @@ __global__ __launch_bounds__(64) void sweep_block_kernel(SegArgs a) {
   }
   const double *lcp = a.lc + static_cast<size_t>(half) * LC_COUNT * stride + ell;
 
-  // ---- stream the segment in 16-row chunks ----
+  // ---- stream the segment in C-row chunks ----
   const int row_bytes = a.Lpad * static_cast<int>(sizeof(double2));
   const int voff = lane * static_cast<int>(sizeof(double2));
   const double2 *Eh = a.E + static_cast<size_t>(half) * a.Nrow * stride + q * 64;

@@ -964,8 +964,8 @@ extern "C" rt_status rt_get_group_ends(rt_solver *s, double *left, double *right
   return RT_OK;
 }
 
-extern "C" rt_status rt_get_balance(rt_solver *s, double *balance) {
-  if (!s || !balance) return fail(s, RT_ERR_ARG, "rt_get_balance: bad argument");
+extern "C" rt_status rt_get_balance_terms(rt_solver *s, double *balance, double *sources_out, double *sinks_out) {
+  if (!s) return fail(s, RT_ERR_ARG, "rt_get_balance_terms: NULL handle");
   HIP_TRY(s, hipSetDevice(s->device));
   const int N = s->p.N, Gl = s->Gl;
   std::vector<double> phi(static_cast<size_t>(Gl) * N);
@@ -987,16 +987,24 @@ extern "C" rt_status rt_get_balance(rt_solver *s, double *balance) {
         jNp += bnode(s, rows, i, gl, true, 1) * mu * s->wt[i];
       }
     }
+    // sequential sums in the reference's order and association (:262-272)
     const double rk = s->gt.rho[g] * s->gt.kappa[g];
+    const double src_term = rk * ac * std::pow(s->p.T, 4) * dx;
     for (int c = 0; c < N; ++c) {
-      ab += s->gt.rho[g] * s->gt.kappa[g] * phi[static_cast<size_t>(c) * Gl + gl] * dx;
-      sr += s->gt.rho[g] * s->gt.kappa[g] * ac * std::pow(s->p.T, 4) * dx;
+      ab += rk * phi[static_cast<size_t>(c) * Gl + gl] * dx;
+      sr += src_term;
     }
-    (void)rk;
     const double sources = jhp + jNm + sr, sinks = jNp + jhm + ab;
-    balance[gl] = std::fabs(sinks - sources) / sources;
+    if (balance) balance[gl] = std::fabs(sinks - sources) / sources;
+    if (sources_out) sources_out[gl] = sources;
+    if (sinks_out) sinks_out[gl] = sinks;
   }
   return RT_OK;
+}
+
+extern "C" rt_status rt_get_balance(rt_solver *s, double *balance) {
+  if (!s || !balance) return fail(s, RT_ERR_ARG, "rt_get_balance: bad argument");
+  return rt_get_balance_terms(s, balance, nullptr, nullptr);
 }
 
 extern "C" rt_status rt_get_e_ave(rt_solver *s, double *e_ave) {
@@ -1127,7 +1135,7 @@ extern "C" const char *rt_status_string(rt_status st) {
     case RT_ERR_VALIDATION: return "correction validation failed";
     case RT_ERR_NOMEM: return "out of memory";
     case RT_ERR_DEVICE: return "device error";
-    case RT_ERR_TIMEOUT: return "in-kernel wait timed out";
+    case RT_ERR_TIMEOUT: return "timeout (reserved)";
     case RT_ERR_ARG: return "bad argument";
   }
   return "unknown";

@@ -5,6 +5,7 @@
 // ColMajor layouts (psi: i + M(g + G c); phi, F: g + G c).
 #pragma once
 
+#include <ostream>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -22,8 +23,11 @@ class SolverError : public std::runtime_error {
 
 class Solver {
  public:
+  // log: where the reference's solver-side messages go (its cout prints:
+  // solver.cpp:55-187, 278-282, 310, 623; correction.cpp:56-57, 115-116, 301),
+  // in the reference's formats; nullptr = quiet.
   Solver(rtamd::ParameterHandler &parameter_handler, std::vector<double> &psi_mat, std::vector<double> &phi,
-         std::vector<double> &F, int device = 0);
+         std::vector<double> &F, int device = 0, std::ostream *log = nullptr);
   ~Solver();
   Solver(const Solver &) = delete;
   Solver &operator=(const Solver &) = delete;
@@ -44,10 +48,13 @@ class Solver {
  private:
   void check(rt_status st, const char *what) const;
   void refresh_psi();
+  void print_constructor() const;
+  bool validation_report() const;  // Correction::validate_correction with its prints
   rtamd::ParameterHandler &ph_;
   std::vector<double> &psi_, &phi_, &F_;
   std::vector<double> phi_plus_, balance_, left_ends_, right_ends_;
   int M_, G_, N_;
+  std::ostream *log_ = nullptr;
   rt_solver *h_ = nullptr;
 };
 

@@ -39,7 +39,9 @@ int main(int argc, char **argv) {
   for (int i = 0; i < N; i++) x[i] = (i + 0.5) * parameter_handler.get_dx();
 
   try {
-    rt::Solver solver(parameter_handler, psi_mat, phi, F);
+    // the reference prints as it goes; RTSN_QUIET=1 keeps only the CLI's own lines
+    std::ostream *log = std::getenv("RTSN_QUIET") ? nullptr : &std::cout;
+    rt::Solver solver(parameter_handler, psi_mat, phi, F, 0, log);
     solver.solve();
     solver.compute_angle_integrated_intensity();
     solver.compute_radiative_flux();

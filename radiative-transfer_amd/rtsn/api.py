@@ -17,7 +17,7 @@ LIB_PATH = Path(os.environ.get("RTSN_LIB", PKG_ROOT / "lib" / "librtsn.so"))  # 
 HEADER = REPO_ROOT / "include" / "rtsn.h"
 
 STATUS = {0: "ok", 1: "io error", 2: "parse error", 3: "invalid parameter", 4: "correction validation failed",
-          5: "out of memory", 6: "device error", 7: "in-kernel wait timed out", 8: "bad argument"}
+          5: "out of memory", 6: "device error", 7: "timeout (reserved)", 8: "bad argument"}
 
 
 class RtError(RuntimeError):
@@ -94,6 +94,7 @@ def lib():
             getattr(L, name).argtypes = [vp, dp]
         L.rt_set_ends.argtypes = [vp, dp]
         L.rt_get_moments.argtypes = [vp, dp, dp, dp]
+        L.rt_get_balance_terms.argtypes = [vp, dp, dp, dp]
         L.rt_get_moments_device.argtypes = [vp, vp, vp, vp]
         L.rt_get_group_ends.argtypes = [vp, dp, dp]
         L.rt_get_group_data.argtypes = [vp, dp, dp, dp, dp]

@@ -136,6 +136,86 @@ def test_transfer_csv_files(oracle_mod, tmp_path, name):
             assert got == text, fname
 
 
+def cpp_g(v: float, showpos: bool = False) -> str:
+    """`os << double` at the default stream precision (printf %g)."""
+    return ("%+g" if showpos else "%g") % v
+
+
+def expected_solver_log(q: dict, orc) -> str:
+    """The reference's solver-side stdout (solver.cpp:55-187, 296-312, 620-625;
+    correction.cpp:301), restated from its iostream calls, up to the balance
+    lines (:278-282, compared numerically by the caller)."""
+    mu, wt = orc.quad()
+    gr = orc.groups()
+    out = ["Solver constructor."]
+    out.append(f"{'Mu':<16}{'Wt':<16}")
+    out.append(f"{'--':<16}{'--':<16}")
+    out += [f"{cpp_g(m, True):<16}{cpp_g(w, True):<16}" for m, w in zip(mu, wt)]
+    out.append("")
+    out.append(f"{'Group Index':<13}{'Average Energy':<16}{'Upper Energy':<14}{'Group Width':<13}")
+    out.append(f"{'-----------':<13}{'(keV)---------':<16}{'(keV)-------':<14}{'(keV)------':<13}")
+    for g in range(q["G"]):
+        out.append(f"{g:<13}{cpp_g(gr['e_ave'][g]):<16}{cpp_g(gr['e_edge'][g + 1]):<14}"
+                   f"{cpp_g(gr['e_edge'][g + 1] - gr['e_edge'][g]):<13}")
+    out += ["", "", "Correction constructor."]
+    text = "\n".join(out) + "\n"
+    text += "B: " + eigen_text(gr["B"][:, None])
+    psi0 = np.repeat(np.repeat(gr["B"][None, :, None], q["M"], 0), q["N"], 2)
+    text += "psi_mat_ref: " + tensor_text(psi0)
+    text += "end solver constructor\n"
+    if q["use_mg_equilib"]:
+        src = orc.psi_source()
+        for i in range(q["M"]):
+            for g in range(q["G"]):
+                text += f"source condition for mu: {cpp_g(mu[i])} and group {g}: {cpp_g(src[i, g])}\n"
+    its = q["max_timesteps"] * (4 if q["ts_method"] == 3 else 1)
+    for it in range(its):
+        if q["ts_method"] != 3 or it % 4 == 0:
+            text += f"============= Timestep: {it} =============\n"
+    return text
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["llnl_slab_test", "multi_group_equilibrium"])
+def test_transfer_stdout(oracle_mod, tmp_path, name):
+    """transfer prints what the reference prints, in its formats."""
+    run = _run_tree(tmp_path)
+    prm = f"../prm/{name}.prm"
+    r = subprocess.run([str(_bin("transfer")), prm], cwd=run, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr
+    q = oracle_mod.parse_prm(str(run / prm), table_dir=str(tmp_path / "prm") + "/")
+    orc = oracle_mod.OracleSolver(q)
+    orc.solve()
+    start = r.stdout.index("Solver constructor.")
+    bal_at = r.stdout.index("sources: ")
+    assert r.stdout[start:bal_at] == expected_solver_log(q, orc)
+    # balance lines: sources / sinks / balance per group; balance = |sinks - sources| /
+    # sources cancels, so compare the numbers, not their 6-digit text
+    lines = r.stdout[bal_at:].splitlines()
+    bal_o = orc.balance()
+    for g in range(q["G"]):
+        s_line, k_line, b_line = lines[3 * g: 3 * g + 3]
+        assert s_line.startswith("sources: ") and k_line.startswith("sinks: ")
+        assert b_line.startswith(f"balance at ({g}): ")
+        assert float(b_line.split(": ")[1]) == pytest.approx(bal_o[g], rel=1e-4, abs=1e-12)
+    assert r.stdout.startswith(f"filename: {prm}\n") and len(lines) == 3 * q["G"]
+
+
+@pytest.mark.gpu
+def test_transfer_validation_assert(tmp_path):
+    """include_validation with the LLNL tabulated opacities: the reference prints
+    the failed emission check and its assert aborts (llnl_slab_test.prm:54)."""
+    run = _run_tree(tmp_path)
+    src = (tmp_path / "prm" / "llnl_slab_test.prm").read_text()
+    (tmp_path / "prm" / "llnl_validate.prm").write_text(src.replace("include_validation=false",
+                                                                    "include_validation=true"))
+    r = subprocess.run([str(_bin("transfer")), "../prm/llnl_validate.prm"], cwd=run, capture_output=True,
+                       text=True, timeout=600)
+    assert r.returncode in (-6, 134), (r.returncode, r.stderr)
+    assert "Total Emission = " in r.stdout and "kappa_ref*acT^4 = " in r.stdout
+    assert "Assertion" in r.stderr
+
+
 @pytest.mark.gpu
 def test_gray_binary(tmp_path):
     run = _run_tree(tmp_path)
