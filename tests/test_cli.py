@@ -26,18 +26,21 @@ from conftest import REPO, PRM_DIR
 PKG = REPO / "radiative-transfer_amd"
 
 
-def eigen_text(a: np.ndarray) -> str:
-    """`os << m << std::endl` for a 2-D array under Eigen's default IOFormat."""
+def eigen_text(a: np.ndarray, left: bool = False) -> str:
+    """`os << m << std::endl` for a 2-D array under Eigen's default IOFormat.
+    left: the stream carries std::left (sticky) -- as std::cout does in the
+    reference after its first setw/left table -- so the padding goes right."""
     a = np.atleast_2d(np.asarray(a, dtype=np.float64))
     s = [["%.6g" % v for v in row] for row in a]
     w = max(len(x) for row in s for x in row)
-    return "\n".join(" ".join(x.rjust(w) for x in row) for row in s) + "\n"
+    pad = (lambda x: x.ljust(w)) if left else (lambda x: x.rjust(w))
+    return "\n".join(" ".join(pad(x) for x in row) for row in s) + "\n"
 
 
-def tensor_text(psi: np.ndarray) -> str:
+def tensor_text(psi: np.ndarray, left: bool = False) -> str:
     """Eigen::Tensor<double,3>(M,G,N): dim0 x (G*N) ColMajor view."""
     M, G, N = psi.shape
-    return eigen_text(psi.transpose(0, 2, 1).reshape(M, N * G))
+    return eigen_text(psi.transpose(0, 2, 1).reshape(M, N * G), left)
 
 
 DRIVER = r"""
@@ -159,9 +162,10 @@ def expected_solver_log(q: dict, orc) -> str:
                    f"{cpp_g(gr['e_edge'][g + 1] - gr['e_edge'][g]):<13}")
     out += ["", "", "Correction constructor."]
     text = "\n".join(out) + "\n"
-    text += "B: " + eigen_text(gr["B"][:, None])
+    # std::left is still set on cout from the tables above, so Eigen pads on the right
+    text += "B: " + eigen_text(gr["B"][:, None], left=True)
     psi0 = np.repeat(np.repeat(gr["B"][None, :, None], q["M"], 0), q["N"], 2)
-    text += "psi_mat_ref: " + tensor_text(psi0)
+    text += "psi_mat_ref: " + tensor_text(psi0, left=True)
     text += "end solver constructor\n"
     if q["use_mg_equilib"]:
         src = orc.psi_source()
