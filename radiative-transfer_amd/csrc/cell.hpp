@@ -128,29 +128,6 @@ __host__ __device__ __forceinline__ void cell_step(const LineConst &L, double hd
   }
 }
 
-// First cell of a line (k = 0) with per-substep inflow values b[0..3]
-// (solver.cpp:695-697: local_bdry = half_local_bdry = local_bdry_prev_it = bdry_cond).
-template <int S>
-__host__ __device__ __forceinline__ void cell_first(const LineConst &L, double hd, bool neg, double pin, double pout,
-                                                    const double *b, double *X, double &oin, double &oout) {
-  if constexpr (S == SCHEME_BE) {
-    X[0] = b[0];
-    cell_step<S>(L, hd, neg, pin, pout, X, oin, oout);
-  } else if constexpr (S == SCHEME_CN) {
-    X[0] = b[0];
-    X[1] = b[0];
-    cell_step<S>(L, hd, neg, pin, pout, X, oin, oout);
-  } else {
-    double a, bb, c;
-    cell_bdf2_explicit(L, hd, neg, pin, pout, b[0], b[1], b[2], b[3], b[1], b[3], b[3], a, bb, c, oin, oout);
-    X[0] = pout;
-    X[1] = a;
-    X[2] = bb;
-    X[3] = c;
-    X[4] = oout;
-  }
-}
-
 // Carried state entering the first cell of a line from per-substep inflow
 // values b[0..3] (solver.cpp:695-697: local_bdry = half_local_bdry =
 // local_bdry_prev_it = bdry_cond).
