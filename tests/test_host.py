@@ -134,3 +134,21 @@ def test_solver_without_gpu_fails_loudly(rtsn_mod):
     with pytest.raises(rtsn_mod.RtError) as e:
         rtsn_mod.Solver(rtsn_mod.params_default())
     assert e.value.status == 6  # RT_ERR_DEVICE: no CPU fallback
+
+
+def test_host_code_under_sanitizers(tmp_path):
+    """The library's host code (prm reader, Planck/GLQuad/correction tables,
+    equilibrium sources) over every golden .prm under ASan + UBSan
+    (tools/host_sanitize.cpp; GPU sanitizers are not available)."""
+    import shutil
+    import subprocess
+    if not shutil.which("g++"):
+        pytest.skip("no g++")
+    exe = tmp_path / "host_sanitize"
+    csrc = REPO / "radiative-transfer_amd" / "csrc"
+    subprocess.run(["g++", "-std=c++17", "-O1", "-g", "-fsanitize=address,undefined", "-fno-omit-frame-pointer",
+                    "-fno-sanitize-recover=all", f"-I{csrc}", str(REPO / "tools" / "host_sanitize.cpp"),
+                    str(csrc / "prm.cpp"), str(csrc / "physics.cpp"), "-o", str(exe)], check=True)
+    r = subprocess.run([str(exe), str(PRM_DIR) + "/"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "6 files, 0 bad" in r.stdout and "ERROR" not in r.stderr

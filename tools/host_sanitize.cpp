@@ -1,0 +1,53 @@
+// host_sanitize -- the host-side code of librtsn (the .prm reader, Planck /
+// GLQuad / correction tables, equilibrium sources, affine cell maps of
+// cell.hpp) under AddressSanitizer + UBSan, over every .prm in a directory.
+// Host code only: GPU sanitizers are not available on this pool.
+//   g++ -std=c++17 -O1 -g -fsanitize=address,undefined -fno-omit-frame-pointer \
+//       -I radiative-transfer_amd/csrc tools/host_sanitize.cpp \
+//       radiative-transfer_amd/csrc/prm.cpp radiative-transfer_amd/csrc/physics.cpp -o /tmp/host_sanitize
+//   /tmp/host_sanitize tests/golden/prm/
+#include <dirent.h>
+
+#include <cmath>
+#include <cstdio>
+#include <string>
+#include <vector>
+
+#include "physics.hpp"
+#include "prm.hpp"
+
+int main(int argc, char **argv) {
+  const std::string dir = argc > 1 ? argv[1] : "tests/golden/prm/";
+  DIR *d = opendir(dir.c_str());
+  if (!d) return 2;
+  int files = 0, bad = 0;
+  while (dirent *e = readdir(d)) {
+    const std::string name = e->d_name;
+    if (name.size() < 5 || name.substr(name.size() - 4) != ".prm") continue;
+    rtamd::ParameterHandler ph(dir + name, dir);
+    ++files;
+    if (ph.status() != RT_OK) {
+      std::printf("%-40s parse status %d\n", name.c_str(), ph.status());
+      continue;
+    }
+    const rt_params p = ph.as_params();
+    rtamd::phys::GroupTable t;
+    if (rtamd::phys::build_group_table(p, t) != RT_OK) {
+      std::printf("%-40s group table failed\n", name.c_str());
+      ++bad;
+      continue;
+    }
+    std::vector<double> mu(p.M), wt(p.M), src;
+    rtamd::phys::gauss_legendre(p.M, rtamd::phys::kFourPi, mu.data(), wt.data());
+    rtamd::phys::solver_psi_source(p, t, mu.data(), src);
+    double bsum = 0;
+    for (int g = 0; g < p.G; ++g) bsum += t.B[g];
+    const bool valid = rtamd::phys::validate_correction(p, t);
+    std::printf("%-40s M=%d G=%d N=%d  sum B=%.6g  validation %s\n", name.c_str(), p.M, p.G, p.N, bsum,
+                valid ? "ok" : "fails");
+    if (!std::isfinite(bsum)) ++bad;
+  }
+  closedir(d);
+  std::printf("%d files, %d bad\n", files, bad);
+  return bad ? 1 : 0;
+}
