@@ -52,6 +52,7 @@ import numpy as np  # noqa: E402
 
 METRIC = "cell·angle·group updates/sec (Sn sweep) + BDF2 steps/sec, llnl_slab_test"
 HBM_PEAK = 8.0e12
+SUPPORTED_TIME_BLOCKS = (1, 2, 3, 4, 5, 6, 7, 8, 12, 16)  # rt_set_time_block
 FP64_PEAK = 78.6e12  # MI355X FP64 vector spec (256 CU x 4 SIMD x 16 FMA lanes x 2 x 2.4 GHz); measured 71 TF: profiles/r01_fp64_peak.txt
 KAPPA_TABLE = REPO / "tests" / "golden" / "prm" / "llnl_slab_test_group_kappa_a.txt"
 
@@ -205,11 +206,21 @@ def run_rank(solver, p: dict, steps: int, warmup: int, world: int, device, shard
 
     t_start = time.perf_counter()
     solver.advance(warmup)
+    if solver.pipeline_state()["queued_steps"]:  # W not whole passes: complete them untimed
+        solver.finish()
     solver.synchronize()
     barrier()
+    before = solver.pipeline_state()
     solver.set_profiling(True)
     t0 = time.perf_counter()
     solver.advance(steps)
+    # The timed region must hold exactly K steps of work.  It does when the schedule
+    # ends as it started (a filled pipeline one pass per segment apart, or an aligned
+    # pass's pending correction): every segment advanced K steps.  Otherwise (the
+    # pipeline filled inside the region, or K is not whole passes) complete them here.
+    steady = solver.pipeline_state() == before
+    if not steady:
+        solver.finish()
     solver.synchronize()
     barrier()
     wall = time.perf_counter() - t0
@@ -267,6 +278,7 @@ def run_rank(solver, p: dict, steps: int, warmup: int, world: int, device, shard
         "data": "synthetic",
         "bdf2_steps_per_s": 1e3 / ms_per_step,
         "schedule": {"pipeline_mode": int(getattr(solver, "pipeline", 0)), "steps_per_pass": tb,
+                     "steady_state_at_start": steady, "lag_steps": before["lag_steps"],
                      "warmup_steps": warmup, "drain_ms": 1e3 * (t_end - t1),
                      "end_to_end_ms": 1e3 * (t_end - t_start),
                      "end_to_end_updates_per_s": upd_step * (warmup + steps) / (t_end - t_start)},
@@ -341,14 +353,14 @@ def main():
     if args.time_block:
         solver.time_block = args.time_block
     solver.pipeline = 1 if args.schedule == "pipelined" else 0  # 1: pipelined when the run fills it
+    # exactly K timed steps: the time block is the largest supported one dividing K
     tb = solver.time_block
+    steps = args.steps if args.steps > 0 else 2 * tb
+    tb = max(t for t in SUPPORTED_TIME_BLOCKS if t <= tb and steps % t == 0)
+    solver.time_block = tb
     warmup = args.warmup
     if warmup < 0:  # pipeline depth (segments per line) passes: fill + one steady pass
         warmup = solver.sweep_geometry()[1] * tb if solver.pipeline else tb
-    # whole passes only: steps are launched in passes of tb (a remainder would be
-    # queued until the next read-out, outside the timed region)
-    steps = -(-args.steps // tb) * tb if args.steps > 0 else 2 * tb
-    warmup = -(-warmup // tb) * tb
     shards = [shard(args.scaling, args.groups, world, r)[1:] for r in range(world)]
     line, _, _ = run_rank(solver, p, steps, warmup, world, device, info, args.scaling, shards)
     line["roofline"]["traffic"] = load_traffic(args.variant, solver.time_block)

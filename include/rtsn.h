@@ -175,6 +175,9 @@ rt_status rt_set_time_block(rt_solver *s, int steps_per_pass);
  * passes as the pipeline is deep, else aligned; 2: always pipelined. */
 rt_status rt_set_pipeline(rt_solver *s, int on);
 rt_status rt_get_pipeline(rt_solver *s, int *on);
+/* Schedule state: steps the chain head is ahead of the tail (0 = aligned),
+ * steps queued but not launched, whether a correction is pending; any NULL skipped. */
+rt_status rt_pipeline_state(rt_solver *s, long long *lag_steps, int *queued_steps, int *pending);
 rt_status rt_get_time_block(rt_solver *s, int *steps_per_pass);
 /* Sweep geometry actually used: waves launched per step (one per line group
  * and segment) and segments per line. */

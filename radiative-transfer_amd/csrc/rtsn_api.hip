@@ -1098,6 +1098,14 @@ extern "C" rt_status rt_set_pipeline(rt_solver *s, int on) {
   return RT_OK;
 }
 
+extern "C" rt_status rt_pipeline_state(rt_solver *s, long long *lag_steps, int *queued_steps, int *pending) {
+  if (!s) return fail(nullptr, RT_ERR_ARG, "rt_pipeline_state: NULL handle");
+  if (lag_steps) *lag_steps = s->tau.front() - s->tau.back();
+  if (queued_steps) *queued_steps = s->queued;
+  if (pending) *pending = s->pending ? 1 : 0;
+  return RT_OK;
+}
+
 extern "C" rt_status rt_get_pipeline(rt_solver *s, int *on) {
   if (!s || !on) return fail(s, RT_ERR_ARG, "rt_get_pipeline: bad argument");
   *on = s->pipe;

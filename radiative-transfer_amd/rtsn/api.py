@@ -107,6 +107,7 @@ def lib():
         L.rt_set_time_block.argtypes = [vp, C.c_int]
         L.rt_set_pipeline.argtypes = [vp, C.c_int]
         L.rt_get_pipeline.argtypes = [vp, C.POINTER(C.c_int)]
+        L.rt_pipeline_state.argtypes = [vp, C.POINTER(C.c_longlong), C.POINTER(C.c_int), C.POINTER(C.c_int)]
         L.rt_get_time_block.argtypes = [vp, C.POINTER(C.c_int)]
         L.rt_status_string.argtypes = [C.c_int]
         L.rt_status_string.restype = C.c_char_p
@@ -403,6 +404,12 @@ class Solver:
     @pipeline.setter
     def pipeline(self, mode):
         _check(lib().rt_set_pipeline(self._h, int(mode)), "rt_set_pipeline", self._h)
+
+    def pipeline_state(self) -> dict:
+        """{"lag_steps", "queued_steps", "pending"} (rt_pipeline_state)."""
+        lag, q, pend = C.c_longlong(), C.c_int(), C.c_int()
+        _check(lib().rt_pipeline_state(self._h, C.byref(lag), C.byref(q), C.byref(pend)), "rt_pipeline_state", self._h)
+        return {"lag_steps": lag.value, "queued_steps": q.value, "pending": bool(pend.value)}
 
     def sweep_traffic(self):
         b = C.c_double()

@@ -83,6 +83,9 @@ class OracleShard:
     def finish(self):
         pass
 
+    def pipeline_state(self):
+        return {"lag_steps": 0, "queued_steps": 0, "pending": False}
+
     def set_profiling(self, on):
         self.prof = bool(on)
         if on:
