@@ -710,7 +710,7 @@ static rt_status pipe_launch(rt_solver *s) {
     if (hi >= 0 && hi != c - 1) return fail(s, RT_ERR_PARAM, "pipeline: active positions not contiguous");
     hi = c;
   }
-  if (lo < 0) return RT_OK;
+  if (lo < 0) return fail(s, RT_ERR_PARAM, "pipeline: no position can advance");  // loops below rely on progress
   for (int c = lo; c <= hi; ++c)
     if (s->tau[c] != s->tau[lo] - static_cast<long long>(c - lo) * T)
       return fail(s, RT_ERR_PARAM, "pipeline: positions out of step");
