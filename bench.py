@@ -333,6 +333,9 @@ def main():
     ap.add_argument("--schedule", choices=["pipelined", "aligned"], default="pipelined",
                     help="staggered segments (exact starts) or aligned segments with deferred correction")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    # rehearsal of the multi-rank path on a one-GPU box: every rank on cuda:0, gloo
+    ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl", help=argparse.SUPPRESS)
+    ap.add_argument("--share-device", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
 
     import torch
@@ -341,11 +344,14 @@ def main():
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = 0 if args.share_device else int(os.environ.get("LOCAL_RANK", "0"))
     device = torch.device("cuda", local)
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=device)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=device)
+        else:
+            dist.init_process_group("gloo")
 
     info = shard(args.scaling, args.groups, world, rank)
     p = slab_params(info[0], args.variant, N=args.cells)
