@@ -127,16 +127,18 @@ def reference_config_timings() -> dict:
     return out
 
 
-def load_traffic(variant: str, tb: int):
+def load_traffic(variant: str, tb: int, algorithmic_bytes: float):
     """Measured HBM bytes per sweep launch (rocprofv3 PMC, scripts/gpu_profile.sh) for
-    this variant and time block, or None."""
+    this variant and time block, or None -- also None when the profile was taken on a
+    different problem size (its bytes are not within 10% of this launch's)."""
     f = REPO / "profiles" / f"pmc_{variant}_t{tb}.json"
     if not f.exists():
         return None
     try:
-        return json.loads(f.read_text()).get("hbm_bytes_per_launch")
+        b = json.loads(f.read_text()).get("hbm_bytes_per_launch")
     except (OSError, ValueError):
         return None
+    return b if b and abs(b / algorithmic_bytes - 1.0) < 0.1 else None
 
 
 def shard(scaling: str, groups: int, world: int, rank: int):
@@ -369,7 +371,8 @@ def main():
         warmup = solver.sweep_geometry()[1] * tb if solver.pipeline else tb
     shards = [shard(args.scaling, args.groups, world, r)[1:] for r in range(world)]
     line, _, _ = run_rank(solver, p, steps, warmup, world, device, info, args.scaling, shards)
-    line["roofline"]["traffic"] = load_traffic(args.variant, solver.time_block)
+    line["roofline"]["traffic"] = load_traffic(args.variant, solver.time_block,
+                                               line["roofline"]["algorithmic_bytes_per_launch"])
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(args.variant)
         line["reference_config"] = reference_config_timings()
