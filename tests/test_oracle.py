@@ -162,3 +162,18 @@ def test_threaded_oracle_bitwise(oracle_mod):
         outs.append((s.ends(), s.psi()))
     np.testing.assert_array_equal(outs[0][0], outs[1][0])
     np.testing.assert_array_equal(outs[0][1], outs[1][1])
+
+
+def test_equilibrium_known_answer(oracle_mod):
+    """SURVEY §8(c) KAT 3: multi_group_equilibrium.prm (source BCs at the
+    equilibrium psi_source = B + mu beta (4B - dEB), 500 BDF2 steps) stays at
+    the equilibrium profile: every psi(i, g, c) within 0.5% of psi_source(i, g).
+    (compute_balance is not ~0 here: solver.cpp:258-265 takes the mu>0 inflow
+    from node 1 of cell 0 and the mu<0 inflow from node 0 of cell N-1 -- we
+    reproduce the formula, tests/test_gpu_parity.py compares it.)"""
+    p = oracle_mod.parse_prm(PRM_DIR / "multi_group_equilibrium.prm", table_dir=PRM_DIR)
+    s = oracle_mod.OracleSolver(p)
+    s.solve()
+    src = s.psi_source()
+    dev = np.abs(s.psi() - src[:, :, None]).max(axis=2) / np.abs(src)
+    assert dev.max() < 5e-3, dev
