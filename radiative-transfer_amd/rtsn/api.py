@@ -310,6 +310,13 @@ class Solver:
         self._balance = out
         return out
 
+    def compute_balance_terms(self):
+        """(balance, sources, sinks) per group (rt_get_balance_terms, solver.cpp:240-284)."""
+        b, src, snk = np.empty(self.G), np.empty(self.G), np.empty(self.G)
+        _check(lib().rt_get_balance_terms(self._h, _dp(b), _dp(src), _dp(snk)), "rt_get_balance_terms", self._h)
+        self._balance = b
+        return b, src, snk
+
     def get_balance(self) -> np.ndarray:
         return self._balance
 

@@ -57,10 +57,11 @@ def compare_all(gpu, orc, tol=TOL, plus_vs_group=False):
     err["F"] = flux_rel(F_g, F_o, psi_o, mu, wt)
     l_g, r_g = gpu.compute_group_ends()
     l_o, r_o = orc.group_ends()
-    # balance = |sinks - sources| / sources: absolute (relative to the sources it cancels)
-    # when it is below 1, relative when above (sinks >> sources in the unstable runs)
-    bal_o = orc.balance()
-    err["balance"] = float(np.max(np.abs(gpu.compute_balance() - bal_o) / np.maximum(np.abs(bal_o), 1.0)))
+    # balance = |sinks - sources| / sources cancels: its error is measured against the
+    # size of what it is computed from, (|sinks| + |sources|) / |sources|
+    bal_g, src_g, snk_g = gpu.compute_balance_terms()
+    scale = (np.abs(snk_g) + np.abs(src_g)) / np.abs(src_g)
+    err["balance"] = float(np.max(np.abs(bal_g - orc.balance()) / scale))
     err["left_ends"] = float(np.max(np.abs(l_g - l_o) / np.maximum(np.abs(l_o), 1e-300)))
     err["right_ends"] = float(np.max(np.abs(r_g - r_o) / np.maximum(np.abs(r_o), 1e-300)))
     for k, v in err.items():
