@@ -97,6 +97,9 @@ static rt_status fail(rt_solver *s, rt_status st, const std::string &msg) {
 // 9.5 / 9.0 / 8.4 ms per step at T = 1 / 2 / 3 / 4 / 8 / 12 / 16.
 static int default_time_block(int) { return 16; }
 
+// rt_set_time_block's domain: the instantiated sweep kernels (kernels.hip launch_s)
+static bool supported_time_block(int T) { return (T >= 1 && T <= 8) || T == 12 || T == 16; }
+
 static int map_count_of(int scheme) {
   switch (scheme) {
     case SCHEME_BE: return map_count<SCHEME_BE>();
@@ -479,7 +482,8 @@ extern "C" rt_status rt_create_from_params(const rt_params *pin, int g_lo, int g
   // segments: enough waves to fill the chip (occupancy x CUs), Ls a multiple of the chunk
   int waves_per_cu = 0;
   h->T = default_time_block(h->scheme);
-  if (const char *t = std::getenv("RTSN_TIME_BLOCK")) h->T = std::atoi(t);  // experiments: segment count follows
+  if (const char *t = std::getenv("RTSN_TIME_BLOCK"))  // experiments: the segment count follows
+    if (supported_time_block(std::atoi(t))) h->T = std::atoi(t);
   HIP_TRY(h, sweep_occupancy(h->scheme, h->T, &waves_per_cu));
   // tuning knob for experiments: target resident waves per CU (segments per line follow)
   if (const char *w = std::getenv("RTSN_WAVES_PER_CU")) waves_per_cu = std::atoi(w);
@@ -1114,8 +1118,7 @@ extern "C" rt_status rt_get_pipeline(rt_solver *s, int *on) {
 
 extern "C" rt_status rt_set_time_block(rt_solver *s, int steps_per_pass) {
   if (!s) return fail(nullptr, RT_ERR_ARG, "rt_set_time_block: NULL handle");
-  if (steps_per_pass < 1 || steps_per_pass > kMaxTimeBlock ||
-      (steps_per_pass > 8 && steps_per_pass != 12 && steps_per_pass != 16))
+  if (!supported_time_block(steps_per_pass))
     return fail(s, RT_ERR_ARG, "rt_set_time_block: steps per pass must be 1.." + std::to_string(kMaxTimeBlock));
   s->T = steps_per_pass;
   return RT_OK;
