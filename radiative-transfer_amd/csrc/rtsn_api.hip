@@ -1119,7 +1119,7 @@ extern "C" rt_status rt_get_pipeline(rt_solver *s, int *on) {
 extern "C" rt_status rt_set_time_block(rt_solver *s, int steps_per_pass) {
   if (!s) return fail(nullptr, RT_ERR_ARG, "rt_set_time_block: NULL handle");
   if (!supported_time_block(steps_per_pass))
-    return fail(s, RT_ERR_ARG, "rt_set_time_block: steps per pass must be 1.." + std::to_string(kMaxTimeBlock));
+    return fail(s, RT_ERR_ARG, "rt_set_time_block: steps per pass must be 1..8, 12 or 16");
   s->T = steps_per_pass;
   return RT_OK;
 }
