@@ -42,6 +42,8 @@ namespace rtamd {
 // lane*16 (one VGPR), instead of a 64-bit VGPR address per row.
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
+// Descriptor word 3 = 0x00020000: DATA_FORMAT (bits 15-18) = 4, 32-bit, as for raw
+// dword buffers on gfx9-family parts; num_records = the chunk's bytes (bounds-checked).
 template <int C>
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rows_rsrc(const double2 *base, int row_bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<double2 *>(base), 0, C * row_bytes, 0x00020000);
@@ -100,9 +102,8 @@ __global__ void fold_kernel(FoldArgs f) {
 // level by level.  Rare (one cell per line per pass): line constants are
 // read from memory here instead of being kept in registers.
 template <int S, int T>
-__device__ __forceinline__ void head_cell(const double *lcp, size_t stride, double hd,
-                                                    const double (&b)[T][4], double (&X)[T][SchemeDim<S>::K],
-                                                    double &oi, double &oo) {
+__device__ __forceinline__ void head_cell(const double *lcp, size_t stride, double hd, const double (&b)[T][4],
+                                          double (&X)[T][SchemeDim<S>::K], double &oi, double &oo) {
   LineConst L;
 #pragma unroll
   for (int n = 0; n < LC_COUNT; ++n) L.c[n] = lcp[n * stride];
