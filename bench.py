@@ -15,8 +15,9 @@ State is resident in HBM before timing.
 
 Multi-GPU: one process per GPU (torch.distributed.run), groups sharded across
 ranks with no collective in the data path (groups are independent for the
-whole run: T is constant).  weak scaling (default): every rank owns 128 groups
-of a 128*N-group grid; strong: the 128 groups are split N ways.  Timing:
+whole run: T is constant).  strong scaling (default, the north_star's "same
+slab"): the 128 groups are split N ways (16 per GPU at N = 8); weak: every
+rank owns 128 groups of a 128*N-group grid.  Timing:
 barrier + device synchronise on both sides of the K timed steps, max over
 ranks.  After timing, the group-summed absorption rate is all-reduced over
 RCCL once (the north_star group-sum hook) and checked.
@@ -327,7 +328,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=-1,
                     help="untimed steps before timing (default: fill the pipeline plus one pass)")
     ap.add_argument("--variant", choices=["v0", "corr"], default="v0")
-    ap.add_argument("--scaling", choices=["weak", "strong"], default="weak")
+    ap.add_argument("--scaling", choices=["weak", "strong"], default="strong")
     ap.add_argument("--groups", type=int, default=128, help="groups per GPU (weak) or in total (strong)")
     ap.add_argument("--cells", type=int, default=1_000_000)
     ap.add_argument("--time-block", type=int, default=0,
