@@ -35,7 +35,6 @@ struct SegArgs {
   double2 *E;                 // [2][Nrow][Lpad] (e_in, e_out)
   const double *map;          // [2][map_count<S>][Lpad] per-line affine cell map (cell.hpp)
   const double *lc;           // [2][LC_COUNT][Lpad] line constants (reflective head cell only)
-  const double *prop;         // [2][prop_count(K, T)][Lpad] segment propagators for this T
   const double *bdry;         // [2][Lpad] inflow value per line (non-reflective)
   const double *yseg;         // [2][Sg+1][T K][Lpad] true incoming state per segment (fold_kernel)
   const double *yrefl;        // [T K][Lpad] this pass's mu < 0 line outflow state (reflective)

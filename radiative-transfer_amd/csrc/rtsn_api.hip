@@ -9,6 +9,7 @@
 #include <cstring>
 #include <memory>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/rtsn.h"
@@ -50,6 +51,8 @@ struct rt_solver {
   hipStream_t stream = nullptr;
   // device state
   DeviceBuf E, map, lc, prop[kMaxAlignedBlock + 1], bdry, agg[2], yseg, yrefl, lineB, muwt, mom, rows, sigma;
+  std::vector<double> map_host;  // [2][WN][Lpad], kept for the lazily built propagators
+  bool prop_ready[kMaxAlignedBlock + 1] = {};
   int agg_cur = 0;               // aggregates of the last pass live in agg[agg_cur ^ 1]
   bool pending = false;          // E holds provisional segments (correction outstanding)
   // pipelined schedule (rt_set_pipeline): chain positions (segments; half 0 then
@@ -346,14 +349,12 @@ static void line_inflow(const rt_solver &s, std::vector<double> &bd) {
 
 template <int S>
 static rt_status setup_lines_s(rt_solver *s) {
-  constexpr int K = SchemeDim<S>::K, WN = map_count<S>();
+  constexpr int WN = map_count<S>();
   const double hd = 0.5 * (s->p.X / s->p.N);
-  const long long L_last = s->p.N - static_cast<long long>(s->Sg - 1) * s->Ls;
   const size_t Lp = s->Lpad;
-  std::vector<double> lc(2 * LC_COUNT * Lp, 0.0), map(2 * WN * Lp, 0.0), lineB(2 * Lp, 0.0);
-  std::vector<std::vector<double>> pr(kMaxAlignedBlock + 1);
-  for (int T = 1; T <= kMaxAlignedBlock; ++T) pr[T].assign(2 * prop_count(K, T) * Lp, 0.0);
-  std::vector<double> A, Aseg, Alast;
+  std::vector<double> lc(2 * LC_COUNT * Lp, 0.0), lineB(2 * Lp, 0.0);
+  std::vector<double> &map = s->map_host;
+  map.assign(2 * WN * Lp, 0.0);
   double W[WN];
   for (int half = 0; half < 2; ++half)
     for (int gl = 0; gl < s->Gl; ++gl)
@@ -366,27 +367,10 @@ static rt_status setup_lines_s(rt_solver *s) {
         if (!cell_map<S>(L, hd, half == 0, W))
           return fail(s, RT_ERR_PARAM, "cell map: a structurally zero coefficient is not zero");
         for (int n = 0; n < WN; ++n) map[(half * WN + n) * Lp + ell] = W[n];
-        for (int T = 1; T <= kMaxAlignedBlock; ++T) {
-          const int KC = T * K, NTC = KC * (KC + 1) / 2;
-          A.assign(KC * KC, 0.0);
-          Aseg.resize(KC * KC);
-          Alast.resize(KC * KC);
-          combined_linear<S>(W, T, A.data());
-          matpow(KC, A.data(), s->Ls, Aseg.data());
-          matpow(KC, A.data(), L_last, Alast.data());
-          double *dst = pr[T].data() + half * prop_count(K, T) * Lp + ell;
-          for (int r = 0; r < KC; ++r)
-            for (int c = 0; c <= r; ++c) {
-              dst[tri(r, c) * Lp] = Aseg[r * KC + c];
-              dst[(NTC + tri(r, c)) * Lp] = Alast[r * KC + c];
-            }
-        }
       }
   rt_status st;
   if ((st = upload(s, s->lc, lc.data(), lc.size() * sizeof(double)))) return st;
   if ((st = upload(s, s->map, map.data(), map.size() * sizeof(double)))) return st;
-  for (int T = 1; T <= kMaxAlignedBlock; ++T)
-    if ((st = upload(s, s->prop[T], pr[T].data(), pr[T].size() * sizeof(double)))) return st;
   if ((st = upload(s, s->lineB, lineB.data(), lineB.size() * sizeof(double)))) return st;
   std::vector<double> sig(s->Gl);
   for (int gl = 0; gl < s->Gl; ++gl) sig[gl] = s->gt.rho[s->g_lo + gl] * s->gt.kappa[s->g_lo + gl];
@@ -397,6 +381,54 @@ static rt_status setup_lines_s(rt_solver *s) {
   if ((st = upload(s, s->muwt, muwt.data(), muwt.size() * sizeof(double)))) return st;
   HIP_TRY(s, hipStreamSynchronize(s->stream));  // host vectors die at return
   return RT_OK;
+}
+
+// Segment propagators A_T^Ls, A_T^Llast of every line for the aligned schedule
+// (fold_kernel), built on first use of a time block T: the pipelined schedule
+// never needs them.  Lines are independent: host threads split them.
+template <int S>
+static rt_status build_propagators_s(rt_solver *s, int T) {
+  constexpr int K = SchemeDim<S>::K, WN = map_count<S>();
+  const int KC = T * K, NTC = KC * (KC + 1) / 2;
+  const long long L_last = s->p.N - static_cast<long long>(s->Sg - 1) * s->Ls;
+  const size_t Lp = s->Lpad, lines = 2 * Lp;
+  std::vector<double> pr(2 * prop_count(K, T) * Lp, 0.0);
+  auto work = [&](size_t l0, size_t l1) {
+    std::vector<double> A(KC * KC), Aseg(KC * KC), Alast(KC * KC);
+    double W[WN];
+    for (size_t idx = l0; idx < l1; ++idx) {
+      const size_t half = idx / Lp, ell = idx % Lp;
+      for (int n = 0; n < WN; ++n) W[n] = s->map_host[(half * WN + n) * Lp + ell];
+      std::fill(A.begin(), A.end(), 0.0);
+      combined_linear<S>(W, T, A.data());
+      matpow(KC, A.data(), s->Ls, Aseg.data());
+      matpow(KC, A.data(), L_last, Alast.data());
+      double *dst = pr.data() + half * prop_count(K, T) * Lp + ell;
+      for (int r = 0; r < KC; ++r)
+        for (int c = 0; c <= r; ++c) {
+          dst[tri(r, c) * Lp] = Aseg[r * KC + c];
+          dst[(NTC + tri(r, c)) * Lp] = Alast[r * KC + c];
+        }
+    }
+  };
+  const size_t nt = std::max<size_t>(1, std::min<size_t>(16, std::thread::hardware_concurrency()));
+  std::vector<std::thread> pool;
+  for (size_t t = 0; t < nt; ++t) pool.emplace_back(work, lines * t / nt, lines * (t + 1) / nt);
+  for (std::thread &th : pool) th.join();
+  rt_status st = upload(s, s->prop[T], pr.data(), pr.size() * sizeof(double));
+  if (st) return st;
+  HIP_TRY(s, hipStreamSynchronize(s->stream));  // pr dies at return
+  s->prop_ready[T] = true;
+  return RT_OK;
+}
+
+static rt_status ensure_propagators(rt_solver *s, int T) {
+  if (s->prop_ready[T]) return RT_OK;
+  switch (s->scheme) {
+    case SCHEME_BE: return build_propagators_s<SCHEME_BE>(s, T);
+    case SCHEME_CN: return build_propagators_s<SCHEME_CN>(s, T);
+    default: return build_propagators_s<SCHEME_BDF2>(s, T);
+  }
 }
 
 static rt_status setup_lines(rt_solver *s) {
@@ -574,12 +606,11 @@ static rt_status fold_events(rt_solver *s) {
   return RT_OK;
 }
 
-static SegArgs seg_args(rt_solver *s, int T) {
+static SegArgs seg_args(rt_solver *s) {
   SegArgs a{};
   a.E = static_cast<double2 *>(s->E.p);
   a.map = static_cast<const double *>(s->map.p);
   a.lc = static_cast<const double *>(s->lc.p);
-  a.prop = static_cast<const double *>(s->prop[T].p);
   a.bdry = static_cast<const double *>(s->bdry.p);
   a.yseg = static_cast<const double *>(s->yseg.p);
   a.yrefl = static_cast<const double *>(s->yrefl.p);
@@ -601,6 +632,7 @@ static SegArgs seg_args(rt_solver *s, int T) {
 // previous pass (agg_prev) -> yseg for the pending correction, or this pass's
 // mu < 0 half (agg_cur) -> yrefl for the reflective mu > 0 heads.
 static rt_status enqueue_fold(rt_solver *s, int T, bool reflective_outflow) {
+  if (rt_status st = ensure_propagators(s, T)) return st;
   FoldArgs f{};
   const int slot = reflective_outflow ? s->agg_cur : (s->agg_cur ^ 1);
   f.agg = static_cast<const double *>(s->agg[slot].p);
@@ -623,7 +655,7 @@ static rt_status apply_correction(rt_solver *s) {
   if (!s->pending) return RT_OK;
   rt_status st = enqueue_fold(s, s->Tp, false);
   if (st) return st;
-  SegArgs a = seg_args(s, s->Tp);
+  SegArgs a = seg_args(s);
   HIP_TRY(s, launch_sweep(s->scheme, s->Tp, SWEEP_FINALIZE, a, 2 * s->Q * s->Sg, s->stream));
   s->pending = false;
   return RT_OK;
@@ -658,7 +690,7 @@ static rt_status enqueue_pass(rt_solver *s, int T) {
     if (st) return st;
   }
   const int per_half = s->Q * s->Sg;
-  SegArgs a = seg_args(s, T);
+  SegArgs a = seg_args(s);
   hipEvent_t e1;
   rt_status st = event_begin(s, &e1);
   if (st) return st;
@@ -718,7 +750,7 @@ static rt_status pipe_launch(rt_solver *s) {
   for (int c = lo; c <= hi; ++c)
     if (s->tau[c] != s->tau[lo] - static_cast<long long>(c - lo) * T)
       return fail(s, RT_ERR_PARAM, "pipeline: positions out of step");
-  SegArgs a = seg_args(s, T);
+  SegArgs a = seg_args(s);
   a.aggs[0] = static_cast<double *>(s->agg[0].p);
   a.aggs[1] = static_cast<double *>(s->agg[1].p);
   a.pending = 0;
