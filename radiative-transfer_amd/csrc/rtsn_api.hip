@@ -72,6 +72,7 @@ struct rt_solver {
   std::string err;
 
   ~rt_solver() {
+    if (stream) (void)hipStreamSynchronize(stream);  // no kernel may outlive the buffers it uses
     for (hipEvent_t e : ev_pool) (void)hipEventDestroy(e);
     if (stream) (void)hipStreamDestroy(stream);
   }
