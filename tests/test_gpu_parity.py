@@ -12,7 +12,7 @@ import numpy as np
 import pytest
 
 import fused_np  # noqa: F401  (oracle-side restatement, used in a check below)
-from conftest import PRM_DIR, SEED
+from conftest import PRM_DIR, REPO, SEED
 from parity import flux_rel, per_group_rel
 
 pytestmark = pytest.mark.gpu
@@ -323,3 +323,36 @@ def test_moments_device(rtsn_mod, oracle_mod):
         host = s.moments()
         for k in range(3):
             np.testing.assert_array_equal(t[k].cpu().numpy().reshape(s.N, s.G).T, host[k])
+
+
+@pytest.fixture(scope="module")
+def sl_line_oracle(oracle_mod):
+    """One group of the SL slab at its full line length, N = 1e6,
+    M = 64, V = 5.994 with the correction on, 2 BDF2 steps, on the oracle."""
+    import sys
+    sys.path.insert(0, str(REPO))
+    import bench
+    p = bench.slab_params(128, "corr")
+    p["max_timesteps"] = 2
+    q = dict(p)
+    q.update(bc_left=0, bc_right=0, dx=p["X"] / p["N"], have_group_bounds=0, have_group_kappa=1, prm_found=1)
+    o = oracle_mod.OracleSolver(q, g_lo=100, g_hi=101)
+    o.solve()
+    return p, o
+
+
+@pytest.mark.parametrize("pipe,tb", [(0, 2), (2, 1), (2, 2)])
+def test_full_length_sl_line(rtsn_mod, sl_line_oracle, pipe, tb):
+    """Maximum line length: 1e6 cells cut into hundreds of segments, aligned and
+    pipelined (fill and drain over every position), against the oracle."""
+    p, orc = sl_line_oracle
+    with rtsn_mod.Solver(p, g_lo=100, g_hi=101) as gpu:
+        gpu.time_block = tb
+        gpu.pipeline = pipe
+        _, segs = gpu.sweep_geometry()
+        assert segs >= 100
+        gpu.solve()
+        assert per_group_rel(gpu.psi(), orc.psi(), 1) <= TOL
+        phi_g, F_g, _ = gpu.moments()
+        phi_o, F_o, _ = orc.moments()
+        assert per_group_rel(phi_g, phi_o, 0) <= TOL
