@@ -152,3 +152,20 @@ def test_host_code_under_sanitizers(tmp_path):
     r = subprocess.run([str(exe), str(PRM_DIR) + "/"], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "6 files, 0 bad" in r.stdout and "ERROR" not in r.stderr
+
+
+def test_c_client_links_and_runs(tmp_path):
+    """include/rtsn.h compiles as C99 and librtsn.so links from C: host-only entry
+    points work, rt_create_from_params reports RT_ERR_DEVICE without a gfx950
+    (or succeeds on one)."""
+    import shutil
+    import subprocess
+    if not shutil.which("gcc") or not LIB.exists():
+        pytest.skip("no gcc or library")
+    exe = tmp_path / "abi_check"
+    subprocess.run(["gcc", "-std=c99", "-Wall", "-Wextra", "-Werror", "-pedantic", f"-I{REPO / 'include'}",
+                    str(REPO / "tests" / "c_abi" / "abi_check.c"), "-o", str(exe), f"-L{LIB.parent}", "-lrtsn",
+                    f"-Wl,-rpath,{LIB.parent}", "-lm"], check=True)
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, (r.returncode, r.stdout, r.stderr)
+    assert r.stdout.strip().endswith("ok")
