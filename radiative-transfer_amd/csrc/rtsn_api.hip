@@ -532,6 +532,8 @@ extern "C" rt_status rt_create_from_params(const rt_params *pin, int g_lo, int g
     h->Sg = static_cast<int>((q.N + ls - 1) / ls);
   }
   if (2LL * h->Q * h->Sg >= (1LL << 31)) return fail(nullptr, RT_ERR_PARAM, "too many lines for one handle: shard the groups");
+  // a chunk's rows are addressed through one buffer descriptor with 32-bit offsets
+  if (16LL * 16 * h->Lpad >= (1LL << 31)) return fail(nullptr, RT_ERR_PARAM, "too many lines per row: shard the groups");
 
   const size_t Lp = h->Lpad;
   const int K = h->K;
