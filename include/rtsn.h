@@ -43,7 +43,8 @@ typedef enum {
   RT_ERR_NOMEM = 5,       /* host or device allocation failed */
   RT_ERR_DEVICE = 6,      /* HIP runtime error / no usable gfx950 device */
   RT_ERR_TIMEOUT = 7,     /* reserved (no in-kernel waits in this version) */
-  RT_ERR_ARG = 8          /* NULL handle / bad argument */
+  RT_ERR_ARG = 8,         /* NULL handle / bad argument */
+  RT_ERR_STATE = 9        /* call not valid in the handle's mode (e.g. rt_advance with material coupling on) */
 } rt_status;
 
 /* Every .prm key (ParameterHandler.cpp:100-212) with the reference's meaning.
@@ -182,6 +183,35 @@ rt_status rt_get_time_block(rt_solver *s, int *steps_per_pass);
 /* Sweep geometry actually used: waves launched per step (one per line group
  * and segment) and segments per line. */
 rt_status rt_sweep_geometry(rt_solver *s, int *workgroups, long long *tiles);
+
+/* ---- material-temperature coupling (beyond the reference) ---------------
+ * The reference holds T constant (solver.cpp:157).  With coupling enabled the
+ * handle carries a cell temperature T(x) and, per full time step n (duration
+ * dt; ts_method 3's four substeps form one step):
+ *   1. sweep with the per-cell emission B_g(T^n(x)) (Planck group integrals
+ *      on the device, Planck.cpp:44-337's algorithm; the last group is the
+ *      grey remainder a c T^4 - integral over groups 0..G-2, when positive);
+ *   2. q(x) = sum_g sigma_g (phi_g^{n+1}(x) - W B_g(T^n(x))), W = sum_i w_i:
+ *      this handle's groups only -- with sharded groups the callers sum the
+ *      ranks' q (one all-reduce of N doubles per step, e.g. RCCL);
+ *   3. T^{n+1}(x) = T^n(x) + dt q(x) / rho_cv.
+ * With ts_method 1 (BE) the total energy sum_x dx (sum_g phi_g / c + rho_cv T)
+ * changes by exactly -dt x (net boundary outflow) per step (up to rounding).
+ * Requires the v/c correction to be inactive (V == 0 or use_correction == 0). */
+/* Turn coupling on: rho_cv > 0 (material energy per volume per keV), T_cells
+ * (N, host) the initial T(x), NULL for the uniform p.T.  The state psi is kept. */
+rt_status rt_material_enable(rt_solver *s, double rho_cv, const double *T_cells);
+/* Steps 1-2: one coupled sweep, then this handle's q into d_q (DEVICE, N
+ * doubles; NULL: an internal buffer), on the handle's stream, asynchronous. */
+rt_status rt_material_sweep(rt_solver *s, double *d_q);
+/* Step 3 from the (group-summed) q in d_q (DEVICE, N; NULL: the internal
+ * buffer), then B_g(T(x)) for the next step; handle's stream, asynchronous. */
+rt_status rt_material_update(rt_solver *s, const double *d_q);
+/* nsteps x (sweep + update) for a handle that holds all G groups. */
+rt_status rt_material_step(rt_solver *s, int nsteps);
+/* T(x) (N) and the per-cell emission B (G_local*N, g + G_local*c) to host memory. */
+rt_status rt_get_temperature(rt_solver *s, double *T_cells);
+rt_status rt_get_cell_planck(rt_solver *s, double *B);
 
 const char *rt_status_string(rt_status st);
 /* Last error message recorded on the handle (or the global one for s == NULL). */

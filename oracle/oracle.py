@@ -77,6 +77,16 @@ def lib():
         L.orc_glquad.argtypes = [C.c_int, C.c_double, dp, dp]
         L.orc_planck_groups.argtypes = [C.c_double, C.c_int, dp, dp, dp, dp]
         L.orc_eigen_inverse2.argtypes = [dp, dp]
+        L.orc_material_enable.argtypes = [C.c_void_p, C.c_double, dp]
+        L.orc_material_sweep.argtypes = [C.c_void_p, dp]
+        L.orc_material_update.argtypes = [C.c_void_p, dp]
+        L.orc_material_update.restype = None
+        L.orc_get_temperature.argtypes = [C.c_void_p, dp]
+        L.orc_get_temperature.restype = None
+        L.orc_get_cell_planck.argtypes = [C.c_void_p, dp]
+        L.orc_get_cell_planck.restype = None
+        L.orc_planck_cell.argtypes = [C.c_double, C.c_int, dp, C.c_int]
+        L.orc_planck_cell.restype = C.c_double
         _lib = L
     return _lib
 
@@ -240,6 +250,40 @@ class OracleSolver:
     def validate(self) -> bool:
         return bool(lib().orc_validate(self._h))
 
+    # ---- material-temperature coupling (beyond the reference; rtsn.h rt_material_*) ----
+    def material_enable(self, rho_cv: float, T_cells=None):
+        T = None if T_cells is None else np.ascontiguousarray(T_cells, dtype=np.float64)
+        st = lib().orc_material_enable(self._h, float(rho_cv), None if T is None else _dp(T))
+        if st:
+            raise OracleError(f"material_enable -> {ORC_ERRORS.get(st, st)}")
+
+    def material_sweep(self) -> np.ndarray:
+        """One coupled full step; returns this solver's q (N)."""
+        q = np.empty(self.N)
+        st = lib().orc_material_sweep(self._h, _dp(q))
+        if st:
+            raise OracleError(f"material_sweep -> {ORC_ERRORS.get(st, st)}")
+        return q
+
+    def material_update(self, q):
+        qq = np.ascontiguousarray(q, dtype=np.float64)
+        lib().orc_material_update(self._h, _dp(qq))
+
+    def material_step(self, n: int = 1):
+        for _ in range(n):
+            self.material_update(self.material_sweep())
+
+    def temperature(self) -> np.ndarray:
+        out = np.empty(self.N)
+        lib().orc_get_temperature(self._h, _dp(out))
+        return out
+
+    def cell_planck(self) -> np.ndarray:
+        """(G_local, N) per-cell emission."""
+        out = np.empty(self.N * self.Gl)
+        lib().orc_get_cell_planck(self._h, _dp(out))
+        return out.reshape(self.N, self.Gl).T.copy()
+
 
 def glquad(M: int, norm: float = 4.0 * 3.1415926546):
     mu = np.empty(M)
@@ -256,6 +300,12 @@ def planck_groups(T: float, e_lo, e_hi):
     dB = np.empty(G)
     lib().orc_planck_groups(T, G, _dp(e_lo), _dp(e_hi), _dp(B), _dp(dB))
     return B, dB
+
+
+def planck_cell(T: float, e_edge, g: int) -> float:
+    """kcon x B_g(T) per the material coupling's definition (rt_oracle.c orc_planck_cell)."""
+    e = np.ascontiguousarray(e_edge, dtype=np.float64)
+    return lib().orc_planck_cell(float(T), len(e) - 1, _dp(e), int(g))
 
 
 def eigen_inverse2(m) -> np.ndarray:

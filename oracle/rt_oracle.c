@@ -525,8 +525,16 @@ struct orc_solver {
   double *total_correction; /* M x Gl x N ColMajor */
   /* state */
   double *psi, *ends, *prev_ends, *half_ends;
+  /* material-temperature coupling (not in the reference; orc_material_*) */
+  double *Tcell;      /* N */
+  double *Bcell;      /* N x Gl, c*Gl + gl; NULL = the reference's constant-T B_g */
+  double rho_cv, wsum;
+  int mat_it;         /* substep counter of the coupled steps (_it of solve()) */
+  int equil_done;
 };
 
+/* emission of cell c, local group gl: per cell when coupled, else B_g (solver.cpp:338,...) */
+#define SRC_B(s, gl, c) ((s)->Bcell ? (s)->Bcell[(size_t)(c) * (s)->Gl + (size_t)(gl)] : (s)->B[(s)->g_lo + (gl)])
 #define PSI(s, i, g, c) ((s)->psi[(size_t)(i) + (size_t)(s)->M * ((size_t)(g) + (size_t)(s)->Gl * (size_t)(c))])
 #define TC(s, i, g, c) ((s)->total_correction[(size_t)(i) + (size_t)(s)->M * ((size_t)(g) + (size_t)(s)->Gl * (size_t)(c))])
 #define E4(arr, s, i, g, c, k) \
@@ -754,6 +762,7 @@ void orc_destroy(orc_solver *s) {
   free(s->cB); free(s->cdBdT); free(s->kappa_edge); free(s->dEB); free(s->dsigEdE); free(s->dkapEB);
   free(s->cor1); free(s->cor2); free(s->cor3); free(s->total_correction);
   free(s->psi); free(s->ends); free(s->prev_ends); free(s->half_ends);
+  free(s->Tcell); free(s->Bcell);
   free(s);
 }
 
@@ -771,7 +780,7 @@ static void cell_be(orc_solver *s, sweep_t *w, int cell, int i, int gl, double t
   if (mu < 0) {
     tv = (const_A * dx - const_B) / 2.;
     mat[0] = tv; mat[1] = const_B / 2.; mat[2] = -const_B / 2.; mat[3] = tv;
-    tv = 0.5 * c * timestep * dx * s->rho[g] * s->kappa[g] * s->B[g];
+    tv = 0.5 * c * timestep * dx * s->rho[g] * s->kappa[g] * SRC_B(s, gl, cell);
     if (s->p.use_correction) tv += 0.5 * c * timestep * dx * TC(s, i, gl, cell);
     rhs[0] = tv + dx * E4(s->ends, s, i, gl, cell, 0) / 2.;
     rhs[1] = tv - (const_B * w->local_bdry) + dx * E4(s->ends, s, i, gl, cell, 1) / 2.;
@@ -783,7 +792,7 @@ static void cell_be(orc_solver *s, sweep_t *w, int cell, int i, int gl, double t
   } else {
     tv = (const_A * dx + const_B) / 2.;
     mat[0] = tv; mat[1] = const_B / 2.; mat[2] = -const_B / 2.; mat[3] = tv;
-    tv = 0.5 * c * timestep * dx * s->rho[g] * s->kappa[g] * s->B[g];
+    tv = 0.5 * c * timestep * dx * s->rho[g] * s->kappa[g] * SRC_B(s, gl, cell);
     if (s->p.use_correction) tv += 0.5 * c * timestep * dx * TC(s, i, gl, cell);
     rhs[0] = tv + (const_B * w->local_bdry) + dx * E4(s->ends, s, i, gl, cell, 0) / 2.;
     rhs[1] = tv + dx * E4(s->ends, s, i, gl, cell, 1) / 2.;
@@ -808,7 +817,7 @@ static void cell_cn(orc_solver *s, sweep_t *w, int cell, int i, int gl, double t
   if (mu < 0) {
     tv = 0.5 * (const_B * dx - const_A);
     mat[0] = tv; mat[1] = 0.5 * const_A; mat[2] = -0.5 * const_A; mat[3] = tv;
-    tv = 0.5 * c * timestep * dx * s->rho[g] * s->kappa[g] * s->B[g];
+    tv = 0.5 * c * timestep * dx * s->rho[g] * s->kappa[g] * SRC_B(s, gl, cell);
     if (s->p.use_correction) tv += 0.5 * c * timestep * dx * TC(s, i, gl, cell);
     rhs[0] = tv + 0.5 * (const_C * dx + const_A) * e0 - 0.5 * const_A * e1;
     rhs[1] = tv + 0.5 * const_A * e0 + 0.5 * (const_C * dx + const_A) * e1 -
@@ -822,7 +831,7 @@ static void cell_cn(orc_solver *s, sweep_t *w, int cell, int i, int gl, double t
   } else {
     tv = 0.5 * (const_A + const_B * dx);
     mat[0] = tv; mat[1] = const_A / 2.; mat[2] = -const_A / 2.; mat[3] = tv;
-    tv = 0.5 * c * timestep * dx * s->rho[g] * s->kappa[g] * s->B[g];
+    tv = 0.5 * c * timestep * dx * s->rho[g] * s->kappa[g] * SRC_B(s, gl, cell);
     if (s->p.use_correction) tv += 0.5 * c * timestep * dx * TC(s, i, gl, cell);
     rhs[0] = tv + 0.5 * (const_C * dx - const_A) * e0 - 0.5 * const_A * e1 +
              const_A * (w->local_bdry_prev_it + w->half_local_bdry);
@@ -851,7 +860,7 @@ static void cell_bdf(orc_solver *s, sweep_t *w, int cell, int i, int gl, double 
   if (mu < 0) {
     tv = 0.5 * (const_A * dx - const_B);
     mat[0] = tv; mat[1] = 0.5 * const_B; mat[2] = -0.5 * const_B; mat[3] = tv;
-    tv = 0.5 * c * timestep * dx * s->rho[g] * s->kappa[g] * s->B[g];
+    tv = 0.5 * c * timestep * dx * s->rho[g] * s->kappa[g] * SRC_B(s, gl, cell);
     if (s->p.use_correction) tv += 0.5 * c * timestep * dx * TC(s, i, gl, cell);
     rhs[0] = tv + 0.5 * (const_C * dx + 4. * const_B) * h0 - 2. * const_B * h1;
     rhs[0] += 0.5 * (const_B - const_D * dx) * p0 - 0.5 * const_B * p1;
@@ -868,7 +877,7 @@ static void cell_bdf(orc_solver *s, sweep_t *w, int cell, int i, int gl, double 
   } else {
     tv = 0.5 * (const_A * dx + const_B);
     mat[0] = tv; mat[1] = 0.5 * const_B; mat[2] = -0.5 * const_B; mat[3] = tv;
-    tv = 0.5 * c * timestep * dx * s->rho[g] * s->kappa[g] * s->B[g];
+    tv = 0.5 * c * timestep * dx * s->rho[g] * s->kappa[g] * SRC_B(s, gl, cell);
     if (s->p.use_correction) tv += 0.5 * c * timestep * dx * TC(s, i, gl, cell);
     rhs[0] = tv + 0.5 * (const_C * dx - 4. * const_B) * h0 - 2. * const_B * h1;
     rhs[0] -= 0.5 * (const_B + const_D * dx) * p0 + 0.5 * const_B * p1;
@@ -1005,6 +1014,92 @@ int orc_solve(orc_solver *s) {
     if (st) return st;
   }
   return orc_run_substeps(s, 0, steps);
+}
+
+/* ======================================================================== */
+/* Material-temperature coupling (beyond the reference; include/rtsn.h)      */
+/* ======================================================================== */
+/* B_g(T) x kcon for one group g: Planck::integrate_B (Planck.cpp:85-154) for
+ * g < G-1; the last group is the grey remainder a c T^4 minus the integral
+ * over groups 0..G-2 taken as ONE integral over [e_0, e_{G-1}], assigned only
+ * when positive (Planck.cpp:73-76), else 0.  T <= 0 or not finite: 0. */
+static double planck_cell(const planck_t *P, double T, int G, const double *e_edge, int g) {
+  if (!(T > 0.0) || !isfinite(T)) return 0.0;
+  if (g < G - 1) return C_BOLTZ_JPK * planck_integrate_B(P, T, e_edge[g], e_edge[g + 1]);
+  double rest = rad_a_long() * C_LIGHT * pow(T, 4.0) - planck_integrate_B(P, T, e_edge[0], e_edge[G - 1]);
+  return rest > 0.0 ? C_BOLTZ_JPK * rest : 0.0;
+}
+
+double orc_planck_cell(double T, int G, const double *e_edge, int g) {
+  planck_t P;
+  planck_setup(&P);
+  return planck_cell(&P, T, G, e_edge, g);
+}
+
+static void material_planck(orc_solver *s) {
+#pragma omp parallel for schedule(static) num_threads(s->threads) if (s->threads > 1)
+  for (int c = 0; c < s->N; ++c)
+    for (int gl = 0; gl < s->Gl; ++gl)
+      s->Bcell[(size_t)c * s->Gl + gl] = planck_cell(&s->planck, s->Tcell[c], s->G, s->e_edge, s->g_lo + gl);
+}
+
+int orc_material_enable(orc_solver *s, double rho_cv, const double *T_cells) {
+  if (!(rho_cv > 0.0)) return ORC_ERR_PARAM;
+  if (s->p.use_correction && s->p.V != 0.0) return ORC_ERR_PARAM;
+  int ok = 1;
+  if (!s->Tcell) s->Tcell = (double *)xcalloc(s->N, sizeof(double), &ok);
+  if (!s->Bcell) s->Bcell = (double *)xcalloc((size_t)s->N * s->Gl, sizeof(double), &ok);
+  if (!ok) return ORC_ERR_NOMEM;
+  for (int c = 0; c < s->N; ++c) s->Tcell[c] = T_cells ? T_cells[c] : s->p.T;
+  s->rho_cv = rho_cv;
+  s->wsum = 0.0;
+  for (int i = 0; i < s->M; ++i) s->wsum += s->wt[i];
+  material_planck(s);
+  return ORC_OK;
+}
+
+/* One full step with the per-cell emission (ts 3: four substeps), then
+ * q(c) = sum_gl sigma_g (phi_g(c) - W B_g(c)) over the local groups. */
+int orc_material_sweep(orc_solver *s, double *q) {
+  if (!s->Bcell) return ORC_ERR_PARAM;
+  if (s->p.use_mg_equilib && !s->equil_done) {
+    int st = equilibrium_sources(s);
+    if (st) return st;
+    s->equil_done = 1;
+  }
+  const int sub = s->p.ts_method == 3 ? 4 : 1;
+  int st = orc_run_substeps(s, s->mat_it, sub);
+  if (st) return st;
+  s->mat_it += sub;
+  const size_t GN = (size_t)s->Gl * s->N;
+  double *phi = (double *)malloc(sizeof(double) * (GN ? GN : 1));
+  if (!phi) return ORC_ERR_NOMEM;
+  orc_moments(s, phi, NULL, NULL);
+  for (int c = 0; c < s->N; ++c) {
+    double acc = 0.0;
+    for (int gl = 0; gl < s->Gl; ++gl) {
+      int g = s->g_lo + gl;
+      double sigma = s->rho[g] * s->kappa[g];
+      acc += sigma * (phi[(size_t)c * s->Gl + gl] - s->wsum * s->Bcell[(size_t)c * s->Gl + gl]);
+    }
+    q[c] = acc;
+  }
+  free(phi);
+  return ORC_OK;
+}
+
+/* T(c) += dt q(c) / rho_cv (q summed over all groups), then B_g(T(c)). */
+void orc_material_update(orc_solver *s, const double *q) {
+  for (int c = 0; c < s->N; ++c) s->Tcell[c] = s->Tcell[c] + s->dt * q[c] / s->rho_cv;
+  material_planck(s);
+}
+
+void orc_get_temperature(const orc_solver *s, double *T) {
+  for (int c = 0; c < s->N; ++c) T[c] = s->Tcell ? s->Tcell[c] : s->p.T;
+}
+
+void orc_get_cell_planck(const orc_solver *s, double *B) {
+  if (s->Bcell) memcpy(B, s->Bcell, sizeof(double) * (size_t)s->N * s->Gl);
 }
 
 int orc_num_groups_local(const orc_solver *s) { return s->Gl; }

@@ -99,6 +99,20 @@ void orc_get_psi_source(const orc_solver *s, double *out);
 /* validate_correction() (correction.cpp:366-369): 1 pass, 0 fail. */
 int orc_validate(orc_solver *s);
 
+/* Material-temperature coupling (NOT in the reference: the product's
+ * rt_material_* of include/rtsn.h restated on the CPU).  Per full step:
+ * orc_material_sweep runs the step with the per-cell emission B_g(T(c)) and
+ * writes this solver's q(c) = sum_g sigma_g (phi_g - W B_g) (N); the caller
+ * sums q over group shards and calls orc_material_update (T += dt q / rho_cv,
+ * then B_g(T)).  Requires the v/c correction off. */
+int orc_material_enable(orc_solver *s, double rho_cv, const double *T_cells /* N or NULL */);
+int orc_material_sweep(orc_solver *s, double *q);
+void orc_material_update(orc_solver *s, const double *q);
+void orc_get_temperature(const orc_solver *s, double *T);
+void orc_get_cell_planck(const orc_solver *s, double *B); /* N x Gl, c*Gl + gl */
+/* kcon x B_g(T) of one group, the last one the grey remainder (see .c) */
+double orc_planck_cell(double T, int G, const double *e_edge, int g);
+
 /* Stand-alone building blocks exposed for unit tests. */
 void orc_glquad(int M, double norm, double *mu, double *wt);
 void orc_planck_groups(double T, int G, const double *e_lo, const double *e_hi,

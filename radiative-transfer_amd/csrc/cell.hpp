@@ -235,9 +235,12 @@ __host__ __device__ constexpr int map_count() {
 }
 
 // Apply the map (CONST: with the affine constants; otherwise its linear part).
+// cs scales the constants: the material-coupled sweep stores them for B = 1
+// and passes the cell's B_g(T(x)) (with the correction off they are linear in
+// the source); 1.0 elsewhere, which the compiler folds away.
 template <int S, bool CONST>
 __host__ __device__ __forceinline__ void map_apply(const double *W, const double *X, double din, double dout,
-                                                   double *Xn, double &oin, double &oout) {
+                                                   double *Xn, double &oin, double &oout, double cs = 1.0) {
   constexpr int K = SchemeDim<S>::K;
 #pragma unroll
   for (int r = 0; r <= K; ++r) {
@@ -245,7 +248,7 @@ __host__ __device__ __forceinline__ void map_apply(const double *W, const double
       Xn[0] = dout;
       continue;
     }
-    double acc = CONST ? W[map_slot<S>(r, K + 2)] : 0.0;
+    double acc = CONST ? W[map_slot<S>(r, K + 2)] * cs : 0.0;
 #pragma unroll
     for (int c = 0; c < K + 2; ++c) {
       if (!map_dep<S>(r, c)) continue;

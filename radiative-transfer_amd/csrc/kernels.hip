@@ -103,10 +103,11 @@ __global__ void fold_kernel(FoldArgs f) {
 // read from memory here instead of being kept in registers.
 template <int S, int T>
 __device__ __forceinline__ void head_cell(const double *lcp, size_t stride, double hd, const double (&b)[T][4],
-                                          double (&X)[T][SchemeDim<S>::K], double &oi, double &oo) {
+                                          double (&X)[T][SchemeDim<S>::K], double &oi, double &oo, double bs) {
   LineConst L;
 #pragma unroll
   for (int n = 0; n < LC_COUNT; ++n) L.c[n] = lcp[n * stride];
+  L.c[LC_SC] *= bs;  // material coupling: the cell's B_g(T(x)) (1 otherwise)
 #pragma unroll
   for (int t = 0; t < T; ++t) {
     double a, c;
@@ -122,13 +123,14 @@ __device__ __forceinline__ void head_cell(const double *lcp, size_t stride, doub
 // the per-line affine map W (level t's outputs are level t+1's inputs),
 // store, and prefetch the next chunk's rows into the registers just
 // consumed.  LAST: the segment's final chunk -- no prefetch, and only its
-// first nv cells are real (X is left after cell nv-1).
-template <int S, int T, int MODE, int C, bool LAST>
-__device__ __forceinline__ void sweep_chunk(const double *W, double (&ein)[C], double (&eout)[C],
+// first nv cells are real (X is left after cell nv-1).  CB: the map constants
+// are scaled by the cell's B_g(T(x)) (bv, prefetched with the rows by bload).
+template <int S, int T, int MODE, int C, bool LAST, bool CB, typename BL>
+__device__ __forceinline__ void sweep_chunk(const double *W, double (&ein)[C], double (&eout)[C], double (&bv)[C],
                                             double (&X)[T][SchemeDim<S>::K], bool corr,
                                             double (&Z)[T][SchemeDim<S>::K], bool head, double h_oi, double h_oo,
                                             __amdgpu_buffer_rsrc_t Rw, __amdgpu_buffer_rsrc_t Rn, int voff,
-                                            int row_bytes, int nv) {
+                                            int row_bytes, int nv, int k0, const BL &bload) {
   constexpr int K = SchemeDim<S>::K;
 #pragma unroll
   for (int c = 0; c < C; ++c) {
@@ -157,7 +159,7 @@ __device__ __forceinline__ void sweep_chunk(const double *W, double (&ein)[C], d
 #pragma unroll
         for (int t = 0; t < T; ++t) {
           double Xn[K], a, e;
-          map_apply<S, true>(W, X[t], oi, oo, Xn, a, e);
+          map_apply<S, true>(W, X[t], oi, oo, Xn, a, e, CB ? bv[c] : 1.0);
 #pragma unroll
           for (int r = 0; r < K; ++r) X[t][r] = Xn[r];
           oi = a;
@@ -170,6 +172,7 @@ __device__ __forceinline__ void sweep_chunk(const double *W, double (&ein)[C], d
       const double2 v = row_load(Rn, voff, c * row_bytes);
       ein[c] = v.x;
       eout[c] = v.y;
+      if constexpr (CB) bv[c] = bload(k0 + C + c);
     }
   }
 }
@@ -180,7 +183,7 @@ __device__ __forceinline__ void sweep_chunk(const double *W, double (&ein)[C], d
 // levels, each one pass behind its upwind neighbour, so every segment starts
 // from the exact incoming state that neighbour published in the previous
 // launch -- no provisional state, no correction.
-template <int S, int T, int MODE>
+template <int S, int T, int MODE, bool CB = false>
 __global__ __launch_bounds__(64) void sweep_block_kernel(SegArgs a) {
   constexpr int K = SchemeDim<S>::K;
   constexpr int KC = T * K;
@@ -290,7 +293,19 @@ __global__ __launch_bounds__(64) void sweep_block_kernel(SegArgs a) {
   const int voff = lane * static_cast<int>(sizeof(double2));
   const double2 *Eh = a.E + static_cast<size_t>(half) * a.Nrow * stride + q * 64;
   auto rows = [&](int k0) { return rows_rsrc<C>(Eh + static_cast<size_t>(k0) * stride, row_bytes); };
-  double ein[C], eout[C];
+  // material coupling: B_g(T(x)) of row k (physical cell N-1-k for mu < 0);
+  // padding lanes and rows read a clamped, unused value
+  const double *bl = nullptr;
+  if constexpr (CB) bl = a.bcell + min(ell / a.H, a.Gl - 1);
+  auto bload = [&](int k) -> double {
+    if constexpr (CB) {
+      const int kk = min(k, a.N - 1);
+      return bl[static_cast<size_t>(neg ? a.N - 1 - kk : kk) * a.Gl];
+    } else {
+      return 1.0;
+    }
+  };
+  double ein[C], eout[C], bv[C];
   {
     const __amdgpu_buffer_rsrc_t R0 = rows(k_begin);
 #pragma unroll
@@ -298,6 +313,7 @@ __global__ __launch_bounds__(64) void sweep_block_kernel(SegArgs a) {
       const double2 v = row_load(R0, voff, c * row_bytes);
       ein[c] = v.x;
       eout[c] = v.y;
+      bv[c] = bload(k_begin + c);
     }
   }
   // reflective head cell (cell 0 of segment 0, distinct per-substep inflows)
@@ -305,7 +321,7 @@ __global__ __launch_bounds__(64) void sweep_block_kernel(SegArgs a) {
   if (refl_head) {
     h_oi = ein[0];
     h_oo = eout[0];
-    head_cell<S, T>(lcp, stride, a.hd, b, X, h_oi, h_oo);
+    head_cell<S, T>(lcp, stride, a.hd, b, X, h_oi, h_oo, bv[0]);
   }
 
   // ---- the line's cell map ----
@@ -315,11 +331,11 @@ __global__ __launch_bounds__(64) void sweep_block_kernel(SegArgs a) {
 
   int k0 = k_begin;
   for (; k0 + C < k_end; k0 += C) {  // full chunks with a successor
-    sweep_chunk<S, T, MODE, C, false>(W, ein, eout, X, corr, Z, refl_head && k0 == 0, h_oi, h_oo, rows(k0),
-                                      rows(k0 + C), voff, row_bytes, C);
+    sweep_chunk<S, T, MODE, C, false, CB>(W, ein, eout, bv, X, corr, Z, refl_head && k0 == 0, h_oi, h_oo, rows(k0),
+                                          rows(k0 + C), voff, row_bytes, C, k0, bload);
   }
-  sweep_chunk<S, T, MODE, C, true>(W, ein, eout, X, corr, Z, refl_head && k0 == 0, h_oi, h_oo, rows(k0), rows(k0),
-                                   voff, row_bytes, k_end - k0);
+  sweep_chunk<S, T, MODE, C, true, CB>(W, ein, eout, bv, X, corr, Z, refl_head && k0 == 0, h_oi, h_oo, rows(k0),
+                                       rows(k0), voff, row_bytes, k_end - k0, k0, bload);
   if constexpr (MODE != 1) {
     double *ag = (MODE == 2 ? a.aggs[slot] : a.agg_cur) + half * half_stride + static_cast<size_t>(s) * seg_stride + ell;
 #pragma unroll
@@ -497,10 +513,127 @@ __global__ void group_absorption_kernel(const double *phi, const double *sigma, 
 }
 
 // ------------------------------------------------------------------------
+// Material coupling: Planck group integrals per cell, exchange term, T update
+// ------------------------------------------------------------------------
+// Planck.h:84-90 (2 ulps)
+__device__ __forceinline__ bool nearly_equal(double a, double b) {
+  const double d = fabs(a - b);
+  return d <= 2.220446049250313e-16 * fabs(a + b) * 2 || d < 2.2250738585072014e-308;
+}
+
+// Bose series of the normalised integral from z1 to z2 (Planck.cpp:94-118):
+// n_terms is the first n >= 32 whose next term falls below the accuracy
+// relative to the leading one (capped so a bad input cannot spin).
+__device__ double planck_series(double z1, double z2, double accuracy) {
+  auto poly = [](double y) { return y * y * y + 3.0 * (y * y) + 6.0 * y + 6.0; };
+  double lead = exp(-z1) * poly(z1);
+  lead = fmax(lead, 2.220446049250313e-16);
+  const double q = 1.0 - exp(-z1);
+  int n = 32;
+  for (; n < 4096; ++n) {
+    const double m = n + 1.0;
+    const double next = exp(-m * z1) / q / (m * m * m * m) * poly(m * z1) / lead;
+    if (!(next > accuracy)) break;
+  }
+  double s1 = 0.0, s2 = 0.0;
+  for (int k = n; k > 0; --k) {
+    const double m = k, m4 = m * m * m * m;
+    s1 += exp(-m * z1) / m4 * poly(m * z1);
+    s2 += exp(-m * z2) / m4 * poly(m * z2);
+  }
+  return s1 - s2;
+}
+
+// 12-point Gauss-Legendre of the Planck density over [mid - hw, mid + hw]
+// (Planck.cpp:129-140; k_B = 1 keV/keV)
+__device__ double planck_gauss(const PlanckCells &pc, double T, double mid, double hw, double pre) {
+  double acc = 0.0;
+#pragma unroll
+  for (int r = 0; r < 12; ++r) {
+    const double E = mid + hw * pc.node[r];
+    const double f = nearly_equal(T, 0.0) ? 0.0 : pre * (E * E * E) / (exp(E / T) - 1.0);
+    acc += hw * pc.weight[r] * f;
+  }
+  return acc;
+}
+
+// Planck::integrate_B (Planck.cpp:85-154): Gauss below z = 0.7, series above
+// z = 0.5, split at z = 0.6; x 4 pi.  pre = 2 / (h^3 c^2).
+__device__ double planck_integral(const PlanckCells &pc, double T, double e_min, double e_max, double pre) {
+  if (nearly_equal(T, 0.0) || nearly_equal(e_min, e_max)) return 0.0;
+  const double z1 = e_min / T, z2 = e_max / T;
+  const double t4 = (T * T) * (T * T);
+  double v;
+  if (z2 <= 0.7) {
+    v = planck_gauss(pc, T, 0.5 * (e_max + e_min), 0.5 * (e_max - e_min), pre);
+  } else if (z1 >= 0.5) {
+    v = pre * t4 * planck_series(z1, z2, pc.accuracy);
+  } else {
+    const double e6 = 0.6 * T;
+    v = planck_gauss(pc, T, 0.5 * (e6 + e_min), 0.5 * (e6 - e_min), pre) + pre * t4 * planck_series(0.6, z2, pc.accuracy);
+  }
+  return v * 4.0 * 3.1415926546;
+}
+
+// B[x][gl] = kcon * integral over group g_lo + gl at T(x); the last group takes
+// the grey remainder a c T^4 - (integral over groups 0..G-2) when positive
+// (Planck.cpp:73-76; the sum of the other groups as one integral over their
+// joint range, so no shard needs another shard's groups).  T <= 0 or not
+// finite: 0.
+__global__ void planck_cells_kernel(PlanckCells pc, const double *Tc, double *B) {
+  const size_t total = static_cast<size_t>(pc.N) * pc.Gl;
+  const double hc = 4.141895e-10, c = 299.792458;
+  const double pre = 2.0 / ((hc * hc * hc) * (c * c));
+  for (size_t idx = blockIdx.x * static_cast<size_t>(blockDim.x) + threadIdx.x; idx < total;
+       idx += static_cast<size_t>(gridDim.x) * blockDim.x) {
+    const int x = static_cast<int>(idx / pc.Gl), gl = static_cast<int>(idx % pc.Gl);
+    const int g = pc.g_lo + gl;
+    const double T = Tc[x];
+    double b = 0.0;
+    if (T > 0.0 && isfinite(T)) {
+      if (g < pc.G - 1) {
+        b = pc.kcon * planck_integral(pc, T, pc.e_edge[g], pc.e_edge[g + 1], pre);
+      } else {
+        const double rest = pc.a_c * ((T * T) * (T * T)) - planck_integral(pc, T, pc.e_edge[0], pc.e_edge[pc.G - 1], pre);
+        b = rest > 0.0 ? pc.kcon * rest : 0.0;
+      }
+    }
+    B[idx] = b;
+  }
+}
+
+// q(x) = sum_g sigma_g (phi_g(x) - W B_g(x)), groups in order (no contraction)
+__global__ void material_q_kernel(const double *phi, const double *B, const double *sigma, double W, double *q, int Gl,
+                                  int N) {
+#pragma clang fp contract(off)
+  for (int x = blockIdx.x * blockDim.x + threadIdx.x; x < N; x += gridDim.x * blockDim.x) {
+    double acc = 0.0;
+    const size_t o = static_cast<size_t>(x) * Gl;
+    for (int g = 0; g < Gl; ++g) acc += sigma[g] * (phi[o + g] - W * B[o + g]);
+    q[x] = acc;
+  }
+}
+
+__global__ void material_update_kernel(double *T, const double *q, double dt, double rho_cv, int N) {
+#pragma clang fp contract(off)
+  for (int x = blockIdx.x * blockDim.x + threadIdx.x; x < N; x += gridDim.x * blockDim.x)
+    T[x] = T[x] + dt * q[x] / rho_cv;
+}
+
+// ------------------------------------------------------------------------
 // launchers
 // ------------------------------------------------------------------------
 template <int S, int T>
 static hipError_t launch_t(int mode, const SegArgs &a, int grid, hipStream_t st) {
+  if (a.bcell) {  // material coupling: one full step per aligned pass
+    if constexpr (T == 1) {
+      if (mode == SWEEP_PASS) {
+        hipLaunchKernelGGL((sweep_block_kernel<S, 1, 0, true>), dim3(grid), dim3(64), 0, st, a);
+        return hipGetLastError();
+      }
+    }
+    if (mode != SWEEP_FINALIZE) return hipErrorInvalidValue;  // the correction has no source term
+  }
   if (mode == SWEEP_PIPELINED) {
     hipLaunchKernelGGL((sweep_block_kernel<S, T, 2>), dim3(grid), dim3(64), 0, st, a);
     return hipGetLastError();
@@ -640,6 +773,25 @@ hipError_t launch_group_absorption(const double *phi, const double *sigma, doubl
                                    hipStream_t st) {
   hipLaunchKernelGGL(group_absorption_kernel, dim3(grid_for(static_cast<size_t>(g.N), 256)), dim3(256), 0, st, phi,
                      sigma, out, g.Gl, g.N);
+  return hipGetLastError();
+}
+
+hipError_t launch_planck_cells(const PlanckCells &pc, const double *T, double *B, hipStream_t st) {
+  hipLaunchKernelGGL(planck_cells_kernel, dim3(grid_for(static_cast<size_t>(pc.N) * pc.Gl, 256)), dim3(256), 0, st, pc,
+                     T, B);
+  return hipGetLastError();
+}
+
+hipError_t launch_material_q(const double *phi, const double *B, const double *sigma, double W, double *q, int Gl,
+                             int N, hipStream_t st) {
+  hipLaunchKernelGGL(material_q_kernel, dim3(grid_for(static_cast<size_t>(N), 256)), dim3(256), 0, st, phi, B, sigma,
+                     W, q, Gl, N);
+  return hipGetLastError();
+}
+
+hipError_t launch_material_update(double *T, const double *q, double dt, double rho_cv, int N, hipStream_t st) {
+  hipLaunchKernelGGL(material_update_kernel, dim3(grid_for(static_cast<size_t>(N), 256)), dim3(256), 0, st, T, q, dt,
+                     rho_cv, N);
   return hipGetLastError();
 }
 

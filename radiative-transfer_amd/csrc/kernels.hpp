@@ -47,6 +47,10 @@ struct SegArgs {
   int pending;                // the stored state is provisional: apply the correction
   int pos_lo, npos, pass_lo;  // pipelined: active chain positions and the pass of the first
   double hd;                  // dx / 2
+  // material coupling (SWEEP_PASS, T = 1 only): per-cell emission B_g(T(x)),
+  // [N][Gl] (g fastest), scaling the map constants stored for B = 1
+  const double *bcell;        // nullptr: line-constant source (the reference's constant T)
+  int Gl, H;                  // local groups, lines per half per group (line l = i' + H g)
 };
 
 struct FoldArgs {
@@ -77,5 +81,22 @@ hipError_t launch_moments(const double2 *E, const double *mu, const double *wt, 
 hipError_t launch_boundary_rows(const double2 *E, double2 *rows, const Geometry &g, hipStream_t st);
 hipError_t launch_group_absorption(const double *phi, const double *sigma, double *out, const Geometry &g,
                                    hipStream_t st);
+
+// Planck group integrals per cell (material coupling): the algorithm of
+// Planck.cpp:44-337 in double precision on the device.
+struct PlanckCells {
+  double node[12], weight[12];  // Gauss-Legendre on [-1, 1] (Planck.cpp:231-337, rounded to double)
+  const double *e_edge;         // [G+1] all groups' edges (device)
+  int G, g_lo, Gl, N;
+  double a_c;                   // rad_a_long() * c (Constants.h:22-23)
+  double kcon;                  // jk per keV (correction.cpp:25-36)
+  double accuracy;              // series tolerance (Planck.h:96, DBL_EPSILON)
+};
+hipError_t launch_planck_cells(const PlanckCells &pc, const double *T, double *B, hipStream_t st);
+// q(x) = sum_g sigma_g (phi_g(x) - W B_g(x)) over the handle's groups
+hipError_t launch_material_q(const double *phi, const double *B, const double *sigma, double W, double *q, int Gl,
+                             int N, hipStream_t st);
+// T(x) += dt q(x) / rho_cv
+hipError_t launch_material_update(double *T, const double *q, double dt, double rho_cv, int N, hipStream_t st);
 
 }  // namespace rtamd

@@ -39,6 +39,13 @@ class PlanckIntegrator {
   void group_integrals(double T, int G, const double *e_lo, const double *e_hi, double *B, double *dBdT) const;
   double integral_B(double T, double e_min, double e_max) const;
   double integral_dBdT(double T, double e_min, double e_max) const;
+  // the Gauss-Legendre nodes and weights rounded to double (device copy)
+  void nodes(double *x, double *w) const {
+    for (int r = 0; r < 12; ++r) {
+      x[r] = static_cast<double>(node_[r]);
+      w[r] = static_cast<double>(weight_[r]);
+    }
+  }
 
  private:
   double gauss(double T, double mid, double half_width, bool dBdT) const;

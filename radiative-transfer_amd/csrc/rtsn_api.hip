@@ -7,6 +7,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <limits>
 #include <memory>
 #include <string>
 #include <thread>
@@ -27,6 +28,9 @@ thread_local std::string g_last_error;
 struct DeviceBuf {
   void *p = nullptr;
   size_t bytes = 0;
+  DeviceBuf() = default;
+  DeviceBuf(const DeviceBuf &) = delete;  // owns p
+  DeviceBuf &operator=(const DeviceBuf &) = delete;
   ~DeviceBuf() {
     if (p) (void)hipFree(p);
   }
@@ -63,6 +67,11 @@ struct rt_solver {
   long long pipe_base = 0;       // tau of every position when the pipeline started
   int queued = 0;                // requested steps not yet enqueued (< T)
   int Tpipe = 0;                 // time block of the running pipeline (0: positions aligned)
+  // material-temperature coupling (rt_material_enable)
+  bool material = false;
+  double rho_cv = 0.0, wsum = 0.0;
+  DeviceBuf Tcell, Bcell, qbuf, edges, map_unit, lc_unit;
+  PlanckCells pc{};
   // profiling
   bool profiling = false;
   std::vector<hipEvent_t> ev_pool;   // (start, stop) pairs of profiled launches
@@ -196,7 +205,8 @@ extern "C" rt_status rt_planck_groups(double T, int G, const double *e_edge, dou
 // a reflective mu > 0 line and its mirror have the same l.
 static int line_direction(int H, int half, int ip) { return half == 0 ? H - 1 - ip : H + ip; }
 
-static LineConst line_constants(const rt_solver &s, int i, int g) {
+// unit_B: the source for B_g = 1 (material coupling scales it per cell)
+static LineConst line_constants(const rt_solver &s, int i, int g, bool unit_B = false) {
   const rt_params &p = s.p;
   const double c = phys::kLight;
   const double dx = p.X / p.N;
@@ -207,7 +217,7 @@ static LineConst line_constants(const rt_solver &s, int i, int g) {
   LineConst L{};
   const double half = 0.5 * c * tau * dx;
   // S = 1/2 c tau dx (sigma B_g + total_correction), psi = (e_in + e_out)/2
-  L.c[LC_SC] = half * sigma * s.gt.B[g];
+  L.c[LC_SC] = half * sigma * (unit_B ? 1.0 : s.gt.B[g]);
   L.c[LC_SL] = 0.0;
   if (p.use_correction) {
     const double beta = p.V / c;
@@ -348,13 +358,15 @@ static void line_inflow(const rt_solver &s, std::vector<double> &bd) {
   (void)M;
 }
 
+// Per-line maps and constants into (map, lc); unit_B: sources for B_g = 1
+// (material coupling), leaving map_host (the propagators' source) alone.
 template <int S>
-static rt_status setup_lines_s(rt_solver *s) {
+static rt_status line_maps_s(rt_solver *s, bool unit_B, DeviceBuf &map_dev, DeviceBuf &lc_dev) {
   constexpr int WN = map_count<S>();
   const double hd = 0.5 * (s->p.X / s->p.N);
   const size_t Lp = s->Lpad;
-  std::vector<double> lc(2 * LC_COUNT * Lp, 0.0), lineB(2 * Lp, 0.0);
-  std::vector<double> &map = s->map_host;
+  std::vector<double> lc(2 * LC_COUNT * Lp, 0.0), unit_map;
+  std::vector<double> &map = unit_B ? unit_map : s->map_host;
   map.assign(2 * WN * Lp, 0.0);
   double W[WN];
   for (int half = 0; half < 2; ++half)
@@ -362,16 +374,28 @@ static rt_status setup_lines_s(rt_solver *s) {
       for (int ip = 0; ip < s->H; ++ip) {
         const int i = line_direction(s->H, half, ip), g = s->g_lo + gl;
         const size_t ell = ip + static_cast<size_t>(s->H) * gl;
-        const LineConst L = line_constants(*s, i, g);
+        const LineConst L = line_constants(*s, i, g, unit_B);
         for (int n = 0; n < LC_COUNT; ++n) lc[(half * LC_COUNT + n) * Lp + ell] = L.c[n];
-        lineB[half * Lp + ell] = s->gt.B[g];
         if (!cell_map<S>(L, hd, half == 0, W))
           return fail(s, RT_ERR_PARAM, "cell map: a structurally zero coefficient is not zero");
         for (int n = 0; n < WN; ++n) map[(half * WN + n) * Lp + ell] = W[n];
       }
   rt_status st;
-  if ((st = upload(s, s->lc, lc.data(), lc.size() * sizeof(double)))) return st;
-  if ((st = upload(s, s->map, map.data(), map.size() * sizeof(double)))) return st;
+  if ((st = upload(s, lc_dev, lc.data(), lc.size() * sizeof(double)))) return st;
+  if ((st = upload(s, map_dev, map.data(), map.size() * sizeof(double)))) return st;
+  HIP_TRY(s, hipStreamSynchronize(s->stream));  // host vectors die at return
+  return RT_OK;
+}
+
+template <int S>
+static rt_status setup_lines_s(rt_solver *s) {
+  const size_t Lp = s->Lpad;
+  rt_status st;
+  if ((st = line_maps_s<S>(s, false, s->map, s->lc))) return st;
+  std::vector<double> lineB(2 * Lp, 0.0);
+  for (int half = 0; half < 2; ++half)
+    for (int gl = 0; gl < s->Gl; ++gl)
+      for (int ip = 0; ip < s->H; ++ip) lineB[half * Lp + ip + static_cast<size_t>(s->H) * gl] = s->gt.B[s->g_lo + gl];
   if ((st = upload(s, s->lineB, lineB.data(), lineB.size() * sizeof(double)))) return st;
   std::vector<double> sig(s->Gl);
   for (int gl = 0; gl < s->Gl; ++gl) sig[gl] = s->gt.rho[s->g_lo + gl] * s->gt.kappa[s->g_lo + gl];
@@ -687,13 +711,21 @@ static rt_status event_end(rt_solver *s, hipEvent_t e1) {
 }
 
 // One pass of T full steps, every segment at the same time level.
-static rt_status enqueue_pass(rt_solver *s, int T) {
+// coupled: the material-coupled sweep (T = 1, per-cell emission).
+static rt_status enqueue_pass(rt_solver *s, int T, bool coupled = false) {
   if (s->pending && s->Tp != T) {
     rt_status st = apply_correction(s);
     if (st) return st;
   }
   const int per_half = s->Q * s->Sg;
   SegArgs a = seg_args(s);
+  if (coupled) {
+    a.map = static_cast<const double *>(s->map_unit.p);
+    a.lc = static_cast<const double *>(s->lc_unit.p);
+    a.bcell = static_cast<const double *>(s->Bcell.p);
+    a.Gl = s->Gl;
+    a.H = s->H;
+  }
   hipEvent_t e1;
   rt_status st = event_begin(s, &e1);
   if (st) return st;
@@ -826,6 +858,7 @@ static rt_status finalize(rt_solver *s) {
 
 extern "C" rt_status rt_advance(rt_solver *s, int nsteps) {
   if (!s || nsteps < 0) return fail(s, RT_ERR_ARG, "rt_advance: bad argument");
+  if (s->material) return fail(s, RT_ERR_STATE, "material coupling is on: step with rt_material_step / rt_material_sweep");
   HIP_TRY(s, hipSetDevice(s->device));
   rt_status st = check_validation(s);
   if (st) return st;
@@ -854,6 +887,125 @@ extern "C" rt_status rt_solve(rt_solver *s) {
 }
 
 extern "C" void *rt_stream(rt_solver *s) { return s ? static_cast<void *>(s->stream) : nullptr; }
+
+// ---------------------------------------------------------------------------
+// material-temperature coupling (include/rtsn.h)
+// ---------------------------------------------------------------------------
+static rt_status compute_moments(rt_solver *s);
+
+template <int S>
+static rt_status unit_maps_s(rt_solver *s) {
+  return line_maps_s<S>(s, true, s->map_unit, s->lc_unit);
+}
+
+static rt_status material_planck(rt_solver *s) {
+  HIP_TRY(s, launch_planck_cells(s->pc, static_cast<const double *>(s->Tcell.p), static_cast<double *>(s->Bcell.p),
+                                 s->stream));
+  return RT_OK;
+}
+
+extern "C" rt_status rt_material_enable(rt_solver *s, double rho_cv, const double *T_cells) {
+  if (!s) return fail(nullptr, RT_ERR_ARG, "rt_material_enable: NULL handle");
+  if (!(rho_cv > 0.0) || !std::isfinite(rho_cv)) return fail(s, RT_ERR_ARG, "rt_material_enable: rho_cv must be > 0");
+  if (s->p.use_correction && s->p.V != 0.0)
+    return fail(s, RT_ERR_PARAM, "material coupling needs the v/c correction off (V = 0 or use_correction = 0)");
+  HIP_TRY(s, hipSetDevice(s->device));
+  rt_status st = finalize(s);  // the state at the requested time, exact
+  if (st) return st;
+  const size_t N = s->p.N, NG = N * s->Gl;
+  if (!s->Tcell.p) {
+    hipError_t e = dalloc(s->Tcell, sizeof(double) * N);
+    if (!e) e = dalloc(s->Bcell, sizeof(double) * NG);
+    if (!e) e = dalloc(s->qbuf, sizeof(double) * N);
+    if (!e) e = dalloc(s->edges, sizeof(double) * (s->p.G + 1));
+    if (!e) e = dalloc(s->map_unit, s->map.bytes);
+    if (!e) e = dalloc(s->lc_unit, s->lc.bytes);
+    if (e) return fail(s, RT_ERR_NOMEM, std::string("material buffers: ") + hipGetErrorString(e));
+  }
+  switch (s->scheme) {
+    case SCHEME_BE: st = unit_maps_s<SCHEME_BE>(s); break;
+    case SCHEME_CN: st = unit_maps_s<SCHEME_CN>(s); break;
+    default: st = unit_maps_s<SCHEME_BDF2>(s); break;
+  }
+  if (st) return st;
+  std::vector<double> T0(N, s->p.T);
+  if (T_cells) std::copy(T_cells, T_cells + N, T0.begin());
+  if ((st = upload(s, s->Tcell, T0.data(), N * sizeof(double)))) return st;
+  if ((st = upload(s, s->edges, s->gt.e_edge.data(), (s->p.G + 1) * sizeof(double)))) return st;
+  PlanckCells &pc = s->pc;
+  phys::PlanckIntegrator().nodes(pc.node, pc.weight);
+  pc.e_edge = static_cast<const double *>(s->edges.p);
+  pc.G = s->p.G;
+  pc.g_lo = s->g_lo;
+  pc.Gl = s->Gl;
+  pc.N = s->p.N;
+  pc.a_c = phys::rad_a_long() * phys::kLight;
+  pc.kcon = phys::kBoltzmannJPK;
+  pc.accuracy = std::numeric_limits<double>::epsilon();
+  s->wsum = 0.0;
+  for (double w : s->wt) s->wsum += w;
+  s->rho_cv = rho_cv;
+  if ((st = material_planck(s))) return st;
+  HIP_TRY(s, hipStreamSynchronize(s->stream));  // T0 dies at return
+  s->material = true;
+  return RT_OK;
+}
+
+extern "C" rt_status rt_material_sweep(rt_solver *s, double *d_q) {
+  if (!s) return fail(nullptr, RT_ERR_ARG, "rt_material_sweep: NULL handle");
+  if (!s->material) return fail(s, RT_ERR_STATE, "rt_material_sweep: call rt_material_enable first");
+  HIP_TRY(s, hipSetDevice(s->device));
+  rt_status st = check_validation(s);
+  if (st) return st;
+  if ((st = ensure_equilibrium(s))) return st;
+  if ((st = finalize(s))) return st;
+  if ((st = enqueue_pass(s, 1, true))) return st;
+  if ((st = compute_moments(s))) return st;  // finalizes the pass
+  HIP_TRY(s, launch_material_q(static_cast<const double *>(s->mom.p), static_cast<const double *>(s->Bcell.p),
+                               static_cast<const double *>(s->sigma.p), s->wsum,
+                               d_q ? d_q : static_cast<double *>(s->qbuf.p), s->Gl, s->p.N, s->stream));
+  return RT_OK;
+}
+
+extern "C" rt_status rt_material_update(rt_solver *s, const double *d_q) {
+  if (!s) return fail(nullptr, RT_ERR_ARG, "rt_material_update: NULL handle");
+  if (!s->material) return fail(s, RT_ERR_STATE, "rt_material_update: call rt_material_enable first");
+  HIP_TRY(s, hipSetDevice(s->device));
+  HIP_TRY(s, launch_material_update(static_cast<double *>(s->Tcell.p), d_q ? d_q : static_cast<const double *>(s->qbuf.p),
+                                    s->p.dt, s->rho_cv, s->p.N, s->stream));
+  return material_planck(s);
+}
+
+extern "C" rt_status rt_material_step(rt_solver *s, int nsteps) {
+  if (!s || nsteps < 0) return fail(s, RT_ERR_ARG, "rt_material_step: bad argument");
+  if (s->g_lo != 0 || s->g_hi != s->p.G)
+    return fail(s, RT_ERR_STATE, "rt_material_step: the handle holds a group shard; sum q over the shards "
+                                 "(rt_material_sweep, all-reduce, rt_material_update)");
+  for (int n = 0; n < nsteps; ++n) {
+    rt_status st = rt_material_sweep(s, nullptr);
+    if (st) return st;
+    if ((st = rt_material_update(s, nullptr))) return st;
+  }
+  return RT_OK;
+}
+
+// which: 0 T(x), 1 B per cell
+static rt_status material_fetch(rt_solver *s, int which, double *out, const char *what) {
+  if (!s || !out) return fail(s, RT_ERR_ARG, std::string(what) + ": bad argument");
+  if (!s->material) return fail(s, RT_ERR_STATE, std::string(what) + ": material coupling is off");
+  HIP_TRY(s, hipSetDevice(s->device));
+  const size_t count = which == 0 ? s->p.N : static_cast<size_t>(s->p.N) * s->Gl;
+  const void *src = which == 0 ? s->Tcell.p : s->Bcell.p;
+  HIP_TRY(s, hipMemcpyAsync(out, src, sizeof(double) * count, hipMemcpyDeviceToHost, s->stream));
+  HIP_TRY(s, hipStreamSynchronize(s->stream));
+  return RT_OK;
+}
+
+extern "C" rt_status rt_get_temperature(rt_solver *s, double *T_cells) {
+  return material_fetch(s, 0, T_cells, "rt_get_temperature");
+}
+
+extern "C" rt_status rt_get_cell_planck(rt_solver *s, double *B) { return material_fetch(s, 1, B, "rt_get_cell_planck"); }
 
 // ---------------------------------------------------------------------------
 // results
@@ -1183,6 +1335,7 @@ extern "C" const char *rt_status_string(rt_status st) {
     case RT_ERR_DEVICE: return "device error";
     case RT_ERR_TIMEOUT: return "timeout (reserved)";
     case RT_ERR_ARG: return "bad argument";
+    case RT_ERR_STATE: return "not valid in the handle's mode";
   }
   return "unknown";
 }

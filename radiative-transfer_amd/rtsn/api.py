@@ -17,7 +17,8 @@ LIB_PATH = Path(os.environ.get("RTSN_LIB", PKG_ROOT / "lib" / "librtsn.so"))  # 
 HEADER = REPO_ROOT / "include" / "rtsn.h"
 
 STATUS = {0: "ok", 1: "io error", 2: "parse error", 3: "invalid parameter", 4: "correction validation failed",
-          5: "out of memory", 6: "device error", 7: "timeout (reserved)", 8: "bad argument"}
+          5: "out of memory", 6: "device error", 7: "timeout (reserved)", 8: "bad argument",
+          9: "not valid in the handle's mode"}
 
 
 class RtError(RuntimeError):
@@ -109,6 +110,12 @@ def lib():
         L.rt_get_pipeline.argtypes = [vp, C.POINTER(C.c_int)]
         L.rt_pipeline_state.argtypes = [vp, C.POINTER(C.c_longlong), C.POINTER(C.c_int), C.POINTER(C.c_int)]
         L.rt_get_time_block.argtypes = [vp, C.POINTER(C.c_int)]
+        L.rt_material_enable.argtypes = [vp, C.c_double, dp]
+        L.rt_material_sweep.argtypes = [vp, vp]
+        L.rt_material_update.argtypes = [vp, vp]
+        L.rt_material_step.argtypes = [vp, C.c_int]
+        L.rt_get_temperature.argtypes = [vp, dp]
+        L.rt_get_cell_planck.argtypes = [vp, dp]
         L.rt_status_string.argtypes = [C.c_int]
         L.rt_status_string.restype = C.c_char_p
         L.rt_last_error.argtypes = [vp]
@@ -379,6 +386,50 @@ class Solver:
                 and out.is_contiguous() and out.numel() == self.N):
             raise ValueError("group_absorption: need a contiguous float64 CUDA tensor of N elements")
         self.group_absorption_device(out.data_ptr())
+
+    # ---- material-temperature coupling (beyond the reference; rtsn.h rt_material_*) ----
+    def material_enable(self, rho_cv: float, T_cells=None):
+        """T(x) coupling on: rho_cv > 0, T_cells (N) or None for the uniform .prm T."""
+        T = None if T_cells is None else np.ascontiguousarray(T_cells, dtype=np.float64)
+        if T is not None and T.size != self.N:
+            raise ValueError("material_enable: T_cells must hold N values")
+        _check(lib().rt_material_enable(self._h, float(rho_cv), None if T is None else _dp(T)),
+               "rt_material_enable", self._h)
+
+    @staticmethod
+    def _device_vec(t, n: int, what: str):
+        if t is None:
+            return None
+        import torch
+        if not (isinstance(t, torch.Tensor) and t.is_cuda and t.dtype == torch.float64
+                and t.is_contiguous() and t.numel() == n):
+            raise ValueError(f"{what}: need a contiguous float64 CUDA tensor of {n} elements")
+        return t.data_ptr()
+
+    def material_sweep(self, q=None):
+        """One coupled full step; this handle's q (N) into the CUDA tensor q (None:
+        kept inside the handle), ordered on the handle's stream."""
+        _check(lib().rt_material_sweep(self._h, self._device_vec(q, self.N, "material_sweep")),
+               "rt_material_sweep", self._h)
+
+    def material_update(self, q=None):
+        """T += dt q / rho_cv from the group-summed q (CUDA tensor, or None: the handle's own)."""
+        _check(lib().rt_material_update(self._h, self._device_vec(q, self.N, "material_update")),
+               "rt_material_update", self._h)
+
+    def material_step(self, nsteps: int = 1):
+        _check(lib().rt_material_step(self._h, int(nsteps)), "rt_material_step", self._h)
+
+    def temperature(self) -> np.ndarray:
+        out = np.empty(self.N)
+        _check(lib().rt_get_temperature(self._h, _dp(out)), "rt_get_temperature", self._h)
+        return out
+
+    def cell_planck(self) -> np.ndarray:
+        """(G_local, N) per-cell emission B_g(T(x)) used by the next coupled step."""
+        out = np.empty(self.N * self.G)
+        _check(lib().rt_get_cell_planck(self._h, _dp(out)), "rt_get_cell_planck", self._h)
+        return out.reshape(self.N, self.G).T.copy()
 
     # ---- measurement ----
     def set_profiling(self, on: bool):

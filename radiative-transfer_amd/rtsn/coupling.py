@@ -1,0 +1,37 @@
+"""Material-temperature coupling across group shards (include/rtsn.h,
+rt_material_*; beyond the reference, whose T is constant, solver.cpp:157).
+
+One process per GPU, each holding a block of energy groups.  Per full step
+every rank sweeps its groups with the per-cell emission B_g(T(x)) and writes
+its share of the exchange term q(x) = sum_g sigma_g (phi_g - W B_g); ONE
+all-reduce (sum) of those N doubles over the ranks -- RCCL over xGMI on the
+GPU box -- gives every rank the same q, and with it the same T update.  The
+all-reduce is issued on the solver's own HIP stream, so sweep, collective and
+update stay stream-ordered with no host synchronisation.
+"""
+from __future__ import annotations
+
+
+def coupled_steps(solver, nsteps: int, q, world_size: int = 1, group=None):
+    """nsteps coupled full steps of this rank's group shard.
+
+    solver: rtsn.Solver after material_enable (or anything with its
+    material_sweep(q) / material_update(q) methods); q: float64 tensor of N
+    elements on the solver's device (the exchange buffer); world_size > 1 sums
+    q over the ranks of `group` with torch.distributed.
+    """
+    import torch
+    import torch.distributed as dist
+
+    stream = None
+    if q.is_cuda:
+        stream = torch.cuda.ExternalStream(solver.stream, device=q.device)
+    for _ in range(int(nsteps)):
+        solver.material_sweep(q)
+        if world_size > 1:
+            if stream is not None:
+                with torch.cuda.stream(stream):
+                    dist.all_reduce(q, group=group)
+            else:
+                dist.all_reduce(q, group=group)
+        solver.material_update(q)

@@ -1,0 +1,225 @@
+"""Material-temperature coupling (include/rtsn.h rt_material_*), CPU side.
+
+The reference holds T constant (solver.cpp:157); SURVEY §8(f)-4 names the
+T(x) update fed by the group-sum all-reduce as the next row.  Its definition
+ is restated in the oracle (rt_oracle.c orc_material_*), which
+these tests pin by properties the definition guarantees -- there is no
+reference output to pin it against ("parity unpinned" beyond these
+properties):
+  * the per-cell Planck emission at a uniform T is the reference's group
+    table (Planck.cpp:44-77) -- bitwise for every group but the last, whose
+    remainder takes the other groups as one integral;
+  * backward Euler conserves sum_x dx (sum_g phi_g / c + rho_cv T) up to the
+    boundary outflow, to rounding;
+  * a uniform equilibrium (psi = B_g(T), source inflow B_g) stays put;
+  * material colder than the radiation heats monotonically toward it;
+  * group shards whose q are summed reproduce the one-shard run (gloo,
+    world_size 2, through rtsn.coupling.coupled_steps -- the product's
+    multi-rank driver).
+"""
+from __future__ import annotations
+
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+
+from conftest import REPO
+
+C_LIGHT = 299.792458
+A_C = None  # a c of Constants.h:22-23, from the oracle's table below
+
+
+def params(oracle_mod, ts=1, M=4, G=4, N=40, bc_left=2, bc_right=0, kappa=10.0, dt=1e-3, **over):
+    p = oracle_mod.default_params()
+    p.update(M=M, G=G, N=N, X=0.4, dx=0.4 / N, efirst=0.1, elast=10.0, bc_left=bc_left, bc_right=bc_right,
+             use_mg_equilib=0, rho=1.0, kappa_grey=kappa, T=1.0, V=0.0, use_correction=0, ts_method=ts, dt=dt,
+             max_timesteps=1, include_validation=0)
+    p["psi_source"] = np.zeros((M, G))
+    p.update(over)
+    return p
+
+
+def t_profile(N, lo=0.7, hi=1.3):
+    x = (np.arange(N) + 0.5) / N
+    return lo + (hi - lo) * 0.5 * (1.0 + np.sin(2.0 * np.pi * x))
+
+
+def total_energy(s, p, rho_cv):
+    """sum_x dx (sum_g phi_g / c + rho_cv T) over the solver's groups and T."""
+    phi, _, _ = s.moments()
+    return p["dx"] * float((phi.sum(axis=0) / C_LIGHT + rho_cv * s.temperature()).sum())
+
+
+def net_outflow(s, p):
+    """sum_i w_i |mu_i| (outflow node - inflow value) over lines, from the step-end ends."""
+    e = s.ends()
+    mu, w = s.quad()
+    M, N = p["M"], p["N"]
+    net = 0.0
+    for i in range(M):
+        if mu[i] < 0:
+            out, inn = e[i, :, 0, 0], (s.psi_source()[i, :] if p["bc_right"] == 1 else 0.0)
+        else:
+            out = e[i, :, N - 1, 1]
+            inn = e[M - 1 - i, :, 0, 0] if p["bc_left"] == 2 else s.psi_source()[i, :]
+        net += w[i] * abs(mu[i]) * float(np.sum(out - inn))
+    return net
+
+
+def test_cell_planck_uniform_equals_group_table(oracle_mod):
+    p = params(oracle_mod, G=12, efirst=0.01, elast=30.0)
+    for T in (0.05, 0.3, 1.0, 4.0):
+        p["T"] = T
+        s = oracle_mod.OracleSolver(p)
+        table = s.groups()
+        e = table["e_edge"]
+        s.material_enable(1.0)
+        B = s.cell_planck()
+        assert np.all(B == B[:, :1])  # uniform T: every cell the same
+        np.testing.assert_array_equal(B[:-1, 0], table["B"][:-1])
+        acT4 = table["B"].sum()
+        assert abs(B[-1, 0] - table["B"][-1]) <= 1e-14 * acT4
+        for g in (0, 5, 11):
+            assert oracle_mod.planck_cell(T, e, g) == B[g, 0]
+
+
+def test_cell_planck_edge_temperatures(oracle_mod):
+    e = np.array([0.0, 0.1, 1.0, 10.0])
+    for T in (0.0, -1.0, float("nan"), float("inf")):
+        assert all(oracle_mod.planck_cell(T, e, g) == 0.0 for g in range(3))
+    # one group: the grey total a c T^4 (kcon x rad_a_long c T^4)
+    b1 = oracle_mod.planck_cell(2.0, np.array([0.0, 5.0]), 0)
+    b2 = sum(oracle_mod.planck_cell(2.0, e, g) for g in range(3))
+    assert b1 == pytest.approx(b2, rel=1e-14)
+
+
+@pytest.mark.parametrize("bc_left,bc_right", [(2, 0), (0, 0), (1, 1), (2, 1)])
+def test_backward_euler_conserves_energy(oracle_mod, bc_left, bc_right):
+    p = params(oracle_mod, ts=1, bc_left=bc_left, bc_right=bc_right)
+    p["psi_source"] = np.full((p["M"], p["G"]), 0.3)
+    s = oracle_mod.OracleSolver(p)
+    rho_cv = 5.0
+    s.material_enable(rho_cv, t_profile(p["N"]))
+    for _ in range(15):
+        e0 = total_energy(s, p, rho_cv)
+        s.material_step(1)
+        e1 = total_energy(s, p, rho_cv)
+        resid = (e1 - e0) + p["dt"] * net_outflow(s, p)
+        assert abs(resid) <= 1e-13 * e1, (resid, e1)
+
+
+@pytest.mark.parametrize("ts,dt", [(1, 1e-3), (2, 1e-3), (3, 1e-4)])
+def test_uniform_equilibrium_is_stationary(oracle_mod, ts, dt):
+    """psi = B_g(T) everywhere, inflow B_g (use_mg_equilib with V = 0): T and psi stay."""
+    p = params(oracle_mod, ts=ts, dt=dt, bc_left=1, bc_right=1, use_mg_equilib=1)
+    s = oracle_mod.OracleSolver(p)
+    psi0 = s.psi()
+    s.material_enable(3.0)
+    s.material_step(10)
+    np.testing.assert_allclose(s.temperature(), 1.0, rtol=1e-12)
+    np.testing.assert_allclose(s.psi(), psi0, rtol=1e-11)
+
+
+def test_cold_material_heats_toward_radiation(oracle_mod):
+    """Radiation at B_g(1 keV) with inflow B_g(1), material at 0.5 keV: T rises
+    monotonically and stays below the radiation temperature."""
+    p = params(oracle_mod, ts=1, bc_left=1, bc_right=1, use_mg_equilib=1, kappa=20.0)
+    s = oracle_mod.OracleSolver(p)
+    s.material_enable(2.0, np.full(p["N"], 0.5))
+    prev = s.temperature()
+    for _ in range(40):
+        s.material_step(1)
+        T = s.temperature()
+        assert np.all(T >= prev - 1e-14) and np.all(T <= 1.0 + 1e-12)
+        prev = T
+    assert prev.min() > 0.8
+
+
+def test_material_requires_correction_off(oracle_mod):
+    p = params(oracle_mod, V=2.0, use_correction=1)
+    s = oracle_mod.OracleSolver(p)
+    with pytest.raises(oracle_mod.OracleError):
+        s.material_enable(1.0)
+
+
+def test_group_shards_sum_q(oracle_mod):
+    """Two group shards with q summed equal the one-shard run (up to the order of the group sum)."""
+    p = params(oracle_mod, ts=1, G=6)
+    T0 = t_profile(p["N"])
+    full = oracle_mod.OracleSolver(p)
+    full.material_enable(4.0, T0)
+    parts = [oracle_mod.OracleSolver(p, g_lo=lo, g_hi=hi) for lo, hi in ((0, 2), (2, 6))]
+    for s in parts:
+        s.material_enable(4.0, T0)
+    for _ in range(8):
+        full.material_step(1)
+        q = sum(s.material_sweep() for s in parts)
+        for s in parts:
+            s.material_update(q)
+    for s in parts:
+        np.testing.assert_allclose(s.temperature(), full.temperature(), rtol=1e-13)
+    psi = np.concatenate([s.psi() for s in parts], axis=1)
+    np.testing.assert_allclose(psi, full.psi(), rtol=1e-12, atol=1e-14 * np.abs(full.psi()).max())
+
+
+# ---------------------------------------------------------------------------
+# world_size 2 over gloo: rtsn.coupling.coupled_steps with an oracle stand-in
+# ---------------------------------------------------------------------------
+class OracleMaterialShard:
+    """CPU stand-in with the two methods coupled_steps uses (the test's, never the product's)."""
+
+    def __init__(self, orc):
+        self.s = orc
+
+    def material_sweep(self, q):
+        import torch
+        q.copy_(torch.from_numpy(self.s.material_sweep()))
+
+    def material_update(self, q):
+        self.s.material_update(q.numpy())
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, outdir):
+    import torch
+    import torch.distributed as dist
+    sys.path.insert(0, str(REPO / "oracle"))
+    sys.path.insert(0, str(REPO / "radiative-transfer_amd"))
+    import oracle
+    from rtsn.coupling import coupled_steps
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        p = params(oracle, ts=1, G=6)
+        lo, hi = ((0, 3), (3, 6))[rank]
+        s = oracle.OracleSolver(p, g_lo=lo, g_hi=hi)
+        s.material_enable(4.0, t_profile(p["N"]))
+        q = torch.zeros(p["N"], dtype=torch.float64)
+        coupled_steps(OracleMaterialShard(s), 6, q, world_size=world)
+        np.save(os.path.join(outdir, f"T{rank}.npy"), s.temperature())
+        np.save(os.path.join(outdir, f"psi{rank}.npy"), s.psi())
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_rank_coupled_steps(tmp_path, oracle_mod):
+    import torch.multiprocessing as mp
+    mp.start_processes(_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True, start_method="spawn")
+    T = [np.load(tmp_path / f"T{r}.npy") for r in range(2)]
+    np.testing.assert_array_equal(T[0], T[1])  # every rank holds the same T(x)
+    p = params(oracle_mod, ts=1, G=6)
+    full = oracle_mod.OracleSolver(p)
+    full.material_enable(4.0, t_profile(p["N"]))
+    full.material_step(6)
+    np.testing.assert_allclose(T[0], full.temperature(), rtol=1e-13)
+    psi = np.concatenate([np.load(tmp_path / f"psi{r}.npy") for r in range(2)], axis=1)
+    np.testing.assert_allclose(psi, full.psi(), rtol=1e-12, atol=1e-14 * np.abs(full.psi()).max())

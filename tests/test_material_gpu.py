@@ -1,0 +1,292 @@
+"""Material-temperature coupling on the GPU (rt_material_*) against the oracle.
+
+The device Planck kernel (planck_cells_kernel) against the oracle's long
+double restatement; the coupled sweep (sweep_block_kernel<S,1,0,true>, the
+per-cell emission scaling the map constants) + T update against
+orc_material_*; energy conservation of the BE coupling on the device; group
+shards summing q (two handles on one GPU; two ranks over gloo sharing it,
+through rtsn.coupling.coupled_steps).
+
+Tolerances: T(x) relative 1e-12 and the transport fields per group 1e-10
+(the north_star's 1e-10 for intensities); the device evaluates the Planck
+integrals in double (the oracle in the reference's long double Gauss nodes,
+glibc exp), so B_g agrees to ~1e-15 relative, except the last group, a
+remainder a c T^4 - (rest), which carries the rounding of a c T^4 (tolerance
+1e-13 a c T^4 absolute).
+"""
+from __future__ import annotations
+
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+
+from conftest import PRM_DIR, REPO
+from parity import per_group_rel
+from test_material import C_LIGHT, params, t_profile
+
+pytestmark = pytest.mark.gpu
+
+
+def to_rt(p: dict) -> dict:
+    q = dict(p)
+    q["bc_left_indicator"] = p["bc_left"]
+    q["bc_right_indicator"] = p["bc_right"]
+    return q
+
+
+def grey(T):
+    """kcon x rad_a_long c T^4 = sum_g B_g(T) (Planck.cpp:79-83)."""
+    import oracle
+    return oracle.planck_cell(T, np.array([0.0, 1.0]), 0) if T > 0 else 0.0
+
+
+def check_planck(gpu_B, orc_B, T):
+    """gpu_B, orc_B: (G, N) at T (N)."""
+    G = gpu_B.shape[0]
+    acT4 = np.array([grey(t) for t in T])
+    d = np.abs(gpu_B - orc_B)
+    lim = 1e-12 * np.abs(orc_B[:-1]) + 1e-15 * acT4[None, :]
+    assert np.all(d[:-1] <= lim), float(np.max(d[:-1] / np.maximum(lim, 1e-300)))
+    assert np.all(d[-1] <= 1e-13 * acT4 + 1e-300), float(np.max(d[-1] / np.maximum(acT4, 1e-300)))
+    rel = d[:-1] / np.maximum(np.abs(orc_B[:-1]), 1e-300)
+    return float(np.max(np.where(np.abs(orc_B[:-1]) > 1e-200, rel, 0.0))), G
+
+
+@pytest.mark.parametrize("grid", ["log", "llnl"])
+def test_device_planck_matches_oracle(rtsn_mod, oracle_mod, grid):
+    N = 257
+    T = np.geomspace(1e-3, 50.0, N)
+    T[:4] = [0.0, -1.0, 1e-8, 1.0]
+    if grid == "llnl":
+        p = oracle_mod.parse_prm(PRM_DIR / "llnl_slab_test.prm", table_dir=PRM_DIR)
+        p.update(N=N, max_timesteps=1)
+        p["dx"] = p["X"] / N
+    else:
+        p = params(oracle_mod, G=64, N=N, efirst=1e-3, elast=30.0)
+    orc = oracle_mod.OracleSolver(p)
+    orc.material_enable(1.0, T)
+    with rtsn_mod.Solver(to_rt(p)) as gpu:
+        gpu.material_enable(1.0, T)
+        B = gpu.cell_planck()
+    ref = orc.cell_planck()
+    assert np.all(B[:, :2] == 0.0)  # T = 0 and T < 0 emit nothing
+    check_planck(B, ref, T)
+
+
+def test_device_planck_uniform_matches_host_table(rtsn_mod, oracle_mod):
+    p = oracle_mod.parse_prm(PRM_DIR / "llnl_slab_test.prm", table_dir=PRM_DIR)
+    with rtsn_mod.Solver(to_rt(p)) as gpu:
+        table = gpu.groups()["B"]  # host Planck (long double, rt_planck_groups' algorithm)
+        gpu.material_enable(1.0)
+        B = gpu.cell_planck()
+    assert np.all(B == B[:, :1])
+    # the series difference s(z1) - s(z2) of a narrow group cancels: 1 ulp of exp
+    # becomes ~1e-13 relative, the scale check_planck allows
+    check_planck(B[:, :1], table[:, None], np.array([1.0]))
+
+
+def run_pair(rtsn_mod, oracle_mod, p, steps, rho_cv=5.0, T0=None, g_lo=0, g_hi=0):
+    T0 = t_profile(p["N"]) if T0 is None else T0
+    orc = oracle_mod.OracleSolver(p, g_lo=g_lo, g_hi=g_hi)
+    orc.material_enable(rho_cv, T0)
+    orc.material_step(steps)
+    gpu = rtsn_mod.Solver(to_rt(p), g_lo=g_lo, g_hi=g_hi)
+    gpu.material_enable(rho_cv, T0)
+    for _ in range(steps):  # a shard's own q, as the oracle shard does
+        gpu.material_sweep()
+        gpu.material_update()
+    return gpu, orc
+
+
+def compare(gpu, orc, tol=1e-10):
+    err = {"T": float(np.max(np.abs(gpu.temperature() - orc.temperature()) / np.abs(orc.temperature()))),
+           "psi": per_group_rel(gpu.psi(), orc.psi(), 1),
+           "ends": per_group_rel(gpu.ends(), orc.ends(), 1),
+           "phi": per_group_rel(gpu.moments()[0], orc.moments()[0], 0),
+           "B": per_group_rel(gpu.cell_planck(), orc.cell_planck(), 0)}
+    assert err["T"] <= 1e-12, err
+    for k in ("psi", "ends", "phi", "B"):
+        assert err[k] <= tol, err
+    return err
+
+
+@pytest.mark.parametrize("ts,dt", [(1, 1e-3), (2, 1e-3), (3, 1e-4)])
+@pytest.mark.parametrize("bc_left,bc_right", [(2, 0), (1, 1), (0, 0), (2, 1)])
+def test_coupled_steps_match_oracle(rtsn_mod, oracle_mod, ts, dt, bc_left, bc_right):
+    p = params(oracle_mod, ts=ts, dt=dt, M=6, G=5, N=150, bc_left=bc_left, bc_right=bc_right)
+    p["psi_source"] = np.linspace(0.5, 2.0, p["M"] * p["G"]).reshape(p["M"], p["G"])
+    gpu, orc = run_pair(rtsn_mod, oracle_mod, p, 6)
+    with gpu:
+        compare(gpu, orc)
+
+
+@pytest.mark.parametrize("ts", [1, 2])
+def test_coupled_long_lines_llnl_groups(rtsn_mod, oracle_mod, ts):
+    """20k-cell lines in many segments (fold + finalize of every coupled pass),
+    reflective left boundary, LL opacities (up to 1e6) on groups 10..26.  (The
+    reference's BDF2 grows ~30x per step at these opacities, DESIGN.md §4, so
+    BE and CN here; BDF2 is covered on the small configurations.)"""
+    p = oracle_mod.parse_prm(PRM_DIR / "llnl_slab_test.prm", table_dir=PRM_DIR)
+    p.update(N=20000, M=4, bc_left=2, dt=1e-5, max_timesteps=1, ts_method=ts)
+    p["dx"] = p["X"] / p["N"]
+    p["psi_source"] = np.zeros((p["M"], p["G"]))
+    gpu, orc = run_pair(rtsn_mod, oracle_mod, p, 3, rho_cv=0.5, T0=t_profile(p["N"], 0.5, 1.5), g_lo=10, g_hi=26)
+    with gpu:
+        compare(gpu, orc)
+
+
+def test_backward_euler_energy_on_device(rtsn_mod, oracle_mod):
+    from test_material import net_outflow, total_energy
+    p = params(oracle_mod, ts=1, M=8, G=6, N=300, bc_left=2, bc_right=0)
+    rho_cv = 5.0
+    with rtsn_mod.Solver(to_rt(p)) as gpu:
+        gpu.material_enable(rho_cv, t_profile(p["N"]))
+        for _ in range(10):
+            e0 = total_energy(gpu, p, rho_cv)
+            gpu.material_step(1)
+            e1 = total_energy(gpu, p, rho_cv)
+            resid = (e1 - e0) + p["dt"] * net_outflow(GpuView(gpu), p)
+            assert abs(resid) <= 1e-12 * e1, (resid, e1)
+
+
+class GpuView:
+    """rtsn.Solver with the oracle-named accessors net_outflow reads."""
+
+    def __init__(self, s):
+        self.s = s
+
+    def ends(self):
+        return self.s.ends()
+
+    def quad(self):
+        return self.s.quad()
+
+    def psi_source(self):
+        return self.s.psi_source()
+
+
+def test_group_shards_on_one_gpu(rtsn_mod, oracle_mod):
+    """Two shard handles, q summed on the device, equal one full handle."""
+    import torch
+    p = to_rt(params(oracle_mod, ts=2, G=7, N=200, M=6, bc_left=2))
+    T0 = t_profile(p["N"])
+    with rtsn_mod.Solver(p) as full:
+        full.material_enable(4.0, T0)
+        full.material_step(5)
+        T_full, psi_full = full.temperature(), full.psi()
+    shards = [rtsn_mod.Solver(p, g_lo=lo, g_hi=hi) for lo, hi in ((0, 3), (3, 7))]
+    q = [torch.zeros(p["N"], dtype=torch.float64, device="cuda") for _ in shards]
+    for s in shards:
+        s.material_enable(4.0, T0)
+    for _ in range(5):
+        for s, qq in zip(shards, q):
+            s.material_sweep(qq)
+        for s in shards:
+            s.synchronize()
+        tot = q[0] + q[1]
+        torch.cuda.synchronize()
+        for s in shards:
+            s.material_update(tot)
+        for s in shards:
+            s.synchronize()
+    for s in shards:
+        np.testing.assert_allclose(s.temperature(), T_full, rtol=1e-13)
+    psi = np.concatenate([s.psi() for s in shards], axis=1)
+    assert per_group_rel(psi, psi_full, 1) <= 1e-12
+    for s in shards:
+        s.close()
+
+
+def test_coupled_steps_driver_single_rank(rtsn_mod, oracle_mod):
+    """rtsn.coupling.coupled_steps (the multi-rank driver, here one rank) == rt_material_step."""
+    import torch
+    from rtsn.coupling import coupled_steps
+    p = to_rt(params(oracle_mod, ts=3, dt=1e-4, G=5, N=100))
+    out = []
+    for use_driver in (False, True):
+        with rtsn_mod.Solver(p) as s:
+            s.material_enable(4.0, t_profile(p["N"]))
+            if use_driver:
+                coupled_steps(s, 4, torch.zeros(p["N"], dtype=torch.float64, device="cuda"))
+            else:
+                s.material_step(4)
+            out.append((s.temperature(), s.ends()))
+    np.testing.assert_array_equal(out[0][0], out[1][0])
+    np.testing.assert_array_equal(out[0][1], out[1][1])
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _rank(rank, world, port, outdir):
+    """One rank of the coupled run: its group shard on the (shared) GPU, q
+    all-reduced over gloo on the solver's stream (RCCL needs one GPU per rank;
+    the 8-GPU run uses it through the same coupled_steps)."""
+    import torch
+    import torch.distributed as dist
+    sys.path.insert(0, str(REPO / "radiative-transfer_amd"))
+    sys.path.insert(0, str(REPO / "oracle"))
+    sys.path.insert(0, str(REPO / "tests"))
+    import oracle
+    import rtsn
+    from rtsn.coupling import coupled_steps
+    from test_material import params as mparams
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        p = to_rt(mparams(oracle, ts=1, G=6, N=120, M=4))
+        lo, hi = ((0, 2), (2, 6))[rank]
+        with rtsn.Solver(p, g_lo=lo, g_hi=hi) as s:
+            s.material_enable(4.0, t_profile(p["N"]))
+            q = torch.zeros(p["N"], dtype=torch.float64, device="cuda")
+            coupled_steps(s, 5, q, world_size=world)
+            np.save(os.path.join(outdir, f"T{rank}.npy"), s.temperature())
+            np.save(os.path.join(outdir, f"psi{rank}.npy"), s.psi())
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_ranks_share_gpu_coupled(tmp_path, rtsn_mod, oracle_mod):
+    import torch.multiprocessing as mp
+    mp.start_processes(_rank, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True, start_method="spawn")
+    T = [np.load(tmp_path / f"T{r}.npy") for r in range(2)]
+    np.testing.assert_array_equal(T[0], T[1])
+    p = params(oracle_mod, ts=1, G=6, N=120, M=4)
+    orc = oracle_mod.OracleSolver(p)
+    orc.material_enable(4.0, t_profile(p["N"]))
+    orc.material_step(5)
+    np.testing.assert_allclose(T[0], orc.temperature(), rtol=1e-12)
+    psi = np.concatenate([np.load(tmp_path / f"psi{r}.npy") for r in range(2)], axis=1)
+    assert per_group_rel(psi, orc.psi(), 1) <= 1e-10
+
+
+def test_material_mode_errors(rtsn_mod, oracle_mod):
+    p = to_rt(params(oracle_mod, G=4))
+    with rtsn_mod.Solver(p) as s:
+        for bad in (0.0, -1.0, float("nan")):
+            with pytest.raises(rtsn_mod.RtError) as e:
+                s.material_enable(bad)
+            assert e.value.status == 8
+        with pytest.raises(rtsn_mod.RtError) as e:
+            s.material_sweep()
+        assert e.value.status == 9
+        s.material_enable(2.0)
+        with pytest.raises(rtsn_mod.RtError) as e:
+            s.advance(1)
+        assert e.value.status == 9
+    with rtsn_mod.Solver(p, g_lo=1, g_hi=3) as s:
+        s.material_enable(2.0)
+        with pytest.raises(rtsn_mod.RtError) as e:
+            s.material_step(1)
+        assert e.value.status == 9
+    q = dict(p, V=2.0, use_correction=1)
+    with rtsn_mod.Solver(q) as s:
+        with pytest.raises(rtsn_mod.RtError) as e:
+            s.material_enable(2.0)
+        assert e.value.status == 3
