@@ -3,6 +3,7 @@
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--variant v0|corr]
                     [--scaling weak|strong] [--time-block T] [--no-cpu-baseline]
+                    [--material-steps K]
 
 Workload (SURVEY.md §8(d) "SL"): 1D slab X = 0.4 cm, N = 1e6 cells, S64
 Gauss-Legendre (M = 64), 128 energy groups per GPU on a log grid 0.001-30 keV
@@ -23,7 +24,13 @@ ranks.  After timing, the group-summed absorption rate is all-reduced over
 RCCL once (the north_star group-sum hook) and checked.
 
 Time blocking: one sweep launch (a "pass") advances T full steps (default
-T = 4, --time-block), reading and writing the state once.
+T = 16, --time-block), reading and writing the state once.
+
+material (--material-steps, default 3; 0 skips): after the sweep measurement
+the same shard runs the material-temperature coupling (rt_material_*, beyond
+the reference): BE steps with the per-cell Planck emission, the shard's
+exchange term q(x), one all-reduce of q over the ranks and the T update.
+Reported under "material"; not part of value.
 
 roofline: per pass, the algorithmic HBM bytes (16 B read + 16 B write per
 cell x line) and the algorithmic FP64 flops (2 per coefficient of the
@@ -320,6 +327,54 @@ def run_rank(solver, p: dict, steps: int, warmup: int, world: int, device, shard
     return line, absorb, gathered
 
 
+def run_material(p: dict, info, world: int, device, local: int, steps: int) -> dict:
+    """The material-temperature coupling (rt_material_*, beyond the reference) on
+    the same SL shard: BE steps (the reference's BDF2 diverges on SL within a few
+    steps, DESIGN.md §4, which would leave T meaningless) from T = 1 keV, each
+    step = coupled sweep + phi + the shard's q(x) + ONE all-reduce (sum) of q
+    over the ranks (RCCL on the GPU box) + T update + per-cell Planck.  One
+    warm-up step, then `steps` timed between barrier + device sync, max over
+    ranks.  Host-synchronised around the all-reduce (coupled_steps(host_sync=True))."""
+    import torch
+    import torch.distributed as dist
+    import rtsn
+    from rtsn.coupling import coupled_steps
+
+    G_total, g_lo, g_hi = info
+    q = dict(p, ts_method=1)
+    with rtsn.Solver(q, device=local, g_lo=g_lo, g_hi=g_hi) as s:
+        s.material_enable(1.0)
+        buf = torch.zeros(q["N"], dtype=torch.float64, device=device)
+        coupled_steps(s, 1, buf, world_size=world, host_sync=True)
+
+        def barrier():
+            s.synchronize()
+            if world > 1:
+                dist.barrier()
+            torch.cuda.synchronize(device)
+
+        barrier()
+        t0 = time.perf_counter()
+        coupled_steps(s, steps, buf, world_size=world, host_sync=True)
+        barrier()
+        wall = time.perf_counter() - t0
+        T = s.temperature()
+    t = torch.tensor([wall], dtype=torch.float64, device=device)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    wall = float(t[0])
+    u = torch.tensor([float(q["M"]) * (g_hi - g_lo) * q["N"] * steps], dtype=torch.float64, device=device)
+    if world > 1:
+        dist.all_reduce(u)
+    upd = float(u[0])
+    return {"what": "material-temperature coupling (beyond the reference): BE step with per-cell Planck "
+                    "emission, q(x) all-reduce over ranks, T update",
+            "ts_method": 1, "steps": steps, "warmup": 1, "ms_per_step": 1e3 * wall / steps,
+            "updates_per_s": upd / wall, "allreduce_bytes_per_step": 8 * q["N"],
+            "rho_cv": 1.0, "T_range_keV": [float(T.min()), float(T.max())],
+            "state_finite": bool(np.isfinite(T).all())}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -336,6 +391,8 @@ def main():
     ap.add_argument("--schedule", choices=["pipelined", "aligned"], default="pipelined",
                     help="staggered segments (exact starts) or aligned segments with deferred correction")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--material-steps", type=int, default=3,
+                    help="timed steps of the material-coupled run reported under 'material' (0: skip)")
     # rehearsal of the multi-rank path on a one-GPU box: every rank on cuda:0, gloo
     ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl", help=argparse.SUPPRESS)
     ap.add_argument("--share-device", action="store_true", help=argparse.SUPPRESS)
@@ -374,12 +431,14 @@ def main():
     line, _, _ = run_rank(solver, p, steps, warmup, world, device, info, args.scaling, shards)
     line["roofline"]["traffic"] = load_traffic(args.variant, solver.time_block,
                                                line["roofline"]["algorithmic_bytes_per_launch"])
+    solver.close()  # frees the sweep's state before the coupled run allocates its own
+    if args.material_steps > 0:
+        line["material"] = run_material(p, info, world, device, local, args.material_steps)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(args.variant)
         line["reference_config"] = reference_config_timings()
     if rank == 0:
         print(json.dumps(line), flush=True)
-    solver.close()
     if world > 1:
         dist.destroy_process_group()
 

@@ -124,14 +124,16 @@ __device__ __forceinline__ void head_cell(const double *lcp, size_t stride, doub
 // store, and prefetch the next chunk's rows into the registers just
 // consumed.  LAST: the segment's final chunk -- no prefetch, and only its
 // first nv cells are real (X is left after cell nv-1).  CB: the map constants
-// are scaled by the cell's B_g(T(x)) (bv, prefetched with the rows by bload).
-template <int S, int T, int MODE, int C, bool LAST, bool CB, typename BL>
+// are scaled by the cell's B_g(T(x)) (bv, prefetched with the rows by bload),
+// and phisum accumulates the cell's psi into the fused angular sums.
+template <int S, int T, int MODE, int C, bool LAST, bool CB, typename BL, typename PS>
 __device__ __forceinline__ void sweep_chunk(const double *W, double (&ein)[C], double (&eout)[C], double (&bv)[C],
                                             double (&X)[T][SchemeDim<S>::K], bool corr,
                                             double (&Z)[T][SchemeDim<S>::K], bool head, double h_oi, double h_oo,
                                             __amdgpu_buffer_rsrc_t Rw, __amdgpu_buffer_rsrc_t Rn, int voff,
-                                            int row_bytes, int nv, int k0, const BL &bload) {
+                                            int row_bytes, int nv, int k0, const BL &bload, const PS &phisum) {
   constexpr int K = SchemeDim<S>::K;
+  double pv[C];  // CB: the chunk's psi, for the fused angular sums
 #pragma unroll
   for (int c = 0; c < C; ++c) {
     if (LAST && c >= nv) continue;  // wave-uniform: past the end of the segment
@@ -167,6 +169,7 @@ __device__ __forceinline__ void sweep_chunk(const double *W, double (&ein)[C], d
         }
       }
     }
+    if constexpr (CB) pv[c] = 0.5 * (oi + oo);
     row_store(Rw, voff, c * row_bytes, oi, oo);
     if constexpr (!LAST) {
       const double2 v = row_load(Rn, voff, c * row_bytes);
@@ -175,6 +178,42 @@ __device__ __forceinline__ void sweep_chunk(const double *W, double (&ein)[C], d
       if constexpr (CB) bv[c] = bload(k0 + C + c);
     }
   }
+  if constexpr (CB) phisum(pv, LAST ? nv : C, k0);
+}
+
+// Fused angular sums of one chunk: vals[c] is this lane's psi in chunk cell c
+// (rows k0 + c, c < nv); w psi goes through LDS (one row of 64 lines per
+// cell) and each (cell, group) sum over the group's H lines (H divides 64)
+// is taken by one lane in the reference's direction order (i ascending:
+// i' descending in the mu < 0 half), then stored to dst[x][g], x the
+// physical cell.  gw0: the wave's first local group.
+// LDS tile of group_sums: per cell a row of 64/H groups of H + 1 slots (+1):
+// the summing lanes then read from different banks.
+constexpr int group_tile_row(int H) { return (64 / H) * (H + 1) + 1; }
+constexpr int kGroupTileMax = 16 * 129;  // C = 16 rows, H = 1 (the widest row)
+
+template <int C>
+__device__ __forceinline__ void group_sums(const double (&vals)[C], double w, int nv, double *tile, int lane, int H,
+                                           int gw0, int Gl, bool neg, int N, int k0, double *dst) {
+  const int ngw = 64 / H, RS = group_tile_row(H);
+  const int slot = (lane / H) * (H + 1) + lane % H;
+#pragma unroll
+  for (int c = 0; c < C; ++c) tile[c * RS + slot] = w * vals[c];
+  __syncthreads();  // one-wave workgroup: orders the LDS writes before the reads
+  const int tasks = ngw * nv;
+  for (int t = lane; t < tasks; t += 64) {
+    const int c = t / ngw, j = t - c * ngw;
+    const double *r = tile + c * RS + j * (H + 1);
+    double acc = 0.0;
+    if (neg) {
+      for (int i = H - 1; i >= 0; --i) acc += r[i];
+    } else {
+      for (int i = 0; i < H; ++i) acc += r[i];
+    }
+    const int g = gw0 + j, k = k0 + c;
+    if (g < Gl) dst[static_cast<size_t>(neg ? N - 1 - k : k) * Gl + g] = acc;
+  }
+  __syncthreads();  // the tile is rewritten by the next chunk
 }
 
 // One pass of T full steps over every line (MODE 0), only the pending
@@ -305,6 +344,24 @@ __global__ __launch_bounds__(64) void sweep_block_kernel(SegArgs a) {
       return 1.0;
     }
   };
+  // material coupling, fused angular sums (group_sums): w_i psi summed over
+  // the lines of each group into phi[half][x][g]
+  static_assert(C <= 16, "group_sums tile holds 16 rows");
+  __shared__ double ptile[CB ? kGroupTileMax : 1];
+  double wl = 0.0;
+  if constexpr (CB) {
+    if (a.phi) {
+      const int ip = ell % a.H;
+      wl = a.wt[neg ? a.H - 1 - ip : a.H + ip];
+    }
+  }
+  auto phisum = [&](const double (&pv)[C], int nv, int k0) {
+    if constexpr (CB) {
+      if (a.phi)  // wave-uniform
+        group_sums<C>(pv, wl, nv, ptile, lane, a.H, q * 64 / a.H, a.Gl, neg, a.N, k0,
+                      a.phi + static_cast<size_t>(half) * a.N * a.Gl);
+    }
+  };
   double ein[C], eout[C], bv[C];
   {
     const __amdgpu_buffer_rsrc_t R0 = rows(k_begin);
@@ -332,10 +389,10 @@ __global__ __launch_bounds__(64) void sweep_block_kernel(SegArgs a) {
   int k0 = k_begin;
   for (; k0 + C < k_end; k0 += C) {  // full chunks with a successor
     sweep_chunk<S, T, MODE, C, false, CB>(W, ein, eout, bv, X, corr, Z, refl_head && k0 == 0, h_oi, h_oo, rows(k0),
-                                          rows(k0 + C), voff, row_bytes, C, k0, bload);
+                                          rows(k0 + C), voff, row_bytes, C, k0, bload, phisum);
   }
   sweep_chunk<S, T, MODE, C, true, CB>(W, ein, eout, bv, X, corr, Z, refl_head && k0 == 0, h_oi, h_oo, rows(k0),
-                                       rows(k0), voff, row_bytes, k_end - k0, k0, bload);
+                                       rows(k0), voff, row_bytes, k_end - k0, k0, bload, phisum);
   if constexpr (MODE != 1) {
     double *ag = (MODE == 2 ? a.aggs[slot] : a.agg_cur) + half * half_stride + static_cast<size_t>(s) * seg_stride + ell;
 #pragma unroll
@@ -523,54 +580,64 @@ __device__ __forceinline__ bool nearly_equal(double a, double b) {
 
 // Bose series of the normalised integral from z1 to z2 (Planck.cpp:94-118):
 // n_terms is the first n >= 32 whose next term falls below the accuracy
-// relative to the leading one (capped so a bad input cannot spin).
-__device__ double planck_series(double z1, double z2, double accuracy) {
-  auto poly = [](double y) { return y * y * y + 3.0 * (y * y) + 6.0 * y + 6.0; };
-  double lead = exp(-z1) * poly(z1);
-  lead = fmax(lead, 2.220446049250313e-16);
-  const double q = 1.0 - exp(-z1);
+// relative to the leading one (capped so a bad input cannot spin).  The
+// powers e^{-k z} come from one exp and a running product, and
+// P(k z) / k^4 = r (z^3 + r (3 z^2 + r (6 z + 6 r))) with r = 1/k (rk: a
+// table for k <= 64); the terms are summed in ascending k (the reference sums
+// descending): the same value to a few ulps, for two exps per integral
+// instead of two per term.
+__device__ double planck_series(double z1, double z2, double accuracy, const double *rk) {
+  const double e1 = exp(-z1), f1 = exp(-z2);
+  const double a1 = z1 * z1 * z1, b1 = 3.0 * (z1 * z1), c1 = 6.0 * z1;
+  const double a2 = z2 * z2 * z2, b2 = 3.0 * (z2 * z2), c2 = 6.0 * z2;
+  auto pr = [](double r, double a, double b, double c) { return r * (a + r * (b + r * (c + 6.0 * r))); };
+  auto recip = [rk](int k) { return k <= 64 ? rk[k] : 1.0 / k; };
+  const double lead = fmax(e1 * (a1 + b1 + c1 + 6.0), 2.220446049250313e-16);
+  const double stop = accuracy * (1.0 - e1) * lead;  // next term <= accuracy, without the divisions
   int n = 32;
-  for (; n < 4096; ++n) {
-    const double m = n + 1.0;
-    const double next = exp(-m * z1) / q / (m * m * m * m) * poly(m * z1) / lead;
-    if (!(next > accuracy)) break;
-  }
-  double s1 = 0.0, s2 = 0.0;
-  for (int k = n; k > 0; --k) {
-    const double m = k, m4 = m * m * m * m;
-    s1 += exp(-m * z1) / m4 * poly(m * z1);
-    s2 += exp(-m * z2) / m4 * poly(m * z2);
+  for (double em = exp(-33.0 * z1); n < 4096; ++n, em *= e1)
+    if (!(em * pr(recip(n + 1), a1, b1, c1) > stop)) break;
+  double s1 = 0.0, s2 = 0.0, p1 = 1.0, p2 = 1.0;
+  for (int k = 1; k <= n; ++k) {
+    p1 *= e1;
+    p2 *= f1;
+    if (p1 == 0.0) break;  // e^{-k z1} underflowed: so has every later term
+    const double r = recip(k);
+    s1 += p1 * pr(r, a1, b1, c1);
+    s2 += p2 * pr(r, a2, b2, c2);
   }
   return s1 - s2;
 }
 
 // 12-point Gauss-Legendre of the Planck density over [mid - hw, mid + hw]
 // (Planck.cpp:129-140; k_B = 1 keV/keV)
-__device__ double planck_gauss(const PlanckCells &pc, double T, double mid, double hw, double pre) {
+__device__ double planck_gauss(const PlanckCells &pc, double inv_T, double mid, double hw, double pre) {
   double acc = 0.0;
 #pragma unroll
   for (int r = 0; r < 12; ++r) {
     const double E = mid + hw * pc.node[r];
-    const double f = nearly_equal(T, 0.0) ? 0.0 : pre * (E * E * E) / (exp(E / T) - 1.0);
-    acc += hw * pc.weight[r] * f;
+    acc += hw * pc.weight[r] * (pre * (E * E * E) / (exp(E * inv_T) - 1.0));
   }
   return acc;
 }
 
-// Planck::integrate_B (Planck.cpp:85-154): Gauss below z = 0.7, series above
-// z = 0.5, split at z = 0.6; x 4 pi.  pre = 2 / (h^3 c^2).
-__device__ double planck_integral(const PlanckCells &pc, double T, double e_min, double e_max, double pre) {
-  if (nearly_equal(T, 0.0) || nearly_equal(e_min, e_max)) return 0.0;
-  const double z1 = e_min / T, z2 = e_max / T;
+// Planck::integrate_B (Planck.cpp:85-154) for T > 0: Gauss below z = 0.7,
+// series above z = 0.5, split at z = 0.6; x 4 pi.  pre = 2 / (h^3 c^2).
+__device__ double planck_integral(const PlanckCells &pc, double T, double e_min, double e_max, double pre,
+                                  const double *rk) {
+  if (nearly_equal(e_min, e_max)) return 0.0;
+  const double inv_T = 1.0 / T;
+  const double z1 = e_min * inv_T, z2 = e_max * inv_T;
   const double t4 = (T * T) * (T * T);
   double v;
   if (z2 <= 0.7) {
-    v = planck_gauss(pc, T, 0.5 * (e_max + e_min), 0.5 * (e_max - e_min), pre);
+    v = planck_gauss(pc, inv_T, 0.5 * (e_max + e_min), 0.5 * (e_max - e_min), pre);
   } else if (z1 >= 0.5) {
-    v = pre * t4 * planck_series(z1, z2, pc.accuracy);
+    v = pre * t4 * planck_series(z1, z2, pc.accuracy, rk);
   } else {
     const double e6 = 0.6 * T;
-    v = planck_gauss(pc, T, 0.5 * (e6 + e_min), 0.5 * (e6 - e_min), pre) + pre * t4 * planck_series(0.6, z2, pc.accuracy);
+    v = planck_gauss(pc, inv_T, 0.5 * (e6 + e_min), 0.5 * (e6 - e_min), pre) +
+        pre * t4 * planck_series(0.6, z2, pc.accuracy, rk);
   }
   return v * 4.0 * 3.1415926546;
 }
@@ -578,39 +645,120 @@ __device__ double planck_integral(const PlanckCells &pc, double T, double e_min,
 // B[x][gl] = kcon * integral over group g_lo + gl at T(x); the last group takes
 // the grey remainder a c T^4 - (integral over groups 0..G-2) when positive
 // (Planck.cpp:73-76; the sum of the other groups as one integral over their
-// joint range, so no shard needs another shard's groups).  T <= 0 or not
-// finite: 0.
-__global__ void planck_cells_kernel(PlanckCells pc, const double *Tc, double *B) {
-  const size_t total = static_cast<size_t>(pc.N) * pc.Gl;
+// joint range, so no shard needs another shard's groups).  T <= 0 (or
+// nearly 0, Planck.h:84-90) or not finite: 0.
+//
+// A block owns 64 cells (one per lane) and walks the groups wave by wave, so
+// a wave evaluates ONE group at 64 temperatures -- the branch (Gauss / series
+// / split) and the series length are then nearly uniform across the wave --
+// and stages the tile in LDS to write it back as contiguous [x][g] rows.
+constexpr int kPlanckCells = 64, kPlanckGroups = 64;
+__global__ __launch_bounds__(256) void planck_cells_kernel(PlanckCells pc, const double *Tc, double *B) {
+  __shared__ double tile[kPlanckCells * (kPlanckGroups + 1)];
+  __shared__ double rk[65];
   const double hc = 4.141895e-10, c = 299.792458;
   const double pre = 2.0 / ((hc * hc * hc) * (c * c));
-  for (size_t idx = blockIdx.x * static_cast<size_t>(blockDim.x) + threadIdx.x; idx < total;
-       idx += static_cast<size_t>(gridDim.x) * blockDim.x) {
-    const int x = static_cast<int>(idx / pc.Gl), gl = static_cast<int>(idx % pc.Gl);
-    const int g = pc.g_lo + gl;
-    const double T = Tc[x];
-    double b = 0.0;
-    if (T > 0.0 && isfinite(T)) {
-      if (g < pc.G - 1) {
-        b = pc.kcon * planck_integral(pc, T, pc.e_edge[g], pc.e_edge[g + 1], pre);
-      } else {
-        const double rest = pc.a_c * ((T * T) * (T * T)) - planck_integral(pc, T, pc.e_edge[0], pc.e_edge[pc.G - 1], pre);
-        b = rest > 0.0 ? pc.kcon * rest : 0.0;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nwave = blockDim.x >> 6;
+  if (threadIdx.x <= 64) rk[threadIdx.x] = threadIdx.x ? 1.0 / threadIdx.x : 0.0;
+  const int ntiles = (pc.N + kPlanckCells - 1) / kPlanckCells;
+  for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const int x0 = t * kPlanckCells, nx = min(kPlanckCells, pc.N - x0);
+    const double T = lane < nx ? Tc[x0 + lane] : 0.0;
+    const bool hot = T > 0.0 && isfinite(T) && !nearly_equal(T, 0.0);
+    for (int g0 = 0; g0 < pc.Gl; g0 += kPlanckGroups) {
+      const int ng = min(kPlanckGroups, pc.Gl - g0);
+      __syncthreads();  // rk ready; the previous chunk's tile written out
+      for (int j = wave; j < ng; j += nwave) {
+        const int g = pc.g_lo + g0 + j;
+        double b = 0.0;
+        if (hot) {
+          if (g < pc.G - 1) {
+            b = pc.kcon * planck_integral(pc, T, pc.e_edge[g], pc.e_edge[g + 1], pre, rk);
+          } else {
+            const double rest =
+                pc.a_c * ((T * T) * (T * T)) - planck_integral(pc, T, pc.e_edge[0], pc.e_edge[pc.G - 1], pre, rk);
+            b = rest > 0.0 ? pc.kcon * rest : 0.0;
+          }
+        }
+        tile[lane * (kPlanckGroups + 1) + j] = b;
+      }
+      __syncthreads();
+      for (int i = threadIdx.x; i < nx * ng; i += blockDim.x) {
+        const int xl = i / ng, j = i - xl * ng;
+        B[static_cast<size_t>(x0 + xl) * pc.Gl + g0 + j] = tile[xl * (kPlanckGroups + 1) + j];
       }
     }
-    B[idx] = b;
   }
 }
 
-// q(x) = sum_g sigma_g (phi_g(x) - W B_g(x)), groups in order (no contraction)
-__global__ void material_q_kernel(const double *phi, const double *B, const double *sigma, double W, double *q, int Gl,
-                                  int N) {
-#pragma clang fp contract(off)
-  for (int x = blockIdx.x * blockDim.x + threadIdx.x; x < N; x += gridDim.x * blockDim.x) {
-    double acc = 0.0;
+// The cross-segment correction's share of the fused angular sums after a
+// coupled pass (T = 1) whose segments s > 0 started from X = 0: the linear
+// chain of the map on the true incoming state Z = Y_s (fold_kernel) gives
+// each cell's correction (d_in, d_out) -- no state traffic -- and
+// group_sums stores the sums of w (d_in + d_out)/2 to phic[half][x][g]
+// (segment 0 cells, exact, are never written: zero).  The stored state keeps
+// its correction pending (the next pass or a finalize applies it).
+template <int S>
+__global__ __launch_bounds__(64) void phi_correction_kernel(SegArgs a) {
+  constexpr int K = SchemeDim<S>::K;
+  constexpr int WN = map_count<S>();
+  constexpr int C = 16;
+  __shared__ double tile[kGroupTileMax];
+  const int lane = threadIdx.x;
+  const size_t stride = static_cast<size_t>(a.Lpad);
+  const int per_half = a.Q * a.Sg;
+  const int half = static_cast<int>(blockIdx.x) / per_half;
+  const int rem = static_cast<int>(blockIdx.x) % per_half;
+  const int s = rem / a.Q, q = rem - s * a.Q;
+  const int ell = q * 64 + lane;
+  const bool neg = half == 0;
+  const int k_begin = s * a.Ls, k_end = min(a.N, k_begin + a.Ls);
+  if (s == 0 || k_begin >= k_end) return;  // segment 0 starts exact
+  double Z[K];
+  const double *y = a.yseg + (static_cast<size_t>(half) * (a.Sg + 1) + s) * K * stride + ell;
+#pragma unroll
+  for (int r = 0; r < K; ++r) Z[r] = y[r * stride];
+  double W[WN];
+#pragma unroll
+  for (int n = 0; n < WN; ++n) W[n] = a.map[(static_cast<size_t>(half) * WN + n) * stride + ell];
+  const int ip = ell % a.H;
+  const double wl = a.wt[neg ? a.H - 1 - ip : a.H + ip];
+  double *dst = a.phic + static_cast<size_t>(half) * a.N * a.Gl;
+  for (int k0 = k_begin; k0 < k_end; k0 += C) {
+    const int nv = min(C, k_end - k0);
+    double d[C];
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      d[c] = 0.0;
+      if (c >= nv) continue;  // wave-uniform
+      double Zn[K], di, dd;
+      map_apply<S, false>(W, Z, 0.0, 0.0, Zn, di, dd);
+#pragma unroll
+      for (int r = 0; r < K; ++r) Z[r] = Zn[r];
+      d[c] = 0.5 * (di + dd);
+    }
+    group_sums<C>(d, wl, nv, tile, lane, a.H, q * 64 / a.H, a.Gl, neg, a.N, k0, dst);
+  }
+}
+
+// q(x) = sum_g sigma_g (phi_g(x) - W B_g(x)), phi the sum of nparts arrays
+// [part][x][g] (the fused halves and their corrections, or one full phi):
+// one wave per cell, lanes over groups, then a butterfly over the wave
+__global__ void material_q_kernel(const double *phi, int nparts, const double *B, const double *sigma, double W,
+                                  double *q, int Gl, int N) {
+  const int lane = threadIdx.x & 63;
+  const int nw = (gridDim.x * blockDim.x) >> 6;
+  const size_t NG = static_cast<size_t>(N) * Gl;
+  for (int x = (blockIdx.x * blockDim.x + threadIdx.x) >> 6; x < N; x += nw) {
     const size_t o = static_cast<size_t>(x) * Gl;
-    for (int g = 0; g < Gl; ++g) acc += sigma[g] * (phi[o + g] - W * B[o + g]);
-    q[x] = acc;
+    double acc = 0.0;
+    for (int g = lane; g < Gl; g += 64) {
+      double ph = phi[o + g];
+      for (int p = 1; p < nparts; ++p) ph += phi[p * NG + o + g];
+      acc += sigma[g] * (ph - W * B[o + g]);
+    }
+    for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off);
+    if (lane == 0) q[x] = acc;
   }
 }
 
@@ -713,6 +861,14 @@ hipError_t sweep_occupancy(int scheme, int T, int *waves_per_cu) {
   }
 }
 
+hipError_t coupled_occupancy(int scheme, int *w) {
+  switch (scheme) {
+    case SCHEME_BE: return hipOccupancyMaxActiveBlocksPerMultiprocessor(w, sweep_block_kernel<SCHEME_BE, 1, 0, true>, 64, 0);
+    case SCHEME_CN: return hipOccupancyMaxActiveBlocksPerMultiprocessor(w, sweep_block_kernel<SCHEME_CN, 1, 0, true>, 64, 0);
+    default: return hipOccupancyMaxActiveBlocksPerMultiprocessor(w, sweep_block_kernel<SCHEME_BDF2, 1, 0, true>, 64, 0);
+  }
+}
+
 static int grid_for(size_t total, int block) {
   size_t g = (total + block - 1) / block;
   if (g > 8192) g = 8192;
@@ -777,15 +933,24 @@ hipError_t launch_group_absorption(const double *phi, const double *sigma, doubl
 }
 
 hipError_t launch_planck_cells(const PlanckCells &pc, const double *T, double *B, hipStream_t st) {
-  hipLaunchKernelGGL(planck_cells_kernel, dim3(grid_for(static_cast<size_t>(pc.N) * pc.Gl, 256)), dim3(256), 0, st, pc,
-                     T, B);
+  hipLaunchKernelGGL(planck_cells_kernel, dim3(grid_for(static_cast<size_t>(pc.N), kPlanckCells)), dim3(256), 0, st,
+                     pc, T, B);
   return hipGetLastError();
 }
 
-hipError_t launch_material_q(const double *phi, const double *B, const double *sigma, double W, double *q, int Gl,
-                             int N, hipStream_t st) {
-  hipLaunchKernelGGL(material_q_kernel, dim3(grid_for(static_cast<size_t>(N), 256)), dim3(256), 0, st, phi, B, sigma,
-                     W, q, Gl, N);
+hipError_t launch_phi_correction(int scheme, const SegArgs &a, int grid, hipStream_t st) {
+  switch (scheme) {
+    case SCHEME_BE: hipLaunchKernelGGL(phi_correction_kernel<SCHEME_BE>, dim3(grid), dim3(64), 0, st, a); break;
+    case SCHEME_CN: hipLaunchKernelGGL(phi_correction_kernel<SCHEME_CN>, dim3(grid), dim3(64), 0, st, a); break;
+    default: hipLaunchKernelGGL(phi_correction_kernel<SCHEME_BDF2>, dim3(grid), dim3(64), 0, st, a); break;
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_material_q(const double *phi, int nparts, const double *B, const double *sigma, double W, double *q,
+                             int Gl, int N, hipStream_t st) {
+  hipLaunchKernelGGL(material_q_kernel, dim3(grid_for(static_cast<size_t>(N) * 64, 256)), dim3(256), 0, st, phi, nparts,
+                     B, sigma, W, q, Gl, N);
   return hipGetLastError();
 }
 

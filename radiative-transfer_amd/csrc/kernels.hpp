@@ -51,6 +51,12 @@ struct SegArgs {
   // [N][Gl] (g fastest), scaling the map constants stored for B = 1
   const double *bcell;        // nullptr: line-constant source (the reference's constant T)
   int Gl, H;                  // local groups, lines per half per group (line l = i' + H g)
+  // ... with the angular sums fused (H divides 64): the pass writes
+  // phi[half][x][g] = sum over the half's directions of w_i psi (provisional
+  // state), phi_correction_kernel adds the cross-segment correction's share
+  double *phi;                // nullptr: not fused (phi from moments_kernel after a finalize)
+  double *phic;               // [half][x][g] the correction's share (phi_correction_kernel)
+  const double *wt;           // [M] quadrature weights
 };
 
 struct FoldArgs {
@@ -71,6 +77,7 @@ enum SweepMode {
 };
 hipError_t launch_sweep(int scheme, int T, int mode, const SegArgs &a, int grid, hipStream_t st);
 hipError_t sweep_occupancy(int scheme, int T, int *waves_per_cu);
+hipError_t coupled_occupancy(int scheme, int *waves_per_cu);  // the material-coupled pass (T = 1)
 hipError_t launch_fold(int KC, const FoldArgs &f, hipStream_t st);
 hipError_t launch_init_state(double2 *E, const double *lineB, const Geometry &g, hipStream_t st);
 hipError_t launch_export_psi(const double2 *E, double *psi, const Geometry &g, hipStream_t st);
@@ -93,9 +100,13 @@ struct PlanckCells {
   double accuracy;              // series tolerance (Planck.h:96, DBL_EPSILON)
 };
 hipError_t launch_planck_cells(const PlanckCells &pc, const double *T, double *B, hipStream_t st);
-// q(x) = sum_g sigma_g (phi_g(x) - W B_g(x)) over the handle's groups
-hipError_t launch_material_q(const double *phi, const double *B, const double *sigma, double W, double *q, int Gl,
-                             int N, hipStream_t st);
+// the correction's share of the fused angular sums (SegArgs.phi) after a
+// coupled pass with segments started from X = 0 (T = 1; grid 2 Q Sg)
+hipError_t launch_phi_correction(int scheme, const SegArgs &a, int grid, hipStream_t st);
+// q(x) = sum_g sigma_g (phi_g(x) - W B_g(x)) over the handle's groups, phi the
+// sum of nparts [N][Gl] arrays at phi (the fused parts, or one full phi)
+hipError_t launch_material_q(const double *phi, int nparts, const double *B, const double *sigma, double W, double *q,
+                             int Gl, int N, hipStream_t st);
 // T(x) += dt q(x) / rho_cv
 hipError_t launch_material_update(double *T, const double *q, double dt, double rho_cv, int N, hipStream_t st);
 

@@ -51,7 +51,7 @@ struct rt_solver {
   int T = 1;                     // full steps fused per pass (time block)
   int Tp = 0;                    // steps of the pass whose correction is pending
   int Sg = 1, Ls = 16;           // segments per line and cells per segment
-  int device = 0;
+  int device = 0, cus = 0;
   hipStream_t stream = nullptr;
   // device state
   DeviceBuf E, map, lc, prop[kMaxAlignedBlock + 1], bdry, agg[2], yseg, yrefl, lineB, muwt, mom, rows, sigma;
@@ -70,7 +70,8 @@ struct rt_solver {
   // material-temperature coupling (rt_material_enable)
   bool material = false;
   double rho_cv = 0.0, wsum = 0.0;
-  DeviceBuf Tcell, Bcell, qbuf, edges, map_unit, lc_unit;
+  DeviceBuf Tcell, Bcell, qbuf, edges, map_unit, lc_unit, phi_part;
+  bool phi_fused = false;        // angular sums fused into the coupled pass (M/2 divides 64)
   PlanckCells pc{};
   // profiling
   bool profiling = false;
@@ -475,6 +476,39 @@ static rt_status upload_inflow(rt_solver *s) {
 
 static Geometry geometry(const rt_solver *s) { return Geometry{s->p.M, s->Gl, s->p.N, s->J * kSweepTile, s->Lpad}; }
 
+// Segments per line: enough waves (2 Q Sg) to fill the chip at the sweep
+// kernel's occupancy, Ls a multiple of the register chunk.
+static void segment_lines(rt_solver *h, int waves_per_cu) {
+  waves_per_cu = std::max(1, std::min(waves_per_cu, 32));
+  const long long target = static_cast<long long>(h->cus) * waves_per_cu;
+  long long sg = std::max<long long>(1, target / (2LL * h->Q));
+  const long long max_sg = (h->p.N + kSweepCells - 1) / kSweepCells;
+  sg = std::min(sg, max_sg);
+  long long ls = (h->p.N + sg - 1) / sg;
+  ls = ((ls + kSweepCells - 1) / kSweepCells) * kSweepCells;
+  h->Ls = static_cast<int>(ls);
+  h->Sg = static_cast<int>((h->p.N + ls - 1) / ls);
+}
+
+// Per-segment buffers (aggregates, folded incoming states), zeroed; the
+// segment propagators are rebuilt on their next use.
+static hipError_t alloc_segments(rt_solver *h) {
+  const size_t Lp = h->Lpad;
+  const int K = h->K;
+  for (DeviceBuf *b : {&h->agg[0], &h->agg[1], &h->yseg})
+    if (b->p) {
+      (void)hipFree(b->p);
+      b->p = nullptr;
+    }
+  hipError_t e = dalloc(h->agg[0], sizeof(double) * 2 * h->Sg * kMaxTimeBlock * K * Lp);
+  if (!e) e = dalloc(h->agg[1], sizeof(double) * 2 * h->Sg * kMaxTimeBlock * K * Lp);
+  if (!e) e = dalloc(h->yseg, sizeof(double) * 2 * (h->Sg + 1) * kMaxAlignedBlock * K * Lp);
+  if (!e) e = hipMemsetAsync(h->agg[0].p, 0, h->agg[0].bytes, h->stream);
+  if (!e) e = hipMemsetAsync(h->agg[1].p, 0, h->agg[1].bytes, h->stream);
+  for (bool &r : h->prop_ready) r = false;
+  return e;
+}
+
 // ---------------------------------------------------------------------------
 // lifecycle
 // ---------------------------------------------------------------------------
@@ -544,17 +578,8 @@ extern "C" rt_status rt_create_from_params(const rt_params *pin, int g_lo, int g
   HIP_TRY(h, sweep_occupancy(h->scheme, h->T, &waves_per_cu));
   // tuning knob for experiments: target resident waves per CU (segments per line follow)
   if (const char *w = std::getenv("RTSN_WAVES_PER_CU")) waves_per_cu = std::atoi(w);
-  waves_per_cu = std::max(1, std::min(waves_per_cu, 32));
-  {
-    const long long target = static_cast<long long>(prop.multiProcessorCount) * waves_per_cu;
-    long long sg = std::max<long long>(1, target / (2LL * h->Q));
-    const long long max_sg = (q.N + kSweepCells - 1) / kSweepCells;
-    sg = std::min(sg, max_sg);
-    long long ls = (q.N + sg - 1) / sg;
-    ls = ((ls + kSweepCells - 1) / kSweepCells) * kSweepCells;
-    h->Ls = static_cast<int>(ls);
-    h->Sg = static_cast<int>((q.N + ls - 1) / ls);
-  }
+  h->cus = prop.multiProcessorCount;
+  segment_lines(h, waves_per_cu);
   if (2LL * h->Q * h->Sg >= (1LL << 31)) return fail(nullptr, RT_ERR_PARAM, "too many lines for one handle: shard the groups");
   // a chunk's rows are addressed through one buffer descriptor with 32-bit offsets
   if (16LL * 16 * h->Lpad >= (1LL << 31)) return fail(nullptr, RT_ERR_PARAM, "too many lines per row: shard the groups");
@@ -569,9 +594,7 @@ extern "C" rt_status rt_create_from_params(const rt_params *pin, int g_lo, int g
   for (int T = 1; T <= kMaxAlignedBlock; ++T)
     if (!e) e = dalloc(h->prop[T], sizeof(double) * 2 * prop_count(K, T) * Lp);
   if (!e) e = dalloc(h->bdry, sizeof(double) * 2 * Lp);
-  if (!e) e = dalloc(h->agg[0], sizeof(double) * 2 * h->Sg * kMaxTimeBlock * K * Lp);
-  if (!e) e = dalloc(h->agg[1], sizeof(double) * 2 * h->Sg * kMaxTimeBlock * K * Lp);
-  if (!e) e = dalloc(h->yseg, sizeof(double) * 2 * (h->Sg + 1) * kMaxAlignedBlock * K * Lp);
+  if (!e) e = alloc_segments(h);
   if (!e) e = dalloc(h->yrefl, sizeof(double) * kMaxAlignedBlock * K * Lp);
   if (!e) e = dalloc(h->lineB, sizeof(double) * 2 * Lp);
   if (!e) e = dalloc(h->muwt, sizeof(double) * 2 * q.M);
@@ -585,8 +608,6 @@ extern "C" rt_status rt_create_from_params(const rt_params *pin, int g_lo, int g
   if ((st = upload_inflow(h))) return st;
   HIP_TRY(h, launch_init_state(static_cast<double2 *>(h->E.p), static_cast<const double *>(h->lineB.p), geometry(h),
                                h->stream));
-  HIP_TRY(h, hipMemsetAsync(h->agg[0].p, 0, h->agg[0].bytes, h->stream));
-  HIP_TRY(h, hipMemsetAsync(h->agg[1].p, 0, h->agg[1].bytes, h->stream));
 
   HIP_TRY(h, hipStreamSynchronize(h->stream));
   *out = s.release();
@@ -725,6 +746,8 @@ static rt_status enqueue_pass(rt_solver *s, int T, bool coupled = false) {
     a.bcell = static_cast<const double *>(s->Bcell.p);
     a.Gl = s->Gl;
     a.H = s->H;
+    a.phi = s->phi_fused ? static_cast<double *>(s->phi_part.p) : nullptr;
+    a.wt = static_cast<const double *>(s->muwt.p) + s->p.M;
   }
   hipEvent_t e1;
   rt_status st = event_begin(s, &e1);
@@ -920,6 +943,8 @@ extern "C" rt_status rt_material_enable(rt_solver *s, double rho_cv, const doubl
     if (!e) e = dalloc(s->edges, sizeof(double) * (s->p.G + 1));
     if (!e) e = dalloc(s->map_unit, s->map.bytes);
     if (!e) e = dalloc(s->lc_unit, s->lc.bytes);
+    s->phi_fused = 64 % s->H == 0;  // a group's lines never straddle a wave
+    if (!e && s->phi_fused) e = dalloc(s->phi_part, sizeof(double) * 4 * NG);  // [half sums, corrections][half]
     if (e) return fail(s, RT_ERR_NOMEM, std::string("material buffers: ") + hipGetErrorString(e));
   }
   switch (s->scheme) {
@@ -928,8 +953,23 @@ extern "C" rt_status rt_material_enable(rt_solver *s, double rho_cv, const doubl
     default: st = unit_maps_s<SCHEME_BDF2>(s); break;
   }
   if (st) return st;
+  {  // coupled passes are single steps: segments for the coupled kernel's occupancy
+     // (measured on SL: 16 waves per CU instead is slower for BE, even for BDF2)
+    int w = 0;
+    HIP_TRY(s, coupled_occupancy(s->scheme, &w));
+    if (const char *env = std::getenv("RTSN_WAVES_PER_CU")) w = std::atoi(env);
+    const int sg0 = s->Sg;
+    segment_lines(s, w);
+    if (s->Sg != sg0) {
+      if (2LL * s->Q * s->Sg >= (1LL << 31)) return fail(s, RT_ERR_PARAM, "too many segments");
+      HIP_TRY(s, alloc_segments(s));
+      s->tau.assign(chain_positions(s), s->target);  // every position at the same, requested time
+    }
+  }
   std::vector<double> T0(N, s->p.T);
   if (T_cells) std::copy(T_cells, T_cells + N, T0.begin());
+  if (s->phi_fused)  // the correction sums of segment-0 cells are never written: zero
+    HIP_TRY(s, hipMemsetAsync(s->phi_part.p, 0, s->phi_part.bytes, s->stream));
   if ((st = upload(s, s->Tcell, T0.data(), N * sizeof(double)))) return st;
   if ((st = upload(s, s->edges, s->gt.e_edge.data(), (s->p.G + 1) * sizeof(double)))) return st;
   PlanckCells &pc = s->pc;
@@ -958,12 +998,32 @@ extern "C" rt_status rt_material_sweep(rt_solver *s, double *d_q) {
   rt_status st = check_validation(s);
   if (st) return st;
   if ((st = ensure_equilibrium(s))) return st;
+  double *q = d_q ? d_q : static_cast<double *>(s->qbuf.p);
+  const double *B = static_cast<const double *>(s->Bcell.p), *sig = static_cast<const double *>(s->sigma.p);
+  if (s->phi_fused) {
+    // one pass over the state: the pass sums w psi of its provisional cells, the
+    // correction kernel adds the cross-segment correction's share (no state
+    // traffic) and the stored state keeps its correction pending for the next pass
+    if ((st = complete(s))) return st;
+    if ((st = enqueue_pass(s, 1, true))) return st;
+    if (s->pending) {
+      if ((st = enqueue_fold(s, 1, false))) return st;
+      SegArgs a = seg_args(s);
+      a.Gl = s->Gl;
+      a.H = s->H;
+      a.phic = static_cast<double *>(s->phi_part.p) + 2 * static_cast<size_t>(s->p.N) * s->Gl;
+      a.wt = static_cast<const double *>(s->muwt.p) + s->p.M;
+      HIP_TRY(s, launch_phi_correction(s->scheme, a, 2 * s->Q * s->Sg, s->stream));
+    }
+    HIP_TRY(s, launch_material_q(static_cast<const double *>(s->phi_part.p), s->pending ? 4 : 2, B, sig, s->wsum, q,
+                                 s->Gl, s->p.N, s->stream));
+    return RT_OK;
+  }
   if ((st = finalize(s))) return st;
   if ((st = enqueue_pass(s, 1, true))) return st;
   if ((st = compute_moments(s))) return st;  // finalizes the pass
-  HIP_TRY(s, launch_material_q(static_cast<const double *>(s->mom.p), static_cast<const double *>(s->Bcell.p),
-                               static_cast<const double *>(s->sigma.p), s->wsum,
-                               d_q ? d_q : static_cast<double *>(s->qbuf.p), s->Gl, s->p.N, s->stream));
+  HIP_TRY(s, launch_material_q(static_cast<const double *>(s->mom.p), 1, B, sig, s->wsum, q, s->Gl, s->p.N,
+                               s->stream));
   return RT_OK;
 }
 

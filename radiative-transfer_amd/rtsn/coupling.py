@@ -12,19 +12,22 @@ update stay stream-ordered with no host synchronisation.
 from __future__ import annotations
 
 
-def coupled_steps(solver, nsteps: int, q, world_size: int = 1, group=None):
+def coupled_steps(solver, nsteps: int, q, world_size: int = 1, group=None, host_sync: bool = False):
     """nsteps coupled full steps of this rank's group shard.
 
     solver: rtsn.Solver after material_enable (or anything with its
     material_sweep(q) / material_update(q) methods); q: float64 tensor of N
     elements on the solver's device (the exchange buffer); world_size > 1 sums
-    q over the ranks of `group` with torch.distributed.
+    q over the ranks of `group` with torch.distributed.  host_sync: instead
+    of ordering the all-reduce on the solver's stream, wait for the sweep on
+    the host, all-reduce on the current stream and wait for it (two host
+    synchronisations per step).
     """
     import torch
     import torch.distributed as dist
 
     stream = None
-    if q.is_cuda:
+    if q.is_cuda and not host_sync:
         stream = torch.cuda.ExternalStream(solver.stream, device=q.device)
     for _ in range(int(nsteps)):
         solver.material_sweep(q)
@@ -33,5 +36,9 @@ def coupled_steps(solver, nsteps: int, q, world_size: int = 1, group=None):
                 with torch.cuda.stream(stream):
                     dist.all_reduce(q, group=group)
             else:
+                if q.is_cuda:
+                    solver.synchronize()
                 dist.all_reduce(q, group=group)
+                if q.is_cuda:
+                    torch.cuda.synchronize(q.device)
         solver.material_update(q)

@@ -10,9 +10,11 @@ through rtsn.coupling.coupled_steps).
 Tolerances: T(x) relative 1e-12 and the transport fields per group 1e-10
 (the north_star's 1e-10 for intensities); the device evaluates the Planck
 integrals in double (the oracle in the reference's long double Gauss nodes,
-glibc exp), so B_g agrees to ~1e-15 relative, except the last group, a
-remainder a c T^4 - (rest), which carries the rounding of a c T^4 (tolerance
-1e-13 a c T^4 absolute).
+glibc exp per series term; the device one exp and a running product), so B_g
+agrees to 1e-12 relative plus 1e-14 a c T^4 absolute -- the series difference
+s(z1) - s(z2) of the reference's algorithm cancels in narrow groups, leaving a
+few ulps of a c T^4 -- and the last group, a remainder a c T^4 - (rest), to
+1e-13 a c T^4.
 """
 from __future__ import annotations
 
@@ -48,7 +50,9 @@ def check_planck(gpu_B, orc_B, T):
     G = gpu_B.shape[0]
     acT4 = np.array([grey(t) for t in T])
     d = np.abs(gpu_B - orc_B)
-    lim = 1e-12 * np.abs(orc_B[:-1]) + 1e-15 * acT4[None, :]
+    # the series difference s(z1) - s(z2) cancels in narrow groups: its rounding is
+    # a few ulps of a c T^4, whatever the group's size (hence the absolute term)
+    lim = 1e-12 * np.abs(orc_B[:-1]) + 1e-14 * acT4[None, :]
     assert np.all(d[:-1] <= lim), float(np.max(d[:-1] / np.maximum(lim, 1e-300)))
     assert np.all(d[-1] <= 1e-13 * acT4 + 1e-300), float(np.max(d[-1] / np.maximum(acT4, 1e-300)))
     rel = d[:-1] / np.maximum(np.abs(orc_B[:-1]), 1e-300)
@@ -83,8 +87,6 @@ def test_device_planck_uniform_matches_host_table(rtsn_mod, oracle_mod):
         gpu.material_enable(1.0)
         B = gpu.cell_planck()
     assert np.all(B == B[:, :1])
-    # the series difference s(z1) - s(z2) of a narrow group cancels: 1 ulp of exp
-    # becomes ~1e-13 relative, the scale check_planck allows
     check_planck(B[:, :1], table[:, None], np.array([1.0]))
 
 
@@ -113,10 +115,13 @@ def compare(gpu, orc, tol=1e-10):
     return err
 
 
+@pytest.mark.parametrize("M", [6, 8, 2])
 @pytest.mark.parametrize("ts,dt", [(1, 1e-3), (2, 1e-3), (3, 1e-4)])
 @pytest.mark.parametrize("bc_left,bc_right", [(2, 0), (1, 1), (0, 0), (2, 1)])
-def test_coupled_steps_match_oracle(rtsn_mod, oracle_mod, ts, dt, bc_left, bc_right):
-    p = params(oracle_mod, ts=ts, dt=dt, M=6, G=5, N=150, bc_left=bc_left, bc_right=bc_right)
+def test_coupled_steps_match_oracle(rtsn_mod, oracle_mod, ts, dt, bc_left, bc_right, M):
+    """M = 8, 2: the angular sums fused into the pass (M/2 divides 64) with the
+    correction pending; M = 6: finalize + moments_kernel after each pass."""
+    p = params(oracle_mod, ts=ts, dt=dt, M=M, G=5, N=150, bc_left=bc_left, bc_right=bc_right)
     p["psi_source"] = np.linspace(0.5, 2.0, p["M"] * p["G"]).reshape(p["M"], p["G"])
     gpu, orc = run_pair(rtsn_mod, oracle_mod, p, 6)
     with gpu:
@@ -168,10 +173,11 @@ class GpuView:
         return self.s.psi_source()
 
 
-def test_group_shards_on_one_gpu(rtsn_mod, oracle_mod):
+@pytest.mark.parametrize("M", [6, 16])
+def test_group_shards_on_one_gpu(rtsn_mod, oracle_mod, M):
     """Two shard handles, q summed on the device, equal one full handle."""
     import torch
-    p = to_rt(params(oracle_mod, ts=2, G=7, N=200, M=6, bc_left=2))
+    p = to_rt(params(oracle_mod, ts=2, G=7, N=200, M=M, bc_left=2))
     T0 = t_profile(p["N"])
     with rtsn_mod.Solver(p) as full:
         full.material_enable(4.0, T0)
