@@ -194,7 +194,7 @@ def gather_results(solver, N: int, world: int, shard_info, shards, device):
 
 
 def run_rank(solver, p: dict, steps: int, warmup: int, world: int, device, shard_info, scaling: str,
-             scaling_shards=None):
+             scaling_shards=None, gather: bool = True):
     """Warmup, K timed steps between barrier + device sync, max over ranks,
     then the absorption all-reduce.  Collectives go through torch.distributed
     on whatever backend is initialised (RCCL on the GPU box, gloo in the CPU
@@ -255,7 +255,7 @@ def run_rank(solver, p: dict, steps: int, warmup: int, world: int, device, shard
     # fastest) and its group ends and balance, assembled into the reference's (N, G)
     # / (G) arrays on every rank; ragged shards are padded to the largest
     t2 = time.perf_counter()
-    gathered = gather_results(solver, p["N"], world, shard_info, scaling_shards, device)
+    gathered = gather_results(solver, p["N"], world, shard_info, scaling_shards, device) if gather else None
     gather_ms = 1e3 * (time.perf_counter() - t2)
 
     t = torch.tensor([wall, kern_ms / max(nlaunch, 1)], dtype=torch.float64, device=device)
@@ -294,7 +294,7 @@ def run_rank(solver, p: dict, steps: int, warmup: int, world: int, device, shard
                      "end_to_end_updates_per_s": upd_step * (warmup + steps) / (t_end - t_start)},
         "config": {
             "workload": f"SL slab: N={p['N']} cells x S{p['M']} x {g_hi - g_lo} groups per GPU "
-                        f"({G_total} total), BDF2 dt=1e-3, V={p['V']}, use_correction=1, vacuum BCs",
+                        f"({G_total} total), BDF2 dt={p['dt']:g}, V={p['V']}, use_correction=1, vacuum BCs",
             "cells": p["N"], "angles": p["M"], "groups_per_gpu": g_hi - g_lo, "groups_total": G_total,
             "time_scheme": "BDF2 (4 fused substeps per step)",
             "steps_per_pass": tb,
@@ -321,10 +321,37 @@ def run_rank(solver, p: dict, steps: int, warmup: int, world: int, device, shard
                      "frac": achieved_fl / FP64_PEAK},
         },
         "state_finite": finite,
-        "gather": {"fields": "phi, F, phi_plus (N x G) + left/right ends, balance (G)",
-                   "bytes_per_rank": 8 * 3 * p["N"] * (g_hi - g_lo), "ms": gather_ms},
     }
+    if gather:
+        line["gather"] = {"fields": "phi, F, phi_plus (N x G) + left/right ends, balance (G)",
+                          "bytes_per_rank": 8 * 3 * p["N"] * (g_hi - g_lo), "ms": gather_ms}
     return line, absorb, gathered
+
+
+def side_leg(p: dict, info, world: int, device, local: int, scaling: str, tb: int, what: str) -> dict:
+    """A second sweep measurement on the same shard, reported beside `value` (never as
+    it): the state is created fresh, the pipeline filled untimed, then two passes timed
+    exactly as the headline.  Used for (a) the HBM-bound T = 1 pass (one HBM round trip
+    of the state per BDF2 step: the north_star's HBM-roofline view of the sweep) and (b)
+    the finite-state control (dt = 1e-7: the reference's BDF2 stays bounded, so the
+    timing of the headline -- whose state overflows, DESIGN.md §5 -- is shown to be
+    data-independent)."""
+    import rtsn
+    with rtsn.Solver(p, device=local, g_lo=info[1], g_hi=info[2]) as s:
+        s.time_block = tb
+        s.pipeline = 1
+        warm = s.sweep_geometry()[1] * tb
+        line, _, _ = run_rank(s, p, 2 * tb, warm, world, device, info, scaling, gather=False)
+    r = line["roofline"]
+    out = {"what": what, "dt": p["dt"], "steps_per_pass": tb, "steps": 2 * tb, "warmup": warm,
+           "value": line["value"], "ms_per_step": line["ms_per_step"], "kernel_ms": r["kernel_ms"],
+           "state_finite": line["state_finite"]}
+    if tb == 1:
+        out["hbm"] = dict(r["hbm"], traffic=load_traffic(p["variant"], 1, r["algorithmic_bytes_per_launch"]),
+                          algorithmic_bytes_per_launch=r["algorithmic_bytes_per_launch"])
+    else:
+        out["fp64"] = r["fp64"]
+    return out
 
 
 def run_material(p: dict, info, world: int, device, local: int, steps: int) -> dict:
@@ -391,6 +418,8 @@ def main():
     ap.add_argument("--schedule", choices=["pipelined", "aligned"], default="pipelined",
                     help="staggered segments (exact starts) or aligned segments with deferred correction")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--side-legs", type=int, default=1,
+                    help="1: also time the T=1 (HBM-bound) pass and the finite-state control (dt=1e-7)")
     ap.add_argument("--material-steps", type=int, default=3,
                     help="timed steps of the material-coupled run reported under 'material' (0: skip)")
     # rehearsal of the multi-rank path on a one-GPU box: every rank on cuda:0, gloo
@@ -428,10 +457,18 @@ def main():
     if warmup < 0:  # pipeline depth (segments per line) passes: fill + one steady pass
         warmup = solver.sweep_geometry()[1] * tb if solver.pipeline else tb
     shards = [shard(args.scaling, args.groups, world, r)[1:] for r in range(world)]
+    solver_tb = solver.time_block
     line, _, _ = run_rank(solver, p, steps, warmup, world, device, info, args.scaling, shards)
     line["roofline"]["traffic"] = load_traffic(args.variant, solver.time_block,
                                                line["roofline"]["algorithmic_bytes_per_launch"])
-    solver.close()  # frees the sweep's state before the coupled run allocates its own
+    solver.close()  # frees the sweep's state before the next run allocates its own
+    if args.side_legs:
+        pv = dict(p, variant=args.variant)
+        line["hbm_pass_t1"] = side_leg(pv, info, world, device, local, args.scaling, 1,
+                                       "same workload, one full step per pass: HBM-bound sweep")
+        line["finite_control"] = side_leg(dict(pv, dt=1e-7), info, world, device, local, args.scaling,
+                                          solver_tb, "same workload at dt=1e-7 (state stays finite): "
+                                                     "timing control for the headline")
     if args.material_steps > 0:
         line["material"] = run_material(p, info, world, device, local, args.material_steps)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

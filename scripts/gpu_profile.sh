@@ -7,7 +7,7 @@ mkdir -p gpurun_out
 V=${VARIANT:-v0}
 TB=${TB:-0}
 TAG=${TAG:-r01}
-B="bench.py --no-cpu-baseline --variant $V --time-block $TB"
+B="bench.py --no-cpu-baseline --side-legs 0 --material-steps 0 --variant $V --time-block $TB"
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_kt_$V -o run --output-format csv -- python3 $B > gpurun_out/prof_kt_$V.log 2>&1 || { tail -20 gpurun_out/prof_kt_$V.log; exit 1; }
 T=$(python3 -c "import json;print([json.loads(l) for l in open('gpurun_out/prof_kt_$V.log') if l.startswith('{\"metric')][-1]['config']['steps_per_pass'])")
 i=0

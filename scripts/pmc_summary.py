@@ -21,8 +21,9 @@ def counters(d):
     for f in Path(d).rglob("*counter_collection.csv"):
         for r in csv.DictReader(open(f)):
             name = r["Kernel_Name"]
-            mode = name.replace(" ", "").split("(")[0]
-            if KERNEL in name and (mode.endswith(",0>") or mode.endswith(",2>")):  # a pass (aligned or pipelined)
+            targs = name.replace(" ", "").split("(")[0].split("<")[-1].rstrip(">").split(",")
+            # a sweep pass <S, T, mode[, material]>: mode 0 aligned, 2 pipelined (1 = finalize)
+            if KERNEL in name and len(targs) >= 3 and targs[2] in ("0", "2") and "true" not in targs[3:]:
                 out.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
     return out
 
