@@ -485,66 +485,89 @@ __global__ void import_ends_kernel(double2 *E, const double *ends, LineMap m) {
 
 // phi, F, phi_plus (Gl, N) ColMajor: sequential sums over i in the
 // reference's order (solver.cpp:191-237), no FMA contraction.
-// A task is (cell c, chunk of gpc groups): the block reads the chunk's rows
-// of both halves coalesced (row k = N-1-c of half 0, k = c of half 1), stages
-// psi in LDS with one padding slot per group (conflict-free strided reads),
-// then 3 * gpc threads run the three sums, one per (group, moment).  The
-// weights live in LDS too (WL) unless M is too large for that.
-template <bool WL>
-__global__ void moments_kernel(const double2 *E, const double *mu, const double *wt, double *phi, double *F,
-                               double *phi_plus, LineMap m, int gpc) {
+// One wave per task (cell c, 64 groups): lane = group, running the three sums
+// side by side.  The task's rows (row k = N-1-c of half 0 walked with i'
+// descending, i = 0..H-1; row k = c of half 1, i = H..M-1) are read in chunks
+// of MOM_W directions: each group's MOM_W nodes are one contiguous 128 B run
+// (l = i' + H g), so an instruction covers 8 whole cache lines; the chunk is
+// transposed through LDS (lane g then reads its MOM_W values), and the next
+// chunk's loads are in flight while the current one is summed.  The weights
+// are wave-uniform (scalar loads).
+constexpr int MOM_W = 8;  // directions per chunk: 8 x 16 B = one 128 B line per group
+
+__global__ void __launch_bounds__(64) moments_kernel(const double2 *__restrict__ E, const double *__restrict__ mu,
+                                                     const double *__restrict__ wt, double *phi, double *F,
+                                                     double *phi_plus, LineMap m) {
 #pragma clang fp contract(off)
-  extern __shared__ double mom_lds[];
-  const int H = m.H, HP = H + 1;
-  double *s0 = mom_lds, *s1 = mom_lds + gpc * HP;
-  const double *w = wt, *x = mu;
-  if constexpr (WL) {
-    double *lw = s1 + gpc * HP, *lx = lw + m.M;
-    for (int i = threadIdx.x; i < m.M; i += blockDim.x) {
-      lw[i] = wt[i];
-      lx[i] = mu[i];
-    }
-    w = lw;
-    x = lx;
-  }
-  const int nchunks = (m.Gl + gpc - 1) / gpc;
+  __shared__ double tile[64 * (MOM_W + 1)];
+  const int lane = threadIdx.x;
+  const int H = m.H;
+  const int nchunks = (m.Gl + 63) / 64;
+  const int nj = (H + MOM_W - 1) / MOM_W;  // chunks per half
   const size_t tasks = static_cast<size_t>(m.N) * nchunks;
-  for (size_t task = blockIdx.x; task < tasks; task += gridDim.x) {
+  double2 v[MOM_W];
+  // chunk `step` of a task: half 0 chunks j = nj-1 .. 0 (i' descending), then half 1 j = 0 .. nj-1
+  auto load = [&](size_t task, int step) {
     const int c = static_cast<int>(task / nchunks);
-    const int g0 = static_cast<int>(task % nchunks) * gpc;
-    const int ng = min(gpc, m.Gl - g0);
-    const double2 *r0 = E + m.at(0, m.N - 1 - c, H * g0);
-    const double2 *r1 = E + m.at(1, c, H * g0);
-    for (int t = threadIdx.x; t < ng * H; t += blockDim.x) {
-      const int slot = (t / H) * HP + t % H;
-      const double2 a = r0[t], b = r1[t];
-      s0[slot] = 0.5 * (a.x + a.y);
-      s1[slot] = 0.5 * (b.x + b.y);
+    const int g0 = static_cast<int>(task % nchunks) * 64;
+    const int ng = min(64, m.Gl - g0);
+    const int half = step < nj ? 0 : 1;
+    const int i0 = (half == 0 ? nj - 1 - step : step - nj) * MOM_W;
+    const int w = min(MOM_W, H - i0);
+    const double2 *row = E + m.at(half, half == 0 ? m.N - 1 - c : c, H * g0 + i0);
+#pragma unroll
+    for (int r = 0; r < MOM_W; ++r) {
+      const int e = lane + 64 * r;
+      if (e < ng * w) v[r] = row[static_cast<size_t>(H) * (e / w) + e % w];
     }
-    __syncthreads();
-    const int which = threadIdx.x / gpc, gl = threadIdx.x % gpc;
-    if (which < 3 && gl < ng) {
-      const double *p0 = s0 + gl * HP, *p1 = s1 + gl * HP;
-      double acc = 0.0;
-      if (which == 0) {
-#pragma unroll 8
-        for (int i = 0; i < H; ++i) acc += w[i] * p0[H - 1 - i];
-#pragma unroll 8
-        for (int i = H; i < m.M; ++i) acc += w[i] * p1[i - H];
-        phi[static_cast<size_t>(c) * m.Gl + g0 + gl] = acc;
-      } else if (which == 1) {
-#pragma unroll 8
-        for (int i = 0; i < H; ++i) acc += x[i] * w[i] * p0[H - 1 - i];
-#pragma unroll 8
-        for (int i = H; i < m.M; ++i) acc += x[i] * w[i] * p1[i - H];
-        F[static_cast<size_t>(c) * m.Gl + g0 + gl] = acc;
-      } else {
-#pragma unroll 8
-        for (int i = H; i < m.M; ++i) acc += w[i] * p1[i - H];
-        phi_plus[static_cast<size_t>(c) * m.Gl + g0 + gl] = acc;
+  };
+  size_t task = blockIdx.x;
+  if (task < tasks) load(task, 0);
+  for (; task < tasks; task += gridDim.x) {
+    const int c = static_cast<int>(task / nchunks);
+    const int g0 = static_cast<int>(task % nchunks) * 64;
+    const int ng = min(64, m.Gl - g0);
+    double sphi = 0.0, sF = 0.0, splus = 0.0;
+    for (int step = 0; step < 2 * nj; ++step) {
+      const int half = step < nj ? 0 : 1;
+      const int i0 = (half == 0 ? nj - 1 - step : step - nj) * MOM_W;
+      const int w = min(MOM_W, H - i0);
+#pragma unroll
+      for (int r = 0; r < MOM_W; ++r) {
+        const int e = lane + 64 * r;
+        if (e < ng * w) tile[(e / w) * (MOM_W + 1) + e % w] = 0.5 * (v[r].x + v[r].y);
       }
+      __syncthreads();
+      // next chunk (of this task or the next one) in flight during the sums
+      if (step + 1 < 2 * nj) load(task, step + 1);
+      else if (task + gridDim.x < tasks) load(task + gridDim.x, 0);
+      if (lane < ng) {
+        const double *t = tile + lane * (MOM_W + 1);
+        if (half == 0) {
+          for (int ii = w - 1; ii >= 0; --ii) {
+            const int i = H - 1 - (i0 + ii);
+            const double q = t[ii];
+            sphi += wt[i] * q;
+            sF += mu[i] * wt[i] * q;
+          }
+        } else {
+          for (int ii = 0; ii < w; ++ii) {
+            const int i = H + i0 + ii;
+            const double q = t[ii];
+            sphi += wt[i] * q;
+            sF += mu[i] * wt[i] * q;
+            splus += wt[i] * q;
+          }
+        }
+      }
+      __syncthreads();
     }
-    __syncthreads();
+    if (lane < ng) {
+      const size_t o = static_cast<size_t>(c) * m.Gl + g0 + lane;
+      phi[o] = sphi;
+      F[o] = sF;
+      phi_plus[o] = splus;
+    }
   }
 }
 
@@ -905,17 +928,10 @@ hipError_t launch_import_ends(double2 *E, const double *ends, const Geometry &g,
 hipError_t launch_moments(const double2 *E, const double *mu, const double *wt, double *phi, double *F,
                           double *phi_plus, const Geometry &g, hipStream_t st) {
   const LineMap m = make_map(g);
-  // groups per task: ~512 lines, at most 85 so that 3 sums per group fit 256 threads
-  const int gpc = max(1, min(85, 512 / m.H));
-  const size_t lds = static_cast<size_t>(2) * gpc * (m.H + 1) * sizeof(double);
-  const size_t ldsw = lds + static_cast<size_t>(2) * m.M * sizeof(double);
-  if (lds > 65536) return hipErrorInvalidValue;  // M > ~8000
-  const size_t tasks = static_cast<size_t>(g.N) * ((g.Gl + gpc - 1) / gpc);
-  const dim3 grid(static_cast<unsigned>(tasks < 8192 ? tasks : 8192));
-  if (ldsw <= 65536)
-    hipLaunchKernelGGL(moments_kernel<true>, grid, dim3(256), ldsw, st, E, mu, wt, phi, F, phi_plus, m, gpc);
-  else
-    hipLaunchKernelGGL(moments_kernel<false>, grid, dim3(256), lds, st, E, mu, wt, phi, F, phi_plus, m, gpc);
+  const size_t tasks = static_cast<size_t>(g.N) * ((g.Gl + 63) / 64);
+  // resident waves: 16 per CU (114 VGPRs) on 256 CUs; each walks its tasks with a one-chunk prefetch
+  const dim3 grid(static_cast<unsigned>(tasks < 4096 ? tasks : 4096));
+  hipLaunchKernelGGL(moments_kernel, grid, dim3(64), 0, st, E, mu, wt, phi, F, phi_plus, m);
   return hipGetLastError();
 }
 
