@@ -495,6 +495,9 @@ __global__ void import_ends_kernel(double2 *E, const double *ends, LineMap m) {
 // are wave-uniform (scalar loads).
 constexpr int MOM_W = 8;  // directions per chunk: 8 x 16 B = one 128 B line per group
 
+// FAST: H % MOM_W == 0, so every chunk is 64 groups x MOM_W directions and lane
+// (gr, col) = (lane / 8, lane % 8) loads group gr + 8 r, direction col of it.
+template <bool FAST>
 __global__ void __launch_bounds__(64) moments_kernel(const double2 *__restrict__ E, const double *__restrict__ mu,
                                                      const double *__restrict__ wt, double *phi, double *F,
                                                      double *phi_plus, LineMap m) {
@@ -513,12 +516,21 @@ __global__ void __launch_bounds__(64) moments_kernel(const double2 *__restrict__
     const int ng = min(64, m.Gl - g0);
     const int half = step < nj ? 0 : 1;
     const int i0 = (half == 0 ? nj - 1 - step : step - nj) * MOM_W;
-    const int w = min(MOM_W, H - i0);
     const double2 *row = E + m.at(half, half == 0 ? m.N - 1 - c : c, H * g0 + i0);
+    if constexpr (FAST) {
+      // descriptor over the chunk's ng groups: groups >= ng read as 0 (bounds-checked), never stored
+      const __amdgpu_buffer_rsrc_t R =
+          __builtin_amdgcn_make_buffer_rsrc(const_cast<double2 *>(row), 0, ng * H * 16, 0x00020000);
+      const int voff = (H * (lane / MOM_W) + lane % MOM_W) * 16;
 #pragma unroll
-    for (int r = 0; r < MOM_W; ++r) {
-      const int e = lane + 64 * r;
-      if (e < ng * w) v[r] = row[static_cast<size_t>(H) * (e / w) + e % w];
+      for (int r = 0; r < MOM_W; ++r) v[r] = row_load(R, voff, r * 8 * H * 16);
+    } else {
+      const int w = min(MOM_W, H - i0);
+#pragma unroll
+      for (int r = 0; r < MOM_W; ++r) {
+        const int e = lane + 64 * r;
+        if (e < ng * w) v[r] = row[static_cast<size_t>(H) * (e / w) + e % w];
+      }
     }
   };
   size_t task = blockIdx.x;
@@ -531,32 +543,52 @@ __global__ void __launch_bounds__(64) moments_kernel(const double2 *__restrict__
     for (int step = 0; step < 2 * nj; ++step) {
       const int half = step < nj ? 0 : 1;
       const int i0 = (half == 0 ? nj - 1 - step : step - nj) * MOM_W;
-      const int w = min(MOM_W, H - i0);
+      const int w = FAST ? MOM_W : min(MOM_W, H - i0);
+      if constexpr (FAST) {
+        const int gr = lane / MOM_W, col = lane % MOM_W;
 #pragma unroll
-      for (int r = 0; r < MOM_W; ++r) {
-        const int e = lane + 64 * r;
-        if (e < ng * w) tile[(e / w) * (MOM_W + 1) + e % w] = 0.5 * (v[r].x + v[r].y);
+        for (int r = 0; r < MOM_W; ++r)
+          if (gr + 8 * r < ng) tile[(gr + 8 * r) * (MOM_W + 1) + col] = 0.5 * (v[r].x + v[r].y);
+      } else {
+#pragma unroll
+        for (int r = 0; r < MOM_W; ++r) {
+          const int e = lane + 64 * r;
+          if (e < ng * w) tile[(e / w) * (MOM_W + 1) + e % w] = 0.5 * (v[r].x + v[r].y);
+        }
       }
       __syncthreads();
       // next chunk (of this task or the next one) in flight during the sums
       if (step + 1 < 2 * nj) load(task, step + 1);
       else if (task + gridDim.x < tasks) load(task + gridDim.x, 0);
+      // the chunk's weights, ascending in i (wave-uniform: one scalar load each)
+      const int ib = half == 0 ? H - i0 - w : H + i0;  // lowest i of the chunk
+      double wv[MOM_W], xv[MOM_W];
+#pragma unroll
+      for (int k = 0; k < MOM_W; ++k) {
+        wv[k] = k < w ? wt[ib + k] : 0.0;
+        xv[k] = k < w ? mu[ib + k] : 0.0;
+      }
       if (lane < ng) {
         const double *t = tile + lane * (MOM_W + 1);
-        if (half == 0) {
-          for (int ii = w - 1; ii >= 0; --ii) {
-            const int i = H - 1 - (i0 + ii);
-            const double q = t[ii];
-            sphi += wt[i] * q;
-            sF += mu[i] * wt[i] * q;
+        if (half == 0) {  // i = H-1-(i0+ii) = ib + (w-1-ii)
+#pragma unroll
+          for (int ii = MOM_W - 1; ii >= 0; --ii) {
+            if (ii < w) {
+              const int k = w - 1 - ii;
+              const double q = t[ii];
+              sphi += wv[k] * q;
+              sF += xv[k] * wv[k] * q;
+            }
           }
-        } else {
-          for (int ii = 0; ii < w; ++ii) {
-            const int i = H + i0 + ii;
-            const double q = t[ii];
-            sphi += wt[i] * q;
-            sF += mu[i] * wt[i] * q;
-            splus += wt[i] * q;
+        } else {  // i = H + i0 + ii = ib + ii
+#pragma unroll
+          for (int ii = 0; ii < MOM_W; ++ii) {
+            if (ii < w) {
+              const double q = t[ii];
+              sphi += wv[ii] * q;
+              sF += xv[ii] * wv[ii] * q;
+              splus += wv[ii] * q;
+            }
           }
         }
       }
@@ -905,6 +937,16 @@ hipError_t launch_init_state(double2 *E, const double *lineB, const Geometry &g,
   return hipGetLastError();
 }
 
+// blocks of `threads` the device keeps resident at once (occupancy x CUs)
+template <typename K>
+static size_t resident_blocks(K kernel, int threads) {
+  int dev = 0, cus = 0, per_cu = 0;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, threads, 0) != hipSuccess || cus * per_cu <= 0)
+    return 4096;
+  return static_cast<size_t>(cus) * per_cu;
+}
+
 static LineMap make_map(const Geometry &g) { return LineMap{g.M, g.M / 2, g.Gl, g.N, g.Nrow, g.Lpad}; }
 
 hipError_t launch_export_psi(const double2 *E, double *psi, const Geometry &g, hipStream_t st) {
@@ -929,9 +971,14 @@ hipError_t launch_moments(const double2 *E, const double *mu, const double *wt, 
                           double *phi_plus, const Geometry &g, hipStream_t st) {
   const LineMap m = make_map(g);
   const size_t tasks = static_cast<size_t>(g.N) * ((g.Gl + 63) / 64);
-  // resident waves: 16 per CU (114 VGPRs) on 256 CUs; each walks its tasks with a one-chunk prefetch
-  const dim3 grid(static_cast<unsigned>(tasks < 4096 ? tasks : 4096));
-  hipLaunchKernelGGL(moments_kernel, grid, dim3(64), 0, st, E, mu, wt, phi, F, phi_plus, m);
+  // as many waves as the chip holds at once; each walks its tasks with a one-chunk prefetch
+  const bool fast = m.H % MOM_W == 0;
+  static const size_t resident[2] = {resident_blocks(moments_kernel<false>, 64), resident_blocks(moments_kernel<true>, 64)};
+  const dim3 grid(static_cast<unsigned>(tasks < resident[fast] ? tasks : resident[fast]));
+  if (fast)
+    hipLaunchKernelGGL(moments_kernel<true>, grid, dim3(64), 0, st, E, mu, wt, phi, F, phi_plus, m);
+  else
+    hipLaunchKernelGGL(moments_kernel<false>, grid, dim3(64), 0, st, E, mu, wt, phi, F, phi_plus, m);
   return hipGetLastError();
 }
 

@@ -138,7 +138,7 @@ def test_ragged_cell_counts(rtsn_mod, oracle_mod, N, tb):
         compare_all(gpu, orc)
 
 
-@pytest.mark.parametrize("M,G", [(2, 1), (4, 31), (8, 17), (16, 9), (64, 3), (130, 1)])
+@pytest.mark.parametrize("M,G", [(2, 1), (4, 31), (8, 17), (16, 9), (64, 3), (130, 1), (32, 70), (10, 130)])
 def test_line_counts(rtsn_mod, oracle_mod, M, G):
     """Lines per half = M/2 * G: partial line groups and several line groups."""
     p = load(oracle_mod, "template.prm", M=M, G=G, N=300, max_timesteps=2, bc_left=2, V=1.0)
@@ -149,6 +149,20 @@ def test_line_counts(rtsn_mod, oracle_mod, M, G):
     with rtsn_mod.Solver(to_rt(p)) as gpu:
         gpu.solve()
         compare_all(gpu, orc)
+        # moments_kernel sums in the reference's order (solver.cpp:191-237) without FMA:
+        # bitwise equal to the same sequential sums over the device's own psi
+        psi = gpu.psi()
+        mu, wt = orc.quad()
+        phi = np.zeros(psi.shape[1:])
+        F = np.zeros_like(phi)
+        pp = np.zeros_like(phi)
+        for i in range(M):
+            phi = phi + wt[i] * psi[i]
+            F = F + (mu[i] * wt[i]) * psi[i]
+            if i >= M // 2:
+                pp = pp + wt[i] * psi[i]
+        for got, want in zip(gpu.moments(), (phi, F, pp)):
+            assert np.array_equal(got, want)
 
 
 @pytest.mark.parametrize("pipe", [True, False])
