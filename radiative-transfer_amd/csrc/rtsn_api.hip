@@ -1225,9 +1225,23 @@ extern "C" rt_status rt_get_balance_terms(rt_solver *s, double *balance, double 
   std::vector<double> rows;
   if ((st = fetch_rows(s, rows))) return st;
   const double ac = phys::kRadA * phys::kLight, dx = s->p.X / N;
+  // absorption and source sums: sequential in c per group in the reference's order and
+  // association (:262-272), with the group loop innermost so phi (N x Gl, g fastest) is
+  // read contiguously
+  std::vector<double> rk(Gl), src(Gl), ab(Gl, 0.), sr(Gl, 0.);
+  for (int gl = 0; gl < Gl; ++gl) {
+    rk[gl] = s->gt.rho[s->g_lo + gl] * s->gt.kappa[s->g_lo + gl];
+    src[gl] = rk[gl] * ac * std::pow(s->p.T, 4) * dx;
+  }
+  for (int c = 0; c < N; ++c) {
+    const double *row = phi.data() + static_cast<size_t>(c) * Gl;
+    for (int gl = 0; gl < Gl; ++gl) {
+      ab[gl] += rk[gl] * row[gl] * dx;
+      sr[gl] += src[gl];
+    }
+  }
   for (int gl = 0; gl < Gl; ++gl) {  // solver.cpp:240-284
-    const int g = s->g_lo + gl;
-    double jhm = 0., jhp = 0., jNm = 0., jNp = 0., ab = 0., sr = 0.;
+    double jhm = 0., jhp = 0., jNm = 0., jNp = 0.;
     for (int i = 0; i < s->p.M; ++i) {
       const double mu = s->mu[i];
       if (mu < 0.) {
@@ -1238,14 +1252,7 @@ extern "C" rt_status rt_get_balance_terms(rt_solver *s, double *balance, double 
         jNp += bnode(s, rows, i, gl, true, 1) * mu * s->wt[i];
       }
     }
-    // sequential sums in the reference's order and association (:262-272)
-    const double rk = s->gt.rho[g] * s->gt.kappa[g];
-    const double src_term = rk * ac * std::pow(s->p.T, 4) * dx;
-    for (int c = 0; c < N; ++c) {
-      ab += rk * phi[static_cast<size_t>(c) * Gl + gl] * dx;
-      sr += src_term;
-    }
-    const double sources = jhp + jNm + sr, sinks = jNp + jhm + ab;
+    const double sources = jhp + jNm + sr[gl], sinks = jNp + jhm + ab[gl];
     if (balance) balance[gl] = std::fabs(sinks - sources) / sources;
     if (sources_out) sources_out[gl] = sources;
     if (sinks_out) sinks_out[gl] = sinks;
