@@ -60,7 +60,7 @@ import numpy as np  # noqa: E402
 
 METRIC = "cell·angle·group updates/sec (Sn sweep) + BDF2 steps/sec, llnl_slab_test"
 HBM_PEAK = 8.0e12
-SUPPORTED_TIME_BLOCKS = (1, 2, 3, 4, 5, 6, 7, 8, 12, 16)  # rt_set_time_block
+SUPPORTED_TIME_BLOCKS = (1, 2, 3, 4, 5, 6, 7, 8, 10, 12, 16)  # rt_set_time_block
 FP64_PEAK = 78.6e12  # MI355X FP64 vector spec (256 CU x 4 SIMD x 16 FMA lanes x 2 x 2.4 GHz); measured 71 TF: profiles/r01_fp64_peak.txt
 KAPPA_TABLE = REPO / "tests" / "golden" / "prm" / "llnl_slab_test_group_kappa_a.txt"
 
@@ -408,7 +408,7 @@ def main():
     # defaults: the timed region is 2 steady-state passes (steps are rounded up to whole passes)
     ap.add_argument("--steps", type=int, default=0, help="timed steps (default: two passes)")
     ap.add_argument("--warmup", type=int, default=-1,
-                    help="untimed steps before timing (default: fill the pipeline plus one pass)")
+                    help="untimed steps before timing, at least the pipeline fill (default: the fill)")
     ap.add_argument("--variant", choices=["v0", "corr"], default="v0")
     ap.add_argument("--scaling", choices=["weak", "strong"], default="strong")
     ap.add_argument("--groups", type=int, default=128, help="groups per GPU (weak) or in total (strong)")
@@ -453,12 +453,16 @@ def main():
     steps = args.steps if args.steps > 0 else 2 * tb
     tb = max(t for t in SUPPORTED_TIME_BLOCKS if t <= tb and steps % t == 0)
     solver.time_block = tb
-    warmup = args.warmup
-    if warmup < 0:  # pipeline depth (segments per line) passes: fill + one steady pass
-        warmup = solver.sweep_geometry()[1] * tb if solver.pipeline else tb
+    # Warmup: at least W steps, and always whole passes that fill the pipeline (segments
+    # per line passes: every segment position running, one pass apart), so that the K timed
+    # steps are the schedule's steady state whatever W the caller asks for; the steps run
+    # are reported as "warmup" (W as "warmup_requested").
+    fill = solver.sweep_geometry()[1] * tb if solver.pipeline else tb
+    warmup = fill if args.warmup < 0 else max(fill, -(-args.warmup // tb) * tb)
     shards = [shard(args.scaling, args.groups, world, r)[1:] for r in range(world)]
     solver_tb = solver.time_block
     line, _, _ = run_rank(solver, p, steps, warmup, world, device, info, args.scaling, shards)
+    line["warmup_requested"] = args.warmup if args.warmup >= 0 else None
     line["roofline"]["traffic"] = load_traffic(args.variant, solver.time_block,
                                                line["roofline"]["algorithmic_bytes_per_launch"])
     solver.close()  # frees the sweep's state before the next run allocates its own

@@ -162,7 +162,7 @@ rt_status rt_sweep_traffic(rt_solver *s, double *bytes_per_launch, double *updat
  * affine cell map (BDF2 28, CN 8, BE 6 FMAs per cell x line x step) times T
  * steps; the cross-segment correction is parallelisation overhead, not counted. */
 rt_status rt_sweep_flops(rt_solver *s, double *flops_per_launch);
-/* Time blocking: full steps advanced per pass over HBM: 1..8, 12 or 16
+/* Time blocking: full steps advanced per pass over HBM: 1..8, 10, 12 or 16
  * (default 16; aligned passes take at most 4).  Results do not depend on it
  * beyond rounding. */
 rt_status rt_set_time_block(rt_solver *s, int steps_per_pass);

@@ -864,6 +864,7 @@ static hipError_t launch_s(int T, int mode, const SegArgs &a, int grid, hipStrea
     case 6: return launch_t<S, 6>(mode, a, grid, st);
     case 7: return launch_t<S, 7>(mode, a, grid, st);
     case 8: return launch_t<S, 8>(mode, a, grid, st);
+    case 10: return launch_t<S, 10>(mode, a, grid, st);
     case 12: return launch_t<S, 12>(mode, a, grid, st);
     case 16: return launch_t<S, 16>(mode, a, grid, st);
     default: return hipErrorInvalidValue;
@@ -902,6 +903,7 @@ static hipError_t occupancy_s(int T, int *w) {
     case 6: return hipOccupancyMaxActiveBlocksPerMultiprocessor(w, sweep_block_kernel<S, 6, 2>, 64, 0);
     case 7: return hipOccupancyMaxActiveBlocksPerMultiprocessor(w, sweep_block_kernel<S, 7, 2>, 64, 0);
     case 8: return hipOccupancyMaxActiveBlocksPerMultiprocessor(w, sweep_block_kernel<S, 8, 2>, 64, 0);
+    case 10: return hipOccupancyMaxActiveBlocksPerMultiprocessor(w, sweep_block_kernel<S, 10, 2>, 64, 0);
     case 12: return hipOccupancyMaxActiveBlocksPerMultiprocessor(w, sweep_block_kernel<S, 12, 2>, 64, 0);
     case 16: return hipOccupancyMaxActiveBlocksPerMultiprocessor(w, sweep_block_kernel<S, 16, 2>, 64, 0);
     default: return hipErrorInvalidValue;

@@ -112,7 +112,7 @@ static rt_status fail(rt_solver *s, rt_status st, const std::string &msg) {
 static int default_time_block(int) { return 16; }
 
 // rt_set_time_block's domain: the instantiated sweep kernels (kernels.hip launch_s)
-static bool supported_time_block(int T) { return (T >= 1 && T <= 8) || T == 12 || T == 16; }
+static bool supported_time_block(int T) { return (T >= 1 && T <= 8) || T == 10 || T == 12 || T == 16; }
 
 static int map_count_of(int scheme) {
   switch (scheme) {
@@ -1373,7 +1373,7 @@ extern "C" rt_status rt_get_pipeline(rt_solver *s, int *on) {
 extern "C" rt_status rt_set_time_block(rt_solver *s, int steps_per_pass) {
   if (!s) return fail(nullptr, RT_ERR_ARG, "rt_set_time_block: NULL handle");
   if (!supported_time_block(steps_per_pass))
-    return fail(s, RT_ERR_ARG, "rt_set_time_block: steps per pass must be 1..8, 12 or 16");
+    return fail(s, RT_ERR_ARG, "rt_set_time_block: steps per pass must be 1..8, 10, 12 or 16");
   s->T = steps_per_pass;
   return RT_OK;
 }

@@ -191,7 +191,7 @@ def test_random_state_long_lines(rtsn_mod, oracle_mod, tb, steps, pipe):
 
 
 @pytest.mark.parametrize("ts,tb,steps", [(3, 12, 13), (3, 16, 17), (3, 8, 16), (2, 16, 40), (1, 16, 40),
-                                         (2, 12, 30), (1, 5, 11)])
+                                         (2, 12, 30), (1, 5, 11), (3, 10, 15), (3, 10, 20), (2, 10, 20), (1, 10, 30)])
 def test_large_time_blocks(rtsn_mod, oracle_mod, ts, tb, steps):
     """Pipelined passes of up to 16 fused steps (and their aligned remainder)
     on many-segment lines with a random start state."""
@@ -260,7 +260,7 @@ def test_pipeline_long_run_many_segments(rtsn_mod, oracle_mod, ts):
 def test_time_block_range(rtsn_mod):
     d = rtsn_mod.params_default()
     with rtsn_mod.Solver(d) as s:
-        for ok in (1, 4, 8, 12, 16):
+        for ok in (1, 4, 8, 10, 12, 16):
             s.time_block = ok
             assert s.time_block == ok
         for bad in (0, 9, 13, 17, -1):
