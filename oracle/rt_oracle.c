@@ -11,7 +11,9 @@
 #include "rt_oracle.h"
 
 #include <ctype.h>
+#include <errno.h>
 #include <float.h>
+#include <limits.h>
 #include <math.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -95,22 +97,26 @@ static int kv_load(kvmap_t *m, const char *path) {
   return 1;
 }
 
-/* param.cpp:447-453: std::stoi -- leading whitespace, sign, digits; throws
- * when nothing converts. */
+/* std::stoi (param.cpp:30): strtol base 10; invalid_argument when nothing
+ * converts, out_of_range on ERANGE or outside int (the reference terminates). */
 static int kv_get_int(const kvmap_t *m, const char *key, int def, int *err) {
   const char *v = kv_find(m, key);
   if (!v) return def;
   char *end;
+  errno = 0;
   long x = strtol(v, &end, 10);
-  if (end == v) { *err = ORC_ERR_PARSE; return def; }
+  if (end == v || errno == ERANGE || x > INT_MAX || x < INT_MIN) { *err = ORC_ERR_PARSE; return def; }
   return (int)x;
 }
+/* std::stod (param.cpp:44): strtod; invalid_argument when nothing converts,
+ * out_of_range on ERANGE (overflow, or underflow to a subnormal / zero). */
 static double kv_get_double(const kvmap_t *m, const char *key, double def, int *err) {
   const char *v = kv_find(m, key);
   if (!v) return def;
   char *end;
+  errno = 0;
   double x = strtod(v, &end);
-  if (end == v) { *err = ORC_ERR_PARSE; return def; }
+  if (end == v || errno == ERANGE) { *err = ORC_ERR_PARSE; return def; }
   return x;
 }
 /* param.cpp:427-439: true only for the exact strings yes/Yes/true/True. */
@@ -121,23 +127,42 @@ static int kv_get_bool(const kvmap_t *m, const char *key, int def) {
          strcmp(v, "True") == 0;
 }
 
-/* operator>>(double) over whitespace-separated text, stopping at the first
- * token that does not start with a number. */
+/* `while (stream >> d)` over text (ParameterHandler.cpp:122-128, :152, :184)
+ * as libstdc++'s num_get<char> does it in the C locale: skip whitespace; take
+ * [+-], digits with at most one '.', then 'e'/'E' (only after a digit) with an
+ * optional sign and digits; the token must convert in full (strtod) and must
+ * not overflow, else the extraction fails and the loop ends ("inf", "nan",
+ * "1e" stop it; "0x10" yields 0; "1.2.3" yields 1.2 and 0.3). */
 static int read_doubles(const char *s, double **out, int *n) {
   int cap = 16;
   *n = 0;
   *out = (double *)malloc(sizeof(double) * cap);
+  char *tok = (char *)malloc(strlen(s) + 2);
   const char *p = s;
   for (;;) {
     while (*p && isspace((unsigned char)*p)) ++p;
-    if (!*p) break;
+    size_t t = 0;
+    if (*p == '+' || *p == '-') tok[t++] = *p++;
+    int mant = 0, dec = 0, sci = 0;
+    for (;; ++p) {
+      const char c = *p;
+      if (c >= '0' && c <= '9') { tok[t++] = c; mant = 1; }
+      else if (c == '.' && !dec && !sci) { tok[t++] = c; dec = 1; }
+      else if ((c == 'e' || c == 'E') && !sci && mant) {
+        tok[t++] = 'e';
+        sci = 1;
+        if (p[1] == '+' || p[1] == '-') tok[t++] = *++p;
+      } else break;
+    }
+    tok[t] = 0;
+    if (t == 0) break;
     char *end;
-    double d = strtod(p, &end);
-    if (end == p) break;
+    double d = strtod(tok, &end);
+    if (end == tok || *end != 0 || isinf(d)) break;
     if (*n == cap) { cap *= 2; *out = (double *)realloc(*out, sizeof(double) * cap); }
     (*out)[(*n)++] = d;
-    p = end;
   }
+  free(tok);
   return *n;
 }
 

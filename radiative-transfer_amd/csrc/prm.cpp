@@ -1,7 +1,9 @@
 // prm.cpp -- see prm.hpp.
 #include "prm.hpp"
 
+#include <cctype>
 #include <cerrno>
+#include <cmath>
 #include <cstdlib>
 #include <cstring>
 #include <fstream>
@@ -26,6 +28,8 @@ KeyValueFile::KeyValueFile(const std::string &path) {
   }
 }
 
+// std::stoi (param.cpp:30): strtol base 10; throws invalid_argument when nothing
+// converts and out_of_range on ERANGE or a value outside int -- a parse error here
 int KeyValueFile::get_int(const std::string &key, int fallback) {
   auto it = kv_.find(key);
   if (it == kv_.end()) return fallback;
@@ -40,13 +44,16 @@ int KeyValueFile::get_int(const std::string &key, int fallback) {
   return static_cast<int>(v);
 }
 
+// std::stod (param.cpp:44): strtod; invalid_argument when nothing converts,
+// out_of_range on ERANGE (overflow, and underflow to a subnormal or zero)
 double KeyValueFile::get_double(const std::string &key, double fallback) {
   auto it = kv_.find(key);
   if (it == kv_.end()) return fallback;
   const char *s = it->second.c_str();
   char *end = nullptr;
+  errno = 0;
   const double v = std::strtod(s, &end);
-  if (end == s) {
+  if (end == s || errno == ERANGE) {
     status_ = RT_ERR_PARSE;
     return fallback;
   }
@@ -65,17 +72,43 @@ std::string KeyValueFile::get_string(const std::string &key, const std::string &
   return it == kv_.end() ? fallback : it->second;
 }
 
-std::vector<double> leading_numbers(const std::string &text) {
+// `while (is >> d)` over text (ParameterHandler.cpp:122-128 psi_source, :152 and
+// :184 tables), as libstdc++'s num_get<char> in the C locale does it: skip
+// whitespace; take [+-], digits with at most one '.', then 'e'/'E' (only after a
+// digit) with an optional sign and digits; the token must convert in full
+// (strtod) and not overflow, else the extraction fails and the loop ends.  So
+// "inf", "nan", "0x..", "1e" stop it, "0x10" yields 0, "1.2.3" yields 1.2, 0.3,
+// and an underflow yields the subnormal / zero.
+std::vector<double> stream_doubles(const std::string &text) {
   std::vector<double> out;
   const char *p = text.c_str();
+  std::string tok;
   for (;;) {
     while (*p && std::isspace(static_cast<unsigned char>(*p))) ++p;
-    if (!*p) break;
+    tok.clear();
+    if (*p == '+' || *p == '-') tok += *p++;
+    bool mant = false, dec = false, sci = false;
+    for (;; ++p) {
+      const char c = *p;
+      if (c >= '0' && c <= '9') {
+        tok += c;
+        mant = true;
+      } else if (c == '.' && !dec && !sci) {
+        tok += c;
+        dec = true;
+      } else if ((c == 'e' || c == 'E') && !sci && mant) {
+        tok += 'e';
+        sci = true;
+        if (p[1] == '+' || p[1] == '-') tok += *++p;
+      } else {
+        break;
+      }
+    }
+    if (tok.empty()) break;
     char *end = nullptr;
-    const double v = std::strtod(p, &end);
-    if (end == p) break;
+    const double v = std::strtod(tok.c_str(), &end);
+    if (end == tok.c_str() || *end != '\0' || std::isinf(v)) break;
     out.push_back(v);
-    p = end;
   }
   return out;
 }
@@ -95,7 +128,7 @@ bool ParameterHandler::read_table(const std::string &path, size_t expect, std::v
   }
   std::stringstream ss;
   ss << in.rdbuf();
-  out = leading_numbers(ss.str());
+  out = stream_doubles(ss.str());
   if (out.size() != expect) {
     fail(RT_ERR_PARAM, "table " + path + " holds " + std::to_string(out.size()) + " values, expected " +
                            std::to_string(expect));
@@ -127,7 +160,7 @@ ParameterHandler::ParameterHandler(const std::string &filename, const std::strin
 
   psi_source_.assign(static_cast<size_t>(M_) * G_, 0.0);
   if (!use_mg_equilib_) {
-    const std::vector<double> v = leading_numbers(kv.get_string("psi_source", "no_sources_provided"));
+    const std::vector<double> v = stream_doubles(kv.get_string("psi_source", "no_sources_provided"));
     if (v.size() > psi_source_.size()) {
       fail(RT_ERR_PARAM, "psi_source holds more than M*G values");
     } else {

@@ -37,9 +37,9 @@ class KeyValueFile {
   rt_status status_ = RT_OK;
 };
 
-// All numbers of a whitespace-separated text up to the first token that does
-// not start with a number (stringstream >> double, ParameterHandler.cpp:126,152).
-std::vector<double> leading_numbers(const std::string &text);
+// The numbers `while (stream >> d)` extracts from a text under libstdc++'s
+// num_get (ParameterHandler.cpp:126,152,184): see prm.cpp.
+std::vector<double> stream_doubles(const std::string &text);
 
 class ParameterHandler {
  public:
