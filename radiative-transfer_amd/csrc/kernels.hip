@@ -184,8 +184,9 @@ __device__ __forceinline__ void sweep_chunk(const double *W, double (&ein)[C], d
 // Fused angular sums of one chunk: vals[c] is this lane's psi in chunk cell c
 // (rows k0 + c, c < nv); w psi goes through LDS (one row of 64 lines per
 // cell) and each (cell, group) sum over the group's H lines (H divides 64)
-// is taken by one lane in the reference's direction order (i ascending:
-// i' descending in the mu < 0 half), then stored to dst[x][g], x the
+// is taken by one lane as four interleaved partial sums (the material path is
+// held to a tolerance: the per-half split already departs from the
+// reference's single sequential sum), then stored to dst[x][g], x the
 // physical cell.  gw0: the wave's first local group.
 // LDS tile of group_sums: per cell a row of 64/H groups of H + 1 slots (+1):
 // the summing lanes then read from different banks.
@@ -204,12 +205,17 @@ __device__ __forceinline__ void group_sums(const double (&vals)[C], double w, in
   for (int t = lane; t < tasks; t += 64) {
     const int c = t / ngw, j = t - c * ngw;
     const double *r = tile + c * RS + j * (H + 1);
-    double acc = 0.0;
-    if (neg) {
-      for (int i = H - 1; i >= 0; --i) acc += r[i];
-    } else {
-      for (int i = 0; i < H; ++i) acc += r[i];
+    // four interleaved partial sums: a quarter of the dependent-add chain
+    double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+    int i = 0;
+    for (; i + 4 <= H; i += 4) {
+      a0 += r[i];
+      a1 += r[i + 1];
+      a2 += r[i + 2];
+      a3 += r[i + 3];
     }
+    for (; i < H; ++i) a0 += r[i];
+    const double acc = (a0 + a1) + (a2 + a3);
     const int g = gw0 + j, k = k0 + c;
     if (g < Gl) dst[static_cast<size_t>(neg ? N - 1 - k : k) * Gl + g] = acc;
   }
