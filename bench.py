@@ -106,32 +106,44 @@ def cpu_baseline(variant: str) -> dict:
                       f"1 group on 1 thread = {u1:.3g} updates in {t1:.2f} s"}
 
 
+REFERENCE_CONFIGS = ("single_group.prm", "multi_group_equilibrium.prm", "llnl_slab_test.prm",
+                     "llnl_slab_test_uncapped.prm")
+
+
 def reference_config_timings() -> dict:
-    """the reference's own llnl_slab_test (M2 G124 N50, 2 BDF2 steps) end to
-    end -- create + solve + moments on the GPU, and the oracle on one core, in the
-    reference's loop order with the per-cell half_ends copy done lazily and literally
-    (solver.cpp:733, quadratic in the state size)."""
+    """BASELINE.json's small configs (the reference's own .prm files, SURVEY §8(d) SG, EQ,
+    LL, LL-uncapped) end to end -- create + solve + moments on the GPU, and the oracle
+    (the reference's loop order) on one core -- with the GPU's phi checked against the
+    oracle's (max per-group relative difference).  For llnl_slab_test also the oracle with
+    the reference's literal per-cell half_ends copy (solver.cpp:733, quadratic in the
+    state size)."""
     import rtsn
     sys.path.insert(0, str(REPO / "oracle"))
     import oracle
     oracle.build()
-    prm = REPO / "tests" / "golden" / "prm" / "llnl_slab_test.prm"
-    tdir = str(prm.parent) + "/"
-    out = {"config": "llnl_slab_test.prm (M=2, G=124, N=50, 2 BDF2 steps)"}
-    ph = rtsn.ParameterHandler(prm, table_dir=tdir)
-    for _ in range(2):  # second round timed (first pays module/kernel loading)
-        t0 = time.perf_counter()
-        with rtsn.Solver(ph) as s:
-            s.solve()
-            s.moments()
-        out["gpu_end_to_end_ms"] = 1e3 * (time.perf_counter() - t0)
-    q = oracle.parse_prm(prm, table_dir=tdir)
-    for literal in (False, True):
-        o = oracle.OracleSolver(q, half_copy_literal=literal)
-        t0 = time.perf_counter()
-        o.solve()
-        o.moments()
-        out["cpu_literal_half_copy_ms" if literal else "cpu_ms"] = 1e3 * (time.perf_counter() - t0)
+    pdir = REPO / "tests" / "golden" / "prm"
+    tdir = str(pdir) + "/"
+    out = {}
+    for name in REFERENCE_CONFIGS:
+        ph = rtsn.ParameterHandler(pdir / name, table_dir=tdir)
+        q = oracle.parse_prm(pdir / name, table_dir=tdir)
+        r = {"M": q["M"], "G": q["G"], "N": q["N"], "steps": q["max_timesteps"],
+             "ts_method": q["ts_method"]}
+        for _ in range(2):  # second round timed (first pays module/kernel loading)
+            t0 = time.perf_counter()
+            with rtsn.Solver(ph) as s:
+                s.solve()
+                phi = s.moments()[0]
+            r["gpu_end_to_end_ms"] = 1e3 * (time.perf_counter() - t0)
+        for literal in ((False, True) if name == "llnl_slab_test.prm" else (False,)):
+            o = oracle.OracleSolver(q, half_copy_literal=literal)
+            t0 = time.perf_counter()
+            o.solve()
+            phi_o = o.moments()[0]
+            r["cpu_literal_half_copy_ms" if literal else "cpu_ms"] = 1e3 * (time.perf_counter() - t0)
+        scale = np.maximum(np.abs(phi_o).max(axis=1, keepdims=True), 1e-300)
+        r["phi_max_rel_diff"] = float((np.abs(phi - phi_o) / scale).max())
+        out[name] = r
     return out
 
 
