@@ -121,7 +121,7 @@ void *rt_stream(rt_solver *s);
 rt_status rt_get_dims(rt_solver *s, int *M, int *G_local, int *N, int *g_lo, int *g_hi);
 rt_status rt_get_psi(rt_solver *s, double *psi);                /* psi_mat_ref */
 rt_status rt_get_ends(rt_solver *s, double *ends);              /* Solver::ends */
-rt_status rt_set_ends(rt_solver *s, const double *ends);        /* test hook: load a state */
+rt_status rt_set_ends(rt_solver *s, const double *ends);        /* load a state: checkpoint resume, tests */
 /* compute_angle_integrated_intensity, compute_radiative_flux,
  * compute_positive_angle_integrated_intensity (solver.cpp:191-237); any NULL skipped */
 rt_status rt_get_moments(rt_solver *s, double *phi, double *F, double *phi_plus);

@@ -239,6 +239,35 @@ def test_time_block_switching(rtsn_mod, oracle_mod, toggle):
 
 
 @pytest.mark.parametrize("ts", [1, 2, 3])
+def test_checkpoint_resume(rtsn_mod, oracle_mod, ts, tmp_path):
+    """Checkpoint / resume: the state at a full-step boundary is the node
+    array ends (solver.cpp:620-625 rebuilds prev_ends from it each step), so a run
+    saved after 3 steps (rt_get_ends, to a .npy file) and loaded into a fresh handle
+    (rt_set_ends) that runs 5 more equals one 8-step oracle run; with the same
+    schedule on both sides the resumed state is bitwise the one of a handle that
+    never stopped (both read out at step 3).  (8 steps: beyond ~10 the reference's
+    BDF2 growth on this line amplifies rounding past 1e-10 in the group ends.)"""
+    p = load(oracle_mod, "llnl_slab_test.prm", N=3000, M=8, use_correction=1, V=5.994, bc_left=2, ts_method=ts)
+    p["dx"] = p["X"] / p["N"]
+    p["psi_source"] = np.full((p["M"], p["G"]), 0.25)
+    p["max_timesteps"] = 8
+    orc = oracle_mod.OracleSolver(p)
+    orc.solve()
+    ck = tmp_path / "state.npy"
+    with rtsn_mod.Solver(to_rt(p)) as a:
+        a.advance(3)
+        np.save(ck, a.ends())
+        a.advance(5)
+        straight = a.ends()
+        compare_all(a, orc)
+    with rtsn_mod.Solver(to_rt(p)) as b:
+        b.set_ends(np.load(ck))
+        b.advance(5)
+        compare_all(b, orc)
+        assert np.array_equal(b.ends(), straight)
+
+
+@pytest.mark.parametrize("ts", [1, 2, 3])
 def test_pipeline_long_run_many_segments(rtsn_mod, oracle_mod, ts):
     """Enough passes to fill, run and drain the pipeline (reflective: one chain
     of 2 Sg positions), split over several advance() calls."""
