@@ -323,7 +323,8 @@ def run_rank(solver, p: dict, steps: int, warmup: int, world: int, device, shard
             "unit": "TFLOP/s" if tb > 1 else "GB/s",
             "frac": achieved_fl / FP64_PEAK if tb > 1 else achieved / HBM_PEAK,
             "traffic": None,
-            "kernel": f"sweep_block_kernel<3, {tb}, {2 if getattr(solver, 'pipeline', False) else 0}>",
+            # the pass the timed region ran: pipelined (MODE 2) when the pipeline was filled
+            "kernel": f"sweep_block_kernel<3, {tb}, {2 if before['lag_steps'] > 0 else 0}, false>",
             "kernel_ms": kern_avg_ms,
             "algorithmic_flops_per_launch": flops_launch,
             "algorithmic_bytes_per_launch": bytes_launch,
