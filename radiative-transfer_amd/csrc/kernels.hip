@@ -423,16 +423,18 @@ __global__ __launch_bounds__(64) void sweep_block_kernel(SegArgs a) {
 // Non-hot kernels: state initialisation, layout conversion, moments
 // ------------------------------------------------------------------------
 // psi = ends = B_g (solver.cpp:165-181); padding rows k >= N are zero
+// E = B_g on every node of every line (solver.cpp:165-181), zero on padding rows:
+// a block per row (no 64-bit index division), nt stores (written once, read next pass)
 __global__ void init_state_kernel(double2 *E, const double *lineB, int N, int Nrow, int Lpad) {
-  const size_t total = static_cast<size_t>(2) * Nrow * Lpad;
-  for (size_t idx = blockIdx.x * static_cast<size_t>(blockDim.x) + threadIdx.x; idx < total;
-       idx += static_cast<size_t>(gridDim.x) * blockDim.x) {
-    const size_t row = idx / Lpad;
-    const size_t half = row / Nrow;
-    const int k = static_cast<int>(row - half * Nrow);
-    const int ell = static_cast<int>(idx % Lpad);
-    const double v = k < N ? lineB[half * Lpad + ell] : 0.0;
-    E[idx] = make_double2(v, v);
+  typedef double d2v __attribute__((ext_vector_type(2)));
+  for (int row = blockIdx.x; row < 2 * Nrow; row += gridDim.x) {
+    const int half = row / Nrow, k = row - half * Nrow;
+    d2v *dst = reinterpret_cast<d2v *>(E) + static_cast<size_t>(row) * Lpad;
+    const double *b = lineB + static_cast<size_t>(half) * Lpad;
+    for (int ell = threadIdx.x; ell < Lpad; ell += blockDim.x) {
+      const double v = k < N ? b[ell] : 0.0;
+      __builtin_nontemporal_store(d2v{v, v}, dst + ell);
+    }
   }
 }
 
@@ -951,8 +953,8 @@ static int grid_for(size_t total, int block) {
 }
 
 hipError_t launch_init_state(double2 *E, const double *lineB, const Geometry &g, hipStream_t st) {
-  hipLaunchKernelGGL(init_state_kernel, dim3(grid_for(static_cast<size_t>(2) * g.Nrow * g.Lpad, 256)), dim3(256), 0, st,
-                     E, lineB, g.N, g.Nrow, g.Lpad);
+  hipLaunchKernelGGL(init_state_kernel, dim3(grid_for(static_cast<size_t>(2) * g.Nrow * 256, 256)), dim3(256), 0, st,
+                     E, lineB, g.N, g.Nrow, g.Lpad);  // one block per row
   return hipGetLastError();
 }
 
