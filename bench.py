@@ -161,6 +161,15 @@ def load_traffic(variant: str, tb: int, algorithmic_bytes: float):
     return b if b and abs(b / algorithmic_bytes - 1.0) < 0.1 else None
 
 
+def warmup_steps(requested: int, fill: int, tb: int) -> int:
+    """Untimed steps before the K timed ones: at least the `requested` W (negative: none
+    asked) rounded up to whole passes of tb steps, and at least the pipeline `fill`
+    (segments per line x tb), so the timed passes are the schedule's steady state."""
+    if requested < 0:
+        return fill
+    return max(fill, -(-requested // tb) * tb)
+
+
 def shard(scaling: str, groups: int, world: int, rank: int):
     """(G_total, g_lo, g_hi) of this rank.  weak: every rank owns `groups`
     groups of a groups*world grid; strong: `groups` split into contiguous
@@ -471,7 +480,7 @@ def main():
     # steps are the schedule's steady state whatever W the caller asks for; the steps run
     # are reported as "warmup" (W as "warmup_requested").
     fill = solver.sweep_geometry()[1] * tb if solver.pipeline else tb
-    warmup = fill if args.warmup < 0 else max(fill, -(-args.warmup // tb) * tb)
+    warmup = warmup_steps(args.warmup, fill, tb)
     shards = [shard(args.scaling, args.groups, world, r)[1:] for r in range(world)]
     solver_tb = solver.time_block
     line, _, _ = run_rank(solver, p, steps, warmup, world, device, info, args.scaling, shards)

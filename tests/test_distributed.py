@@ -194,3 +194,13 @@ def test_shard_table():
     assert bench.shard("strong", 128, 3, 2) == (128, 86, 128)
     spans = [bench.shard("strong", 10, 4, r)[1:] for r in range(4)]
     assert spans == [(0, 3), (3, 6), (6, 9), (9, 10)]
+
+
+def test_warmup_rule():
+    """bench.py: the warmup covers the pipeline fill and whole passes, whatever W is asked."""
+    import bench
+    assert bench.warmup_steps(-1, 128, 16) == 128   # default: the fill
+    assert bench.warmup_steps(1, 128, 16) == 128    # BASELINE's W = 1
+    assert bench.warmup_steps(200, 128, 16) == 208  # more than the fill: whole passes
+    assert bench.warmup_steps(5, 80, 10) == 80
+    assert bench.warmup_steps(0, 2, 2) == 2         # aligned schedule: one pass
