@@ -17,8 +17,8 @@
  *
  * Array layouts are the reference's Eigen ColMajor layouts:
  *   psi  (M, G, N)    index i + M*(g + G*c)          main.cc:88
- *   ends (M, G, N, 2) index i + M*(g + G*(c + N*s))  solver.h:135
- *   phi / F / phi_plus (G, N) index g + G*c          main.cc:91-92, solver.h:131
+ *   ends (M, G, N, 2) index i + M*(g + G*(c + N*s))  solver.h:36
+ *   phi / F / phi_plus (G, N) index g + G*c          main.cc:91-92, solver.h:31-33
  * where G is the number of groups held by the handle (all groups, or the
  * [g_lo, g_hi) shard given to rt_create_from_params).
  *
@@ -37,7 +37,7 @@ extern "C" {
 typedef enum {
   RT_OK = 0,
   RT_ERR_IO = 1,          /* a group table could not be opened (ParameterHandler.cpp:146-149 exit(1)) */
-  RT_ERR_PARSE = 2,       /* std::stoi / std::stod would throw (param.cpp:452,466) */
+  RT_ERR_PARSE = 2,       /* std::stoi / std::stod would throw (param.cpp:30,44) */
   RT_ERR_PARAM = 3,       /* invalid configuration (odd M -> mu = 0 assert solver.cpp:402, bad BC :660, ...) */
   RT_ERR_VALIDATION = 4,  /* assert(validate_correction()) would fire (solver.cpp:609-612) */
   RT_ERR_NOMEM = 5,       /* host or device allocation failed */
@@ -132,7 +132,7 @@ rt_status rt_get_balance(rt_solver *s, double *balance);
 /* ... with the sources and sinks it is built from (printed by the reference,
  * solver.cpp:278-279); any NULL skipped */
 rt_status rt_get_balance_terms(rt_solver *s, double *balance, double *sources, double *sinks);
-/* get_e_ave (solver.h:194): all G groups */
+/* get_e_ave (solver.h:95): all G groups */
 rt_status rt_get_e_ave(rt_solver *s, double *e_ave);
 /* Group data of all G groups: e_edge (G+1), B, dBdT, kappa (G); any NULL skipped. */
 rt_status rt_get_group_data(rt_solver *s, double *e_edge, double *B, double *dBdT, double *kappa);

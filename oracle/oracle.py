@@ -131,7 +131,7 @@ def default_params() -> dict:
 
 
 class OracleSolver:
-    """The reference's Solver (solver.h:117-197) on the CPU restatement."""
+    """The reference's Solver (solver.h:18-98) on the CPU restatement."""
 
     def __init__(self, params: dict, half_copy_literal: bool = False, g_lo: int = 0, g_hi: int = 0):
         L = lib()

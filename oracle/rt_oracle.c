@@ -119,7 +119,7 @@ static double kv_get_double(const kvmap_t *m, const char *key, double def, int *
   if (end == v || errno == ERANGE) { *err = ORC_ERR_PARSE; return def; }
   return x;
 }
-/* param.cpp:427-439: true only for the exact strings yes/Yes/true/True. */
+/* param.cpp:5-18: true only for the exact strings yes/Yes/true/True. */
 static int kv_get_bool(const kvmap_t *m, const char *key, int def) {
   const char *v = kv_find(m, key);
   if (!v) return def;
@@ -537,7 +537,7 @@ struct orc_solver {
   double dx, dt;
   int literal_half;
   int threads;        /* OpenMP threads over the lines of a direction (orc_set_threads); 1 = serial */
-  double ac;          /* RADIATION_CONSTANT_A * c (solver.h:128, correction.h:25) */
+  double ac;          /* RADIATION_CONSTANT_A * c (solver.h:29, correction.h:25) */
   double *mu, *wt;
   double *e_edge, *e_ave, *de_ave;
   double *kappa, *rho, *temperature;
@@ -791,7 +791,7 @@ void orc_destroy(orc_solver *s) {
   free(s);
 }
 
-/* Per-sweep scratch mirroring Solver's members (solver.h:145-152) */
+/* Per-sweep scratch mirroring Solver's members (solver.h:45-53) */
 typedef struct { double local_bdry, half_local_bdry, local_bdry_prev_it; } sweep_t;
 
 /* Solver::backwardEuler (solver.cpp:319-404) */

@@ -1,4 +1,4 @@
-// solver.hpp -- the reference's Solver class surface (include/solver.h:117-197)
+// solver.hpp -- the reference's Solver class surface (include/solver.h:18-98)
 // over the C ABI (include/rtsn.h).  Caller-owned psi/phi/F buffers are
 // written through, as Solver writes through its Eigen references
 // (solver.cpp:50-53); here they are std::vector<double> in the reference's

@@ -217,7 +217,7 @@ def _to_struct(params: dict, keep: list) -> rt_params:
 
 
 class Solver:
-    """The reference's Solver (include/solver.h:117-197) on librtsn.
+    """The reference's Solver (include/solver.h:18-98) on librtsn.
 
     Solver(parameter_handler_or_params, device=0, g_lo=0, g_hi=0).  Results
     are numpy arrays in the reference's index order: psi (M, G, N), phi / F /
