@@ -270,7 +270,12 @@ def run_rank(solver, p: dict, steps: int, warmup: int, world: int, device, shard
     solver.synchronize()
     if world > 1:
         dist.all_reduce(absorb)
-    finite = bool(torch.isfinite(absorb).all().item())  # see DESIGN.md §5: the reference's BDF2 grows ~10^3 per step on SL
+    # NaN/Inf scan of the state (rt_state_finite), every rank; see DESIGN.md §5: the
+    # reference's BDF2 grows ~10^3 per step on SL
+    fin = torch.tensor([1.0 if solver.state_finite() else 0.0], dtype=torch.float64, device=device)
+    if world > 1:
+        dist.all_reduce(fin, op=dist.ReduceOp.MIN)
+    finite = bool(fin.item() == 1.0)
 
     # end-of-run gather: every rank's phi, F, phi_plus (N x G_local, g
     # fastest) and its group ends and balance, assembled into the reference's (N, G)

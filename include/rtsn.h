@@ -150,6 +150,11 @@ rt_status rt_get_moments_device(rt_solver *s, double *d_phi, double *d_F, double
  * partial of the group-sum all-reduce (north_star; the reference has no
  * material-temperature update, so nothing consumes it in the solve). */
 rt_status rt_group_absorption_device(rt_solver *s, double *d_out);
+/* NaN/Inf scan of the state (failure detection): *finite = 1 when
+ * every node value of every line and cell is finite at the requested time
+ * (queued steps are completed first), else 0.  One read of the state on the
+ * device; blocks until the answer is on the host. */
+rt_status rt_state_finite(rt_solver *s, int *finite);
 /* Per-launch timing of the sweep kernel with HIP events on the handle's
  * stream (off by default). */
 rt_status rt_set_profiling(rt_solver *s, int on);

@@ -622,6 +622,22 @@ __global__ void __launch_bounds__(64) moments_kernel(const double2 *__restrict__
   }
 }
 
+// NaN/Inf scan of the state: a block per row of the real cells (padding rows and
+// lanes hold zeros), one ballot per wave, one flag store per offending wave.
+__global__ void finite_scan_kernel(const double2 *E, int *flag, int N, int Nrow, int Lpad) {
+  typedef double d2v __attribute__((ext_vector_type(2)));
+  for (int r = blockIdx.x; r < 2 * N; r += gridDim.x) {
+    const int half = r / N, k = r - half * N;
+    const d2v *row = reinterpret_cast<const d2v *>(E) + (static_cast<size_t>(half) * Nrow + k) * Lpad;
+    bool bad = false;
+    for (int ell = threadIdx.x; ell < Lpad; ell += blockDim.x) {
+      const d2v v = __builtin_nontemporal_load(row + ell);
+      bad |= !isfinite(v.x) || !isfinite(v.y);
+    }
+    if (__ballot(bad) && (threadIdx.x & 63) == 0) *flag = 1;
+  }
+}
+
 // Boundary rows k = 0 and k = N-1 of both halves (for group ends / balance)
 __global__ void boundary_rows_kernel(const double2 *E, double2 *rows, int N, int Nrow, int Lpad) {
   const int total = 4 * Lpad;
@@ -1000,6 +1016,12 @@ hipError_t launch_moments(const double2 *E, const double *mu, const double *wt, 
     hipLaunchKernelGGL(moments_kernel<true>, grid, dim3(64), 0, st, E, mu, wt, phi, F, phi_plus, m);
   else
     hipLaunchKernelGGL(moments_kernel<false>, grid, dim3(64), 0, st, E, mu, wt, phi, F, phi_plus, m);
+  return hipGetLastError();
+}
+
+hipError_t launch_finite_scan(const double2 *E, int *flag, const Geometry &g, hipStream_t st) {
+  hipLaunchKernelGGL(finite_scan_kernel, dim3(grid_for(static_cast<size_t>(2) * g.N * 256, 256)), dim3(256), 0, st, E,
+                     flag, g.N, g.Nrow, g.Lpad);
   return hipGetLastError();
 }
 

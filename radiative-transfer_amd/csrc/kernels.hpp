@@ -86,6 +86,8 @@ hipError_t launch_import_ends(double2 *E, const double *ends, const Geometry &g,
 hipError_t launch_moments(const double2 *E, const double *mu, const double *wt, double *phi, double *F,
                           double *phi_plus, const Geometry &g, hipStream_t st);
 hipError_t launch_boundary_rows(const double2 *E, double2 *rows, const Geometry &g, hipStream_t st);
+// *flag |= 1 if any node of the N real rows of either half is not finite (flag zeroed by the caller)
+hipError_t launch_finite_scan(const double2 *E, int *flag, const Geometry &g, hipStream_t st);
 hipError_t launch_group_absorption(const double *phi, const double *sigma, double *out, const Geometry &g,
                                    hipStream_t st);
 

@@ -1303,6 +1303,21 @@ extern "C" rt_status rt_group_absorption_device(rt_solver *s, double *d_out) {
   return RT_OK;
 }
 
+extern "C" rt_status rt_state_finite(rt_solver *s, int *finite) {
+  if (!s || !finite) return fail(s, RT_ERR_ARG, "rt_state_finite: bad argument");
+  HIP_TRY(s, hipSetDevice(s->device));
+  rt_status st = finalize(s);  // the state at the requested time, exact
+  if (st) return st;
+  int *flag = static_cast<int *>(s->rows.p);  // scratch: the boundary-row buffer
+  HIP_TRY(s, hipMemsetAsync(flag, 0, sizeof(int), s->stream));
+  HIP_TRY(s, launch_finite_scan(static_cast<const double2 *>(s->E.p), flag, geometry(s), s->stream));
+  int h = 0;
+  HIP_TRY(s, hipMemcpyAsync(&h, flag, sizeof(int), hipMemcpyDeviceToHost, s->stream));
+  HIP_TRY(s, hipStreamSynchronize(s->stream));
+  *finite = h ? 0 : 1;
+  return RT_OK;
+}
+
 extern "C" rt_status rt_set_profiling(rt_solver *s, int on) {
   if (!s) return fail(nullptr, RT_ERR_ARG, "rt_set_profiling: NULL handle");
   rt_status st = fold_events(s);

@@ -101,6 +101,7 @@ def lib():
         L.rt_get_group_data.argtypes = [vp, dp, dp, dp, dp]
         L.rt_get_quadrature.argtypes = [vp, dp, dp]
         L.rt_set_profiling.argtypes = [vp, C.c_int]
+        L.rt_state_finite.argtypes = [vp, C.POINTER(C.c_int)]
         L.rt_get_sweep_time.argtypes = [vp, dp, C.POINTER(C.c_longlong)]
         L.rt_sweep_traffic.argtypes = [vp, dp, dp]
         L.rt_sweep_geometry.argtypes = [vp, C.POINTER(C.c_int), C.POINTER(C.c_longlong)]
@@ -377,6 +378,12 @@ class Solver:
                 raise ValueError("moments_device: need contiguous float64 CUDA tensors of N*G_local elements")
             ptrs.append(t.data_ptr())
         _check(lib().rt_get_moments_device(self._h, *ptrs), "rt_get_moments_device", self._h)
+
+    def state_finite(self) -> bool:
+        """rt_state_finite: every node of the state finite (NaN/Inf scan on the device)."""
+        f = C.c_int(0)
+        _check(lib().rt_state_finite(self._h, C.byref(f)), "rt_state_finite", self._h)
+        return bool(f.value)
 
     def group_absorption(self, out):
         """Group-summed absorption into a contiguous float64 torch tensor of N

@@ -103,6 +103,9 @@ class OracleShard:
     def compute_group_ends(self):
         return self.s.group_ends()
 
+    def state_finite(self):
+        return bool(np.isfinite(self.s.ends()).all())
+
     def compute_balance(self):
         return self.s.balance()
 

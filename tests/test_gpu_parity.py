@@ -238,6 +238,24 @@ def test_time_block_switching(rtsn_mod, oracle_mod, toggle):
         compare_all(gpu, orc)
 
 
+def test_state_finite_scan(rtsn_mod, oracle_mod):
+    """rt_state_finite (SURVEY §5 NaN/Inf scan): finite after llnl_slab_test; one NaN or
+    one Inf node anywhere (first / last cell, either half, a padding-adjacent line) is found."""
+    p = to_rt(load(oracle_mod, "llnl_slab_test.prm"))
+    with rtsn_mod.Solver(p) as s:
+        s.solve()
+        assert s.state_finite()
+        e = s.ends()
+        for idx, bad in (((0, 0, 0, 0), np.nan), ((1, 123, 49, 1), np.inf), ((1, 61, 0, 1), -np.inf),
+                         ((0, 5, 49, 0), np.nan)):
+            f = e.copy()
+            f[idx] = bad
+            s.set_ends(f)
+            assert not s.state_finite(), idx
+        s.set_ends(e)
+        assert s.state_finite()
+
+
 @pytest.mark.parametrize("ts", [1, 2, 3])
 def test_checkpoint_resume(rtsn_mod, oracle_mod, ts, tmp_path):
     """Checkpoint / resume: the state at a full-step boundary is the node
