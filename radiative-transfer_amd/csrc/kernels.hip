@@ -457,48 +457,44 @@ struct LineMap {
   }
 };
 
+// The reference-layout exports / import work on a chunk of cells [c0, c0 + nc) so the
+// device buffer stays small (rtsn_api.hip: kExportChunk doubles); chunk index
+// o = i + M (g + Gl (c - c0)) < M Gl nc < 2^31.
+
 // psi (M, Gl, N) ColMajor = mean of the nodes (solver.cpp:352,389)
-__global__ void export_psi_kernel(const double2 *E, double *psi, LineMap m) {
-  const size_t total = static_cast<size_t>(m.M) * m.Gl * m.N;
-  for (size_t o = blockIdx.x * static_cast<size_t>(blockDim.x) + threadIdx.x; o < total;
-       o += static_cast<size_t>(gridDim.x) * blockDim.x) {
-    const int i = static_cast<int>(o % m.M);
-    const int g = static_cast<int>((o / m.M) % m.Gl);
-    const int c = static_cast<int>(o / (static_cast<size_t>(m.M) * m.Gl));
+__global__ void export_psi_kernel(const double2 *E, double *psi, LineMap m, int c0, int nc) {
+  const int MG = m.M * m.Gl, total = MG * nc;
+  for (int o = blockIdx.x * blockDim.x + threadIdx.x; o < total; o += gridDim.x * blockDim.x) {
+    const int cl = o / MG, r = o - cl * MG, g = r / m.M, i = r - g * m.M;
     int half, ell, k;
-    m.map(i, g, c, half, ell, k);
+    m.map(i, g, c0 + cl, half, ell, k);
     const double2 v = E[m.at(half, k, ell)];
     psi[o] = 0.5 * (v.x + v.y);
   }
 }
 
-// ends (M, Gl, N, 2) ColMajor <-> E; node 0 = left, 1 = right
-__global__ void export_ends_kernel(const double2 *E, double *ends, LineMap m) {
-  const size_t mgn = static_cast<size_t>(m.M) * m.Gl * m.N;
-  for (size_t o = blockIdx.x * static_cast<size_t>(blockDim.x) + threadIdx.x; o < mgn;
-       o += static_cast<size_t>(gridDim.x) * blockDim.x) {
-    const int i = static_cast<int>(o % m.M);
-    const int g = static_cast<int>((o / m.M) % m.Gl);
-    const int c = static_cast<int>(o / (static_cast<size_t>(m.M) * m.Gl));
+// ends (M, Gl, N, 2) ColMajor <-> E; node 0 = left, 1 = right; the chunk buffer
+// holds node 0 of the chunk's cells, then node 1
+__global__ void export_ends_kernel(const double2 *E, double *ends, LineMap m, int c0, int nc) {
+  const int MG = m.M * m.Gl, total = MG * nc;
+  for (int o = blockIdx.x * blockDim.x + threadIdx.x; o < total; o += gridDim.x * blockDim.x) {
+    const int cl = o / MG, r = o - cl * MG, g = r / m.M, i = r - g * m.M;
     int half, ell, k;
-    m.map(i, g, c, half, ell, k);
+    m.map(i, g, c0 + cl, half, ell, k);
     const double2 v = E[m.at(half, k, ell)];
     ends[o] = half == 0 ? v.y : v.x;
-    ends[o + mgn] = half == 0 ? v.x : v.y;
+    ends[o + total] = half == 0 ? v.x : v.y;
   }
 }
 
-__global__ void import_ends_kernel(double2 *E, const double *ends, LineMap m) {
-  const size_t mgn = static_cast<size_t>(m.M) * m.Gl * m.N;
-  for (size_t o = blockIdx.x * static_cast<size_t>(blockDim.x) + threadIdx.x; o < mgn;
-       o += static_cast<size_t>(gridDim.x) * blockDim.x) {
-    const int i = static_cast<int>(o % m.M);
-    const int g = static_cast<int>((o / m.M) % m.Gl);
-    const int c = static_cast<int>(o / (static_cast<size_t>(m.M) * m.Gl));
+__global__ void import_ends_kernel(double2 *E, const double *ends, LineMap m, int c0, int nc) {
+  const int MG = m.M * m.Gl, total = MG * nc;
+  for (int o = blockIdx.x * blockDim.x + threadIdx.x; o < total; o += gridDim.x * blockDim.x) {
+    const int cl = o / MG, r = o - cl * MG, g = r / m.M, i = r - g * m.M;
     int half, ell, k;
-    m.map(i, g, c, half, ell, k);
-    const double l = ends[o], r = ends[o + mgn];
-    E[m.at(half, k, ell)] = half == 0 ? make_double2(r, l) : make_double2(l, r);
+    m.map(i, g, c0 + cl, half, ell, k);
+    const double l = ends[o], rr = ends[o + total];
+    E[m.at(half, k, ell)] = half == 0 ? make_double2(rr, l) : make_double2(l, rr);
   }
 }
 
@@ -986,21 +982,21 @@ static size_t resident_blocks(K kernel, int threads) {
 
 static LineMap make_map(const Geometry &g) { return LineMap{g.M, g.M / 2, g.Gl, g.N, g.Nrow, g.Lpad}; }
 
-hipError_t launch_export_psi(const double2 *E, double *psi, const Geometry &g, hipStream_t st) {
-  hipLaunchKernelGGL(export_psi_kernel, dim3(grid_for(static_cast<size_t>(g.M) * g.Gl * g.N, 256)), dim3(256), 0, st,
-                     E, psi, make_map(g));
+hipError_t launch_export_psi(const double2 *E, double *psi, const Geometry &g, int c0, int nc, hipStream_t st) {
+  hipLaunchKernelGGL(export_psi_kernel, dim3(grid_for(static_cast<size_t>(g.M) * g.Gl * nc, 256)), dim3(256), 0, st,
+                     E, psi, make_map(g), c0, nc);
   return hipGetLastError();
 }
 
-hipError_t launch_export_ends(const double2 *E, double *ends, const Geometry &g, hipStream_t st) {
-  hipLaunchKernelGGL(export_ends_kernel, dim3(grid_for(static_cast<size_t>(g.M) * g.Gl * g.N, 256)), dim3(256), 0, st,
-                     E, ends, make_map(g));
+hipError_t launch_export_ends(const double2 *E, double *ends, const Geometry &g, int c0, int nc, hipStream_t st) {
+  hipLaunchKernelGGL(export_ends_kernel, dim3(grid_for(static_cast<size_t>(g.M) * g.Gl * nc, 256)), dim3(256), 0, st,
+                     E, ends, make_map(g), c0, nc);
   return hipGetLastError();
 }
 
-hipError_t launch_import_ends(double2 *E, const double *ends, const Geometry &g, hipStream_t st) {
-  hipLaunchKernelGGL(import_ends_kernel, dim3(grid_for(static_cast<size_t>(g.M) * g.Gl * g.N, 256)), dim3(256), 0, st,
-                     E, ends, make_map(g));
+hipError_t launch_import_ends(double2 *E, const double *ends, const Geometry &g, int c0, int nc, hipStream_t st) {
+  hipLaunchKernelGGL(import_ends_kernel, dim3(grid_for(static_cast<size_t>(g.M) * g.Gl * nc, 256)), dim3(256), 0, st,
+                     E, ends, make_map(g), c0, nc);
   return hipGetLastError();
 }
 

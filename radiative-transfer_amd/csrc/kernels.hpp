@@ -80,9 +80,10 @@ hipError_t sweep_occupancy(int scheme, int T, int *waves_per_cu);
 hipError_t coupled_occupancy(int scheme, int *waves_per_cu);  // the material-coupled pass (T = 1)
 hipError_t launch_fold(int KC, const FoldArgs &f, hipStream_t st);
 hipError_t launch_init_state(double2 *E, const double *lineB, const Geometry &g, hipStream_t st);
-hipError_t launch_export_psi(const double2 *E, double *psi, const Geometry &g, hipStream_t st);
-hipError_t launch_export_ends(const double2 *E, double *ends, const Geometry &g, hipStream_t st);
-hipError_t launch_import_ends(double2 *E, const double *ends, const Geometry &g, hipStream_t st);
+// reference-layout psi / ends of the cells [c0, c0 + nc) (ends: node 0 block, then node 1)
+hipError_t launch_export_psi(const double2 *E, double *psi, const Geometry &g, int c0, int nc, hipStream_t st);
+hipError_t launch_export_ends(const double2 *E, double *ends, const Geometry &g, int c0, int nc, hipStream_t st);
+hipError_t launch_import_ends(double2 *E, const double *ends, const Geometry &g, int c0, int nc, hipStream_t st);
 hipError_t launch_moments(const double2 *E, const double *mu, const double *wt, double *phi, double *F,
                           double *phi_plus, const Geometry &g, hipStream_t st);
 hipError_t launch_boundary_rows(const double2 *E, double2 *rows, const Geometry &g, hipStream_t st);

@@ -1080,13 +1080,35 @@ extern "C" rt_status rt_get_dims(rt_solver *s, int *M, int *G_local, int *N, int
   return RT_OK;
 }
 
+// The reference-layout transfers go through a bounded device buffer, a chunk of cells
+// at a time (the layout's slowest index is the cell): kExportChunk doubles per node
+// block, so rt_get_psi / rt_get_ends / rt_set_ends need ~0.5 GB of device memory beside
+// the state instead of a full copy of it (65 / 131 GB on SL).
+constexpr size_t kExportChunk = size_t(1) << 25;  // doubles
+
+static int chunk_cells(const rt_solver *s) {
+  const size_t per_cell = static_cast<size_t>(s->p.M) * s->Gl;
+  size_t chunk = kExportChunk;
+  if (const char *env = std::getenv("RTSN_EXPORT_CHUNK")) chunk = std::max(1L, std::atol(env));  // tests
+  return static_cast<int>(std::max<size_t>(1, std::min<size_t>(s->p.N, chunk / per_cell)));
+}
+
+// nodes: 1 (psi) or 2 (ends, node 0 then node 1 in the host layout, MGN apart)
 template <typename F>
-static rt_status via_device(rt_solver *s, size_t count, double *host, F &&launch) {
+static rt_status export_chunks(rt_solver *s, int nodes, double *host, F &&launch) {
+  const size_t MG = static_cast<size_t>(s->p.M) * s->Gl, MGN = MG * s->p.N;
+  const int cc = chunk_cells(s);
   double *d = nullptr;
-  HIP_TRY(s, hipMalloc(reinterpret_cast<void **>(&d), sizeof(double) * count));
-  hipError_t e = launch(d);
-  if (e == hipSuccess) e = hipMemcpyAsync(host, d, sizeof(double) * count, hipMemcpyDeviceToHost, s->stream);
-  if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
+  HIP_TRY(s, hipMalloc(reinterpret_cast<void **>(&d), sizeof(double) * nodes * MG * cc));
+  hipError_t e = hipSuccess;
+  for (int c0 = 0; c0 < s->p.N && e == hipSuccess; c0 += cc) {
+    const int nc = std::min(cc, s->p.N - c0);
+    const size_t n = MG * nc;
+    e = launch(d, c0, nc);
+    for (int b = 0; b < nodes && e == hipSuccess; ++b)
+      e = hipMemcpyAsync(host + b * MGN + MG * c0, d + b * n, sizeof(double) * n, hipMemcpyDeviceToHost, s->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(s->stream);  // d is reused by the next chunk
+  }
   (void)hipFree(d);
   if (e != hipSuccess) return fail(s, RT_ERR_DEVICE, std::string("result transfer: ") + hipGetErrorString(e));
   return RT_OK;
@@ -1097,8 +1119,8 @@ extern "C" rt_status rt_get_psi(rt_solver *s, double *psi) {
   HIP_TRY(s, hipSetDevice(s->device));
   if (rt_status st = finalize(s)) return st;
   const Geometry g = geometry(s);
-  return via_device(s, static_cast<size_t>(g.M) * g.Gl * g.N, psi, [&](double *d) {
-    return launch_export_psi(static_cast<const double2 *>(s->E.p), d, g, s->stream);
+  return export_chunks(s, 1, psi, [&](double *d, int c0, int nc) {
+    return launch_export_psi(static_cast<const double2 *>(s->E.p), d, g, c0, nc, s->stream);
   });
 }
 
@@ -1107,8 +1129,8 @@ extern "C" rt_status rt_get_ends(rt_solver *s, double *ends) {
   HIP_TRY(s, hipSetDevice(s->device));
   if (rt_status st = finalize(s)) return st;
   const Geometry g = geometry(s);
-  return via_device(s, static_cast<size_t>(2) * g.M * g.Gl * g.N, ends, [&](double *d) {
-    return launch_export_ends(static_cast<const double2 *>(s->E.p), d, g, s->stream);
+  return export_chunks(s, 2, ends, [&](double *d, int c0, int nc) {
+    return launch_export_ends(static_cast<const double2 *>(s->E.p), d, g, c0, nc, s->stream);
   });
 }
 
@@ -1117,13 +1139,20 @@ extern "C" rt_status rt_set_ends(rt_solver *s, const double *ends) {
   HIP_TRY(s, hipSetDevice(s->device));
   if (rt_status st = complete(s)) return st;  // requested steps happen before the state is replaced
   const Geometry g = geometry(s);
-  const size_t n = static_cast<size_t>(2) * g.M * g.Gl * g.N;
+  const size_t MG = static_cast<size_t>(g.M) * g.Gl, MGN = MG * g.N;
+  const int cc = chunk_cells(s);
   double *d = nullptr;
-  HIP_TRY(s, hipMalloc(reinterpret_cast<void **>(&d), sizeof(double) * n));
-  hipError_t e = hipMemcpyAsync(d, ends, sizeof(double) * n, hipMemcpyHostToDevice, s->stream);
-  if (e == hipSuccess) e = launch_import_ends(static_cast<double2 *>(s->E.p), d, g, s->stream);
+  HIP_TRY(s, hipMalloc(reinterpret_cast<void **>(&d), sizeof(double) * 2 * MG * cc));
+  hipError_t e = hipSuccess;
+  for (int c0 = 0; c0 < g.N && e == hipSuccess; c0 += cc) {
+    const int nc = std::min(cc, g.N - c0);
+    const size_t n = MG * nc;
+    for (int b = 0; b < 2 && e == hipSuccess; ++b)
+      e = hipMemcpyAsync(d + b * n, ends + b * MGN + MG * c0, sizeof(double) * n, hipMemcpyHostToDevice, s->stream);
+    if (e == hipSuccess) e = launch_import_ends(static_cast<double2 *>(s->E.p), d, g, c0, nc, s->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(s->stream);  // d is reused by the next chunk
+  }
   s->pending = false;  // the loaded state is exact
-  if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
   (void)hipFree(d);
   if (e != hipSuccess) return fail(s, RT_ERR_DEVICE, std::string("rt_set_ends: ") + hipGetErrorString(e));
   return RT_OK;

@@ -238,6 +238,26 @@ def test_time_block_switching(rtsn_mod, oracle_mod, toggle):
         compare_all(gpu, orc)
 
 
+def test_chunked_transfers(rtsn_mod, oracle_mod, monkeypatch):
+    """rt_get_psi / rt_get_ends / rt_set_ends move the reference layouts through a bounded
+    device buffer, a chunk of cells at a time: with 1000-double chunks (4 cells of
+    llnl_slab_test's M G = 248, 13 chunks, the last one ragged) the results are bitwise
+    those of one chunk, and set_ends(ends()) is the identity."""
+    p = to_rt(load(oracle_mod, "llnl_slab_test.prm"))
+    with rtsn_mod.Solver(p) as s:
+        s.solve()
+        psi, ends = s.psi(), s.ends()
+        monkeypatch.setenv("RTSN_EXPORT_CHUNK", "1000")
+        assert np.array_equal(s.psi(), psi)
+        assert np.array_equal(s.ends(), ends)
+        s.set_ends(ends[..., ::-1].copy())  # nodes swapped: a different state, loaded in chunks
+        assert np.array_equal(s.ends(), ends[..., ::-1])
+        s.set_ends(ends)
+        monkeypatch.delenv("RTSN_EXPORT_CHUNK")
+        assert np.array_equal(s.ends(), ends)
+        assert np.array_equal(s.psi(), psi)
+
+
 def test_state_finite_scan(rtsn_mod, oracle_mod):
     """rt_state_finite (SURVEY §5 NaN/Inf scan): finite after llnl_slab_test; one NaN or
     one Inf node anywhere (first / last cell, either half, a padding-adjacent line) is found."""
