@@ -346,6 +346,9 @@ def run_rank(solver, p: dict, steps: int, warmup: int, world: int, device, shard
                     "frac": achieved / HBM_PEAK},
             "fp64": {"achieved": achieved_fl / 1e12, "peak": FP64_PEAK / 1e12, "unit": "TFLOP/s",
                      "frac": achieved_fl / FP64_PEAK},
+            "note": ("bound 'fp64': the time-blocked pass is FP64 vector-ALU bound (a per-line affine "
+                     "recurrence, no dense contraction, so no MFMA); the same pass at one step per "
+                     "pass is HBM-bound: see hbm_pass_t1") if tb > 1 else "HBM-bound pass",
         },
         "state_finite": finite,
     }
