@@ -10,5 +10,6 @@ timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_ou
 tail -2 gpurun_out/smoke.log
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_kt -o run --output-format csv -- python3 bench.py --no-cpu-baseline > gpurun_out/prof_kt.log 2>&1 || { tail -20 gpurun_out/prof_kt.log; exit 1; }
 cp gpurun_out/prof_kt/run_kernel_stats.csv gpurun_out/${TAG}_kernel_stats.csv
+python3 scripts/trace_summary.py gpurun_out/prof_kt/run_kernel_trace.csv gpurun_out/${TAG}_trace_summary.json
 timeout -k 10 600 python bench.py > gpurun_out/bench_full.log 2>&1 || { tail -20 gpurun_out/bench_full.log; exit 1; }
 tail -1 gpurun_out/bench_full.log | tee gpurun_out/${TAG}_bench.json
