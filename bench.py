@@ -362,10 +362,10 @@ def side_leg(p: dict, info, world: int, device, local: int, scaling: str, tb: in
     """A second sweep measurement on the same shard, reported beside `value` (never as
     it): the state is created fresh, the pipeline filled untimed, then two passes timed
     exactly as the headline.  Used for (a) the HBM-bound T = 1 pass (one HBM round trip
-    of the state per BDF2 step: the north_star's HBM-roofline view of the sweep) and (b)
+    of the state per BDF2 step: the north_star's HBM-roofline view of the sweep), (b)
     the finite-state control (dt = 1e-7: the reference's BDF2 stays bounded, so the
     timing of the headline -- whose state overflows, DESIGN.md §5 -- is shown to be
-    data-independent)."""
+    data-independent) and (c) the other SL variant (v/c correction on / inactive)."""
     import rtsn
     with rtsn.Solver(p, device=local, g_lo=info[1], g_hi=info[2]) as s:
         s.time_block = tb
@@ -503,6 +503,12 @@ def main():
         line["finite_control"] = side_leg(dict(pv, dt=1e-7), info, world, device, local, args.scaling,
                                           solver_tb, "same workload at dt=1e-7 (state stays finite): "
                                                      "timing control for the headline")
+        other = "corr" if args.variant == "v0" else "v0"
+        line[f"variant_{other}"] = side_leg(dict(slab_params(info[0], other, N=args.cells), variant=other), info,
+                                            world, device, local, args.scaling, solver_tb,
+                                            f"SURVEY §8(d) SL variant {other} (V = "
+                                            f"{5.994 if other == 'corr' else 0.0}, v/c correction "
+                                            f"{'on' if other == 'corr' else 'inactive'}), same timing")
     if args.material_steps > 0:
         line["material"] = run_material(p, info, world, device, local, args.material_steps)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
