@@ -242,6 +242,13 @@ def run_rank(solver, p: dict, steps: int, warmup: int, world: int, device, shard
     solver.synchronize()
     barrier()
     before = solver.pipeline_state()
+    # the pass the timed region runs, as rocprof names it: pipelined when the pipeline is
+    # filled, level-split (two waves per segment) for BDF2 at T = 8, 12, 16 unless disabled
+    if before["lag_steps"] > 0:
+        split = solver.level_waves == 2 and p.get("ts_method", 3) == 3 and tb in (8, 12, 16)
+        kernel_name = f"sweep_split_kernel<3, {tb}>" if split else f"sweep_block_kernel<3, {tb}, 2, false>"
+    else:
+        kernel_name = f"sweep_block_kernel<3, {tb}, 0, false>"
     solver.set_profiling(True)
     t0 = time.perf_counter()
     solver.advance(steps)
@@ -338,7 +345,7 @@ def run_rank(solver, p: dict, steps: int, warmup: int, world: int, device, shard
             "frac": achieved_fl / FP64_PEAK if tb > 1 else achieved / HBM_PEAK,
             "traffic": None,
             # the pass the timed region ran: pipelined (MODE 2) when the pipeline was filled
-            "kernel": f"sweep_block_kernel<3, {tb}, {2 if before['lag_steps'] > 0 else 0}, false>",
+            "kernel": kernel_name,
             "kernel_ms": kern_avg_ms,
             "algorithmic_flops_per_launch": flops_launch,
             "algorithmic_bytes_per_launch": bytes_launch,

@@ -185,6 +185,13 @@ rt_status rt_get_pipeline(rt_solver *s, int *on);
  * steps queued but not launched, whether a correction is pending; any NULL skipped. */
 rt_status rt_pipeline_state(rt_solver *s, long long *lag_steps, int *queued_steps, int *pending);
 rt_status rt_get_time_block(rt_solver *s, int *steps_per_pass);
+/* Waves per segment of a pipelined BDF2 pass of 8, 12 or 16 steps: 1 (default)
+ * runs all levels in one wave; 2 shares them between two waves of a workgroup
+ * through LDS, so a SIMD holds two waves instead of one (measured 4% slower on the
+ * SL pass; RTSN_LEVEL_WAVES=2 at creation also sizes the segments for
+ * it).  Bitwise-identical results.  Other passes always use one wave. */
+rt_status rt_set_level_waves(rt_solver *s, int waves);
+rt_status rt_get_level_waves(rt_solver *s, int *waves);
 /* Sweep geometry actually used: waves launched per step (one per line group
  * and segment) and segments per line. */
 rt_status rt_sweep_geometry(rt_solver *s, int *workgroups, long long *tiles);

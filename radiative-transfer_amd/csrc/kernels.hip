@@ -420,6 +420,226 @@ __global__ __launch_bounds__(64) void sweep_block_kernel(SegArgs a) {
 }
 
 // ------------------------------------------------------------------------
+// Level-split pipelined pass: the same launch as sweep_block_kernel<S, T, 2>
+// with its T levels shared by two waves of one workgroup.  Wave 0 runs
+// levels [0, T/2) of chunk j and hands the chunk's level-(T/2 - 1) nodes to
+// wave 1 through LDS (three buffers, one barrier per chunk); wave 1 runs
+// levels [T/2, T) of an earlier chunk and stores it.  Each wave then holds
+// half the carried states (X), so the kernel fits 256 registers and a SIMD
+// runs two waves instead of one -- the FP64 issue rate of one wave with
+// ILP <= 16 is ~59 TF, of two ~62-65 TF (profiles/r01_fp64_peak.txt).  Same
+// arithmetic in the same order per (cell, level) as the one-wave kernel:
+// bitwise equal.  Measured on the SL pass at T = 16: 140.6 ms vs 134.6 ms for
+// the one-wave kernel, so it is opt-in (rt_set_level_waves).
+// ------------------------------------------------------------------------
+template <int S, int TW, int C, bool FIRST, bool LAST>
+__device__ __forceinline__ void split_chunk(const double *W, double (&ein)[C], double (&eout)[C],
+                                            double (&X)[TW][SchemeDim<S>::K], bool head, double h_oi, double h_oo,
+                                            double2 *lds, __amdgpu_buffer_rsrc_t Rw,
+                                            __amdgpu_buffer_rsrc_t Rn, int voff, int row_bytes, int nv, int lane) {
+  constexpr int K = SchemeDim<S>::K;
+#pragma unroll
+  for (int c = 0; c < C; ++c) {
+    if (LAST && c >= nv) continue;  // wave-uniform: past the end of the segment
+    double oi = ein[c], oo = eout[c];
+    if (c == 0 && head) {  // reflective head cell, computed in the prologue
+      oi = h_oi;
+      oo = h_oo;
+    } else {
+#pragma unroll
+      for (int t = 0; t < TW; ++t) {
+        double Xn[K], a, e;
+        map_apply<S, true>(W, X[t], oi, oo, Xn, a, e);
+#pragma unroll
+        for (int r = 0; r < K; ++r) X[t][r] = Xn[r];
+        oi = a;
+        oo = e;
+      }
+    }
+    if constexpr (FIRST) {  // hand the nodes to the second wave; refill from HBM
+      lds[c * 64 + lane] = make_double2(oi, oo);
+      if constexpr (!LAST) {
+        const double2 v = row_load(Rn, voff, c * row_bytes);
+        ein[c] = v.x;
+        eout[c] = v.y;
+      }
+    } else {  // store; refill from the next chunk's level-(TW - 1) nodes
+      row_store(Rw, voff, c * row_bytes, oi, oo);
+      if constexpr (!LAST) {
+        const double2 v = lds[c * 64 + lane];
+        ein[c] = v.x;
+        eout[c] = v.y;
+      }
+    }
+  }
+}
+
+// One wave's role: FIRST = levels [0, T/2), else [T/2, T).  The two roles are
+// compile-time instantiation: with the role a runtime (wave-uniform) branch
+// inside one body the allocation measured ~340 registers, each role alone ~215.
+template <int S, int T, bool FIRST>
+__device__ __forceinline__ void split_role(const SegArgs &a, double2 (*hand)[split_chunk_cells() * 64], double2 *hhead) {
+  constexpr int K = SchemeDim<S>::K;
+  constexpr int TW = T / 2;
+  constexpr int WN = map_count<S>();
+  constexpr int C = split_chunk_cells();
+  const int lane = threadIdx.x & 63;
+  constexpr int t0 = FIRST ? 0 : TW;  // this wave's first level
+  const size_t stride = static_cast<size_t>(a.Lpad);
+  int half, s, q, pos;
+  if (a.reflective) {
+    pos = a.pos_lo + static_cast<int>(blockIdx.x) / a.Q;
+    q = static_cast<int>(blockIdx.x) % a.Q;
+    half = pos / a.Sg;
+    s = pos % a.Sg;
+  } else {
+    const int per_half = a.Q * a.npos;
+    half = static_cast<int>(blockIdx.x) / per_half;
+    const int rem = static_cast<int>(blockIdx.x) % per_half;
+    pos = a.pos_lo + rem / a.Q;
+    q = rem % a.Q;
+    s = pos;
+  }
+  const int slot = (a.pass_lo - (pos - a.pos_lo)) & 1;
+  const int ell = q * 64 + lane;
+  const bool neg = half == 0;
+  const int k_begin = s * a.Ls;
+  const int k_end = min(a.N, k_begin + a.Ls);
+  if (k_begin >= k_end) return;  // workgroup-uniform
+  const size_t seg_stride = static_cast<size_t>(T * K) * stride;
+  const size_t half_stride = static_cast<size_t>(a.Sg) * seg_stride;
+
+  // ---- inflow and carried state of this wave's levels ----
+  const bool head_seg = (s == 0);
+  double b[TW][4];
+  {
+    const double v = a.bdry[static_cast<size_t>(half) * stride + ell];
+#pragma unroll
+    for (int t = 0; t < TW; ++t) b[t][0] = b[t][1] = b[t][2] = b[t][3] = v;
+  }
+  const bool refl_head = head_seg && !neg && a.reflective;
+  if (refl_head) {  // solver.cpp:677-684, as in sweep_block_kernel (MODE 2)
+    const double *src = a.aggs[slot] + (a.Sg - 1) * seg_stride + ell;
+#pragma unroll
+    for (int t = 0; t < TW; ++t) {
+      if constexpr (S == SCHEME_BDF2) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) b[t][r] = src[((t0 + t) * K + 1 + r) * stride];
+      } else {
+        b[t][0] = b[t][1] = b[t][2] = b[t][3] = src[((t0 + t) * K + K - 1) * stride];
+      }
+    }
+  }
+  double X[TW][K];
+  if (head_seg) {
+#pragma unroll
+    for (int t = 0; t < TW; ++t) head_state<S>(b[t], X[t]);
+  } else {
+    const double *up = a.aggs[slot] + half * half_stride + (s - 1) * seg_stride + ell;
+#pragma unroll
+    for (int t = 0; t < TW; ++t)
+#pragma unroll
+      for (int r = 0; r < K; ++r) X[t][r] = up[((t0 + t) * K + r) * stride];
+  }
+
+  // ---- rows: the first wave streams them in, the second stores them ----
+  const int row_bytes = a.Lpad * static_cast<int>(sizeof(double2));
+  const int voff = lane * static_cast<int>(sizeof(double2));
+  const double2 *Eh = a.E + static_cast<size_t>(half) * a.Nrow * stride + q * 64;
+  auto rows = [&](int k0) { return rows_rsrc<C>(Eh + static_cast<size_t>(k0) * stride, row_bytes); };
+  double ein[C], eout[C];
+  if constexpr (FIRST) {
+    const __amdgpu_buffer_rsrc_t R0 = rows(k_begin);
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      const double2 v = row_load(R0, voff, c * row_bytes);
+      ein[c] = v.x;
+      eout[c] = v.y;
+    }
+  } else {
+#pragma unroll
+    for (int c = 0; c < C; ++c) ein[c] = eout[c] = 0.0;
+  }
+  // reflective head cell: levels [0, TW) on the loaded row, [TW, T) on their result
+  double h_oi = 0.0, h_oo = 0.0;
+  if (refl_head) {  // workgroup-uniform: both waves reach the barrier
+    const double *lcp = a.lc + static_cast<size_t>(half) * LC_COUNT * stride + ell;
+    if constexpr (FIRST) {
+      h_oi = ein[0];
+      h_oo = eout[0];
+      head_cell<S, TW>(lcp, stride, a.hd, b, X, h_oi, h_oo, 1.0);
+      hhead[lane] = make_double2(h_oi, h_oo);
+    }
+    __syncthreads();
+    if constexpr (!FIRST) {
+      const double2 v = hhead[lane];
+      h_oi = v.x;
+      h_oo = v.y;
+      head_cell<S, TW>(lcp, stride, a.hd, b, X, h_oi, h_oo, 1.0);
+    }
+  }
+
+  double W[WN];
+#pragma unroll
+  for (int n = 0; n < WN; ++n) W[n] = a.map[(static_cast<size_t>(half) * WN + n) * stride + ell];
+
+  // Barrier interval j: the first wave runs chunk j and writes its nodes to
+  // hand[j % 3]; the second runs chunk j - 2 from registers while it refills
+  // them with chunk j - 1 (complete since the last barrier).  Each wave passes
+  // nch + 2 barriers (s_barrier counts waves, not program points).
+  auto store_aggregate = [&]() {
+    double *ag = a.aggs[slot] + half * half_stride + static_cast<size_t>(s) * seg_stride + ell;
+#pragma unroll
+    for (int t = 0; t < TW; ++t)
+#pragma unroll
+      for (int r = 0; r < K; ++r) ag[((t0 + t) * K + r) * stride] = X[t][r];
+  };
+  const int nch = (k_end - k_begin + C - 1) / C;
+  if constexpr (FIRST) {
+    int k0 = k_begin;
+    for (int jc = 0; jc + 1 < nch; ++jc, k0 += C) {
+      split_chunk<S, TW, C, true, false>(W, ein, eout, X, refl_head && jc == 0, h_oi, h_oo, hand[jc % 3], rows(k0),
+                                         rows(k0 + C), voff, row_bytes, C, lane);
+      __syncthreads();
+    }
+    split_chunk<S, TW, C, true, true>(W, ein, eout, X, refl_head && nch == 1, h_oi, h_oo, hand[(nch - 1) % 3],
+                                      rows(k0), rows(k0), voff, row_bytes, k_end - k0, lane);
+    store_aggregate();
+    __syncthreads();
+    __syncthreads();
+  } else {
+    __syncthreads();  // chunk 0 written
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      const double2 v = hand[0][c * 64 + lane];
+      ein[c] = v.x;
+      eout[c] = v.y;
+    }
+    __syncthreads();  // chunk 1 written (if any); hand[0] is read
+    int k0 = k_begin;
+    for (int jc = 0; jc + 1 < nch; ++jc, k0 += C) {
+      split_chunk<S, TW, C, false, false>(W, ein, eout, X, refl_head && jc == 0, h_oi, h_oo, hand[(jc + 1) % 3],
+                                          rows(k0), rows(k0), voff, row_bytes, C, lane);
+      __syncthreads();
+    }
+    split_chunk<S, TW, C, false, true>(W, ein, eout, X, refl_head && nch == 1, h_oi, h_oo, nullptr, rows(k0),
+                                       rows(k0), voff, row_bytes, k_end - k0, lane);
+    store_aggregate();
+  }
+}
+
+template <int S, int T>
+__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2, 2))) void sweep_split_kernel(SegArgs a) {
+  static_assert(T % 2 == 0, "levels split evenly over two waves");
+  __shared__ double2 hand[3][split_chunk_cells() * 64];  // chunk nodes at level T/2 - 1, chunk jc in hand[jc % 3]
+  __shared__ double2 hhead[64];                          // reflective head cell at level T/2 - 1
+  if (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) == 0)
+    split_role<S, T, true>(a, hand, hhead);
+  else
+    split_role<S, T, false>(a, hand, hhead);
+}
+
+// ------------------------------------------------------------------------
 // Non-hot kernels: state initialisation, layout conversion, moments
 // ------------------------------------------------------------------------
 // psi = ends = B_g (solver.cpp:165-181); padding rows k >= N are zero
@@ -869,6 +1089,12 @@ static hipError_t launch_t(int mode, const SegArgs &a, int grid, hipStream_t st)
     if (mode != SWEEP_FINALIZE) return hipErrorInvalidValue;  // the correction has no source term
   }
   if (mode == SWEEP_PIPELINED) {
+    if constexpr (level_split_supported(S, T)) {
+      if (a.level_waves == 2) {
+        hipLaunchKernelGGL((sweep_split_kernel<S, T>), dim3(grid), dim3(128), 0, st, a);
+        return hipGetLastError();
+      }
+    }
     hipLaunchKernelGGL((sweep_block_kernel<S, T, 2>), dim3(grid), dim3(64), 0, st, a);
     return hipGetLastError();
   }
@@ -924,7 +1150,17 @@ hipError_t launch_fold(int KC, const FoldArgs &f, hipStream_t st) {
 }
 
 template <int S>
-static hipError_t occupancy_s(int T, int *w) {
+static hipError_t occupancy_s(int T, int level_waves, int *w) {
+  if constexpr (level_split_supported(S, 16)) {  // workgroups (segments) per CU of the level-split pass
+    if (level_waves == 2) {
+      switch (T) {
+        case 8: return hipOccupancyMaxActiveBlocksPerMultiprocessor(w, sweep_split_kernel<S, 8>, 128, 0);
+        case 12: return hipOccupancyMaxActiveBlocksPerMultiprocessor(w, sweep_split_kernel<S, 12>, 128, 0);
+        case 16: return hipOccupancyMaxActiveBlocksPerMultiprocessor(w, sweep_split_kernel<S, 16>, 128, 0);
+        default: break;
+      }
+    }
+  }
   switch (T) {
     case 1: return hipOccupancyMaxActiveBlocksPerMultiprocessor(w, sweep_block_kernel<S, 1, 0>, 64, 0);
     case 2: return hipOccupancyMaxActiveBlocksPerMultiprocessor(w, sweep_block_kernel<S, 2, 0>, 64, 0);
@@ -941,11 +1177,11 @@ static hipError_t occupancy_s(int T, int *w) {
   }
 }
 
-hipError_t sweep_occupancy(int scheme, int T, int *waves_per_cu) {
+hipError_t sweep_occupancy(int scheme, int T, int level_waves, int *waves_per_cu) {
   switch (scheme) {
-    case SCHEME_BE: return occupancy_s<SCHEME_BE>(T, waves_per_cu);
-    case SCHEME_CN: return occupancy_s<SCHEME_CN>(T, waves_per_cu);
-    default: return occupancy_s<SCHEME_BDF2>(T, waves_per_cu);
+    case SCHEME_BE: return occupancy_s<SCHEME_BE>(T, level_waves, waves_per_cu);
+    case SCHEME_CN: return occupancy_s<SCHEME_CN>(T, level_waves, waves_per_cu);
+    default: return occupancy_s<SCHEME_BDF2>(T, level_waves, waves_per_cu);
   }
 }
 

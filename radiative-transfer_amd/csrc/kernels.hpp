@@ -22,6 +22,14 @@ constexpr int kSweepCells = RT_SWEEP_CELLS;             // segment lengths are m
 constexpr int chunk_cells(int S, int T) {
   return S == 3 && T >= 12 ? RT_CHUNK_BDF2_T12 : (S == 3 && T >= 2 ? RT_CHUNK_BDF2_T2 : RT_SWEEP_CELLS);
 }
+// pipelined passes whose T levels two waves can share (sweep_split_kernel):
+// BDF2, where the carried states (5 per level) are what overflows 256 registers
+constexpr bool level_split_supported(int S, int T) { return S == 3 && (T == 8 || T == 12 || T == 16); }
+// rows per chunk of the level-split pass (16 rows with T/2 = 8 levels spill past 256 registers)
+#ifndef RT_CHUNK_SPLIT
+#define RT_CHUNK_SPLIT 8
+#endif
+constexpr int split_chunk_cells() { return RT_CHUNK_SPLIT; }
 constexpr int kSweepTile = 64;                          // cells are padded to whole tiles of 64 rows
 
 constexpr int kMaxTimeBlock = 16;                       // full steps fused per pipelined pass (template range)
@@ -46,6 +54,7 @@ struct SegArgs {
   int reflective;             // bc_left == 2
   int pending;                // the stored state is provisional: apply the correction
   int pos_lo, npos, pass_lo;  // pipelined: active chain positions and the pass of the first
+  int level_waves;            // pipelined: 2 = T levels shared by two waves (sweep_split_kernel), else 1
   double hd;                  // dx / 2
   // material coupling (SWEEP_PASS, T = 1 only): per-cell emission B_g(T(x)),
   // [N][Gl] (g fastest), scaling the map constants stored for B = 1
@@ -76,7 +85,8 @@ enum SweepMode {
   SWEEP_PIPELINED = 2   // one launch of the staggered (pipelined) schedule
 };
 hipError_t launch_sweep(int scheme, int T, int mode, const SegArgs &a, int grid, hipStream_t st);
-hipError_t sweep_occupancy(int scheme, int T, int *waves_per_cu);
+// segments resident per CU (workgroups of the pass: one wave, or two with level_waves 2)
+hipError_t sweep_occupancy(int scheme, int T, int level_waves, int *waves_per_cu);
 hipError_t coupled_occupancy(int scheme, int *waves_per_cu);  // the material-coupled pass (T = 1)
 hipError_t launch_fold(int KC, const FoldArgs &f, hipStream_t st);
 hipError_t launch_init_state(double2 *E, const double *lineB, const Geometry &g, hipStream_t st);

@@ -51,6 +51,7 @@ struct rt_solver {
   int T = 1;                     // full steps fused per pass (time block)
   int Tp = 0;                    // steps of the pass whose correction is pending
   int Sg = 1, Ls = 16;           // segments per line and cells per segment
+  int level_waves = 1;           // pipelined BDF2 passes: 2 = levels shared by two waves (RTSN_LEVEL_WAVES=2)
   int device = 0, cus = 0;
   hipStream_t stream = nullptr;
   // device state
@@ -575,7 +576,8 @@ extern "C" rt_status rt_create_from_params(const rt_params *pin, int g_lo, int g
   h->T = default_time_block(h->scheme);
   if (const char *t = std::getenv("RTSN_TIME_BLOCK"))  // experiments: the segment count follows
     if (supported_time_block(std::atoi(t))) h->T = std::atoi(t);
-  HIP_TRY(h, sweep_occupancy(h->scheme, h->T, &waves_per_cu));
+  if (const char *lw = std::getenv("RTSN_LEVEL_WAVES")) h->level_waves = std::atoi(lw) == 1 ? 1 : 2;
+  HIP_TRY(h, sweep_occupancy(h->scheme, h->T, h->level_waves, &waves_per_cu));
   // tuning knob for experiments: target resident waves per CU (segments per line follow)
   if (const char *w = std::getenv("RTSN_WAVES_PER_CU")) waves_per_cu = std::atoi(w);
   h->cus = prop.multiProcessorCount;
@@ -673,6 +675,7 @@ static SegArgs seg_args(rt_solver *s) {
   a.reflective = s->p.bc_left_indicator == 2;
   a.pending = s->pending ? 1 : 0;
   a.hd = 0.5 * (s->p.X / s->p.N);
+  a.level_waves = s->level_waves;
   return a;
 }
 
@@ -1425,6 +1428,19 @@ extern "C" rt_status rt_set_time_block(rt_solver *s, int steps_per_pass) {
 extern "C" rt_status rt_get_time_block(rt_solver *s, int *steps_per_pass) {
   if (!s || !steps_per_pass) return fail(s, RT_ERR_ARG, "rt_get_time_block: bad argument");
   *steps_per_pass = s->T;
+  return RT_OK;
+}
+
+extern "C" rt_status rt_set_level_waves(rt_solver *s, int waves) {
+  if (!s) return fail(nullptr, RT_ERR_ARG, "rt_set_level_waves: NULL handle");
+  if (waves != 1 && waves != 2) return fail(s, RT_ERR_PARAM, "rt_set_level_waves: 1 or 2");
+  s->level_waves = waves;  // segments stay as created: the schedule is exact for any segmentation
+  return RT_OK;
+}
+
+extern "C" rt_status rt_get_level_waves(rt_solver *s, int *waves) {
+  if (!s || !waves) return fail(s, RT_ERR_ARG, "rt_get_level_waves: bad argument");
+  *waves = s->level_waves;
   return RT_OK;
 }
 

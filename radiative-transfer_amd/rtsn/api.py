@@ -108,9 +108,11 @@ def lib():
         L.rt_sweep_flops.argtypes = [vp, dp]
         L.rt_set_time_block.argtypes = [vp, C.c_int]
         L.rt_set_pipeline.argtypes = [vp, C.c_int]
+        L.rt_set_level_waves.argtypes = [vp, C.c_int]
         L.rt_get_pipeline.argtypes = [vp, C.POINTER(C.c_int)]
         L.rt_pipeline_state.argtypes = [vp, C.POINTER(C.c_longlong), C.POINTER(C.c_int), C.POINTER(C.c_int)]
         L.rt_get_time_block.argtypes = [vp, C.POINTER(C.c_int)]
+        L.rt_get_level_waves.argtypes = [vp, C.POINTER(C.c_int)]
         L.rt_material_enable.argtypes = [vp, C.c_double, dp]
         L.rt_material_sweep.argtypes = [vp, vp]
         L.rt_material_update.argtypes = [vp, vp]
@@ -458,6 +460,17 @@ class Solver:
     @time_block.setter
     def time_block(self, steps_per_pass: int):
         _check(lib().rt_set_time_block(self._h, int(steps_per_pass)), "rt_set_time_block", self._h)
+
+    @property
+    def level_waves(self) -> int:
+        """Waves per segment of a pipelined BDF2 pass of 8/12/16 steps (rt_set_level_waves)."""
+        v = C.c_int()
+        _check(lib().rt_get_level_waves(self._h, C.byref(v)), "rt_get_level_waves", self._h)
+        return v.value
+
+    @level_waves.setter
+    def level_waves(self, waves: int):
+        _check(lib().rt_set_level_waves(self._h, int(waves)), "rt_set_level_waves", self._h)
 
     @property
     def pipeline(self) -> int:

@@ -437,3 +437,53 @@ def test_full_length_sl_line(rtsn_mod, sl_line_oracle, pipe, tb):
         phi_g, F_g, _ = gpu.moments()
         phi_o, F_o, _ = orc.moments()
         assert per_group_rel(phi_g, phi_o, 0) <= TOL
+
+
+@pytest.mark.parametrize("tb", [8, 12, 16])
+@pytest.mark.parametrize("bc_left", [0, 2])
+def test_level_split_pass(rtsn_mod, oracle_mod, monkeypatch, tb, bc_left):
+    """The level-split pipelined pass (sweep_split_kernel: the T levels of a BDF2 pass
+    shared by two waves through LDS, the default for T = 8, 12, 16) is bitwise the
+    one-wave pass (rt_set_level_waves 1, and RTSN_LEVEL_WAVES=1 at creation, whose
+    segment count follows the one-wave occupancy) -- same arithmetic per (cell, level)
+    -- over 3 T + 1 steps (fill, steady state, drain, an aligned remainder), and matches
+    the oracle over T + 3 steps (the reference's BDF2 grows the random state so fast
+    that longer runs amplify rounding past 1e-10); ragged lines (N = 4099:
+    a short last chunk in the last segment), reflective head included."""
+    def setup(steps):
+        p = load(oracle_mod, "llnl_slab_test.prm", N=4099, M=4, max_timesteps=steps, use_correction=1, V=5.994,
+                 bc_left=bc_left)
+        p["dx"] = p["X"] / p["N"]
+        p["psi_source"] = np.full((p["M"], p["G"]), 0.5)
+        return p
+
+    lo, hi = 30, 46
+    p = setup(3 * tb + 1)
+    orc = oracle_mod.OracleSolver(setup(tb + 3), g_lo=lo, g_hi=hi)
+    B = orc.groups()["B"][lo:hi]
+    rng = np.random.default_rng(SEED + 7 * tb + bc_left)
+    ends = B[None, :, None, None] * rng.uniform(0.5, 1.5, size=(p["M"], hi - lo, p["N"], 2))
+    orc.set_ends(ends)
+    orc.solve()
+    out = {}
+    for env, lw in (("1", 1), ("2", 2), ("2", 1)):
+        monkeypatch.setenv("RTSN_LEVEL_WAVES", env)
+        with rtsn_mod.Solver(to_rt(p), g_lo=lo, g_hi=hi) as gpu:
+            assert gpu.level_waves == int(env)
+            gpu.level_waves = lw
+            with pytest.raises(rtsn_mod.RtError):
+                gpu.level_waves = 3
+            gpu.time_block = tb
+            gpu.pipeline = 2
+            _, segs = gpu.sweep_geometry()
+            assert segs > 2
+            gpu.set_ends(ends)
+            gpu.solve()
+            out[env, lw] = gpu.ends()
+            if lw == 2:
+                assert np.array_equal(out["1", 1], out["2", 2])
+                gpu.set_ends(ends)
+                gpu.advance(tb + 3)
+                compare_all(gpu, orc, plus_vs_group=True)
+    monkeypatch.delenv("RTSN_LEVEL_WAVES")
+    assert np.array_equal(out["2", 1], out["2", 2])
