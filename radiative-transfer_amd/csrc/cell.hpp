@@ -171,6 +171,7 @@ __host__ __device__ __forceinline__ void cell_step_maybe_head(const LineConst &L
 
 // Index of (r, c), c <= r, in a packed lower triangle.
 __host__ __device__ __forceinline__ constexpr int tri(int r, int c) { return r * (r + 1) / 2 + c; }
+__host__ __device__ __forceinline__ constexpr int tri_count(int K) { return K * (K + 1) / 2; }
 
 // ---------------------------------------------------------------------------
 // The cell step as a per-line affine map.

@@ -1004,26 +1004,96 @@ __global__ __launch_bounds__(256) void planck_cells_kernel(PlanckCells pc, const
 // group_sums stores the sums of w (d_in + d_out)/2 to phic[half][x][g]
 // (segment 0 cells, exact, are never written: zero).  The stored state keeps
 // its correction pending (the next pass or a finalize applies it).
+// A^L of every line's correction propagator (the map's linear X -> X' block, lower
+// triangular: X'_r reads X_0..X_r), packed lower triangle [half][tri_count(K)][Lpad],
+// by binary powering; one thread per (half, line).
 template <int S>
-__global__ __launch_bounds__(64) void phi_correction_kernel(SegArgs a) {
+__global__ void correction_power_kernel(const double *map, double *pow, int L, int Lpad) {
+  constexpr int K = SchemeDim<S>::K;
+  constexpr int WN = map_count<S>();
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= 2 * Lpad) return;
+  const int half = idx / Lpad, ell = idx % Lpad;
+  const size_t stride = static_cast<size_t>(Lpad);
+  double W[WN];
+#pragma unroll
+  for (int n = 0; n < WN; ++n) W[n] = map[(static_cast<size_t>(half) * WN + n) * stride + ell];
+  double A[tri_count(K)], P[tri_count(K)];
+#pragma unroll
+  for (int c = 0; c < K; ++c) {  // column c of A: the map's linear part on unit input c
+    double e[K], Zn[K], di, dd;
+#pragma unroll
+    for (int r = 0; r < K; ++r) e[r] = r == c ? 1.0 : 0.0;
+    map_apply<S, false>(W, e, 0.0, 0.0, Zn, di, dd);
+#pragma unroll
+    for (int r = c; r < K; ++r) A[tri(r, c)] = Zn[r];
+  }
+#pragma unroll
+  for (int r = 0; r < K; ++r)
+#pragma unroll
+    for (int c = 0; c <= r; ++c) P[tri(r, c)] = r == c ? 1.0 : 0.0;
+  auto mul = [&](double (&X)[tri_count(K)], const double (&Y)[tri_count(K)]) {  // X = X Y
+    double R[tri_count(K)];
+#pragma unroll
+    for (int r = 0; r < K; ++r)
+#pragma unroll
+      for (int c = 0; c <= r; ++c) {
+        double acc = 0.0;
+#pragma unroll
+        for (int m = c; m <= r; ++m) acc = fma(X[tri(r, m)], Y[tri(m, c)], acc);
+        R[tri(r, c)] = acc;
+      }
+#pragma unroll
+    for (int n = 0; n < tri_count(K); ++n) X[n] = R[n];
+  };
+  for (int e = L; e > 0; e >>= 1) {
+    if (e & 1) mul(P, A);
+    if (e > 1) mul(A, A);
+  }
+  double *out = pow + static_cast<size_t>(half) * tri_count(K) * stride + ell;
+#pragma unroll
+  for (int n = 0; n < tri_count(K); ++n) out[n * stride] = P[n];
+}
+
+template <int S>
+__global__ __launch_bounds__(64) void phi_correction_kernel(SegArgs a, int nsub, int Lsub, const double *pow) {
   constexpr int K = SchemeDim<S>::K;
   constexpr int WN = map_count<S>();
   constexpr int C = 16;
-  __shared__ double tile[kGroupTileMax];
+  extern __shared__ double tile[];  // C rows of group_tile_row(H) (launch_phi_correction)
   const int lane = threadIdx.x;
   const size_t stride = static_cast<size_t>(a.Lpad);
-  const int per_half = a.Q * a.Sg;
+  // block -> (half, segment, sub-segment, line group)
+  const int per_half = a.Q * a.Sg * nsub;
   const int half = static_cast<int>(blockIdx.x) / per_half;
-  const int rem = static_cast<int>(blockIdx.x) % per_half;
-  const int s = rem / a.Q, q = rem - s * a.Q;
+  int rem = static_cast<int>(blockIdx.x) % per_half;
+  const int q = rem % a.Q;
+  rem /= a.Q;
+  const int j = rem % nsub, s = rem / nsub;
   const int ell = q * 64 + lane;
   const bool neg = half == 0;
-  const int k_begin = s * a.Ls, k_end = min(a.N, k_begin + a.Ls);
+  const int seg_end = min(a.N, s * a.Ls + a.Ls);
+  const int k_begin = s * a.Ls + j * Lsub, k_end = min(seg_end, k_begin + Lsub);
   if (s == 0 || k_begin >= k_end) return;  // segment 0 starts exact
   double Z[K];
   const double *y = a.yseg + (static_cast<size_t>(half) * (a.Sg + 1) + s) * K * stride + ell;
 #pragma unroll
   for (int r = 0; r < K; ++r) Z[r] = y[r * stride];
+  if (j > 0) {  // the state entering sub-segment j: (A^Lsub)^j Z (pow: packed lower triangle)
+    const double *pw = pow + static_cast<size_t>(half) * tri_count(K) * stride + ell;
+    double P[tri_count(K)];
+#pragma unroll
+    for (int n = 0; n < tri_count(K); ++n) P[n] = pw[n * stride];
+    for (int i = 0; i < j; ++i) {
+#pragma unroll
+      for (int r = K - 1; r >= 0; --r) {  // in place, rows from the bottom (lower triangular)
+        double acc = 0.0;
+#pragma unroll
+        for (int m = 0; m <= r; ++m) acc = fma(P[tri(r, m)], Z[m], acc);
+        Z[r] = acc;
+      }
+    }
+  }
   double W[WN];
 #pragma unroll
   for (int n = 0; n < WN; ++n) W[n] = a.map[(static_cast<size_t>(half) * WN + n) * stride + ell];
@@ -1276,11 +1346,23 @@ hipError_t launch_planck_cells(const PlanckCells &pc, const double *T, double *B
   return hipGetLastError();
 }
 
-hipError_t launch_phi_correction(int scheme, const SegArgs &a, int grid, hipStream_t st) {
+hipError_t launch_correction_power(int scheme, const double *map, double *pow, int L, int Lpad, hipStream_t st) {
+  const dim3 grid((2 * Lpad + 255) / 256), block(256);
   switch (scheme) {
-    case SCHEME_BE: hipLaunchKernelGGL(phi_correction_kernel<SCHEME_BE>, dim3(grid), dim3(64), 0, st, a); break;
-    case SCHEME_CN: hipLaunchKernelGGL(phi_correction_kernel<SCHEME_CN>, dim3(grid), dim3(64), 0, st, a); break;
-    default: hipLaunchKernelGGL(phi_correction_kernel<SCHEME_BDF2>, dim3(grid), dim3(64), 0, st, a); break;
+    case SCHEME_BE: hipLaunchKernelGGL(correction_power_kernel<SCHEME_BE>, grid, block, 0, st, map, pow, L, Lpad); break;
+    case SCHEME_CN: hipLaunchKernelGGL(correction_power_kernel<SCHEME_CN>, grid, block, 0, st, map, pow, L, Lpad); break;
+    default: hipLaunchKernelGGL(correction_power_kernel<SCHEME_BDF2>, grid, block, 0, st, map, pow, L, Lpad); break;
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_phi_correction(int scheme, const SegArgs &a, int nsub, int Lsub, const double *pow, hipStream_t st) {
+  const dim3 grid(static_cast<unsigned>(2LL * a.Q * a.Sg * nsub)), block(64);
+  const size_t lds = sizeof(double) * 16 * group_tile_row(a.H);
+  switch (scheme) {
+    case SCHEME_BE: hipLaunchKernelGGL(phi_correction_kernel<SCHEME_BE>, grid, block, lds, st, a, nsub, Lsub, pow); break;
+    case SCHEME_CN: hipLaunchKernelGGL(phi_correction_kernel<SCHEME_CN>, grid, block, lds, st, a, nsub, Lsub, pow); break;
+    default: hipLaunchKernelGGL(phi_correction_kernel<SCHEME_BDF2>, grid, block, lds, st, a, nsub, Lsub, pow); break;
   }
   return hipGetLastError();
 }

@@ -114,8 +114,13 @@ struct PlanckCells {
 };
 hipError_t launch_planck_cells(const PlanckCells &pc, const double *T, double *B, hipStream_t st);
 // the correction's share of the fused angular sums (SegArgs.phi) after a
-// coupled pass with segments started from X = 0 (T = 1; grid 2 Q Sg)
-hipError_t launch_phi_correction(int scheme, const SegArgs &a, int grid, hipStream_t st);
+// coupled pass with segments started from X = 0 (T = 1; each segment walked as
+// sub-segments, enough to fill the chip)
+// nsub sub-segments of Lsub cells per segment (Lsub a multiple of 16), each started from
+// pow^j applied to the segment's correction state, pow = A^Lsub (launch_correction_power)
+hipError_t launch_phi_correction(int scheme, const SegArgs &a, int nsub, int Lsub, const double *pow, hipStream_t st);
+// pow[half][K (K + 1) / 2][Lpad] = A^L, A the map's linear X -> X' block (lower triangular)
+hipError_t launch_correction_power(int scheme, const double *map, double *pow, int L, int Lpad, hipStream_t st);
 // q(x) = sum_g sigma_g (phi_g(x) - W B_g(x)) over the handle's groups, phi the
 // sum of nparts [N][Gl] arrays at phi (the fused parts, or one full phi)
 hipError_t launch_material_q(const double *phi, int nparts, const double *B, const double *sigma, double W, double *q,

@@ -72,6 +72,8 @@ struct rt_solver {
   bool material = false;
   double rho_cv = 0.0, wsum = 0.0;
   DeviceBuf Tcell, Bcell, qbuf, edges, map_unit, lc_unit, phi_part;
+  DeviceBuf corr_pow;            // A^Lsub per line for phi_correction_kernel's sub-segments
+  int corr_pow_L = 0;            // the Lsub it holds (0: none)
   bool phi_fused = false;        // angular sums fused into the coupled pass (M/2 divides 64)
   PlanckCells pc{};
   // profiling
@@ -1016,7 +1018,20 @@ extern "C" rt_status rt_material_sweep(rt_solver *s, double *d_q) {
       a.H = s->H;
       a.phic = static_cast<double *>(s->phi_part.p) + 2 * static_cast<size_t>(s->p.N) * s->Gl;
       a.wt = static_cast<const double *>(s->muwt.p) + s->p.M;
-      HIP_TRY(s, launch_phi_correction(s->scheme, a, 2 * s->Q * s->Sg, s->stream));
+      // the walk along a segment is a dependent chain: cut each segment into sub-segments
+      // (multiples of 16 cells) until the grid holds ~8 waves per SIMD
+      const long long segs = 2LL * s->Q * s->Sg;
+      const int nsub = static_cast<int>(
+          std::max<long long>(1, std::min<long long>((32LL * s->cus + segs - 1) / segs, s->Ls / 16)));
+      const int Lsub = ((s->Ls + nsub - 1) / nsub + 15) / 16 * 16;
+      if (nsub > 1 && s->corr_pow_L != Lsub) {
+        if (!s->corr_pow.p) HIP_TRY(s, dalloc(s->corr_pow, sizeof(double) * 2 * tri_count(s->K) * s->Lpad));
+        HIP_TRY(s, launch_correction_power(s->scheme, static_cast<const double *>(s->map.p),
+                                           static_cast<double *>(s->corr_pow.p), Lsub, s->Lpad, s->stream));
+        s->corr_pow_L = Lsub;
+      }
+      HIP_TRY(s, launch_phi_correction(s->scheme, a, nsub, Lsub, static_cast<const double *>(s->corr_pow.p),
+                                       s->stream));
     }
     HIP_TRY(s, launch_material_q(static_cast<const double *>(s->phi_part.p), s->pending ? 4 : 2, B, sig, s->wsum, q,
                                  s->Gl, s->p.N, s->stream));
