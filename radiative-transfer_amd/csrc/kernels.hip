@@ -1063,13 +1063,15 @@ __global__ __launch_bounds__(64) void phi_correction_kernel(SegArgs a, int nsub,
   extern __shared__ double tile[];  // C rows of group_tile_row(H) (launch_phi_correction)
   const int lane = threadIdx.x;
   const size_t stride = static_cast<size_t>(a.Lpad);
-  // block -> (half, segment, sub-segment, line group)
-  const int per_half = a.Q * a.Sg * nsub;
-  const int half = static_cast<int>(blockIdx.x) / per_half;
-  int rem = static_cast<int>(blockIdx.x) % per_half;
-  const int q = rem % a.Q;
-  rem /= a.Q;
-  const int j = rem % nsub, s = rem / nsub;
+  // block -> (piece t = (half, segment, sub-segment), line group q).  Workgroups go to the
+  // 8 XCDs round-robin by block index; all Q line groups of a piece share blockIdx % 8,
+  // so a cell's row of group sums (written by Q waves) is assembled in one XCD's L2.
+  const int xr = static_cast<int>(blockIdx.x) % kXcds, rest = static_cast<int>(blockIdx.x) / kXcds;
+  const int q = rest % a.Q;
+  const int t = (rest / a.Q) * kXcds + xr;
+  if (t >= 2 * a.Sg * nsub) return;  // padding of the piece count to a multiple of kXcds
+  const int half = t / (a.Sg * nsub);
+  const int j = t % nsub, s = (t / nsub) % a.Sg;
   const int ell = q * 64 + lane;
   const bool neg = half == 0;
   const int seg_end = min(a.N, s * a.Ls + a.Ls);
@@ -1357,7 +1359,8 @@ hipError_t launch_correction_power(int scheme, const double *map, double *pow, i
 }
 
 hipError_t launch_phi_correction(int scheme, const SegArgs &a, int nsub, int Lsub, const double *pow, hipStream_t st) {
-  const dim3 grid(static_cast<unsigned>(2LL * a.Q * a.Sg * nsub)), block(64);
+  const long long pieces = (2LL * a.Sg * nsub + kXcds - 1) / kXcds * kXcds;
+  const dim3 grid(static_cast<unsigned>(pieces * a.Q)), block(64);
   const size_t lds = sizeof(double) * 16 * group_tile_row(a.H);
   switch (scheme) {
     case SCHEME_BE: hipLaunchKernelGGL(phi_correction_kernel<SCHEME_BE>, grid, block, lds, st, a, nsub, Lsub, pow); break;

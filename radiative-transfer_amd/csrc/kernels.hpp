@@ -30,6 +30,7 @@ constexpr bool level_split_supported(int S, int T) { return S == 3 && (T == 8 ||
 #define RT_CHUNK_SPLIT 8
 #endif
 constexpr int split_chunk_cells() { return RT_CHUNK_SPLIT; }
+constexpr int kXcds = 8;                                // gfx950: workgroups are dealt to 8 XCDs round-robin
 constexpr int kSweepTile = 64;                          // cells are padded to whole tiles of 64 rows
 
 constexpr int kMaxTimeBlock = 16;                       // full steps fused per pipelined pass (template range)
