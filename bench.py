@@ -99,7 +99,13 @@ def cpu_baseline(variant: str) -> dict:
     u1, t1 = timed(64, 65, 1)
     cores = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", "16")), len(os.sched_getaffinity(0))))
     un, tn = timed(64 - cores // 2, 64 - cores // 2 + cores, cores)
+    model = "unknown"
+    try:  # name the host CPU the baseline ran on
+        model = next(l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name"))
+    except (OSError, StopIteration):
+        pass
     return {"value": un / tn, "unit": "cell-angle-group updates/s", "cores": cores, "kind": "port",
+            "cpu_model": model, "host_cpus": os.cpu_count(),
             "single_thread_value": u1 / t1,
             "sample": f"oracle/rt_oracle.c (restatement of solver.cpp, gcc -O2), SL {variant}: M=64, N={N}, "
                       f"1 BDF2 step; {cores} groups on {cores} OpenMP threads = {un:.3g} updates in {tn:.2f} s; "
