@@ -365,6 +365,14 @@ def run_rank(solver, p: dict, steps: int, warmup: int, world: int, device, shard
         },
         "state_finite": finite,
     }
+    # BASELINE.md's roofline definition for the north_star target (>= 0.5): updates/s per GPU
+    # x the unfused algorithm's minimal state bytes per update (48 B, 52 B with the
+    # v/c correction active) / 8.0 TB/s.  Above 1 means the fused pass moves fewer bytes per
+    # update than that algorithm could at the HBM peak.
+    b_upd = 52.0 if (p.get("use_correction") and p.get("V", 0.0) != 0.0) else 48.0
+    line["baseline_roofline"] = {
+        "definition": "BASELINE.md: updates/s per GPU x bytes/update / 8.0e12 B/s (unfused algorithm's bytes)",
+        "bytes_per_update": b_upd, "frac": value / world * b_upd / HBM_PEAK, "target": 0.5}
     if gather:
         line["gather"] = {"fields": "phi, F, phi_plus (N x G) + left/right ends, balance (G)",
                           "bytes_per_rank": 8 * 3 * p["N"] * (g_hi - g_lo), "ms": gather_ms}
