@@ -99,6 +99,17 @@ rt_status rt_create(const char *prm_path, const char *table_dir, int device, rt_
  * constant); all G groups' coefficients are still computed (the last Planck
  * group is a remainder, Planck.cpp:73-76).  g_hi <= 0 means G. */
 rt_status rt_create_from_params(const rt_params *p, int g_lo, int g_hi, int device, rt_solver **out);
+/* Direction-pair shard (SURVEY §8e fallback when there are fewer groups than GPUs):
+ * the handle sweeps only the direction pairs [d_lo, d_hi) of the M/2 (pair d = the
+ * directions mu_{H-1-d} < 0 and mu_{H+d} > 0, H = M/2; a line and its reflective
+ * mirror stay together), with the full quadrature's nodes and weights.  Its psi/ends
+ * cover M_l = 2 (d_hi - d_lo) directions in ascending mu; its moments and group ends
+ * are the partial sums over them (sum them over the shards: the reference's
+ * sequential sum over i then differs only by rounding); rt_get_balance* returns
+ * RT_ERR_PARAM.  Lines are independent given their inflow, so each line's psi is
+ * bitwise that of a full handle. */
+rt_status rt_create_direction_shard(const rt_params *p, int g_lo, int g_hi, int d_lo, int d_hi, int device,
+                                    rt_solver **out);
 void rt_destroy(rt_solver *s);
 
 /* Solver::solve (solver.cpp:590-823): max_timesteps full steps (x4 substeps

@@ -52,6 +52,8 @@ struct rt_solver {
   int Tp = 0;                    // steps of the pass whose correction is pending
   int Sg = 1, Ls = 16;           // segments per line and cells per segment
   int level_waves = 1;           // pipelined BDF2 passes: 2 = levels shared by two waves (RTSN_LEVEL_WAVES=2)
+  int d_lo = 0, d_hi = 0;        // direction-pair shard [d_lo, d_hi) of the M/2 pairs (d_hi = 0: all)
+  int M_full = 0;                // the configuration's M (p.M is the handle's own direction count)
   int device = 0, cus = 0;
   hipStream_t stream = nullptr;
   // device state
@@ -515,7 +517,27 @@ static hipError_t alloc_segments(rt_solver *h) {
 // ---------------------------------------------------------------------------
 // lifecycle
 // ---------------------------------------------------------------------------
+// Direction-pair shard [d_lo, d_hi) of the M/2 pairs (i' counted from mu = 0 outward):
+// the handle holds M_l = 2 (d_hi - d_lo) directions, global i in [H - d_hi, H - d_lo) and
+// [H + d_lo, H + d_hi) (ascending mu, mirror pairs together for the reflective BC), with
+// the full quadrature's nodes and weights and the prm psi_source rows of those directions.
+static rt_status create_impl(const rt_params *pin, int g_lo, int g_hi, int d_lo, int d_hi, int device,
+                             rt_solver **out);
+
 extern "C" rt_status rt_create_from_params(const rt_params *pin, int g_lo, int g_hi, int device, rt_solver **out) {
+  return create_impl(pin, g_lo, g_hi, 0, 0, device, out);
+}
+
+extern "C" rt_status rt_create_direction_shard(const rt_params *pin, int g_lo, int g_hi, int d_lo, int d_hi,
+                                               int device, rt_solver **out) {
+  if (!pin || !out) return fail(nullptr, RT_ERR_ARG, "rt_create_direction_shard: NULL argument");
+  if (pin->M > 0 && (d_lo < 0 || d_lo >= d_hi || d_hi > pin->M / 2))
+    return fail(nullptr, RT_ERR_PARAM, "bad direction-pair range (0 <= d_lo < d_hi <= M/2)");
+  return create_impl(pin, g_lo, g_hi, d_lo, d_hi, device, out);
+}
+
+static rt_status create_impl(const rt_params *pin, int g_lo, int g_hi, int d_lo, int d_hi, int device,
+                             rt_solver **out) {
   if (!pin || !out) return fail(nullptr, RT_ERR_ARG, "rt_create_from_params: NULL argument");
   *out = nullptr;
   const rt_params &q = *pin;
@@ -543,6 +565,29 @@ extern "C" rt_status rt_create_from_params(const rt_params *pin, int g_lo, int g
   s->mu.resize(q.M);
   s->wt.resize(q.M);
   phys::gauss_legendre(q.M, phys::kFourPi, s->mu.data(), s->wt.data());
+  s->M_full = q.M;
+  if (d_hi > 0 && !(d_lo == 0 && d_hi == q.M / 2)) {  // direction-pair shard: keep its directions
+    const int H = q.M / 2, n = d_hi - d_lo;
+    std::vector<int> keep;
+    for (int i = H - d_hi; i < H - d_lo; ++i) keep.push_back(i);
+    for (int i = H + d_lo; i < H + d_hi; ++i) keep.push_back(i);
+    std::vector<double> mu(2 * n), wt(2 * n), src;
+    for (int k = 0; k < 2 * n; ++k) {
+      mu[k] = s->mu[keep[k]];
+      wt[k] = s->wt[keep[k]];
+    }
+    if (!s->prm_psi_source.empty())  // rows m of the prm's (M, G) table, index m G + g
+      for (int k = 0; k < 2 * n; ++k)
+        src.insert(src.end(), s->prm_psi_source.begin() + static_cast<size_t>(keep[k]) * q.G,
+                   s->prm_psi_source.begin() + static_cast<size_t>(keep[k] + 1) * q.G);
+    s->mu.swap(mu);
+    s->wt.swap(wt);
+    s->prm_psi_source.swap(src);
+    s->p.psi_source = s->prm_psi_source.empty() ? nullptr : s->prm_psi_source.data();
+    s->p.M = 2 * n;
+    s->d_lo = d_lo;
+    s->d_hi = d_hi;
+  }
   phys::solver_psi_source(s->p, s->gt, s->mu.data(), s->psi_source);
   if (q.use_mg_equilib) {  // only the ph copy until solve() (solver.cpp:601-604)
     rt_params pre = s->p;
@@ -553,7 +598,7 @@ extern "C" rt_status rt_create_from_params(const rt_params *pin, int g_lo, int g
   s->g_lo = g_lo;
   s->g_hi = g_hi;
   s->Gl = g_hi - g_lo;
-  s->H = q.M / 2;
+  s->H = s->p.M / 2;
   s->Lh = s->H * s->Gl;
   s->Q = (s->Lh + 63) / 64;
   s->Lpad = 64 * s->Q;
@@ -601,7 +646,7 @@ extern "C" rt_status rt_create_from_params(const rt_params *pin, int g_lo, int g
   if (!e) e = alloc_segments(h);
   if (!e) e = dalloc(h->yrefl, sizeof(double) * kMaxAlignedBlock * K * Lp);
   if (!e) e = dalloc(h->lineB, sizeof(double) * 2 * Lp);
-  if (!e) e = dalloc(h->muwt, sizeof(double) * 2 * q.M);
+  if (!e) e = dalloc(h->muwt, sizeof(double) * 2 * h->p.M);
   if (!e) e = dalloc(h->mom, sizeof(double) * 3 * h->Gl * static_cast<size_t>(q.N));
   if (!e) e = dalloc(h->rows, sizeof(double2) * 4 * Lp);
   if (!e) e = dalloc(h->sigma, sizeof(double) * h->Gl);
@@ -1264,6 +1309,9 @@ extern "C" rt_status rt_get_group_ends(rt_solver *s, double *left, double *right
 
 extern "C" rt_status rt_get_balance_terms(rt_solver *s, double *balance, double *sources_out, double *sinks_out) {
   if (!s) return fail(s, RT_ERR_ARG, "rt_get_balance_terms: NULL handle");
+  if (s->d_hi > 0)  // its emission/absorption terms need phi over all directions
+    return fail(s, RT_ERR_PARAM, "rt_get_balance_terms: a direction shard holds part of phi; sum the shards' "
+                                 "moments and group ends, then balance on the totals");
   HIP_TRY(s, hipSetDevice(s->device));
   const int N = s->p.N, Gl = s->Gl;
   std::vector<double> phi(static_cast<size_t>(Gl) * N);

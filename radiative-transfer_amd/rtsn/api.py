@@ -82,6 +82,8 @@ def lib():
         L.rt_planck_groups.argtypes = [C.c_double, C.c_int, dp, dp, dp]
         L.rt_create.argtypes = [C.c_char_p, C.c_char_p, C.c_int, C.POINTER(vp)]
         L.rt_create_from_params.argtypes = [C.POINTER(rt_params), C.c_int, C.c_int, C.c_int, C.POINTER(vp)]
+        L.rt_create_direction_shard.argtypes = [C.POINTER(rt_params), C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                                C.POINTER(vp)]
         L.rt_destroy.argtypes = [vp]
         L.rt_destroy.restype = None
         for name in ("rt_solve", "rt_synchronize", "rt_finish"):
@@ -226,18 +228,24 @@ class Solver:
     are numpy arrays in the reference's index order: psi (M, G, N), phi / F /
     phi_plus (G, N), ends (M, G, N, 2)."""
 
-    def __init__(self, ph, device: int = 0, g_lo: int = 0, g_hi: int = 0):
+    def __init__(self, ph, device: int = 0, g_lo: int = 0, g_hi: int = 0, d_lo: int = 0, d_hi: int = 0):
+        """d_hi > 0: a direction-pair shard [d_lo, d_hi) of the M/2 pairs (rt_create_direction_shard)."""
         params = ph.params if isinstance(ph, ParameterHandler) else dict(ph)
         for k, v in params_default().items():
             params.setdefault(k, v)
         keep: list = []
         p = _to_struct(params, keep)
         h = C.c_void_p()
-        _check(lib().rt_create_from_params(C.byref(p), g_lo, g_hi, device, C.byref(h)), "rt_create_from_params")
+        if d_hi > 0:
+            _check(lib().rt_create_direction_shard(C.byref(p), g_lo, g_hi, d_lo, d_hi, device, C.byref(h)),
+                   "rt_create_direction_shard")
+        else:
+            _check(lib().rt_create_from_params(C.byref(p), g_lo, g_hi, device, C.byref(h)), "rt_create_from_params")
         self._h = h
         M, Gl, N, lo, hi = (C.c_int() for _ in range(5))
         lib().rt_get_dims(h, C.byref(M), C.byref(Gl), C.byref(N), C.byref(lo), C.byref(hi))
         self.M, self.G, self.N, self.g_lo, self.g_hi = M.value, Gl.value, N.value, lo.value, hi.value
+        self.d_lo, self.d_hi = (d_lo, d_hi) if d_hi > 0 else (0, self.M // 2)  # M: this handle's directions
         self.G_total = params["G"]
         self.params = params
         self._phi_plus = None

@@ -487,3 +487,51 @@ def test_level_split_pass(rtsn_mod, oracle_mod, monkeypatch, tb, bc_left):
                 compare_all(gpu, orc, plus_vs_group=True)
     monkeypatch.delenv("RTSN_LEVEL_WAVES")
     assert np.array_equal(out["2", 1], out["2", 2])
+
+
+@pytest.mark.parametrize("ts", [1, 2, 3])
+@pytest.mark.parametrize("bc_left,bc_right", [(2, 0), (1, 1), (0, 2)])
+def test_direction_shards(rtsn_mod, oracle_mod, ts, bc_left, bc_right):
+    """SURVEY §8e's fallback when there are fewer groups than GPUs: direction-pair shards
+    (rt_create_direction_shard).  Each shard's psi and ends are bitwise the full handle's
+    rows for its directions (lines are independent given their inflow; a reflective line
+    and its mirror share a shard), its quadrature is the full one's subset, and the
+    shards' moments and group ends sum to the full handle's (the reference's sequential
+    sum over i, regrouped: rounding only), here on multi_group_equilibrium (equilibrium
+    sources, v/c correction) with M = 8 cut into 1 + 2 + 1 pairs."""
+    p = load(oracle_mod, "multi_group_equilibrium.prm", N=700, M=8, max_timesteps=12, bc_left=bc_left,
+             bc_right=bc_right, ts_method=ts)
+    p["dx"] = p["X"] / p["N"]
+    p["psi_source"] = np.linspace(0.5, 2.0, p["M"] * p["G"]).reshape(p["M"], p["G"])
+    rp = to_rt(p)
+    with rtsn_mod.Solver(rp) as full:
+        full.solve()
+        psi_f, ends_f = full.psi(), full.ends()
+        mom_f = full.moments()
+        le_f, re_f = full.compute_group_ends()
+        mu_f, wt_f = full.quad()
+    H = p["M"] // 2
+    mom = [np.zeros_like(m) for m in mom_f]
+    le, re = np.zeros_like(le_f), np.zeros_like(re_f)
+    for lo, hi in ((0, 1), (1, 3), (3, 4)):
+        with rtsn_mod.Solver(rp, d_lo=lo, d_hi=hi) as s:
+            assert s.M == 2 * (hi - lo) and (s.d_lo, s.d_hi) == (lo, hi)
+            idx = list(range(H - hi, H - lo)) + list(range(H + lo, H + hi))
+            mu, wt = s.quad()
+            assert np.array_equal(mu, mu_f[idx]) and np.array_equal(wt, wt_f[idx])
+            s.solve()
+            assert np.array_equal(s.psi(), psi_f[idx])
+            assert np.array_equal(s.ends(), ends_f[idx])
+            for acc, m in zip(mom, s.moments()):
+                acc += m
+            l_s, r_s = s.compute_group_ends()
+            le += l_s
+            re += r_s
+            with pytest.raises(rtsn_mod.RtError):
+                s.compute_balance()
+    for name, a, b in zip(("phi", "F", "phi_plus"), mom, mom_f):
+        scale = np.abs(psi_f).max(axis=(0, 2)) * 4.0 * np.pi  # per group: the sums' summand scale
+        err = (np.abs(a - b).max(axis=1) / scale).max()
+        assert err <= 1e-13, (name, err)
+    for a, b in ((le, le_f), (re, re_f)):
+        assert np.allclose(a, b, rtol=1e-13, atol=0.0), (a, b)

@@ -169,3 +169,17 @@ def test_c_client_links_and_runs(tmp_path):
     r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, (r.returncode, r.stdout, r.stderr)
     assert r.stdout.strip().endswith("ok")
+
+
+def test_direction_shard_argument_checks(rtsn_mod):
+    """rt_create_direction_shard validates the pair range before touching the device
+    (RT_ERR_PARAM), and like every constructor fails loudly without a gfx950 device."""
+    p = rtsn_mod.params_default()
+    p.update(M=8)
+    for lo, hi in ((-1, 2), (2, 2), (3, 1), (0, 5)):
+        with pytest.raises(rtsn_mod.RtError) as e:
+            rtsn_mod.Solver(p, d_lo=lo, d_hi=hi)
+        assert e.value.status == 3  # RT_ERR_PARAM
+    with pytest.raises(rtsn_mod.RtError) as e:
+        rtsn_mod.Solver(p, d_lo=1, d_hi=3)
+    assert e.value.status == 6  # RT_ERR_DEVICE
