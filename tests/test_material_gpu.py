@@ -206,6 +206,42 @@ def test_group_shards_on_one_gpu(rtsn_mod, oracle_mod, M):
         s.close()
 
 
+@pytest.mark.parametrize("pairs", [((0, 4), (4, 8)), ((0, 3), (3, 8))])
+def test_direction_shards_on_one_gpu(rtsn_mod, oracle_mod, pairs):
+    """Direction-pair shards (rt_create_direction_shard, the fallback for fewer groups than
+    GPUs) in the coupled mode: each shard's exchange term q is its directions' share,
+    summed on the device; T(x) and every direction's psi equal one full handle's (4 + 4
+    pairs: the fused angular sums; 3 + 5: the finalize + moments path)."""
+    import torch
+    p = to_rt(params(oracle_mod, ts=2, G=7, N=200, M=16, bc_left=2))
+    T0 = t_profile(p["N"])
+    with rtsn_mod.Solver(p) as full:
+        full.material_enable(4.0, T0)
+        full.material_step(5)
+        T_full, psi_full = full.temperature(), full.psi()
+    shards = [rtsn_mod.Solver(p, d_lo=lo, d_hi=hi) for lo, hi in pairs]
+    q = [torch.zeros(p["N"], dtype=torch.float64, device="cuda") for _ in shards]
+    for s in shards:
+        s.material_enable(4.0, T0)
+    for _ in range(5):
+        for s, qq in zip(shards, q):
+            s.material_sweep(qq)
+        for s in shards:
+            s.synchronize()
+        tot = q[0] + q[1]
+        torch.cuda.synchronize()
+        for s in shards:
+            s.material_update(tot)
+        for s in shards:
+            s.synchronize()
+    H = p["M"] // 2
+    for s, (lo, hi) in zip(shards, pairs):
+        np.testing.assert_allclose(s.temperature(), T_full, rtol=1e-12)
+        idx = list(range(H - hi, H - lo)) + list(range(H + lo, H + hi))
+        assert per_group_rel(s.psi(), psi_full[idx], 1) <= 1e-12
+        s.close()
+
+
 def test_coupled_steps_driver_single_rank(rtsn_mod, oracle_mod):
     """rtsn.coupling.coupled_steps (the multi-rank driver, here one rank) == rt_material_step."""
     import torch
