@@ -535,3 +535,49 @@ def test_direction_shards(rtsn_mod, oracle_mod, ts, bc_left, bc_right):
         assert err <= 1e-13, (name, err)
     for a, b in ((le, le_f), (re, re_f)):
         assert np.allclose(a, b, rtol=1e-13, atol=0.0), (a, b)
+
+
+def test_full_size_sl_properties(rtsn_mod):
+    """BASELINE.json's headline workload at its full size -- SL, N = 1e6 cells x S64 x 128
+    groups, BDF2 -- through size-independent properties (the oracle covers one of its
+    groups at full line length, test_full_length_sl_line): 48 steps pipelined at T = 16
+    (fill, 3 passes, drain) with dt = 1e-7 so the state stays finite, then
+    (1) a second run is bitwise identical (determinism), (2) the two 64-group shards an
+    N = 2 run would own give the full run's groups bitwise (groups are independent),
+    (3) the aligned schedule (segments corrected across passes, T = 4) agrees to 1e-12
+    per group, (4) every node is finite."""
+    import sys
+    import torch
+    sys.path.insert(0, str(REPO))
+    import bench
+    p = bench.slab_params(128, "v0")
+    p["dt"] = 1e-7
+    N, steps = p["N"], 48
+
+    def run(g_lo=0, g_hi=0, pipe=2):
+        with rtsn_mod.Solver(p, g_lo=g_lo, g_hi=g_hi) as s:
+            s.pipeline = pipe
+            if pipe == 0:
+                s.time_block = 4
+            s.advance(steps)
+            s.finish()
+            out = [torch.empty(N * s.G, dtype=torch.float64, device="cuda") for _ in range(3)]
+            s.moments_device(*out)
+            s.synchronize()
+            assert s.state_finite()
+            return [t.view(N, s.G) for t in out]
+
+    full = run()
+    again = run()
+    for a, b in zip(full, again):
+        assert torch.equal(a, b)
+    del again
+    for lo, hi in ((0, 64), (64, 128)):
+        part = run(lo, hi)
+        for a, b in zip(part, full):
+            assert torch.equal(a, b[:, lo:hi])
+        del part
+    aligned = run(pipe=0)
+    phi, phi_a = full[0], aligned[0]
+    err = ((phi_a - phi).abs().amax(dim=0) / phi.abs().amax(dim=0)).max().item()
+    assert err <= 1e-12, err
