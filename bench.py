@@ -187,7 +187,29 @@ def shard(scaling: str, groups: int, world: int, rank: int):
     return groups, lo, min(groups, lo + per)
 
 
-def gather_results(solver, N: int, world: int, shard_info, shards, device):
+def direction_shard(scaling: str, groups: int, M: int, world: int, rank: int):
+    """(d_lo, d_hi) of this rank when strong scaling has fewer groups than ranks: every rank
+    takes all groups and a contiguous block of the M/2 direction pairs (SURVEY §8e fallback,
+    rt_create_direction_shard); None when groups shard (the normal case)."""
+    if scaling != "strong" or groups >= world:
+        return None
+    H = M // 2
+    per = -(-H // world)
+    lo, hi = rank * per, min(H, (rank + 1) * per)
+    if lo >= hi:
+        raise ValueError(f"{world} ranks but only {groups} groups and {H} direction pairs")
+    return lo, hi
+
+
+def make_solver(p: dict, local: int, info, dirs):
+    """The rank's handle: its group shard, or all groups and its direction pairs."""
+    import rtsn
+    if dirs:
+        return rtsn.Solver(p, device=local, d_lo=dirs[0], d_hi=dirs[1])
+    return rtsn.Solver(p, device=local, g_lo=info[1], g_hi=info[2])
+
+
+def gather_results(solver, N: int, world: int, shard_info, shards, device, dirs=None):
     """All-gather of the per-rank result blocks (RCCL on the GPU box, gloo in
     the CPU tests): returns {"phi", "F", "phi_plus"} as (N, G_total) tensors and
     {"left", "right", "balance"} as (G_total,) tensors."""
@@ -195,6 +217,19 @@ def gather_results(solver, N: int, world: int, shard_info, shards, device):
     import torch.distributed as dist
 
     G_total, g_lo, g_hi = shard_info
+    if dirs:  # direction shards: every rank holds partial sums over its directions of all groups
+        mom = torch.empty(3, N * G_total, dtype=torch.float64, device=device)
+        solver.moments_device(mom[0], mom[1], mom[2])
+        left, right = solver.compute_group_ends()
+        solver.synchronize()
+        ends = torch.as_tensor(np.stack([left, right]), device=device)
+        if world > 1:
+            dist.all_reduce(mom)
+            dist.all_reduce(ends)
+        fields = mom.view(3, N, G_total)
+        nan = torch.full((G_total,), float("nan"), dtype=torch.float64, device=device)
+        return {"phi": fields[0], "F": fields[1], "phi_plus": fields[2],
+                "left": ends[0], "right": ends[1], "balance": nan}  # balance needs the total phi
     shards = shards or [(g_lo, g_hi)]
     Gl = g_hi - g_lo
     Gmax = max(hi - lo for lo, hi in shards)
@@ -221,7 +256,7 @@ def gather_results(solver, N: int, world: int, shard_info, shards, device):
 
 
 def run_rank(solver, p: dict, steps: int, warmup: int, world: int, device, shard_info, scaling: str,
-             scaling_shards=None, gather: bool = True):
+             scaling_shards=None, gather: bool = True, dirs=None):
     """Warmup, K timed steps between barrier + device sync, max over ranks,
     then the absorption all-reduce.  Collectives go through torch.distributed
     on whatever backend is initialised (RCCL on the GPU box, gloo in the CPU
@@ -294,7 +329,7 @@ def run_rank(solver, p: dict, steps: int, warmup: int, world: int, device, shard
     # fastest) and its group ends and balance, assembled into the reference's (N, G)
     # / (G) arrays on every rank; ragged shards are padded to the largest
     t2 = time.perf_counter()
-    gathered = gather_results(solver, p["N"], world, shard_info, scaling_shards, device) if gather else None
+    gathered = gather_results(solver, p["N"], world, shard_info, scaling_shards, device, dirs) if gather else None
     gather_ms = 1e3 * (time.perf_counter() - t2)
 
     t = torch.tensor([wall, kern_ms / max(nlaunch, 1)], dtype=torch.float64, device=device)
@@ -337,7 +372,8 @@ def run_rank(solver, p: dict, steps: int, warmup: int, world: int, device, shard
             "cells": p["N"], "angles": p["M"], "groups_per_gpu": g_hi - g_lo, "groups_total": G_total,
             "time_scheme": "BDF2 (4 fused substeps per step)",
             "steps_per_pass": tb,
-            "parallelism": f"group shards x{world}, no data-path collective",
+            "parallelism": (f"direction-pair shards x{world} ({dirs[1] - dirs[0]} of {p['M'] // 2} pairs per GPU), "
+                            "no data-path collective" if dirs else f"group shards x{world}, no data-path collective"),
             "sweep_workgroups": wg, "tiles_per_step": tiles,
         },
         # One pass moves the state once (HBM-bound at T = 1) and runs T steps of
@@ -379,7 +415,8 @@ def run_rank(solver, p: dict, steps: int, warmup: int, world: int, device, shard
     return line, absorb, gathered
 
 
-def side_leg(p: dict, info, world: int, device, local: int, scaling: str, tb: int, what: str) -> dict:
+def side_leg(p: dict, info, world: int, device, local: int, scaling: str, tb: int, what: str,
+             dirs=None) -> dict:
     """A second sweep measurement on the same shard, reported beside `value` (never as
     it): the state is created fresh, the pipeline filled untimed, then two passes timed
     exactly as the headline.  Used for (a) the HBM-bound T = 1 pass (one HBM round trip
@@ -388,11 +425,11 @@ def side_leg(p: dict, info, world: int, device, local: int, scaling: str, tb: in
     timing of the headline -- whose state overflows, DESIGN.md §5 -- is shown to be
     data-independent) and (c) the other SL variant (v/c correction on / inactive)."""
     import rtsn
-    with rtsn.Solver(p, device=local, g_lo=info[1], g_hi=info[2]) as s:
+    with make_solver(p, local, info, dirs) as s:
         s.time_block = tb
         s.pipeline = 1
         warm = s.sweep_geometry()[1] * tb
-        line, _, _ = run_rank(s, p, 2 * tb, warm, world, device, info, scaling, gather=False)
+        line, _, _ = run_rank(s, p, 2 * tb, warm, world, device, info, scaling, gather=False, dirs=dirs)
     r = line["roofline"]
     out = {"what": what, "dt": p["dt"], "steps_per_pass": tb, "steps": 2 * tb, "warmup": warm,
            "value": line["value"], "ms_per_step": line["ms_per_step"], "kernel_ms": r["kernel_ms"],
@@ -405,7 +442,7 @@ def side_leg(p: dict, info, world: int, device, local: int, scaling: str, tb: in
     return out
 
 
-def run_material(p: dict, info, world: int, device, local: int, steps: int) -> dict:
+def run_material(p: dict, info, world: int, device, local: int, steps: int, dirs=None) -> dict:
     """The material-temperature coupling (rt_material_*, beyond the reference) on
     the same SL shard: BE steps (the reference's BDF2 diverges on SL within a few
     steps, DESIGN.md §4, which would leave T meaningless) from T = 1 keV, each
@@ -420,7 +457,7 @@ def run_material(p: dict, info, world: int, device, local: int, steps: int) -> d
 
     G_total, g_lo, g_hi = info
     q = dict(p, ts_method=1)
-    with rtsn.Solver(q, device=local, g_lo=g_lo, g_hi=g_hi) as s:
+    with make_solver(q, local, info, dirs) as s:  # q(x): each rank's groups or directions, summed
         s.material_enable(1.0)
         buf = torch.zeros(q["N"], dtype=torch.float64, device=device)
         coupled_steps(s, 1, buf, world_size=world, host_sync=True)
@@ -495,7 +532,10 @@ def main():
 
     info = shard(args.scaling, args.groups, world, rank)
     p = slab_params(info[0], args.variant, N=args.cells)
-    solver = rtsn.Solver(p, device=local, g_lo=info[1], g_hi=info[2])
+    dirs = direction_shard(args.scaling, args.groups, p["M"], world, rank)
+    if dirs:  # fewer groups than ranks: all groups, a block of direction pairs per rank
+        info = (args.groups, 0, args.groups)
+    solver = make_solver(p, local, info, dirs)
     if args.time_block:
         solver.time_block = args.time_block
     solver.pipeline = 1 if args.schedule == "pipelined" else 0  # 1: pipelined when the run fills it
@@ -512,7 +552,7 @@ def main():
     warmup = warmup_steps(args.warmup, fill, tb)
     shards = [shard(args.scaling, args.groups, world, r)[1:] for r in range(world)]
     solver_tb = solver.time_block
-    line, _, _ = run_rank(solver, p, steps, warmup, world, device, info, args.scaling, shards)
+    line, _, _ = run_rank(solver, p, steps, warmup, world, device, info, args.scaling, shards, dirs=dirs)
     line["warmup_requested"] = args.warmup if args.warmup >= 0 else None
     line["roofline"]["traffic"] = load_traffic(args.variant, solver.time_block,
                                                line["roofline"]["algorithmic_bytes_per_launch"])
@@ -520,18 +560,18 @@ def main():
     if args.side_legs:
         pv = dict(p, variant=args.variant)
         line["hbm_pass_t1"] = side_leg(pv, info, world, device, local, args.scaling, 1,
-                                       "same workload, one full step per pass: HBM-bound sweep")
+                                       "same workload, one full step per pass: HBM-bound sweep", dirs)
         line["finite_control"] = side_leg(dict(pv, dt=1e-7), info, world, device, local, args.scaling,
                                           solver_tb, "same workload at dt=1e-7 (state stays finite): "
-                                                     "timing control for the headline")
+                                                     "timing control for the headline", dirs)
         other = "corr" if args.variant == "v0" else "v0"
         line[f"variant_{other}"] = side_leg(dict(slab_params(info[0], other, N=args.cells), variant=other), info,
                                             world, device, local, args.scaling, solver_tb,
                                             f"SURVEY §8(d) SL variant {other} (V = "
                                             f"{5.994 if other == 'corr' else 0.0}, v/c correction "
-                                            f"{'on' if other == 'corr' else 'inactive'}), same timing")
+                                            f"{'on' if other == 'corr' else 'inactive'}), same timing", dirs)
     if args.material_steps > 0:
-        line["material"] = run_material(p, info, world, device, local, args.material_steps)
+        line["material"] = run_material(p, info, world, device, local, args.material_steps, dirs)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(args.variant)
         line["reference_config"] = reference_config_timings()

@@ -207,3 +207,107 @@ def test_warmup_rule():
     assert bench.warmup_steps(200, 128, 16) == 208  # more than the fill: whole passes
     assert bench.warmup_steps(5, 80, 10) == 80
     assert bench.warmup_steps(0, 2, 2) == 2         # aligned schedule: one pass
+
+
+class OracleDirShard(OracleShard):
+    """CPU stand-in for a direction-pair shard (rt_create_direction_shard): the oracle
+    over all directions and groups, reporting the partial sums over its directions --
+    what the library's shard handle returns (its psi is bitwise the full handle's rows,
+    tests/test_gpu_parity.py::test_direction_shards)."""
+
+    def __init__(self, p: dict, d_lo: int, d_hi: int):
+        super().__init__(p, 0, p["G"])
+        H = p["M"] // 2
+        self.idx = list(range(H - d_hi, H - d_lo)) + list(range(H + d_lo, H + d_hi))
+        self.M_l = len(self.idx)
+
+    def sweep_traffic(self):
+        return 32.0 * self.M_l * self.p["G"] * self.p["N"], 4.0 * self.M_l * self.p["G"] * self.p["N"]
+
+    def sweep_flops(self):
+        return 56.0 * self.M_l * self.p["G"] * self.p["N"]
+
+    def _partial(self):
+        mu, wt = self.s.quad()
+        psi = self.s.psi()  # (M, G, N)
+        phi = F = pp = 0.0
+        for i in self.idx:  # ascending i, as the handle sums its own directions
+            phi = phi + wt[i] * psi[i]
+            F = F + mu[i] * wt[i] * psi[i]
+            if mu[i] > 0:
+                pp = pp + wt[i] * psi[i]
+        return phi, F, pp
+
+    def moments_device(self, phi, F=None, phi_plus=None):
+        for t, a in zip((phi, F, phi_plus), self._partial()):
+            if t is not None:
+                t.copy_(torch.from_numpy(np.ascontiguousarray(np.asarray(a).T).ravel()))
+
+    def compute_group_ends(self):
+        mu, _ = self.s.quad()
+        ends = self.s.ends()  # (M, G, N, 2)
+        de = self.s.groups()["de_ave"] * 299.792458
+        left = sum(ends[i, :, 0, 0] for i in self.idx if mu[i] < 0) / de
+        right = sum(ends[i, :, -1, 1] for i in self.idx if mu[i] > 0) / de
+        return left, right
+
+    def compute_balance(self):
+        raise AssertionError("a direction shard has no balance (rt_get_balance* refuses)")
+
+    def group_absorption(self, out):
+        phi, _, _ = self._partial()
+        kap = self.s.groups()["kappa"]
+        out.copy_(torch.from_numpy((self.p["rho"] * kap[:, None] * phi).sum(axis=0)))
+
+
+def _dir_worker(rank, world, port, groups, steps, outdir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        p = small_params(groups)
+        dirs = bench.direction_shard("strong", groups, p["M"], world, rank)
+        info = (groups, 0, groups)
+        solver = OracleDirShard(p, *dirs)
+        line, absorb, gathered = bench.run_rank(solver, p, steps, 1, world, torch.device("cpu"), info, "strong",
+                                                None, dirs=dirs)
+        np.save(os.path.join(outdir, f"absorb{rank}.npy"), absorb.numpy())
+        np.savez(os.path.join(outdir, f"gathered{rank}.npz"), **{k: v.numpy() for k, v in gathered.items()})
+        with open(os.path.join(outdir, f"line{rank}.json"), "w") as f:
+            json.dump({"line": line, "dirs": list(dirs)}, f)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_rank_direction_shards(tmp_path):
+    """Fewer groups than ranks (1 group, 2 ranks): bench shards direction pairs; the
+    all-reduced absorption and moments and the summed group ends equal one oracle run
+    over all directions to rounding (the reference's sum over i regrouped by rank)."""
+    steps, world, groups = 2, 2, 1
+    mp.start_processes(_dir_worker, args=(world, _free_port(), groups, steps, str(tmp_path)),
+                       nprocs=world, join=True, start_method="spawn")
+    lines = [json.load(open(tmp_path / f"line{r}.json")) for r in range(world)]
+    assert [l["dirs"] for l in lines] == [[0, 2], [2, 4]]  # M = 8: 4 pairs
+    ref_abs, ref = full_run(groups, steps)
+    for r in range(world):
+        a = np.load(tmp_path / f"absorb{r}.npy")
+        np.testing.assert_allclose(a, ref_abs, rtol=1e-13, atol=0)
+        g = dict(np.load(tmp_path / f"gathered{r}.npz"))
+        for k in ("phi", "F", "phi_plus"):
+            scale = np.abs(ref["phi"]).max()
+            assert np.abs(g[k] - ref[k]).max() <= 1e-13 * scale, k
+        for k in ("left", "right"):
+            np.testing.assert_allclose(g[k], ref[k], rtol=1e-13, atol=0)
+        assert np.isnan(g["balance"]).all()
+    line = lines[0]["line"]
+    assert line["config"]["parallelism"].startswith("direction-pair shards x2")
+    total = 4.0 * 8 * groups * 48 * steps  # both ranks' lines = all M = 8 directions
+    assert line["value"] == pytest.approx(total / (line["ms_per_step"] * 1e-3 * steps), rel=1e-12)
+
+
+def test_direction_shard_plan():
+    assert bench.direction_shard("strong", 128, 64, 8, 3) is None  # groups shard
+    assert bench.direction_shard("weak", 1, 64, 8, 3) is None
+    assert [bench.direction_shard("strong", 4, 64, 8, r) for r in range(8)] == [(4 * r, 4 * r + 4) for r in range(8)]
+    assert [bench.direction_shard("strong", 1, 6, 2, r) for r in range(2)] == [(0, 2), (2, 3)]
+    with pytest.raises(ValueError):
+        bench.direction_shard("strong", 1, 4, 4, 3)  # 2 pairs, 4 ranks
