@@ -60,7 +60,11 @@ import numpy as np  # noqa: E402
 
 METRIC = "cell·angle·group updates/sec (Sn sweep) + BDF2 steps/sec, llnl_slab_test"
 HBM_PEAK = 8.0e12
-SUPPORTED_TIME_BLOCKS = (1, 2, 3, 4, 5, 6, 7, 8, 10, 12, 16)  # rt_set_time_block
+SUPPORTED_TIME_BLOCKS = (1, 2, 3, 4, 5, 6, 7, 8, 10, 12, 16, 20)  # rt_set_time_block
+# the bench's choice for K timed steps: the first of these dividing K, fastest per step first
+# (SL pipelined, ms/step: T = 16 8.2-8.4, 20 8.7, 12 ~9.0, 10 8.9-9.0, 8 9.5, 4 12.3, 2 21;
+# profiles/r02a_windows.jsonl)
+TIME_BLOCK_PREFERENCE = (16, 20, 12, 10, 8, 7, 6, 5, 4, 3, 2, 1)
 FP64_PEAK = 78.6e12  # MI355X FP64 vector spec (256 CU x 4 SIMD x 16 FMA lanes x 2 x 2.4 GHz); measured 71 TF: profiles/r01_fp64_peak.txt
 KAPPA_TABLE = REPO / "tests" / "golden" / "prm" / "llnl_slab_test_group_kappa_a.txt"
 
@@ -165,6 +169,13 @@ def load_traffic(variant: str, tb: int, algorithmic_bytes: float):
     except (OSError, ValueError):
         return None
     return b if b and abs(b / algorithmic_bytes - 1.0) < 0.1 else None
+
+
+def choose_time_block(steps: int, cap: int = 0) -> int:
+    """Steps per pass for a timed region of exactly `steps` steps: the first block of
+    TIME_BLOCK_PREFERENCE (measured fastest per step first) that divides it, at most
+    `cap` when given (0: no cap)."""
+    return next(t for t in TIME_BLOCK_PREFERENCE if (not cap or t <= cap) and steps % t == 0)
 
 
 def warmup_steps(requested: int, fill: int, tb: int) -> int:
@@ -539,10 +550,10 @@ def main():
     if args.time_block:
         solver.time_block = args.time_block
     solver.pipeline = 1 if args.schedule == "pipelined" else 0  # 1: pipelined when the run fills it
-    # exactly K timed steps: the time block is the largest supported one dividing K
-    tb = solver.time_block
-    steps = args.steps if args.steps > 0 else 2 * tb
-    tb = max(t for t in SUPPORTED_TIME_BLOCKS if t <= tb and steps % t == 0)
+    # exactly K timed steps: the time block is the fastest supported one dividing K (at
+    # most --time-block when given); the handle re-sizes its segments for that block
+    steps = args.steps if args.steps > 0 else 2 * solver.time_block
+    tb = choose_time_block(steps, args.time_block)
     solver.time_block = tb
     # Warmup: at least W steps, and always whole passes that fill the pipeline (segments
     # per line passes: every segment position running, one pass apart), so that the K timed

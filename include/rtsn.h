@@ -178,9 +178,11 @@ rt_status rt_sweep_traffic(rt_solver *s, double *bytes_per_launch, double *updat
  * affine cell map (BDF2 28, CN 8, BE 6 FMAs per cell x line x step) times T
  * steps; the cross-segment correction is parallelisation overhead, not counted. */
 rt_status rt_sweep_flops(rt_solver *s, double *flops_per_launch);
-/* Time blocking: full steps advanced per pass over HBM: 1..8, 10, 12 or 16
+/* Time blocking: full steps advanced per pass over HBM: 1..8, 10, 12, 16 or 20
  * (default 16; aligned passes take at most 4).  Results do not depend on it
- * beyond rounding. */
+ * beyond rounding.  The segments of a line are re-sized for the new block's
+ * pipelined kernel (its occupancy) as soon as every segment is at the same time
+ * with no correction outstanding (now, or before the next pass). */
 rt_status rt_set_time_block(rt_solver *s, int steps_per_pass);
 /* Pipelined schedule: the segments of a line run at staggered time levels,
  * one pass apart, so each starts from its upwind neighbour's exact exit state

@@ -1196,6 +1196,7 @@ static hipError_t launch_s(int T, int mode, const SegArgs &a, int grid, hipStrea
     case 10: return launch_t<S, 10>(mode, a, grid, st);
     case 12: return launch_t<S, 12>(mode, a, grid, st);
     case 16: return launch_t<S, 16>(mode, a, grid, st);
+    case 20: return launch_t<S, 20>(mode, a, grid, st);
     default: return hipErrorInvalidValue;
   }
 }
@@ -1245,6 +1246,7 @@ static hipError_t occupancy_s(int T, int level_waves, int *w) {
     case 10: return hipOccupancyMaxActiveBlocksPerMultiprocessor(w, sweep_block_kernel<S, 10, 2>, 64, 0);
     case 12: return hipOccupancyMaxActiveBlocksPerMultiprocessor(w, sweep_block_kernel<S, 12, 2>, 64, 0);
     case 16: return hipOccupancyMaxActiveBlocksPerMultiprocessor(w, sweep_block_kernel<S, 16, 2>, 64, 0);
+    case 20: return hipOccupancyMaxActiveBlocksPerMultiprocessor(w, sweep_block_kernel<S, 20, 2>, 64, 0);
     default: return hipErrorInvalidValue;
   }
 }

@@ -19,8 +19,14 @@ constexpr int kSweepCells = RT_SWEEP_CELLS;             // segment lengths are m
 #ifndef RT_CHUNK_BDF2_T12
 #define RT_CHUNK_BDF2_T12 16
 #endif
+// T = 20: 16 rows spill to scratch; 8 rows fit 256 VGPRs + 126 AGPRs
+#ifndef RT_CHUNK_BDF2_T20
+#define RT_CHUNK_BDF2_T20 8
+#endif
 constexpr int chunk_cells(int S, int T) {
-  return S == 3 && T >= 12 ? RT_CHUNK_BDF2_T12 : (S == 3 && T >= 2 ? RT_CHUNK_BDF2_T2 : RT_SWEEP_CELLS);
+  return S == 3 && T >= 20   ? RT_CHUNK_BDF2_T20
+         : S == 3 && T >= 12 ? RT_CHUNK_BDF2_T12
+                             : (S == 3 && T >= 2 ? RT_CHUNK_BDF2_T2 : RT_SWEEP_CELLS);
 }
 // pipelined passes whose T levels two waves can share (sweep_split_kernel):
 // BDF2, where the carried states (5 per level) are what overflows 256 registers
@@ -33,7 +39,7 @@ constexpr int split_chunk_cells() { return RT_CHUNK_SPLIT; }
 constexpr int kXcds = 8;                                // gfx950: workgroups are dealt to 8 XCDs round-robin
 constexpr int kSweepTile = 64;                          // cells are padded to whole tiles of 64 rows
 
-constexpr int kMaxTimeBlock = 16;                       // full steps fused per pipelined pass (template range)
+constexpr int kMaxTimeBlock = 20;                       // full steps fused per pipelined pass (template range)
 constexpr int kMaxAlignedBlock = 4;                     // ... per aligned pass (carries a T K correction state)
 
 // Segment propagators of the T-level combined state (KC = T K, packed lower

@@ -1,6 +1,8 @@
 // prm.cpp -- see prm.hpp.
 #include "prm.hpp"
 
+#include "eigen_text.hpp"
+
 #include <cctype>
 #include <cerrno>
 #include <cmath>
@@ -120,11 +122,11 @@ void ParameterHandler::fail(rt_status st, const std::string &msg) {
   }
 }
 
-bool ParameterHandler::read_table(const std::string &path, size_t expect, std::vector<double> &out) {
+int ParameterHandler::read_table(const std::string &path, size_t expect, std::vector<double> &out) {
   std::ifstream in(path);
   if (!in) {
     fail(RT_ERR_IO, "could not open table " + path);
-    return false;
+    return 1;
   }
   std::stringstream ss;
   ss << in.rdbuf();
@@ -132,9 +134,9 @@ bool ParameterHandler::read_table(const std::string &path, size_t expect, std::v
   if (out.size() != expect) {
     fail(RT_ERR_PARAM, "table " + path + " holds " + std::to_string(out.size()) + " values, expected " +
                            std::to_string(expect));
-    return false;
+    return 2;
   }
-  return true;
+  return 0;
 }
 
 // ParameterHandler::get_parameters (ParameterHandler.cpp:100-212)
@@ -172,12 +174,15 @@ ParameterHandler::ParameterHandler(const std::string &filename, const std::strin
   have_group_bounds_ = kv.get_bool("have_group_bounds", false);
   if (have_group_bounds_) {
     filename_group_bounds_ = dir + kv.get_string("filename_group_bounds", "NA");
-    read_table(filename_group_bounds_, static_cast<size_t>(G_) + 1, group_bounds_);
+    if (read_table(filename_group_bounds_, static_cast<size_t>(G_) + 1, group_bounds_) == 0)  // after :162's assert
+      load_log_ += "specified group bounds: " + filename_group_bounds_ + "\n";
   }
   have_group_kappa_ = kv.get_bool("have_group_absorption_opacities", false);
   if (have_group_kappa_) {
     filename_group_kappa_ = dir + kv.get_string("filename_group_kappa", "NA");
-    read_table(filename_group_kappa_, static_cast<size_t>(G_), group_kappa_);
+    const int r = read_table(filename_group_kappa_, static_cast<size_t>(G_), group_kappa_);
+    if (r != 1) load_log_ += "group_kappa size: " + std::to_string(G_) + "\n";  // :191, before the assert
+    if (r == 0) load_log_ += "specified group opacities filename: " + filename_group_kappa_ + "\n";
   }
   rho_ = kv.get_double("rho", 1.);
   kappa_grey_ = kv.get_double("kappa_grey", 1.);
@@ -224,11 +229,12 @@ void ParameterHandler::display_input_quantities(std::ostream &os) const {
   if (!r) return;
   os << "Left boundary condition: " << (l ? l : "Incorrect boundary conditions provided.") << "\n\n";
   if (!l) return;
-  os << "Psi_source: \n";
-  for (int m = 0; m < M_; ++m) {
-    for (int g = 0; g < G_; ++g) os << (g ? " " : "") << psi_source_[static_cast<size_t>(m) * G_ + g];
-    os << "\n";
-  }
+  os << "Psi_source: \n";  // `cout << psi_source << endl`: an Eigen MatrixXd (M, G)
+  std::vector<double> colmajor(psi_source_.size());
+  for (int m = 0; m < M_; ++m)
+    for (int g = 0; g < G_; ++g) colmajor[m + static_cast<size_t>(M_) * g] = psi_source_[static_cast<size_t>(m) * G_ + g];
+  write_eigen_text(os, colmajor.data(), M_, G_);
+  os << std::endl;
 }
 
 rt_params ParameterHandler::as_params() const {

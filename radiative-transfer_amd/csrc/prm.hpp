@@ -78,16 +78,22 @@ class ParameterHandler {
 
   // ParameterHandler::display_input_quantities (ParameterHandler.cpp:20-96)
   void display_input_quantities(std::ostream &os) const;
+  // what get_parameters itself prints while reading the tables (ParameterHandler.cpp:165,
+  // 191, 195): "specified group bounds: ...", "group_kappa size: G", "specified group
+  // opacities filename: ..." -- kept here for the CLI to print, never by the library
+  const std::string &load_log() const { return load_log_; }
 
   // Borrowed view for rt_create_from_params (valid while *this lives).
   rt_params as_params() const;
 
  private:
   void fail(rt_status st, const std::string &msg);
-  bool read_table(const std::string &path, size_t expect, std::vector<double> &out);
+  // 0: read, 1: could not open, 2: opened but holds another count
+  int read_table(const std::string &path, size_t expect, std::vector<double> &out);
 
   rt_status status_ = RT_OK;
   std::string error_;
+  std::string load_log_;
   bool prm_found_ = false;
   int M_ = 2, G_ = 1, N_ = 100;
   double efirst_ = .1, elast_ = 10., X_ = 1., dx_ = .01;

@@ -51,6 +51,7 @@ struct rt_solver {
   int T = 1;                     // full steps fused per pass (time block)
   int Tp = 0;                    // steps of the pass whose correction is pending
   int Sg = 1, Ls = 16;           // segments per line and cells per segment
+  int seg_T = 0;                 // the time block the segments were sized for (0: none)
   int level_waves = 1;           // pipelined BDF2 passes: 2 = levels shared by two waves (RTSN_LEVEL_WAVES=2)
   int d_lo = 0, d_hi = 0;        // direction-pair shard [d_lo, d_hi) of the M/2 pairs (d_hi = 0: all)
   int M_full = 0;                // the configuration's M (p.M is the handle's own direction count)
@@ -117,7 +118,7 @@ static rt_status fail(rt_solver *s, rt_status st, const std::string &msg) {
 static int default_time_block(int) { return 16; }
 
 // rt_set_time_block's domain: the instantiated sweep kernels (kernels.hip launch_s)
-static bool supported_time_block(int T) { return (T >= 1 && T <= 8) || T == 10 || T == 12 || T == 16; }
+static bool supported_time_block(int T) { return (T >= 1 && T <= 8) || T == 10 || T == 12 || T == 16 || T == 20; }
 
 static int map_count_of(int scheme) {
   switch (scheme) {
@@ -514,6 +515,27 @@ static hipError_t alloc_segments(rt_solver *h) {
   return e;
 }
 
+// Segments sized for the pipelined pass of the current time block (its occupancy: one
+// wave per SIMD at T = 16 and 20, two at T = 10, ...), applied only while every chain
+// position is at the same time with no correction outstanding -- the state rows do not
+// depend on the segmentation, only the aggregates and propagators do.  Called by
+// rt_set_time_block and again before the next pipelined or aligned pass, so a handle
+// always runs its passes with segments for the time block it runs.
+static rt_status resegment(rt_solver *h) {
+  if (h->material || h->pending || h->Tpipe || h->seg_T == h->T) return RT_OK;
+  int w = 0;
+  HIP_TRY(h, sweep_occupancy(h->scheme, h->T, h->level_waves, &w));
+  if (const char *env = std::getenv("RTSN_WAVES_PER_CU")) w = std::atoi(env);  // experiments
+  const int sg0 = h->Sg, ls0 = h->Ls;
+  segment_lines(h, w);
+  h->seg_T = h->T;
+  if (h->Sg == sg0 && h->Ls == ls0) return RT_OK;
+  if (2LL * h->Q * h->Sg >= (1LL << 31)) return fail(h, RT_ERR_PARAM, "too many lines for one handle: shard the groups");
+  HIP_TRY(h, alloc_segments(h));
+  h->tau.assign(chain_positions(h), h->target);  // every position at the same, requested time
+  return RT_OK;
+}
+
 // ---------------------------------------------------------------------------
 // lifecycle
 // ---------------------------------------------------------------------------
@@ -623,12 +645,14 @@ static rt_status create_impl(const rt_params *pin, int g_lo, int g_hi, int d_lo,
   h->T = default_time_block(h->scheme);
   if (const char *t = std::getenv("RTSN_TIME_BLOCK"))  // experiments: the segment count follows
     if (supported_time_block(std::atoi(t))) h->T = std::atoi(t);
-  if (const char *lw = std::getenv("RTSN_LEVEL_WAVES")) h->level_waves = std::atoi(lw) == 1 ? 1 : 2;
+  if (const char *lw = std::getenv("RTSN_LEVEL_WAVES"))  // experiments: only "1" or "2" are read
+    if (!std::strcmp(lw, "1") || !std::strcmp(lw, "2")) h->level_waves = lw[0] - '0';
   HIP_TRY(h, sweep_occupancy(h->scheme, h->T, h->level_waves, &waves_per_cu));
   // tuning knob for experiments: target resident waves per CU (segments per line follow)
   if (const char *w = std::getenv("RTSN_WAVES_PER_CU")) waves_per_cu = std::atoi(w);
   h->cus = prop.multiProcessorCount;
   segment_lines(h, waves_per_cu);
+  h->seg_T = h->T;
   if (2LL * h->Q * h->Sg >= (1LL << 31)) return fail(nullptr, RT_ERR_PARAM, "too many lines for one handle: shard the groups");
   // a chunk's rows are addressed through one buffer descriptor with 32-bit offsets
   if (16LL * 16 * h->Lpad >= (1LL << 31)) return fail(nullptr, RT_ERR_PARAM, "too many lines per row: shard the groups");
@@ -823,6 +847,7 @@ static rt_status enqueue_pass(rt_solver *s, int T, bool coupled = false) {
 
 // nsteps full steps in aligned passes of at most T (and kMaxAlignedBlock) steps.
 static rt_status enqueue_steps(rt_solver *s, int nsteps) {
+  if (rt_status st = resegment(s)) return st;
   const int T = std::min(s->T, kMaxAlignedBlock);
   while (nsteps > 0) {
     const int n = std::min(T, nsteps);
@@ -894,8 +919,9 @@ static rt_status pipe_advance(rt_solver *s, int nsteps) {
       s->queued -= static_cast<int>(passes * T);
       return enqueue_steps(s, static_cast<int>(passes * T));
     }
-    // start from aligned positions with an exact state
+    // start from aligned positions with an exact state, segments sized for this T
     if ((st = apply_correction(s))) return st;
+    if ((st = resegment(s))) return st;
     s->Tpipe = T;
     s->pipe_base = s->tau[0];
   }
@@ -1010,6 +1036,7 @@ extern "C" rt_status rt_material_enable(rt_solver *s, double rho_cv, const doubl
     if (const char *env = std::getenv("RTSN_WAVES_PER_CU")) w = std::atoi(env);
     const int sg0 = s->Sg;
     segment_lines(s, w);
+    s->seg_T = 0;  // sized for the coupled pass
     if (s->Sg != sg0) {
       if (2LL * s->Q * s->Sg >= (1LL << 31)) return fail(s, RT_ERR_PARAM, "too many segments");
       HIP_TRY(s, alloc_segments(s));
@@ -1101,9 +1128,9 @@ extern "C" rt_status rt_material_update(rt_solver *s, const double *d_q) {
 
 extern "C" rt_status rt_material_step(rt_solver *s, int nsteps) {
   if (!s || nsteps < 0) return fail(s, RT_ERR_ARG, "rt_material_step: bad argument");
-  if (s->g_lo != 0 || s->g_hi != s->p.G)
-    return fail(s, RT_ERR_STATE, "rt_material_step: the handle holds a group shard; sum q over the shards "
-                                 "(rt_material_sweep, all-reduce, rt_material_update)");
+  if (s->g_lo != 0 || s->g_hi != s->p.G || s->d_hi > 0)
+    return fail(s, RT_ERR_STATE, "rt_material_step: the handle holds a group or direction-pair shard; sum q "
+                                 "over the shards (rt_material_sweep, all-reduce, rt_material_update)");
   for (int n = 0; n < nsteps; ++n) {
     rt_status st = rt_material_sweep(s, nullptr);
     if (st) return st;
@@ -1215,9 +1242,11 @@ extern "C" rt_status rt_set_ends(rt_solver *s, const double *ends) {
     if (e == hipSuccess) e = launch_import_ends(static_cast<double2 *>(s->E.p), d, g, c0, nc, s->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(s->stream);  // d is reused by the next chunk
   }
-  s->pending = false;  // the loaded state is exact
   (void)hipFree(d);
-  if (e != hipSuccess) return fail(s, RT_ERR_DEVICE, std::string("rt_set_ends: ") + hipGetErrorString(e));
+  if (e != hipSuccess)  // some chunks may hold the new cells, the rest the old ones
+    return fail(s, RT_ERR_DEVICE, std::string("rt_set_ends: ") + hipGetErrorString(e) +
+                                      " (the handle's state is undefined: load it again or destroy the handle)");
+  s->pending = false;  // the loaded state is exact
   return RT_OK;
 }
 
@@ -1483,9 +1512,10 @@ extern "C" rt_status rt_get_pipeline(rt_solver *s, int *on) {
 extern "C" rt_status rt_set_time_block(rt_solver *s, int steps_per_pass) {
   if (!s) return fail(nullptr, RT_ERR_ARG, "rt_set_time_block: NULL handle");
   if (!supported_time_block(steps_per_pass))
-    return fail(s, RT_ERR_ARG, "rt_set_time_block: steps per pass must be 1..8, 10, 12 or 16");
+    return fail(s, RT_ERR_ARG, "rt_set_time_block: steps per pass must be 1..8, 10, 12, 16 or 20");
+  HIP_TRY(s, hipSetDevice(s->device));
   s->T = steps_per_pass;
-  return RT_OK;
+  return resegment(s);  // now if the positions are aligned, else when they next are
 }
 
 extern "C" rt_status rt_get_time_block(rt_solver *s, int *steps_per_pass) {

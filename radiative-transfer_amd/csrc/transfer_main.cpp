@@ -28,6 +28,7 @@ int main(int argc, char **argv) {
   std::cout << "filename: " << filename << std::endl;
   const char *tdir = std::getenv("RT_TABLE_DIR");
   rtamd::ParameterHandler parameter_handler(filename, tdir ? tdir : "");
+  std::cout << parameter_handler.load_log();  // get_parameters' own prints (ParameterHandler.cpp:165-195)
   if (parameter_handler.status() != RT_OK) {
     std::cerr << parameter_handler.error() << std::endl;
     return 1;

@@ -192,6 +192,7 @@ def test_transfer_stdout(oracle_mod, tmp_path, name):
     orc.solve()
     start = r.stdout.index("Solver constructor.")
     bal_at = r.stdout.index("sources: ")
+    assert r.stdout[:start] == expected_display(q, tmp_path / "prm" / f"{name}.prm")
     assert r.stdout[start:bal_at] == expected_solver_log(q, orc)
     # balance lines: sources / sinks / balance per group; balance = |sinks - sources| /
     # sources cancels, so compare the numbers, not their 6-digit text
@@ -203,6 +204,94 @@ def test_transfer_stdout(oracle_mod, tmp_path, name):
         assert b_line.startswith(f"balance at ({g}): ")
         assert float(b_line.split(": ")[1]) == pytest.approx(bal_o[g], rel=1e-4, abs=1e-12)
     assert r.stdout.startswith(f"filename: {prm}\n") and len(lines) == 3 * q["G"]
+
+
+def prm_text_value(path: Path, key: str) -> str:
+    """The raw text of `key=` in a .prm (kaityo256/param: key at column 0, value to the end
+    of the line, first occurrence wins), as get<string> returns it."""
+    for line in path.read_text().splitlines():
+        if line.startswith(key + "="):
+            return line[len(key) + 1:]
+    return "NA"
+
+
+def expected_display(q: dict, prm: Path) -> str:
+    """What the reference prints from main.cc:78 through display_input_quantities: the
+    filename line, get_parameters' own prints while it reads the tables
+    (ParameterHandler.cpp:165, 191, 195) and display_input_quantities
+    (ParameterHandler.cpp:20-96), restated from its iostream calls.  `cout << double` is
+    %g; `cout << psi_source` is an Eigen MatrixXd (M, G) under the default IOFormat."""
+    bc = {0: "vacuum", 2: "reflective", 1: "source"}
+    out = f"filename: ../prm/{prm.name}\n"
+    bounds = "../prm/" + prm_text_value(prm, "filename_group_bounds")
+    kappa = "../prm/" + prm_text_value(prm, "filename_group_kappa")
+    if q["have_group_bounds"]:
+        out += f"specified group bounds: {bounds}\n"
+    if q["have_group_kappa"]:
+        out += f"group_kappa size: {q['G']}\nspecified group opacities filename: {kappa}\n"
+    out += "\n--- Input Parameters ---\n"
+    out += f"Angle quadrature order: {q['M']}\nNumber of energy groups: {q['G']}\n"
+    if q["have_group_bounds"]:
+        out += f"Group bounds (keV) specified in file: {bounds}\n"
+    else:
+        out += ("Group bounds (keV) will be computed logarithmically, with first group edge at "
+                f"{cpp_g(q['efirst'])} and last group edge at {cpp_g(q['elast'])}\n")
+    out += f"Slab thickness (cm): {cpp_g(q['X'])}\nNumber of cells: {q['N']}\n"
+    out += f"Material density (g/cm^3): {cpp_g(q['rho'])}\n"
+    if q["have_group_kappa"]:
+        out += f"Group opacities (cm^2/g) specified in file: {kappa}\n"
+    else:
+        out += f"Group opacities will be set to the constant grey opacity (cm^2/g): {cpp_g(q['kappa_grey'])}\n"
+    out += f"Material temperature (keV): {cpp_g(q['T'])}\nMaterial velocity (cm/shake): {cpp_g(q['V'])}\n"
+    out += f"Beta: {cpp_g(q['V'] / 299.792458)}\n"
+    out += "Right boundary condition: "
+    if q["bc_right"] not in bc:
+        return out + "Incorrect boundary conditions provided.\n"
+    out += bc[q["bc_right"]] + "\n"
+    out += "Left boundary condition: "
+    if q["bc_left"] not in bc:
+        return out + "Incorrect boundary conditions provided.\n\n"
+    out += bc[q["bc_left"]] + "\n\n"
+    return out + "Psi_source: \n" + eigen_text(q["psi_source"])
+
+
+DISPLAY_EDITS = {  # edge cases of the display: (golden .prm, {key: new line text})
+    "widths": ("template.prm", {"psi_source": "psi_source=1.5 -2 1e-7 100 0.333333333 7"}),
+    "bad_right_bc": ("template.prm", {"bc_right_indicator": "bc_right_indicator=7"}),
+    "bad_left_bc": ("single_group.prm", {"bc_left_indicator": "bc_left_indicator=-1"}),
+    "tables_on": ("template.prm", {"have_group_bounds": "have_group_bounds=true",
+                                   "have_group_absorption_opacities": "have_group_absorption_opacities=true"}),
+    "beta": ("multi_group_equilibrium.prm", {"V": "V=5.994"}),
+}
+
+
+@pytest.mark.parametrize("case", sorted(p.name for p in PRM_DIR.glob("*.prm")) + sorted(DISPLAY_EDITS))
+def test_transfer_display_text(oracle_mod, tmp_path, case):
+    """Row f-2: `transfer` prints the reference's input display (ParameterHandler.cpp:20-96,
+    with get_parameters' table prints and main.cc's filename line) byte for byte, for
+    every golden .prm (table / no-table branches, mg_equilib) and edited copies (psi_source
+    of mixed widths, incorrect boundary indicators, both tables on, V != 0).  The display
+    precedes any device call, so this runs without a GPU (there the solver then reports
+    that no device exists; on the GPU box the stdout continues with the solver's log)."""
+    run = _run_tree(tmp_path)
+    name = case
+    if case in DISPLAY_EDITS:
+        base, edits = DISPLAY_EDITS[case]
+        lines = (tmp_path / "prm" / base).read_text().splitlines()
+        for key, text in edits.items():
+            hit = [k for k, l in enumerate(lines) if l.startswith(key + "=")]
+            if hit:
+                lines[hit[0]] = text
+            else:
+                lines.append(text)
+        name = f"edit_{case}.prm"
+        (tmp_path / "prm" / name).write_text("\n".join(lines) + "\n")
+    prm = tmp_path / "prm" / name
+    r = subprocess.run([str(_bin("transfer")), f"../prm/{name}"], cwd=run, capture_output=True, text=True,
+                       timeout=120)
+    q = oracle_mod.parse_prm(str(prm), table_dir=str(tmp_path / "prm") + "/")
+    got = r.stdout.split("Solver constructor.")[0]
+    assert got == expected_display(q, prm)
 
 
 @pytest.mark.gpu

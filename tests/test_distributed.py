@@ -209,6 +209,22 @@ def test_warmup_rule():
     assert bench.warmup_steps(0, 2, 2) == 2         # aligned schedule: one pass
 
 
+def test_time_block_choice():
+    """bench.py: K timed steps run as whole passes of the fastest block dividing K."""
+    import bench
+    assert bench.choose_time_block(20) == 20        # the driver's window
+    assert bench.choose_time_block(32) == 16
+    assert bench.choose_time_block(80) == 16        # 16 before 20 when both divide
+    assert bench.choose_time_block(30) == 10
+    assert bench.choose_time_block(2) == 2
+    assert bench.choose_time_block(7) == 7
+    assert bench.choose_time_block(11) == 1
+    assert bench.choose_time_block(20, cap=10) == 10
+    for k in range(1, 200):
+        t = bench.choose_time_block(k)
+        assert k % t == 0 and t in bench.SUPPORTED_TIME_BLOCKS
+
+
 class OracleDirShard(OracleShard):
     """CPU stand-in for a direction-pair shard (rt_create_direction_shard): the oracle
     over all directions and groups, reporting the partial sums over its directions --

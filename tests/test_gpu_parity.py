@@ -71,9 +71,9 @@ def compare_all(gpu, orc, tol=TOL, plus_vs_group=False):
 
 @pytest.mark.parametrize("name", CONFIGS)
 def test_reference_configs(rtsn_mod, oracle_mod, name):
+    """Every golden .prm at its own length (single_group 1000 BDF2 steps,
+    multi_group_equilibrium 500, llnl_slab_test 2, ...), all fields."""
     p = load(oracle_mod, name)
-    if name in ("single_group.prm", "multi_group_equilibrium.prm"):
-        p["max_timesteps"] = min(p["max_timesteps"], 200)
     orc = oracle_mod.OracleSolver(p)
     orc.solve()
     with rtsn_mod.Solver(to_rt(p)) as gpu:
@@ -190,7 +190,8 @@ def test_random_state_long_lines(rtsn_mod, oracle_mod, tb, steps, pipe):
         compare_all(gpu, orc)
 
 
-@pytest.mark.parametrize("ts,tb,steps", [(3, 12, 13), (3, 16, 17), (3, 8, 16), (2, 16, 40), (1, 16, 40),
+@pytest.mark.parametrize("ts,tb,steps", [(3, 12, 13), (3, 16, 17), (3, 20, 21), (3, 20, 43), (2, 20, 40),
+                                         (1, 20, 41), (3, 8, 16), (2, 16, 40), (1, 16, 40),
                                          (2, 12, 30), (1, 5, 11), (3, 10, 15), (3, 10, 20), (2, 10, 20), (1, 10, 30)])
 def test_large_time_blocks(rtsn_mod, oracle_mod, ts, tb, steps):
     """Pipelined passes of up to 16 fused steps (and their aligned remainder)
@@ -327,10 +328,10 @@ def test_pipeline_long_run_many_segments(rtsn_mod, oracle_mod, ts):
 def test_time_block_range(rtsn_mod):
     d = rtsn_mod.params_default()
     with rtsn_mod.Solver(d) as s:
-        for ok in (1, 4, 8, 10, 12, 16):
+        for ok in (1, 4, 8, 10, 12, 16, 20):
             s.time_block = ok
             assert s.time_block == ok
-        for bad in (0, 9, 13, 17, -1):
+        for bad in (0, 9, 13, 17, 21, 32, -1):
             with pytest.raises(rtsn_mod.RtError) as e:
                 s.time_block = bad
             assert e.value.status == 8
@@ -439,11 +440,72 @@ def test_full_length_sl_line(rtsn_mod, sl_line_oracle, pipe, tb):
         assert per_group_rel(phi_g, phi_o, 0) <= TOL
 
 
+@pytest.fixture(scope="module")
+def sl_pair_oracle(oracle_mod):
+    """The headline kernel's workload at its full line length (verdict r01, item 1): the SL
+    slab's grid, kappa table and N = 1e6 cells, M = 4, dt = 1e-7, groups 126 (kappa set to
+    the table's 1e6: optically thick, tau = 4e5) and 127 (kappa 0.021: thin, tau = 0.008, the
+    upwind carry crosses every segment), for V = 0 and V = 5.994 with the v/c correction on;
+    the oracle's state after 12, 18 and 22 BDF2 steps (T + 2 for T = 10, 16, 20; 2 T + 2 for
+    T = 10)."""
+    import sys
+    sys.path.insert(0, str(REPO))
+    import bench
+    out = {}
+    for V in (0.0, 5.994):
+        p = bench.slab_params(128, "corr" if V else "v0", M=4)
+        p["dt"] = 1e-7
+        kap = p["group_kappa"].copy()
+        kap[126] = kap[0]
+        p["group_kappa"] = kap
+        q = dict(p, bc_left=0, bc_right=0, dx=p["X"] / p["N"], have_group_bounds=0, have_group_kappa=1,
+                 prm_found=1, max_timesteps=22)
+        o = oracle_mod.OracleSolver(q, g_lo=126, g_hi=128)
+        o.set_threads(2)
+        snaps, done = {}, 0
+        for steps in (12, 18, 22):
+            o.run_substeps(4 * done, 4 * (steps - done))
+            done = steps
+            mu, wt = o.quad()
+            snaps[steps] = {"psi": o.psi(), "moments": o.moments(), "ends": o.group_ends(), "mu": mu, "wt": wt}
+        out[V] = (p, snaps)
+    return out
+
+
+@pytest.mark.parametrize("V", [0.0, 5.994])
+@pytest.mark.parametrize("tb,steps", [(10, 12), (16, 18), (20, 22), (10, 22)])
+def test_headline_kernel_full_length(rtsn_mod, sl_pair_oracle, tb, steps, V):
+    """sweep_block_kernel<3, T, 2> -- the pass the bench times -- on full-length SL lines
+    (N = 1e6 cut into ~500-1000 segments sized for the T-step kernel's occupancy) against
+    the oracle: the pipeline fills over every segment position, runs, drains, and an
+    aligned 2-step remainder pass with its finalize follows; psi, phi, phi_plus, F and the
+    group ends per group to 1e-10."""
+    p, snaps = sl_pair_oracle[V]
+    ref = snaps[steps]
+    with rtsn_mod.Solver(p, g_lo=126, g_hi=128) as gpu:
+        gpu.pipeline = 2
+        gpu.time_block = tb
+        _, segs = gpu.sweep_geometry()
+        assert segs >= 400
+        gpu.advance(steps)
+        psi = gpu.psi()
+        phi_g, F_g, pp_g = gpu.moments()
+        l_g, r_g = gpu.compute_group_ends()
+    err = {"psi": per_group_rel(psi, ref["psi"], 1)}
+    phi_o, F_o, pp_o = ref["moments"]
+    err["phi"] = per_group_rel(phi_g, phi_o, 0)
+    err["phi_plus"] = per_group_rel(pp_g, pp_o, 0)
+    err["F"] = flux_rel(F_g, F_o, ref["psi"], ref["mu"], ref["wt"])
+    l_o, r_o = ref["ends"]
+    err["ends"] = float(max(np.max(np.abs(l_g - l_o) / np.abs(l_o)), np.max(np.abs(r_g - r_o) / np.abs(r_o))))
+    assert max(err.values()) <= TOL, err
+
+
 @pytest.mark.parametrize("tb", [8, 12, 16])
 @pytest.mark.parametrize("bc_left", [0, 2])
 def test_level_split_pass(rtsn_mod, oracle_mod, monkeypatch, tb, bc_left):
     """The level-split pipelined pass (sweep_split_kernel: the T levels of a BDF2 pass
-    shared by two waves through LDS, the default for T = 8, 12, 16) is bitwise the
+    shared by two waves through LDS, opt-in for T = 8, 12, 16) is bitwise the
     one-wave pass (rt_set_level_waves 1, and RTSN_LEVEL_WAVES=1 at creation, whose
     segment count follows the one-wave occupancy) -- same arithmetic per (cell, level)
     -- over 3 T + 1 steps (fill, steady state, drain, an aligned remainder), and matches
