@@ -440,21 +440,27 @@ def test_full_length_sl_line(rtsn_mod, sl_line_oracle, pipe, tb):
         assert per_group_rel(phi_g, phi_o, 0) <= TOL
 
 
+PAIR_CASES = [(1e-7, 0.0), (1e-7, 5.994), (1e-9, 5.994)]  # (dt, V)
+
+
 @pytest.fixture(scope="module")
 def sl_pair_oracle(oracle_mod):
     """The headline kernel's workload at its full line length (verdict r01, item 1): the SL
-    slab's grid, kappa table and N = 1e6 cells, M = 4, dt = 1e-7, groups 126 (kappa set to
-    the table's 1e6: optically thick, tau = 4e5) and 127 (kappa 0.021: thin, tau = 0.008, the
-    upwind carry crosses every segment), for V = 0 and V = 5.994 with the v/c correction on;
-    the oracle's state after 12, 18 and 22 BDF2 steps (T + 2 for T = 10, 16, 20; 2 T + 2 for
-    T = 10)."""
+    slab's grid, kappa table and N = 1e6 cells, M = 4, groups 126 (kappa set to the table's
+    1e6: optically thick, tau = 4e5) and 127 (kappa 0.021: thin, tau = 0.008), V = 0 and
+    V = 5.994 with the v/c correction on; the oracle's state after 12, 18 and 22 BDF2 steps
+    (T + 2 for T = 10, 16, 20; 2 T + 2 for T = 10).  dt = 1e-7 (Courant number c mu dt / dx
+    = 64: the upwind carry crosses segment after segment) and dt = 1e-9 (Courant 0.6).
+    The three oracle runs go in parallel threads (ctypes releases the GIL)."""
     import sys
+    from concurrent.futures import ThreadPoolExecutor
     sys.path.insert(0, str(REPO))
     import bench
-    out = {}
-    for V in (0.0, 5.994):
+
+    def run(case):
+        dt, V = case
         p = bench.slab_params(128, "corr" if V else "v0", M=4)
-        p["dt"] = 1e-7
+        p["dt"] = dt
         kap = p["group_kappa"].copy()
         kap[126] = kap[0]
         p["group_kappa"] = kap
@@ -467,20 +473,29 @@ def sl_pair_oracle(oracle_mod):
             o.run_substeps(4 * done, 4 * (steps - done))
             done = steps
             mu, wt = o.quad()
-            snaps[steps] = {"psi": o.psi(), "moments": o.moments(), "ends": o.group_ends(), "mu": mu, "wt": wt}
-        out[V] = (p, snaps)
-    return out
+            snaps[steps] = {"psi": o.psi(), "ends": o.ends(), "moments": o.moments(), "group_ends": o.group_ends(),
+                            "mu": mu, "wt": wt, "de": o.groups()["de_ave"][126:128]}
+        return p, snaps
+
+    with ThreadPoolExecutor(len(PAIR_CASES)) as ex:
+        return dict(zip(PAIR_CASES, ex.map(run, PAIR_CASES)))
 
 
-@pytest.mark.parametrize("V", [0.0, 5.994])
+@pytest.mark.parametrize("case", PAIR_CASES)
 @pytest.mark.parametrize("tb,steps", [(10, 12), (16, 18), (20, 22), (10, 22)])
-def test_headline_kernel_full_length(rtsn_mod, sl_pair_oracle, tb, steps, V):
+def test_headline_kernel_full_length(rtsn_mod, sl_pair_oracle, tb, steps, case):
     """sweep_block_kernel<3, T, 2> -- the pass the bench times -- on full-length SL lines
     (N = 1e6 cut into ~500-1000 segments sized for the T-step kernel's occupancy) against
     the oracle: the pipeline fills over every segment position, runs, drains, and an
-    aligned 2-step remainder pass with its finalize follows; psi, phi, phi_plus, F and the
-    group ends per group to 1e-10."""
-    p, snaps = sl_pair_oracle[V]
+    aligned 2-step remainder pass with its finalize follows.  psi, the node array, phi,
+    phi_plus and F per group to 1e-10 of the group's scale; the group ends (one node sum
+    per group) to 1e-10 relative at dt = 1e-9.  At dt = 1e-7 the reference's BDF2
+    (const_B from the full dt, solver.cpp:501) grows the interior of these lines ~1e7-1e15x
+    in 12 steps while the boundary nodes stay at B, so there the group ends are measured
+    against the group's node scale (max |ends| x M/2 / (dE c)), as phi_plus is in
+    compare_all(plus_vs_group)."""
+    dt, V = case
+    p, snaps = sl_pair_oracle[case]
     ref = snaps[steps]
     with rtsn_mod.Solver(p, g_lo=126, g_hi=128) as gpu:
         gpu.pipeline = 2
@@ -488,16 +503,22 @@ def test_headline_kernel_full_length(rtsn_mod, sl_pair_oracle, tb, steps, V):
         _, segs = gpu.sweep_geometry()
         assert segs >= 400
         gpu.advance(steps)
-        psi = gpu.psi()
+        psi, ends = gpu.psi(), gpu.ends()
         phi_g, F_g, pp_g = gpu.moments()
         l_g, r_g = gpu.compute_group_ends()
-    err = {"psi": per_group_rel(psi, ref["psi"], 1)}
+    err = {"psi": per_group_rel(psi, ref["psi"], 1), "node array": per_group_rel(ends, ref["ends"], 1)}
     phi_o, F_o, pp_o = ref["moments"]
     err["phi"] = per_group_rel(phi_g, phi_o, 0)
     err["phi_plus"] = per_group_rel(pp_g, pp_o, 0)
     err["F"] = flux_rel(F_g, F_o, ref["psi"], ref["mu"], ref["wt"])
-    l_o, r_o = ref["ends"]
-    err["ends"] = float(max(np.max(np.abs(l_g - l_o) / np.abs(l_o)), np.max(np.abs(r_g - r_o) / np.abs(r_o))))
+    l_o, r_o = ref["group_ends"]
+    if dt < 1e-8:
+        scale_l, scale_r = np.abs(l_o), np.abs(r_o)
+    else:
+        node_scale = np.abs(ref["ends"]).max(axis=(0, 2, 3)) * (p["M"] // 2) / (ref["de"] * 299.792458)
+        scale_l = scale_r = node_scale
+    err["left_ends"] = float(np.max(np.abs(l_g - l_o) / scale_l))
+    err["right_ends"] = float(np.max(np.abs(r_g - r_o) / scale_r))
     assert max(err.values()) <= TOL, err
 
 
