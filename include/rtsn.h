@@ -145,6 +145,15 @@ rt_status rt_get_balance(rt_solver *s, double *balance);
 rt_status rt_get_balance_terms(rt_solver *s, double *balance, double *sources, double *sinks);
 /* get_e_ave (solver.h:95): all G groups */
 rt_status rt_get_e_ave(rt_solver *s, double *e_ave);
+/* The shard a handle holds: the configuration's G and M, its groups [g_lo, g_hi) and
+ * its direction pairs [d_lo, d_hi) of the M/2 (all pairs unless a direction shard). */
+rt_status rt_get_shard(rt_solver *s, int *G_total, int *M_total, int *g_lo, int *g_hi, int *d_lo, int *d_hi);
+/* compute_balance's terms (solver.cpp:240-284) split by how they add over direction-pair
+ * shards, per local group: boundary inflow currents (jhp + jNm), outflow currents plus
+ * absorption (jNp + jhm + sum_c rho kappa phi dx) -- both sums over the handle's
+ * directions -- and the emission sum_c rho kappa a c T^4 dx (direction-independent).
+ * sources = inflow + emission, sinks = outflow_absorption.  Any NULL skipped. */
+rt_status rt_get_balance_partials(rt_solver *s, double *inflow, double *outflow_absorption, double *emission);
 /* Group data of all G groups: e_edge (G+1), B, dBdT, kappa (G); any NULL skipped. */
 rt_status rt_get_group_data(rt_solver *s, double *e_edge, double *B, double *dBdT, double *kappa);
 rt_status rt_get_quadrature(rt_solver *s, double *mu, double *wt);
@@ -237,6 +246,48 @@ rt_status rt_material_step(rt_solver *s, int nsteps);
 /* T(x) (N) and the per-cell emission B (G_local*N, g + G_local*c) to host memory. */
 rt_status rt_get_temperature(rt_solver *s, double *T_cells);
 rt_status rt_get_cell_planck(rt_solver *s, double *B);
+
+/* ---- multi-GPU: RCCL behind the ABI (one process per GPU, xGMI) -----------
+ * The reference is single-process (main.cc:79-133).  Energy groups are independent for
+ * the whole run (T constant), so a job gives every rank a contiguous group shard
+ * (rt_create_from_params(p, g_lo, g_hi, device)), or -- with fewer groups than ranks --
+ * a direction-pair shard of all groups (rt_create_direction_shard); time stepping needs
+ * no exchange.  An rt_comm joins the ranks' handles for the collectives after (or
+ * between) the steps: every call below is collective (all ranks, same order), runs on
+ * the handle's stream (RCCL over xGMI) and, where it returns host arrays, synchronises.
+ * Shards must be all group shards that tile [0, G) in rank order, or all direction
+ * shards of the same groups that tile [0, M/2) in rank order (else RT_ERR_PARAM). */
+typedef struct rt_comm rt_comm;
+#define RT_COMM_ID_BYTES 128
+/* ncclGetUniqueId: on one rank, then handed to every rank (file, pipe, MPI, ...). */
+rt_status rt_comm_unique_id(void *id);
+/* ncclCommInitRank on `device` (the device of the rank's handle). */
+rt_status rt_comm_init(int nranks, int rank, const void *id, int device, rt_comm **out);
+void rt_comm_destroy(rt_comm *c);
+rt_status rt_comm_rank(rt_comm *c, int *nranks, int *rank);
+/* phi, F, phi_plus of ALL groups (G x N each, g + G c; NULL skipped; host, every rank):
+ * group shards are gathered, direction shards summed (the reference's sequential sum
+ * over i regrouped by shard: rounding only). */
+rt_status rt_comm_gather_moments(rt_comm *c, rt_solver *s, double *phi, double *F, double *phi_plus);
+/* compute_group_ends + get_ends of all G groups (host, every rank). */
+rt_status rt_comm_gather_group_ends(rt_comm *c, rt_solver *s, double *left, double *right);
+/* compute_balance of all G groups with its sources and sinks (host, every rank; NULL
+ * skipped): group shards gather their own terms (bitwise the single-handle values);
+ * direction shards sum rt_get_balance_partials and add the emission once. */
+rt_status rt_comm_gather_balance(rt_comm *c, rt_solver *s, double *balance, double *sources, double *sinks);
+/* psi_mat (M, G, N) of all groups and directions into host `psi` on `root` (other ranks
+ * may pass NULL); moves M G_local N doubles per rank through the device, so meant for
+ * .prm-sized runs (ψ of large runs stays sharded: rt_get_psi per rank). */
+rt_status rt_comm_gather_psi(rt_comm *c, rt_solver *s, int root, double *psi);
+/* The group-summed absorption A(x) = sum over ALL groups of rho kappa_g phi_g(x): each
+ * rank's rt_group_absorption_device, then one ncclAllReduce(sum) of N doubles into the
+ * DEVICE buffer d_out, stream-ordered, no host synchronisation. */
+rt_status rt_comm_allreduce_absorption(rt_comm *c, rt_solver *s, double *d_out);
+/* nsteps coupled steps (rt_material_*) across the shards: per step the shard's sweep and
+ * q(x), one ncclAllReduce(sum) of q (N doubles) on the handle's stream, then the T
+ * update -- stream-ordered, no host synchronisation; every rank ends with the same T(x). */
+rt_status rt_comm_material_step(rt_comm *c, rt_solver *s, int nsteps);
+const char *rt_comm_last_error(rt_comm *c);
 
 const char *rt_status_string(rt_status st);
 /* Last error message recorded on the handle (or the global one for s == NULL). */

@@ -1170,6 +1170,18 @@ extern "C" rt_status rt_get_dims(rt_solver *s, int *M, int *G_local, int *N, int
   return RT_OK;
 }
 
+extern "C" rt_status rt_get_shard(rt_solver *s, int *G_total, int *M_total, int *g_lo, int *g_hi, int *d_lo,
+                                  int *d_hi) {
+  if (!s) return fail(nullptr, RT_ERR_ARG, "rt_get_shard: NULL handle");
+  if (G_total) *G_total = s->p.G;
+  if (M_total) *M_total = s->M_full;
+  if (g_lo) *g_lo = s->g_lo;
+  if (g_hi) *g_hi = s->g_hi;
+  if (d_lo) *d_lo = s->d_hi > 0 ? s->d_lo : 0;
+  if (d_hi) *d_hi = s->d_hi > 0 ? s->d_hi : s->M_full / 2;
+  return RT_OK;
+}
+
 // The reference-layout transfers go through a bounded device buffer, a chunk of cells
 // at a time (the layout's slowest index is the cell): kExportChunk doubles per node
 // block, so rt_get_psi / rt_get_ends / rt_set_ends need ~0.5 GB of device memory beside
@@ -1380,6 +1392,52 @@ extern "C" rt_status rt_get_balance_terms(rt_solver *s, double *balance, double 
     if (balance) balance[gl] = std::fabs(sinks - sources) / sources;
     if (sources_out) sources_out[gl] = sources;
     if (sinks_out) sinks_out[gl] = sinks;
+  }
+  return RT_OK;
+}
+
+// compute_balance's terms split by how they add over direction-pair shards: the
+// boundary inflow currents (jhp + jNm), the outflow currents plus absorption (jNp + jhm
+// + sum rho kappa phi dx: linear in psi, so the shards' partials sum to the total) and
+// the emission sum (sum rho kappa a c T^4 dx: the same on every shard)
+extern "C" rt_status rt_get_balance_partials(rt_solver *s, double *inflow, double *outflow_absorption,
+                                             double *emission) {
+  if (!s) return fail(nullptr, RT_ERR_ARG, "rt_get_balance_partials: NULL handle");
+  HIP_TRY(s, hipSetDevice(s->device));
+  const int N = s->p.N, Gl = s->Gl;
+  std::vector<double> phi(static_cast<size_t>(Gl) * N);
+  rt_status st = rt_get_moments(s, phi.data(), nullptr, nullptr);
+  if (st) return st;
+  std::vector<double> rows;
+  if ((st = fetch_rows(s, rows))) return st;
+  const double ac = phys::kRadA * phys::kLight, dx = s->p.X / N;
+  std::vector<double> rk(Gl), src(Gl), ab(Gl, 0.), sr(Gl, 0.);
+  for (int gl = 0; gl < Gl; ++gl) {
+    rk[gl] = s->gt.rho[s->g_lo + gl] * s->gt.kappa[s->g_lo + gl];
+    src[gl] = rk[gl] * ac * std::pow(s->p.T, 4) * dx;
+  }
+  for (int c = 0; c < N; ++c) {
+    const double *row = phi.data() + static_cast<size_t>(c) * Gl;
+    for (int gl = 0; gl < Gl; ++gl) {
+      ab[gl] += rk[gl] * row[gl] * dx;
+      sr[gl] += src[gl];
+    }
+  }
+  for (int gl = 0; gl < Gl; ++gl) {
+    double jin = 0., jout = 0.;
+    for (int i = 0; i < s->p.M; ++i) {
+      const double mu = s->mu[i];
+      if (mu < 0.) {
+        jout -= bnode(s, rows, i, gl, false, 0) * mu * s->wt[i];
+        jin -= bnode(s, rows, i, gl, true, 0) * mu * s->wt[i];
+      } else {
+        jin += bnode(s, rows, i, gl, false, 1) * mu * s->wt[i];
+        jout += bnode(s, rows, i, gl, true, 1) * mu * s->wt[i];
+      }
+    }
+    if (inflow) inflow[gl] = jin;
+    if (outflow_absorption) outflow_absorption[gl] = jout + ab[gl];
+    if (emission) emission[gl] = sr[gl];
   }
   return RT_OK;
 }

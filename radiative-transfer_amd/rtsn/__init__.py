@@ -7,6 +7,7 @@ creating a Solver without a gfx950 device raises RtError -- there is no CPU
 fallback in this package.
 """
 from .api import (  # noqa: F401
+    Comm,
     LIB_PATH,
     ParameterHandler,
     RtError,

@@ -121,6 +121,21 @@ def lib():
         L.rt_material_step.argtypes = [vp, C.c_int]
         L.rt_get_temperature.argtypes = [vp, dp]
         L.rt_get_cell_planck.argtypes = [vp, dp]
+        L.rt_get_shard.argtypes = [vp] + [C.POINTER(C.c_int)] * 6
+        L.rt_get_balance_partials.argtypes = [vp, dp, dp, dp]
+        L.rt_comm_unique_id.argtypes = [C.c_char_p]
+        L.rt_comm_init.argtypes = [C.c_int, C.c_int, C.c_char_p, C.c_int, C.POINTER(vp)]
+        L.rt_comm_destroy.argtypes = [vp]
+        L.rt_comm_destroy.restype = None
+        L.rt_comm_rank.argtypes = [vp, C.POINTER(C.c_int), C.POINTER(C.c_int)]
+        L.rt_comm_gather_moments.argtypes = [vp, vp, dp, dp, dp]
+        L.rt_comm_gather_group_ends.argtypes = [vp, vp, dp, dp]
+        L.rt_comm_gather_balance.argtypes = [vp, vp, dp, dp, dp]
+        L.rt_comm_gather_psi.argtypes = [vp, vp, C.c_int, dp]
+        L.rt_comm_allreduce_absorption.argtypes = [vp, vp, vp]
+        L.rt_comm_material_step.argtypes = [vp, vp, C.c_int]
+        L.rt_comm_last_error.argtypes = [vp]
+        L.rt_comm_last_error.restype = C.c_char_p
         L.rt_status_string.argtypes = [C.c_int]
         L.rt_status_string.restype = C.c_char_p
         L.rt_last_error.argtypes = [vp]
@@ -515,3 +530,95 @@ class Solver:
         t = C.c_longlong()
         _check(lib().rt_sweep_geometry(self._h, C.byref(wg), C.byref(t)), "rt_sweep_geometry", self._h)
         return wg.value, t.value
+
+
+def _shard(h) -> dict:
+    v = [C.c_int() for _ in range(6)]
+    _check(lib().rt_get_shard(h, *[C.byref(x) for x in v]), "rt_get_shard", h)
+    return dict(zip(("G", "M", "g_lo", "g_hi", "d_lo", "d_hi"), (x.value for x in v)))
+
+
+class Comm:
+    """rt_comm (include/rtsn.h, multi-GPU): an RCCL communicator joining the ranks' shard
+    handles, one process per GPU.  Every method is collective over the ranks.
+
+    uid = Comm.unique_id() on one rank, handed to the others (e.g. by torch.distributed's
+    broadcast_object_list or a file); Comm(nranks, rank, uid, device)."""
+
+    def __init__(self, nranks: int, rank: int, uid: bytes, device: int = 0):
+        assert len(uid) == 128
+        h = C.c_void_p()
+        st = lib().rt_comm_init(nranks, rank, uid, device, C.byref(h))
+        if st:
+            raise RtError(st, "rt_comm_init (" + lib().rt_comm_last_error(None).decode(errors="replace") + ")")
+        self._h = h
+
+    @staticmethod
+    def unique_id() -> bytes:
+        buf = C.create_string_buffer(128)
+        st = lib().rt_comm_unique_id(buf)
+        if st:
+            raise RtError(st, "rt_comm_unique_id (" + lib().rt_comm_last_error(None).decode(errors="replace") + ")")
+        return buf.raw
+
+    def _check(self, st, what):
+        if st:
+            raise RtError(st, f"{what} ({lib().rt_comm_last_error(self._h).decode(errors='replace')})")
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().rt_comm_destroy(self._h)
+            self._h = None
+
+    __del__ = close
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    @property
+    def rank(self):
+        n, r = C.c_int(), C.c_int()
+        self._check(lib().rt_comm_rank(self._h, C.byref(n), C.byref(r)), "rt_comm_rank")
+        return n.value, r.value
+
+    def gather_moments(self, solver: "Solver"):
+        """phi, F, phi_plus of all groups, (G, N) each, on every rank."""
+        sh = _shard(solver._h)
+        out = [np.empty((solver.N, sh["G"])) for _ in range(3)]
+        self._check(lib().rt_comm_gather_moments(self._h, solver._h, *[_dp(a) for a in out]), "rt_comm_gather_moments")
+        return tuple(a.T for a in out)
+
+    def gather_group_ends(self, solver: "Solver"):
+        G = _shard(solver._h)["G"]
+        left, right = np.empty(G), np.empty(G)
+        self._check(lib().rt_comm_gather_group_ends(self._h, solver._h, _dp(left), _dp(right)),
+                    "rt_comm_gather_group_ends")
+        return left, right
+
+    def gather_balance(self, solver: "Solver"):
+        """(balance, sources, sinks) of all groups."""
+        G = _shard(solver._h)["G"]
+        b, so, si = np.empty(G), np.empty(G), np.empty(G)
+        self._check(lib().rt_comm_gather_balance(self._h, solver._h, _dp(b), _dp(so), _dp(si)), "rt_comm_gather_balance")
+        return b, so, si
+
+    def gather_psi(self, solver: "Solver", root: int = 0):
+        """psi (M, G, N) of the whole configuration on `root` (None elsewhere)."""
+        sh = _shard(solver._h)
+        mine = self.rank[1] == root
+        psi = np.empty((solver.N, sh["G"], sh["M"])) if mine else None
+        ptr = _dp(psi) if mine else None
+        self._check(lib().rt_comm_gather_psi(self._h, solver._h, root, ptr), "rt_comm_gather_psi")
+        return psi.transpose(2, 1, 0) if mine else None
+
+    def allreduce_absorption(self, solver: "Solver", out):
+        """A(x) over all groups into the device tensor `out` (N doubles), stream-ordered."""
+        self._check(lib().rt_comm_allreduce_absorption(self._h, solver._h, C.c_void_p(out.data_ptr())),
+                    "rt_comm_allreduce_absorption")
+
+    def material_step(self, solver: "Solver", nsteps: int = 1):
+        """nsteps coupled steps with one all-reduce of q(x) per step on the handle's stream."""
+        self._check(lib().rt_comm_material_step(self._h, solver._h, int(nsteps)), "rt_comm_material_step")

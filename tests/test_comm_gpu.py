@@ -1,0 +1,84 @@
+"""RCCL behind the C ABI (include/rtsn.h "multi-GPU", csrc/rtsn_comm.hip) on the GPU box.
+
+The box has one GPU and RCCL refuses two ranks on one device, so the communicator runs
+with one rank here: every collective then goes through ncclCommInitRank, ncclAllGather /
+ncclAllReduce / ncclSend-Recv on the handle's stream and the gather assembly, and its
+result must equal the single handle's own getters bitwise.  The split logic across ranks
+(ragged group shards, direction shards) is covered by the world-size-2 gloo tests of the
+same layouts (tests/test_distributed.py) and by the driver's multi-GPU runs.
+"""
+import numpy as np
+import pytest
+
+from conftest import PRM_DIR
+
+pytestmark = pytest.mark.gpu
+
+
+def _params(oracle_mod, name="llnl_slab_test.prm", **over):
+    p = oracle_mod.parse_prm(PRM_DIR / name, table_dir=PRM_DIR)
+    p.update(over)
+    q = dict(p, bc_left_indicator=p["bc_left"], bc_right_indicator=p["bc_right"])
+    return q
+
+
+@pytest.fixture
+def comm(rtsn_mod):
+    with rtsn_mod.Comm(1, 0, rtsn_mod.Comm.unique_id(), 0) as c:
+        yield c
+
+
+@pytest.mark.parametrize("name", ["llnl_slab_test.prm", "multi_group_equilibrium.prm"])
+def test_world_one_gathers_equal_the_handle(rtsn_mod, oracle_mod, comm, name):
+    p = _params(oracle_mod, name)
+    with rtsn_mod.Solver(p) as s:
+        s.solve()
+        assert comm.rank == (1, 0)
+        for got, want in zip(comm.gather_moments(s), s.moments()):
+            assert np.array_equal(got, want)
+        for got, want in zip(comm.gather_group_ends(s), s.compute_group_ends()):
+            assert np.array_equal(got, want)
+        for got, want in zip(comm.gather_balance(s), s.compute_balance_terms()):
+            assert np.array_equal(got, want)
+        assert np.array_equal(comm.gather_psi(s, root=0), s.psi())
+
+
+def test_world_one_absorption_allreduce(rtsn_mod, oracle_mod, comm):
+    import torch
+    p = _params(oracle_mod)
+    with rtsn_mod.Solver(p) as s:
+        s.solve()
+        a = torch.zeros(p["N"], dtype=torch.float64, device="cuda")
+        b = torch.zeros_like(a)
+        s.group_absorption_device(a.data_ptr())
+        comm.allreduce_absorption(s, b)
+        s.synchronize()
+        assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("ts", [1, 3])
+def test_world_one_material_step(rtsn_mod, oracle_mod, comm, ts):
+    """rt_comm_material_step (sweep, all-reduce of q on the stream, update) equals
+    rt_material_step on an identical handle, bitwise."""
+    p = _params(oracle_mod, "multi_group_equilibrium.prm", ts_method=ts, V=0.0, N=300)
+    out = []
+    for use_comm in (False, True):
+        with rtsn_mod.Solver(p) as s:
+            s.material_enable(0.05, np.linspace(0.6, 1.4, p["N"]))  # out of equilibrium
+            if use_comm:
+                comm.material_step(s, 5)
+            else:
+                s.material_step(5)
+            out.append(s.temperature())
+    assert np.array_equal(out[0], out[1])
+    assert not np.array_equal(out[0], np.linspace(0.6, 1.4, p["N"]))
+
+
+def test_shards_must_tile(rtsn_mod, oracle_mod, comm):
+    """One rank holding groups [7, 70) of 124 does not tile the configuration."""
+    p = _params(oracle_mod)
+    with rtsn_mod.Solver(p, g_lo=7, g_hi=70) as s:
+        s.solve()
+        with pytest.raises(rtsn_mod.RtError) as e:
+            comm.gather_moments(s)
+        assert e.value.status == 3
