@@ -44,7 +44,9 @@ typedef enum {
   RT_ERR_DEVICE = 6,      /* HIP runtime error / no usable gfx950 device */
   RT_ERR_TIMEOUT = 7,     /* reserved (no in-kernel waits in this version) */
   RT_ERR_ARG = 8,         /* NULL handle / bad argument */
-  RT_ERR_STATE = 9        /* call not valid in the handle's mode (e.g. rt_advance with material coupling on) */
+  RT_ERR_STATE = 9,       /* call not valid in the handle's mode (e.g. rt_advance with material coupling on) */
+  RT_WARN_UNSTABLE = 10   /* a warning, not a failure: rt_material_enable turned coupling on, but its explicit
+                             emission step is above the stability limit (rt_material_stability) */
 } rt_status;
 
 /* Every .prm key (ParameterHandler.cpp:100-212) with the reference's meaning.
@@ -233,8 +235,16 @@ rt_status rt_sweep_geometry(rt_solver *s, int *workgroups, long long *tiles);
  * changes by exactly -dt x (net boundary outflow) per step (up to rounding).
  * Requires the v/c correction to be inactive (V == 0 or use_correction == 0). */
 /* Turn coupling on: rho_cv > 0 (material energy per volume per keV), T_cells
- * (N, host) the initial T(x), NULL for the uniform p.T.  The state psi is kept. */
+ * (N, host) the initial T(x), NULL for the uniform p.T.  The state psi is kept.
+ * Returns RT_WARN_UNSTABLE (coupling is on) when the explicit emission's stability
+ * number at the hottest cell exceeds 2 -- see rt_material_stability. */
 rt_status rt_material_enable(rt_solver *s, double rho_cv, const double *T_cells);
+/* Stability number of the explicit emission at the current T(x): linearising step 3
+ * around the hottest cell, T' = T - dt (W sum_g rho kappa_g dB_g/dT) / rho_cv T + ...,
+ * so forward-Euler stability needs  number = dt W sum_g rho kappa_g dB_g/dT(T_max) /
+ * rho_cv < 2  (W = sum of all quadrature weights, the sum over ALL G groups -- a shard
+ * reports the whole configuration's number).  Blocks (reads T(x) back). */
+rt_status rt_material_stability(rt_solver *s, double *number);
 /* Steps 1-2: one coupled sweep, then this handle's q into d_q (DEVICE, N
  * doubles; NULL: an internal buffer), on the handle's stream, asynchronous. */
 rt_status rt_material_sweep(rt_solver *s, double *d_q);
@@ -279,6 +289,9 @@ rt_status rt_comm_gather_balance(rt_comm *c, rt_solver *s, double *balance, doub
  * may pass NULL); moves M G_local N doubles per rank through the device, so meant for
  * .prm-sized runs (ψ of large runs stays sharded: rt_get_psi per rank). */
 rt_status rt_comm_gather_psi(rt_comm *c, rt_solver *s, int root, double *psi);
+/* Solver-owned psi_source (M*G, m*G+g) of all directions on every rank (direction shards
+ * hold their rows only; rt_get_psi_source). */
+rt_status rt_comm_gather_psi_source(rt_comm *c, rt_solver *s, double *psi_source);
 /* The group-summed absorption A(x) = sum over ALL groups of rho kappa_g phi_g(x): each
  * rank's rt_group_absorption_device, then one ncclAllReduce(sum) of N doubles into the
  * DEVICE buffer d_out, stream-ordered, no host synchronisation. */

@@ -1003,6 +1003,34 @@ static rt_status material_planck(rt_solver *s) {
   return RT_OK;
 }
 
+// dt W sum_g rho kappa_g dB_g/dT(T_max) / rho_cv over all G groups (rt_material_stability)
+static double material_stability_number(const rt_solver *s, double T_max) {
+  const int G = s->p.G;
+  std::vector<double> lo(s->gt.e_edge.begin(), s->gt.e_edge.begin() + G), hi(s->gt.e_edge.begin() + 1,
+                                                                             s->gt.e_edge.begin() + G + 1);
+  std::vector<double> B(G, 0.0), dB(G, 0.0), mu(s->M_full), wt(s->M_full);
+  if (T_max > 0.0) phys::PlanckIntegrator().group_integrals(T_max, G, lo.data(), hi.data(), B.data(), dB.data());
+  phys::gauss_legendre(s->M_full, phys::kFourPi, mu.data(), wt.data());
+  double W = 0.0, sum = 0.0;
+  for (double w : wt) W += w;
+  for (int g = 0; g < G; ++g) sum += s->gt.rho[g] * s->gt.kappa[g] * dB[g] * phys::kBoltzmannJPK;
+  return s->p.dt * W * sum / s->rho_cv;
+}
+
+extern "C" rt_status rt_material_stability(rt_solver *s, double *number) {
+  if (!s || !number) return fail(s, RT_ERR_ARG, "rt_material_stability: bad argument");
+  if (!s->material) return fail(s, RT_ERR_STATE, "rt_material_stability: material coupling is off");
+  HIP_TRY(s, hipSetDevice(s->device));
+  std::vector<double> T(s->p.N);
+  HIP_TRY(s, hipMemcpyAsync(T.data(), s->Tcell.p, sizeof(double) * T.size(), hipMemcpyDeviceToHost, s->stream));
+  HIP_TRY(s, hipStreamSynchronize(s->stream));
+  double T_max = 0.0;
+  for (double t : T)
+    if (std::isfinite(t)) T_max = std::max(T_max, t);
+  *number = material_stability_number(s, T_max);
+  return RT_OK;
+}
+
 extern "C" rt_status rt_material_enable(rt_solver *s, double rho_cv, const double *T_cells) {
   if (!s) return fail(nullptr, RT_ERR_ARG, "rt_material_enable: NULL handle");
   if (!(rho_cv > 0.0) || !std::isfinite(rho_cv)) return fail(s, RT_ERR_ARG, "rt_material_enable: rho_cv must be > 0");
@@ -1065,6 +1093,16 @@ extern "C" rt_status rt_material_enable(rt_solver *s, double rho_cv, const doubl
   if ((st = material_planck(s))) return st;
   HIP_TRY(s, hipStreamSynchronize(s->stream));  // T0 dies at return
   s->material = true;
+  double T_max = 0.0;
+  for (double t : T0)
+    if (std::isfinite(t)) T_max = std::max(T_max, t);
+  const double number = material_stability_number(s, T_max);
+  if (number > 2.0) {
+    char msg[160];
+    std::snprintf(msg, sizeof(msg), "explicit emission stability number %.4g > 2 at T_max = %.4g keV: "
+                                    "reduce dt or raise rho_cv", number, T_max);
+    return fail(s, RT_WARN_UNSTABLE, msg);
+  }
   return RT_OK;
 }
 
@@ -1614,6 +1652,7 @@ extern "C" const char *rt_status_string(rt_status st) {
     case RT_ERR_TIMEOUT: return "timeout (reserved)";
     case RT_ERR_ARG: return "bad argument";
     case RT_ERR_STATE: return "not valid in the handle's mode";
+    case RT_WARN_UNSTABLE: return "warning: explicit emission above its stability limit";
   }
   return "unknown";
 }

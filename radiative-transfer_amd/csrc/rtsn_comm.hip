@@ -341,6 +341,46 @@ extern "C" rt_status rt_comm_gather_psi(rt_comm *c, rt_solver *s, int root, doub
   return RT_OK;
 }
 
+extern "C" rt_status rt_comm_gather_psi_source(rt_comm *c, rt_solver *s, double *out) {
+  if (!c || !s || !out) return cfail(c, RT_ERR_ARG, "rt_comm_gather_psi_source: bad argument");
+  HC_TRY(c, hipSetDevice(c->device));
+  std::vector<Shard> sh;
+  int mode = 0;
+  if (rt_status st = all_shards(c, s, sh, mode)) return st;
+  const Shard &me = sh[c->rank];
+  const int G = me.G, M = me.M, H = M / 2;
+  if (mode == 0) {  // every group shard holds all M x G rows (the table covers all groups)
+    RT_TRY(c, s, rt_get_psi_source(s, out));
+    return RT_OK;
+  }
+  // direction shards: rows m of the shard's (M_l, G) table, ascending mu, into the (M, G) table
+  int Hm = 0;
+  for (const Shard &a : sh) Hm = std::max(Hm, a.d_hi - a.d_lo);
+  const size_t cnt = static_cast<size_t>(2) * Hm * G;
+  std::vector<double> mine(cnt, 0.0);
+  RT_TRY(c, s, rt_get_psi_source(s, mine.data()));
+  hipStream_t st = static_cast<hipStream_t>(rt_stream(s));
+  Scratch buf;
+  buf.st = st;
+  HC_TRY(c, hipMalloc(&buf.p, sizeof(double) * cnt * (c->nranks + 1)));
+  double *d = static_cast<double *>(buf.p);
+  HC_TRY(c, hipMemcpyAsync(d, mine.data(), sizeof(double) * cnt, hipMemcpyHostToDevice, st));
+  NC_TRY(c, ncclAllGather(d, d + cnt, cnt, ncclFloat64, c->nc, st));
+  std::vector<double> all(cnt * c->nranks);
+  HC_TRY(c, hipMemcpyAsync(all.data(), d + cnt, sizeof(double) * all.size(), hipMemcpyDeviceToHost, st));
+  HC_TRY(c, hipStreamSynchronize(st));
+  for (int r = 0; r < c->nranks; ++r) {
+    const Shard &a = sh[r];
+    const int n = a.d_hi - a.d_lo;
+    const double *src = all.data() + cnt * r;
+    for (int k = 0; k < 2 * n; ++k) {  // shard row k -> global direction (see rt_create_direction_shard)
+      const int i = k < n ? H - a.d_hi + k : H + a.d_lo + (k - n);
+      std::copy(src + static_cast<size_t>(k) * G, src + static_cast<size_t>(k + 1) * G, out + static_cast<size_t>(i) * G);
+    }
+  }
+  return RT_OK;
+}
+
 extern "C" rt_status rt_comm_allreduce_absorption(rt_comm *c, rt_solver *s, double *d_out) {
   if (!c || !s || !d_out) return cfail(c, RT_ERR_ARG, "rt_comm_allreduce_absorption: bad argument");
   HC_TRY(c, hipSetDevice(c->device));

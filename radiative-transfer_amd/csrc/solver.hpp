@@ -21,6 +21,15 @@ class SolverError : public std::runtime_error {
   rt_status status;
 };
 
+// One rank of a multi-GPU job (one process per GPU): the ranks split the groups into
+// contiguous shards (or, with fewer groups than ranks, the direction pairs) and join
+// their handles with an RCCL communicator (include/rtsn.h, rt_comm_*).  comm_id is the
+// RT_COMM_ID_BYTES unique id rt_comm_unique_id made on one rank, handed to all.
+struct Ranks {
+  int nranks = 1, rank = 0;
+  const void *comm_id = nullptr;
+};
+
 class Solver {
  public:
   // log: where the reference's solver-side messages go (its cout prints:
@@ -28,6 +37,11 @@ class Solver {
   // in the reference's formats; nullptr = quiet.
   Solver(rtamd::ParameterHandler &parameter_handler, std::vector<double> &psi_mat, std::vector<double> &phi,
          std::vector<double> &F, int device = 0, std::ostream *log = nullptr);
+  // Multi-GPU: this rank's shard on `device`.  Every member below is then collective
+  // (all ranks call it, in the same order); the result arrays (phi, F, phi_plus,
+  // balance, group ends) hold ALL groups on every rank, psi_mat only on rank 0.
+  Solver(rtamd::ParameterHandler &parameter_handler, std::vector<double> &psi_mat, std::vector<double> &phi,
+         std::vector<double> &F, int device, std::ostream *log, const Ranks &ranks);
   ~Solver();
   Solver(const Solver &) = delete;
   Solver &operator=(const Solver &) = delete;
@@ -44,9 +58,12 @@ class Solver {
   void get_ends(const std::string &side, std::vector<double> &group_ends) const;  // :853-864
 
   rt_solver *handle() { return h_; }
+  rt_comm *comm() { return comm_; }
 
  private:
   void check(rt_status st, const char *what) const;
+  void create(int device, const Ranks &ranks);
+  void moments(double *phi, double *F, double *phi_plus);
   void refresh_psi();
   void print_constructor() const;
   bool validation_report() const;  // Correction::validate_correction with its prints
@@ -56,6 +73,8 @@ class Solver {
   int M_, G_, N_;
   std::ostream *log_ = nullptr;
   rt_solver *h_ = nullptr;
+  rt_comm *comm_ = nullptr;  // multi-GPU only
+  int rank_ = 0;
 };
 
 }  // namespace rt

@@ -18,7 +18,7 @@ HEADER = REPO_ROOT / "include" / "rtsn.h"
 
 STATUS = {0: "ok", 1: "io error", 2: "parse error", 3: "invalid parameter", 4: "correction validation failed",
           5: "out of memory", 6: "device error", 7: "timeout (reserved)", 8: "bad argument",
-          9: "not valid in the handle's mode"}
+          9: "not valid in the handle's mode", 10: "warning: explicit emission above its stability limit"}
 
 
 class RtError(RuntimeError):
@@ -119,6 +119,7 @@ def lib():
         L.rt_material_sweep.argtypes = [vp, vp]
         L.rt_material_update.argtypes = [vp, vp]
         L.rt_material_step.argtypes = [vp, C.c_int]
+        L.rt_material_stability.argtypes = [vp, dp]
         L.rt_get_temperature.argtypes = [vp, dp]
         L.rt_get_cell_planck.argtypes = [vp, dp]
         L.rt_get_shard.argtypes = [vp] + [C.POINTER(C.c_int)] * 6
@@ -132,6 +133,7 @@ def lib():
         L.rt_comm_gather_group_ends.argtypes = [vp, vp, dp, dp]
         L.rt_comm_gather_balance.argtypes = [vp, vp, dp, dp, dp]
         L.rt_comm_gather_psi.argtypes = [vp, vp, C.c_int, dp]
+        L.rt_comm_gather_psi_source.argtypes = [vp, vp, dp]
         L.rt_comm_allreduce_absorption.argtypes = [vp, vp, vp]
         L.rt_comm_material_step.argtypes = [vp, vp, C.c_int]
         L.rt_comm_last_error.argtypes = [vp]
@@ -425,8 +427,19 @@ class Solver:
         T = None if T_cells is None else np.ascontiguousarray(T_cells, dtype=np.float64)
         if T is not None and T.size != self.N:
             raise ValueError("material_enable: T_cells must hold N values")
-        _check(lib().rt_material_enable(self._h, float(rho_cv), None if T is None else _dp(T)),
-               "rt_material_enable", self._h)
+        st = lib().rt_material_enable(self._h, float(rho_cv), None if T is None else _dp(T))
+        if st == 10:  # RT_WARN_UNSTABLE: coupling is on, above the explicit emission's limit
+            import warnings
+            warnings.warn(lib().rt_last_error(self._h).decode(errors="replace"), RuntimeWarning, stacklevel=2)
+        else:
+            _check(st, "rt_material_enable", self._h)
+        return self.material_stability()
+
+    def material_stability(self) -> float:
+        """dt W sum_g rho kappa_g dB_g/dT(T_max) / rho_cv: < 2 for a stable explicit emission."""
+        v = C.c_double()
+        _check(lib().rt_material_stability(self._h, C.byref(v)), "rt_material_stability", self._h)
+        return v.value
 
     @staticmethod
     def _device_vec(t, n: int, what: str):

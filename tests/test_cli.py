@@ -106,11 +106,18 @@ def _run_tree(tmp_path: Path) -> Path:
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("ranks", [None, "1"])
 @pytest.mark.parametrize("name", ["llnl_slab_test", "single_group"])
-def test_transfer_csv_files(oracle_mod, tmp_path, name):
+def test_transfer_csv_files(oracle_mod, tmp_path, name, ranks):
+    """The eight CSV files byte for byte; ranks "1": RTSN_RANKS=1 runs the multi-GPU path
+    (a forked rank, its handle joined by a one-rank RCCL communicator, every result
+    gathered through rt_comm_*) -- the one-GPU box's check of the code the N-GPU CLI runs."""
     run = _run_tree(tmp_path)
     prm = f"../prm/{name}.prm"
-    r = subprocess.run([str(_bin("transfer")), prm], cwd=run, capture_output=True, text=True, timeout=600)
+    env = dict(os.environ)
+    if ranks:
+        env["RTSN_RANKS"] = ranks
+    r = subprocess.run([str(_bin("transfer")), prm], cwd=run, capture_output=True, text=True, timeout=600, env=env)
     assert r.returncode == 0, r.stderr
     assert r.stdout.startswith(f"filename: {prm}\n")
 
@@ -180,12 +187,17 @@ def expected_solver_log(q: dict, orc) -> str:
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("ranks", [None, "1"])
 @pytest.mark.parametrize("name", ["llnl_slab_test", "multi_group_equilibrium"])
-def test_transfer_stdout(oracle_mod, tmp_path, name):
-    """transfer prints what the reference prints, in its formats."""
+def test_transfer_stdout(oracle_mod, tmp_path, name, ranks):
+    """transfer prints what the reference prints, in its formats (also through the
+    multi-GPU path with one rank)."""
     run = _run_tree(tmp_path)
     prm = f"../prm/{name}.prm"
-    r = subprocess.run([str(_bin("transfer")), prm], cwd=run, capture_output=True, text=True, timeout=600)
+    env = dict(os.environ)
+    if ranks:
+        env["RTSN_RANKS"] = ranks
+    r = subprocess.run([str(_bin("transfer")), prm], cwd=run, capture_output=True, text=True, timeout=600, env=env)
     assert r.returncode == 0, r.stderr
     q = oracle_mod.parse_prm(str(run / prm), table_dir=str(tmp_path / "prm") + "/")
     orc = oracle_mod.OracleSolver(q)

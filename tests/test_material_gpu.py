@@ -332,3 +332,34 @@ def test_material_mode_errors(rtsn_mod, oracle_mod):
         with pytest.raises(rtsn_mod.RtError) as e:
             s.material_enable(2.0)
         assert e.value.status == 3
+    with rtsn_mod.Solver(p, d_lo=0, d_hi=1) as s:  # a direction-pair shard holds part of q as well
+        s.material_enable(2.0)
+        with pytest.raises(rtsn_mod.RtError) as e:
+            s.material_step(1)
+        assert e.value.status == 9
+
+
+def test_material_stability_number(rtsn_mod, oracle_mod):
+    """rt_material_stability = dt W sum_g rho kappa_g dB_g/dT(T_max) / rho_cv over all groups
+    (W = the quadrature's weight sum, the host Planck table at the hottest cell), and rt_material_enable warns
+    (RT_WARN_UNSTABLE, coupling on) above 2: a shard reports the whole configuration's."""
+    import warnings
+    p = to_rt(params(oracle_mod, G=4))
+    orc = oracle_mod.OracleSolver(params(oracle_mod, G=4))
+    e = orc.groups()["e_edge"]
+    T = np.linspace(0.5, 1.5, p["N"])
+    _, dB = rtsn_mod.planck_groups(1.5, e)
+    W = orc.quad()[1].sum()  # the reference's 4 pi (pi = 3.1415926546, GLQuad.cpp)
+    want = p["dt"] * W * (p["rho"] * orc.groups()["kappa"] * dB).sum()
+    for lo, hi in ((0, 4), (1, 3)):
+        with rtsn_mod.Solver(p, g_lo=lo, g_hi=hi) as s:
+            with warnings.catch_warnings():
+                warnings.simplefilter("error")
+                got = s.material_enable(want, T)  # number = 1
+            assert got == pytest.approx(1.0, rel=1e-12)
+            assert s.material_stability() == pytest.approx(1.0, rel=1e-12)
+    with rtsn_mod.Solver(p) as s:
+        with pytest.warns(RuntimeWarning, match="stability number"):
+            got = s.material_enable(want / 3.0, T)
+        assert got == pytest.approx(3.0, rel=1e-12)
+        s.material_step(1)  # coupling is on
