@@ -79,54 +79,91 @@ def slab_params(G_total: int, variant: str, N: int = 1_000_000, M: int = 64) -> 
                 group_kappa=kap[(np.arange(G_total) * len(kap)) // G_total])
 
 
+def host_cpus() -> dict:
+    """The host the CPU baseline runs on: model, os.cpu_count(), the process's CPU affinity,
+    the cgroup CPU quota (cpu.max) and OMP_NUM_THREADS -- and the threads used: the
+    lease's CPU share, i.e. OMP_NUM_THREADS where the pool sets it (16 per GPU on the
+    GPU box, whose affinity lists the whole machine), capped by the affinity and quota."""
+    info = {"cpu_model": "unknown", "nproc": os.cpu_count(), "affinity": len(os.sched_getaffinity(0)),
+            "cgroup_quota_cpus": None, "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
+    try:  # SURVEY §8(d): name the host CPU the baseline ran on
+        info["cpu_model"] = next(l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo")
+                                 if l.startswith("model name"))
+    except (OSError, StopIteration):
+        pass
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            info["cgroup_quota_cpus"] = int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    threads = info["affinity"]
+    if info["omp_num_threads"]:
+        threads = min(threads, max(1, int(info["omp_num_threads"])))
+    if info["cgroup_quota_cpus"]:
+        threads = min(threads, max(1, int(info["cgroup_quota_cpus"])))
+    info["threads"] = threads
+    return info
+
+
 def cpu_baseline(variant: str) -> dict:
-    """The C oracle (the reference's algorithm restated, solver.cpp loop order) on bounded
-    samples of the SL workload: all 64 angles, N = 250000 cells, 1 BDF2 step, for 1 group
-    on 1 thread and for one group per thread with OpenMP over the lines of each direction
-    on up to 16 host cores (the GPU box's CPU share)."""
+    """The C oracle (the reference's algorithm restated, solver.cpp loop order, gcc -O3) on
+    a bounded sample of the SL workload -- all 64 angles, N = 200000 cells, 1 BDF2 step --
+    on the lease's CPU share (host_cpus):
+      value: 16 groups (1024 lines), every line of a substep in one OpenMP loop with
+             per-line prev/half snapshots (orc_set_line_parallel: same values);
+      reference_shaped_value: the same sample in the reference's shape -- lines of one
+             direction in parallel, the whole-array prev/half copies (solver.cpp:620-625,
+             733, its one surviving copy) in between;
+      single_thread_value: 1 group on 1 thread."""
     sys.path.insert(0, str(REPO / "oracle"))
     import oracle
     oracle.build()
-    G, N = 128, 250_000
+    host = host_cpus()
+    T = host["threads"]
+    G, N = 128, 200_000
     p = slab_params(G, variant, N=N)
     q = dict(p)
     q.update(bc_left=p["bc_left_indicator"], bc_right=p["bc_right_indicator"], dx=p["X"] / N,
              have_group_bounds=0, have_group_kappa=1, prm_found=1)
 
-    def timed(g_lo, g_hi, threads):
+    def timed(g_lo, g_hi, threads, lines):
         s = oracle.OracleSolver(q, g_lo=g_lo, g_hi=g_hi)
         s.set_threads(threads)
+        s.set_line_parallel(lines)
         t0 = time.perf_counter()
         s.solve()
         return 4.0 * q["M"] * N * (g_hi - g_lo), time.perf_counter() - t0
 
-    u1, t1 = timed(64, 65, 1)
-    cores = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", "16")), len(os.sched_getaffinity(0))))
-    un, tn = timed(64 - cores // 2, 64 - cores // 2 + cores, cores)
-    model = "unknown"
-    try:  # SURVEY §8(d): name the host CPU the baseline ran on
-        model = next(l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name"))
-    except (OSError, StopIteration):
-        pass
-    return {"value": un / tn, "unit": "cell-angle-group updates/s", "cores": cores, "kind": "port",
-            "cpu_model": model, "host_cpus": os.cpu_count(),
-            "single_thread_value": u1 / t1,
-            "sample": f"oracle/rt_oracle.c (restatement of solver.cpp, gcc -O2), SL {variant}: M=64, N={N}, "
-                      f"1 BDF2 step; {cores} groups on {cores} OpenMP threads = {un:.3g} updates in {tn:.2f} s; "
-                      f"1 group on 1 thread = {u1:.3g} updates in {t1:.2f} s"}
+    u1, t1 = timed(64, 65, 1, False)
+    un, tn = timed(56, 72, T, True)
+    ur, tr = timed(56, 72, T, False)
+    return dict({"value": un / tn, "unit": "cell-angle-group updates/s", "cores": T, "kind": "port",
+                 "reference_shaped_value": ur / tr, "single_thread_value": u1 / t1,
+                 "sample": f"oracle/rt_oracle.c (restatement of solver.cpp, gcc -O3), SL {variant}: M=64, N={N}, "
+                           f"1 BDF2 step; 16 groups (1024 lines) on {T} OpenMP threads, line-parallel = "
+                           f"{un:.3g} updates in {tn:.2f} s; the same in the reference's shape (direction by "
+                           f"direction, whole-array snapshot copies) {tr:.2f} s; 1 group on 1 thread = {u1:.3g} "
+                           f"updates in {t1:.2f} s"}, **host)
 
 
 REFERENCE_CONFIGS = ("single_group.prm", "multi_group_equilibrium.prm", "llnl_slab_test.prm",
                      "llnl_slab_test_uncapped.prm")
 
 
-def reference_config_timings() -> dict:
+def reference_config_timings(rate_steps: int = 1000) -> dict:
     """BASELINE.json's small configs (the reference's own .prm files, SURVEY §8(d) SG, EQ,
-    LL, LL-uncapped) end to end -- create + solve + moments on the GPU, and the oracle
-    (the reference's loop order) on one core -- with the GPU's phi checked against the
-    oracle's (max per-group relative difference).  For llnl_slab_test also the oracle with
-    the reference's literal per-cell half_ends copy (solver.cpp:733, quadratic in the
-    state size)."""
+    LL, LL-uncapped):
+      * end to end at the .prm's own length -- create + solve + moments on the GPU, and
+        the oracle (the reference's loop order) on one core -- with the GPU's phi checked
+        against the oracle's (max per-group relative difference); for llnl_slab_test also
+        the oracle with the reference's literal per-cell half_ends copy (solver.cpp:733,
+        quadratic in the state size);
+      * as a rate: `rate_steps` BDF2 steps of the same configuration (handle created and
+        warmed outside the timer; advance + finish + device sync timed), GPU BDF2 steps/s
+        and updates/s beside the oracle's on one core over the same steps, with the
+        number of sweep passes (HIP event pairs) the GPU ran -- the metric's named config,
+        llnl_slab_test, among them."""
     import rtsn
     sys.path.insert(0, str(REPO / "oracle"))
     import oracle
@@ -153,6 +190,35 @@ def reference_config_timings() -> dict:
             r["cpu_literal_half_copy_ms" if literal else "cpu_ms"] = 1e3 * (time.perf_counter() - t0)
         scale = np.maximum(np.abs(phi_o).max(axis=1, keepdims=True), 1e-300)
         r["phi_max_rel_diff"] = float((np.abs(phi - phi_o) / scale).max())
+
+        # the rate over rate_steps BDF2 steps
+        params = dict(ph.params, max_timesteps=rate_steps)
+        upd_step = (4.0 if q["ts_method"] == 3 else 1.0) * q["M"] * q["G"] * q["N"]
+        with rtsn.Solver(params) as s:  # warm: kernels loaded, equilibrium sources built
+            s.advance(16)
+            s.finish()
+            s.synchronize()
+        with rtsn.Solver(params) as s:
+            s.set_profiling(True)
+            s.synchronize()
+            t0 = time.perf_counter()
+            s.advance(rate_steps)
+            s.finish()
+            s.synchronize()
+            gpu_s = time.perf_counter() - t0
+            passes = s.sweep_time()[1]
+            s.set_profiling(False)
+            finite = s.state_finite()
+            tb = s.time_block
+        o = oracle.OracleSolver(dict(q, max_timesteps=rate_steps))
+        t0 = time.perf_counter()
+        o.solve()
+        cpu_s = time.perf_counter() - t0
+        r["rate"] = {"steps": rate_steps, "gpu_bdf2_steps_per_s": rate_steps / gpu_s,
+                     "cpu_bdf2_steps_per_s": rate_steps / cpu_s, "gpu_updates_per_s": upd_step * rate_steps / gpu_s,
+                     "cpu_updates_per_s": upd_step * rate_steps / cpu_s, "gpu_ms": 1e3 * gpu_s, "cpu_ms": 1e3 * cpu_s,
+                     "gpu_sweep_passes": passes, "time_block": tb, "state_finite": finite,
+                     "cpu": "oracle, 1 thread, the reference's loop order"}
         out[name] = r
     return out
 
@@ -453,25 +519,50 @@ def side_leg(p: dict, info, world: int, device, local: int, scaling: str, tb: in
     return out
 
 
-def run_material(p: dict, info, world: int, device, local: int, steps: int, dirs=None) -> dict:
+def material_params(p: dict) -> dict:
+    """The material leg's configuration from the sweep's: BE, and the v/c correction
+    inactive (V = 0) as rt_material_enable requires -- for either SL variant."""
+    return dict(p, ts_method=1, V=0.0)
+
+
+def run_material(p: dict, info, world: int, device, local: int, steps: int, dirs=None, rank: int = 0) -> dict:
     """The material-temperature coupling (rt_material_*, beyond the reference) on
     the same SL shard: BE steps (the reference's BDF2 diverges on SL within a few
-    steps, DESIGN.md §4, which would leave T meaningless) from T = 1 keV, each
-    step = coupled sweep + phi + the shard's q(x) + ONE all-reduce (sum) of q
-    over the ranks (RCCL on the GPU box) + T update + per-cell Planck.  One
-    warm-up step, then `steps` timed between barrier + device sync, max over
-    ranks.  Host-synchronised around the all-reduce (coupled_steps(host_sync=True))."""
+    steps, DESIGN.md §4, which would leave T meaningless; the v/c correction off, as
+    the coupling requires) from T = 1 keV, each step = coupled sweep + phi + the
+    shard's q(x) + ONE all-reduce (sum) of q over the ranks + T update + per-cell
+    Planck.  The all-reduce is RCCL behind the C ABI (rt_comm_material_step: enqueued
+    on the handle's stream, no host synchronisation); where RCCL cannot form the
+    communicator (the one-GPU multi-rank rehearsal: two ranks on one device) the
+    same step runs with torch.distributed's all-reduce on the handle's stream
+    (rtsn.coupling.coupled_steps).  One warm-up step, then `steps` timed between
+    barrier + device sync, max over ranks."""
     import torch
     import torch.distributed as dist
     import rtsn
     from rtsn.coupling import coupled_steps
 
     G_total, g_lo, g_hi = info
-    q = dict(p, ts_method=1)
+    q = material_params(p)
+    comm, path = None, "rt_comm_material_step (RCCL in librtsn, stream-ordered)"
+    try:
+        uid = [rtsn.Comm.unique_id() if rank == 0 else None]
+        if world > 1:
+            dist.broadcast_object_list(uid, src=0)
+        comm = rtsn.Comm(world, rank, uid[0], local)
+    except rtsn.RtError as e:
+        path = f"torch.distributed all-reduce on the handle's stream (rt_comm unavailable: {e})"
     with make_solver(q, local, info, dirs) as s:  # q(x): each rank's groups or directions, summed
-        s.material_enable(1.0)
+        number = s.material_enable(1.0)
         buf = torch.zeros(q["N"], dtype=torch.float64, device=device)
-        coupled_steps(s, 1, buf, world_size=world, host_sync=True)
+
+        def step(n):
+            if comm is not None:
+                comm.material_step(s, n)
+            else:
+                coupled_steps(s, n, buf, world_size=world)
+
+        step(1)
 
         def barrier():
             s.synchronize()
@@ -481,23 +572,26 @@ def run_material(p: dict, info, world: int, device, local: int, steps: int, dirs
 
         barrier()
         t0 = time.perf_counter()
-        coupled_steps(s, steps, buf, world_size=world, host_sync=True)
+        step(steps)
         barrier()
         wall = time.perf_counter() - t0
         T = s.temperature()
+        M_local = s.M  # the handle's directions (a direction shard holds 2 (d_hi - d_lo))
+    if comm is not None:
+        comm.close()
     t = torch.tensor([wall], dtype=torch.float64, device=device)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     wall = float(t[0])
-    u = torch.tensor([float(q["M"]) * (g_hi - g_lo) * q["N"] * steps], dtype=torch.float64, device=device)
+    u = torch.tensor([float(M_local) * (g_hi - g_lo) * q["N"] * steps], dtype=torch.float64, device=device)
     if world > 1:
         dist.all_reduce(u)
     upd = float(u[0])
     return {"what": "material-temperature coupling (beyond the reference): BE step with per-cell Planck "
                     "emission, q(x) all-reduce over ranks, T update",
             "ts_method": 1, "steps": steps, "warmup": 1, "ms_per_step": 1e3 * wall / steps,
-            "updates_per_s": upd / wall, "allreduce_bytes_per_step": 8 * q["N"],
-            "rho_cv": 1.0, "T_range_keV": [float(T.min()), float(T.max())],
+            "updates_per_s": upd / wall, "allreduce_bytes_per_step": 8 * q["N"], "allreduce": path,
+            "stability_number": number, "rho_cv": 1.0, "T_range_keV": [float(T.min()), float(T.max())],
             "state_finite": bool(np.isfinite(T).all())}
 
 
@@ -582,7 +676,7 @@ def main():
                                             f"{5.994 if other == 'corr' else 0.0}, v/c correction "
                                             f"{'on' if other == 'corr' else 'inactive'}), same timing", dirs)
     if args.material_steps > 0:
-        line["material"] = run_material(p, info, world, device, local, args.material_steps, dirs)
+        line["material"] = run_material(p, info, world, device, local, args.material_steps, dirs, rank)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(args.variant)
         line["reference_config"] = reference_config_timings()

@@ -64,6 +64,8 @@ def lib():
         L.orc_run_substeps.argtypes = [C.c_void_p, C.c_int, C.c_int]
         L.orc_set_threads.argtypes = [C.c_void_p, C.c_int]
         L.orc_set_threads.restype = None
+        L.orc_set_line_parallel.argtypes = [C.c_void_p, C.c_int]
+        L.orc_set_line_parallel.restype = None
         L.orc_num_groups_local.argtypes = [C.c_void_p]
         for name in ("orc_get_psi", "orc_get_ends", "orc_set_ends", "orc_get_psi_source"):
             getattr(L, name).argtypes = [C.c_void_p, dp]
@@ -171,6 +173,10 @@ class OracleSolver:
         if h:
             lib().orc_destroy(h)
             self._h = None
+
+    def set_line_parallel(self, on: bool = True):
+        """CPU baseline: all lines of a substep in one OpenMP loop, per-line snapshots."""
+        lib().orc_set_line_parallel(self._h, 1 if on else 0)
 
     def set_threads(self, n: int):
         """OpenMP threads over the lines of a direction (results do not depend on it)."""

@@ -537,6 +537,8 @@ struct orc_solver {
   double dx, dt;
   int literal_half;
   int threads;        /* OpenMP threads over the lines of a direction (orc_set_threads); 1 = serial */
+  int line_parallel;  /* CPU baseline: all lines of a substep in one parallel loop, per-line snapshots */
+  int par_copies;     /* CPU baseline: the whole-array snapshot copies split over the threads */
   double ac;          /* RADIATION_CONSTANT_A * c (solver.h:29, correction.h:25) */
   double *mu, *wt;
   double *e_edge, *e_ave, *de_ave;
@@ -677,6 +679,7 @@ static void *xcalloc(size_t n, size_t sz, int *ok) {
 
 /* Solver::Solver (solver.cpp:46-188) */
 void orc_set_threads(orc_solver *s, int threads) { s->threads = threads > 0 ? threads : 1; }
+void orc_set_line_parallel(orc_solver *s, int on) { s->line_parallel = on; s->par_copies = on; }
 
 orc_solver *orc_create(const orc_params *pin, int half_copy_literal, int g_lo, int g_hi, int *status) {
   *status = ORC_OK;
@@ -992,19 +995,68 @@ static int sweep_line(orc_solver *s, int it, int i, int gl, int *half_pending) {
   return ORC_OK;
 }
 
+/* memcpy split over the OpenMP threads (same bytes, same result) */
+static void par_copy(void *dst, const void *src, size_t bytes, int threads) {
+  if (threads <= 1) {
+    memcpy(dst, src, bytes);
+    return;
+  }
+#pragma omp parallel for schedule(static) num_threads(threads)
+  for (int t = 0; t < threads; ++t) {
+    size_t lo = bytes * (size_t)t / (size_t)threads, hi = bytes * (size_t)(t + 1) / (size_t)threads;
+    memcpy((char *)dst + lo, (const char *)src + lo, hi - lo);
+  }
+}
+
+/* one line's nodes dst(i, gl, :, :) = src(i, gl, :, :) */
+static void copy_line(const orc_solver *s, double *dst, const double *src, int i, int gl) {
+  for (int side = 0; side < 2; ++side)
+    for (int c = 0; c < s->N; ++c) {
+      size_t k = (size_t)i + (size_t)s->M * ((size_t)gl + (size_t)s->Gl * ((size_t)c + (size_t)s->N * side));
+      dst[k] = src[k];
+    }
+}
+
+/* The CPU baseline's line-parallel form of one solve() iteration (orc_set_line_parallel):
+ * with no reflective boundary every (i, g) line of a substep is independent, so all M Gl
+ * lines share one parallel loop, each taking its own slices of the prev (:620-625) and
+ * half (:733) snapshots -- the half snapshot of a line is its state after the CN substep
+ * for mu < 0, and before it for mu > 0 (the last mu < 0 CN cell's copy, which is what
+ * survives) -- instead of the reference's whole-array copies.  Same values. */
+static int solve_iteration_lines(orc_solver *s, int it) {
+  const int M = s->M, ts = s->p.ts_method;
+  corr_compute(s);
+  if (s->p.include_validation && !corr_validate(s)) return ORC_ERR_VALIDATION;
+  memcpy(s->B, s->cB, sizeof(double) * s->G);
+  const int prev = ts != 3 || it % 4 == 0, half = ts == 3 && it % 4 == 1;
+  int err = 0;
+#pragma omp parallel for collapse(2) schedule(dynamic, 1) num_threads(s->threads) reduction(| : err)
+  for (int i = 0; i < M; ++i)
+    for (int gl = 0; gl < s->Gl; ++gl) {
+      const int neg = s->mu[i] < 0.;
+      int hp = 0;
+      if (prev) copy_line(s, s->prev_ends, s->ends, i, gl);
+      if (half && !neg) copy_line(s, s->half_ends, s->ends, i, gl);
+      err |= sweep_line(s, it, i, gl, &hp);
+      if (half && neg) copy_line(s, s->half_ends, s->ends, i, gl);
+    }
+  return err ? ORC_ERR_PARAM : ORC_OK;
+}
+
 static int solve_iteration(orc_solver *s, int it) {
+  if (s->line_parallel && s->p.bc_left != 2 && !s->literal_half) return solve_iteration_lines(s, it);
   const int M = s->M, ts = s->p.ts_method;
   corr_compute(s);                                           /* :608 */
   if (s->p.include_validation && !corr_validate(s)) return ORC_ERR_VALIDATION; /* :609-612 */
   memcpy(s->B, s->cB, sizeof(double) * s->G);                /* :614 */
-  if (ts != 3 || it % 4 == 0) memcpy(s->prev_ends, s->ends, ends_bytes(s)); /* :620-625 */
+  if (ts != 3 || it % 4 == 0) par_copy(s->prev_ends, s->ends, ends_bytes(s), s->par_copies ? s->threads : 1); /* :620-625 */
 
   int half_copy_pending = 0;
   for (int i = 0; i < M; ++i) {
     double mu = s->mu[i];
     /* Lazy form of :733: the surviving copy is the one after the last mu<0 CN cell. */
     if (half_copy_pending && mu >= 0.) {
-      memcpy(s->half_ends, s->ends, ends_bytes(s));
+      par_copy(s->half_ends, s->ends, ends_bytes(s), s->par_copies ? s->threads : 1);
       half_copy_pending = 0;
     }
     int err = 0, pend = 0;
@@ -1018,7 +1070,7 @@ static int solve_iteration(orc_solver *s, int it) {
     if (err) return ORC_ERR_PARAM;
     if (pend) half_copy_pending = 1;
   }
-  if (half_copy_pending) memcpy(s->half_ends, s->ends, ends_bytes(s));
+  if (half_copy_pending) par_copy(s->half_ends, s->ends, ends_bytes(s), s->par_copies ? s->threads : 1);
   return ORC_OK;
 }
 

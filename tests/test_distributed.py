@@ -209,6 +209,16 @@ def test_warmup_rule():
     assert bench.warmup_steps(0, 2, 2) == 2         # aligned schedule: one pass
 
 
+def test_material_params_valid_for_both_variants():
+    """the material leg must not inherit the corr variant's V = 5.994 with the
+    correction on, which rt_material_enable refuses (RT_ERR_PARAM)."""
+    import bench
+    for variant in ("v0", "corr"):
+        q = bench.material_params(bench.slab_params(4, variant, N=100, M=4))
+        assert q["ts_method"] == 1
+        assert q["V"] == 0.0 or not q["use_correction"]
+
+
 def test_time_block_choice():
     """bench.py: K timed steps run as whole passes of the fastest block dividing K."""
     import bench

@@ -177,3 +177,29 @@ def test_equilibrium_known_answer(oracle_mod):
     src = s.psi_source()
     dev = np.abs(s.psi() - src[:, :, None]).max(axis=2) / np.abs(src)
     assert dev.max() < 5e-3, dev
+
+
+@pytest.mark.parametrize("ts", [1, 2, 3])
+@pytest.mark.parametrize("bc", [(0, 0), (1, 1), (0, 2)])
+def test_line_parallel_baseline_mode_is_exact(oracle_mod, ts, bc):
+    """The CPU baseline's line-parallel mode (all lines of a substep in one OpenMP loop,
+    per-line prev/half snapshots, parallel whole-array copies) gives the same bits as the
+    reference-shaped serial run (4 threads; reflective left boundaries keep the
+    reference's shape)."""
+    import sys
+    from conftest import REPO
+    sys.path.insert(0, str(REPO))
+    import bench
+    oracle = oracle_mod
+    p = bench.slab_params(6, "corr", N=300, M=8)
+    q = dict(p, bc_left=bc[0], bc_right=bc[1], bc_left_indicator=bc[0], bc_right_indicator=bc[1], dx=p["X"] / 300,
+             have_group_bounds=0, have_group_kappa=1, prm_found=1, ts_method=ts, max_timesteps=3,
+             psi_source=np.full((8, 6), 0.3))
+    a = oracle.OracleSolver(q)
+    a.solve()
+    b = oracle.OracleSolver(q)
+    b.set_threads(4)
+    b.set_line_parallel(True)
+    b.solve()
+    assert np.array_equal(a.ends(), b.ends())
+    assert np.array_equal(a.psi(), b.psi())
