@@ -110,12 +110,13 @@ def cpu_baseline(variant: str) -> dict:
     """The C oracle (the reference's algorithm restated, solver.cpp loop order, gcc -O3) on
     a bounded sample of the SL workload -- all 64 angles, N = 200000 cells, 1 BDF2 step --
     on the lease's CPU share (host_cpus):
-      value: 16 groups (1024 lines), every line of a substep in one OpenMP loop with
-             per-line prev/half snapshots (orc_set_line_parallel: same values);
-      reference_shaped_value: the same sample in the reference's shape -- lines of one
-             direction in parallel, the whole-array prev/half copies (solver.cpp:620-625,
-             733, its one surviving copy) in between;
-      single_thread_value: 1 group on 1 thread."""
+      value: 16 groups (1024 lines), the lines of each direction over the OpenMP threads
+             and the whole-array prev/half snapshot copies (solver.cpp:620-625, 733, its
+             one surviving copy) split over them too (orc_set_parallel_copies: same values);
+      reference_shaped_value: the same with the copies serial, as the reference makes them;
+      single_thread_value: 1 group on 1 thread.
+    The state arrays sit on transparent huge pages (the reference layout strides M G
+    doubles from cell to cell)."""
     sys.path.insert(0, str(REPO / "oracle"))
     import oracle
     oracle.build()
@@ -127,10 +128,10 @@ def cpu_baseline(variant: str) -> dict:
     q.update(bc_left=p["bc_left_indicator"], bc_right=p["bc_right_indicator"], dx=p["X"] / N,
              have_group_bounds=0, have_group_kappa=1, prm_found=1)
 
-    def timed(g_lo, g_hi, threads, lines):
+    def timed(g_lo, g_hi, threads, par_copies):
         s = oracle.OracleSolver(q, g_lo=g_lo, g_hi=g_hi)
         s.set_threads(threads)
-        s.set_line_parallel(lines)
+        s.set_parallel_copies(par_copies)
         t0 = time.perf_counter()
         s.solve()
         return 4.0 * q["M"] * N * (g_hi - g_lo), time.perf_counter() - t0
@@ -141,10 +142,9 @@ def cpu_baseline(variant: str) -> dict:
     return dict({"value": un / tn, "unit": "cell-angle-group updates/s", "cores": T, "kind": "port",
                  "reference_shaped_value": ur / tr, "single_thread_value": u1 / t1,
                  "sample": f"oracle/rt_oracle.c (restatement of solver.cpp, gcc -O3), SL {variant}: M=64, N={N}, "
-                           f"1 BDF2 step; 16 groups (1024 lines) on {T} OpenMP threads, line-parallel = "
-                           f"{un:.3g} updates in {tn:.2f} s; the same in the reference's shape (direction by "
-                           f"direction, whole-array snapshot copies) {tr:.2f} s; 1 group on 1 thread = {u1:.3g} "
-                           f"updates in {t1:.2f} s"}, **host)
+                           f"1 BDF2 step; 16 groups (1024 lines) on {T} OpenMP threads with the snapshot copies "
+                           f"threaded = {un:.3g} updates in {tn:.2f} s; the same with serial copies as in the "
+                           f"reference {tr:.2f} s; 1 group on 1 thread = {u1:.3g} updates in {t1:.2f} s"}, **host)
 
 
 REFERENCE_CONFIGS = ("single_group.prm", "multi_group_equilibrium.prm", "llnl_slab_test.prm",

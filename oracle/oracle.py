@@ -64,8 +64,8 @@ def lib():
         L.orc_run_substeps.argtypes = [C.c_void_p, C.c_int, C.c_int]
         L.orc_set_threads.argtypes = [C.c_void_p, C.c_int]
         L.orc_set_threads.restype = None
-        L.orc_set_line_parallel.argtypes = [C.c_void_p, C.c_int]
-        L.orc_set_line_parallel.restype = None
+        L.orc_set_parallel_copies.argtypes = [C.c_void_p, C.c_int]
+        L.orc_set_parallel_copies.restype = None
         L.orc_num_groups_local.argtypes = [C.c_void_p]
         for name in ("orc_get_psi", "orc_get_ends", "orc_set_ends", "orc_get_psi_source"):
             getattr(L, name).argtypes = [C.c_void_p, dp]
@@ -174,9 +174,9 @@ class OracleSolver:
             lib().orc_destroy(h)
             self._h = None
 
-    def set_line_parallel(self, on: bool = True):
-        """CPU baseline: all lines of a substep in one OpenMP loop, per-line snapshots."""
-        lib().orc_set_line_parallel(self._h, 1 if on else 0)
+    def set_parallel_copies(self, on: bool = True):
+        """CPU baseline: the whole-array snapshot copies split over the threads."""
+        lib().orc_set_parallel_copies(self._h, 1 if on else 0)
 
     def set_threads(self, n: int):
         """OpenMP threads over the lines of a direction (results do not depend on it)."""

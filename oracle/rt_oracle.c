@@ -7,7 +7,7 @@
  * block cites the reference file:line it restates.  x86-64 baseline build
  * (no FMA contraction), like the reference's default CMake build.
  */
-#define _POSIX_C_SOURCE 200809L
+#define _GNU_SOURCE /* madvise(MADV_HUGEPAGE) */
 #include "rt_oracle.h"
 
 #include <ctype.h>
@@ -18,6 +18,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/mman.h>
 
 /* ---- include/Constants.h:9-23 ------------------------------------------- */
 #define C_PLANCK      4.141895e-10   /* keV-sh */
@@ -537,7 +538,6 @@ struct orc_solver {
   double dx, dt;
   int literal_half;
   int threads;        /* OpenMP threads over the lines of a direction (orc_set_threads); 1 = serial */
-  int line_parallel;  /* CPU baseline: all lines of a substep in one parallel loop, per-line snapshots */
   int par_copies;     /* CPU baseline: the whole-array snapshot copies split over the threads */
   double ac;          /* RADIATION_CONSTANT_A * c (solver.h:29, correction.h:25) */
   double *mu, *wt;
@@ -671,15 +671,31 @@ static int corr_validate(orc_solver *s) {
 
 int orc_validate(orc_solver *s) { return corr_validate(s); }
 
+/* Zeroed arrays; the large ones (the MGN state arrays) 2 MiB-aligned and marked for
+ * transparent huge pages: the reference layout walks a line with a stride of M G doubles,
+ * one 4 KiB page per cell on SL-sized arrays, so with 4 KiB pages nearly every access is
+ * a TLB miss (CPU-baseline speed only; values unaffected). */
 static void *xcalloc(size_t n, size_t sz, int *ok) {
-  void *p = calloc(n ? n : 1, sz);
+  const size_t bytes = (n ? n : 1) * sz, huge = (size_t)2 << 20;
+  void *p = NULL;
+  if (bytes >= huge) {
+    if (posix_memalign(&p, huge, bytes) != 0) p = NULL;
+    if (p) {
+#ifdef MADV_HUGEPAGE
+      (void)madvise(p, (bytes + huge - 1) / huge * huge, MADV_HUGEPAGE);
+#endif
+      memset(p, 0, bytes);
+    }
+  } else {
+    p = calloc(n ? n : 1, sz);
+  }
   if (!p) *ok = 0;
   return p;
 }
 
 /* Solver::Solver (solver.cpp:46-188) */
 void orc_set_threads(orc_solver *s, int threads) { s->threads = threads > 0 ? threads : 1; }
-void orc_set_line_parallel(orc_solver *s, int on) { s->line_parallel = on; s->par_copies = on; }
+void orc_set_parallel_copies(orc_solver *s, int on) { s->par_copies = on; }
 
 orc_solver *orc_create(const orc_params *pin, int half_copy_literal, int g_lo, int g_hi, int *status) {
   *status = ORC_OK;
@@ -1008,43 +1024,7 @@ static void par_copy(void *dst, const void *src, size_t bytes, int threads) {
   }
 }
 
-/* one line's nodes dst(i, gl, :, :) = src(i, gl, :, :) */
-static void copy_line(const orc_solver *s, double *dst, const double *src, int i, int gl) {
-  for (int side = 0; side < 2; ++side)
-    for (int c = 0; c < s->N; ++c) {
-      size_t k = (size_t)i + (size_t)s->M * ((size_t)gl + (size_t)s->Gl * ((size_t)c + (size_t)s->N * side));
-      dst[k] = src[k];
-    }
-}
-
-/* The CPU baseline's line-parallel form of one solve() iteration (orc_set_line_parallel):
- * with no reflective boundary every (i, g) line of a substep is independent, so all M Gl
- * lines share one parallel loop, each taking its own slices of the prev (:620-625) and
- * half (:733) snapshots -- the half snapshot of a line is its state after the CN substep
- * for mu < 0, and before it for mu > 0 (the last mu < 0 CN cell's copy, which is what
- * survives) -- instead of the reference's whole-array copies.  Same values. */
-static int solve_iteration_lines(orc_solver *s, int it) {
-  const int M = s->M, ts = s->p.ts_method;
-  corr_compute(s);
-  if (s->p.include_validation && !corr_validate(s)) return ORC_ERR_VALIDATION;
-  memcpy(s->B, s->cB, sizeof(double) * s->G);
-  const int prev = ts != 3 || it % 4 == 0, half = ts == 3 && it % 4 == 1;
-  int err = 0;
-#pragma omp parallel for collapse(2) schedule(dynamic, 1) num_threads(s->threads) reduction(| : err)
-  for (int i = 0; i < M; ++i)
-    for (int gl = 0; gl < s->Gl; ++gl) {
-      const int neg = s->mu[i] < 0.;
-      int hp = 0;
-      if (prev) copy_line(s, s->prev_ends, s->ends, i, gl);
-      if (half && !neg) copy_line(s, s->half_ends, s->ends, i, gl);
-      err |= sweep_line(s, it, i, gl, &hp);
-      if (half && neg) copy_line(s, s->half_ends, s->ends, i, gl);
-    }
-  return err ? ORC_ERR_PARAM : ORC_OK;
-}
-
 static int solve_iteration(orc_solver *s, int it) {
-  if (s->line_parallel && s->p.bc_left != 2 && !s->literal_half) return solve_iteration_lines(s, it);
   const int M = s->M, ts = s->p.ts_method;
   corr_compute(s);                                           /* :608 */
   if (s->p.include_validation && !corr_validate(s)) return ORC_ERR_VALIDATION; /* :609-612 */

@@ -67,10 +67,10 @@ typedef struct orc_solver orc_solver;
 orc_solver *orc_create(const orc_params *p, int half_copy_literal, int g_lo, int g_hi, int *status);
 /* OpenMP threads over the lines of one direction (default 1; results do not depend on it) */
 void orc_set_threads(orc_solver *s, int threads);
-/* CPU baseline only: 1 = every (i, g) line of a substep in one parallel loop with per-line
- * prev/half snapshots (no reflective boundary), and the whole-array copies of the other
- * paths split over the threads; results identical.  0 (default) = the reference's shape. */
-void orc_set_line_parallel(orc_solver *s, int on);
+/* CPU baseline only: 1 = the whole-array prev/half snapshot copies (solver.cpp:620-625,
+ * 733) split over the OpenMP threads instead of one serial memcpy; results identical.
+ * 0 (default) = serial copies, as the reference. */
+void orc_set_parallel_copies(orc_solver *s, int on);
 void orc_destroy(orc_solver *s);
 /* Solver::solve (solver.cpp:590-823). Returns ORC_ERR_VALIDATION where the
  * reference would hit assert(validate_correction()). */

@@ -181,11 +181,10 @@ def test_equilibrium_known_answer(oracle_mod):
 
 @pytest.mark.parametrize("ts", [1, 2, 3])
 @pytest.mark.parametrize("bc", [(0, 0), (1, 1), (0, 2)])
-def test_line_parallel_baseline_mode_is_exact(oracle_mod, ts, bc):
-    """The CPU baseline's line-parallel mode (all lines of a substep in one OpenMP loop,
-    per-line prev/half snapshots, parallel whole-array copies) gives the same bits as the
-    reference-shaped serial run (4 threads; reflective left boundaries keep the
-    reference's shape)."""
+def test_parallel_copies_baseline_mode_is_exact(oracle_mod, ts, bc):
+    """The CPU baseline's threaded form (lines of a direction over 4 threads, the
+    whole-array prev/half snapshot copies split over them) gives the same bits as the
+    serial run."""
     import sys
     from conftest import REPO
     sys.path.insert(0, str(REPO))
@@ -199,7 +198,7 @@ def test_line_parallel_baseline_mode_is_exact(oracle_mod, ts, bc):
     a.solve()
     b = oracle.OracleSolver(q)
     b.set_threads(4)
-    b.set_line_parallel(True)
+    b.set_parallel_copies(True)
     b.solve()
     assert np.array_equal(a.ends(), b.ends())
     assert np.array_equal(a.psi(), b.psi())
