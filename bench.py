@@ -361,9 +361,9 @@ def run_rank(solver, p: dict, steps: int, warmup: int, world: int, device, shard
     barrier()
     before = solver.pipeline_state()
     # the pass the timed region runs, as rocprof names it: pipelined when the pipeline is
-    # filled, level-split (two waves per segment) for BDF2 at T = 8, 12, 16 unless disabled
+    # filled, level-split (two waves per segment) where the handle runs it (default: T = 20)
     if before["lag_steps"] > 0:
-        split = solver.level_waves == 2 and p.get("ts_method", 3) == 3 and tb in (8, 12, 16)
+        split = solver.level_waves == 2 and p.get("ts_method", 3) == 3 and tb in (8, 12, 16, 20)
         kernel_name = f"sweep_split_kernel<3, {tb}>" if split else f"sweep_block_kernel<3, {tb}, 2, false>"
     else:
         kernel_name = f"sweep_block_kernel<3, {tb}, 0, false>"

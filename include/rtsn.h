@@ -209,11 +209,13 @@ rt_status rt_get_pipeline(rt_solver *s, int *on);
  * steps queued but not launched, whether a correction is pending; any NULL skipped. */
 rt_status rt_pipeline_state(rt_solver *s, long long *lag_steps, int *queued_steps, int *pending);
 rt_status rt_get_time_block(rt_solver *s, int *steps_per_pass);
-/* Waves per segment of a pipelined BDF2 pass of 8, 12 or 16 steps: 1 (default)
- * runs all levels in one wave; 2 shares them between two waves of a workgroup
- * through LDS, so a SIMD holds two waves instead of one (measured 4% slower on the
- * SL pass; RTSN_LEVEL_WAVES=2 at creation also sizes the segments for
- * it).  Bitwise-identical results.  Other passes always use one wave. */
+/* Waves per segment of a pipelined BDF2 pass of 8, 12, 16 or 20 steps: 1 runs all
+ * levels in one wave; 2 shares them between two waves of a workgroup through LDS, so
+ * a SIMD holds two waves instead of one; 0 (default) = 2 at T = 20 (its one-wave
+ * kernel leans on AGPRs; the split one measured 2.7% faster on SL) and 1 otherwise (at
+ * T = 16 one wave is 4% faster).  rt_get_level_waves reports the
+ * effective choice for the current time block; RTSN_LEVEL_WAVES=1|2 at creation forces
+ * one.  Bitwise-identical results.  Other passes always use one wave. */
 rt_status rt_set_level_waves(rt_solver *s, int waves);
 rt_status rt_get_level_waves(rt_solver *s, int *waves);
 /* Sweep geometry actually used: waves launched per step (one per line group

@@ -1230,6 +1230,7 @@ static hipError_t occupancy_s(int T, int level_waves, int *w) {
         case 8: return hipOccupancyMaxActiveBlocksPerMultiprocessor(w, sweep_split_kernel<S, 8>, 128, 0);
         case 12: return hipOccupancyMaxActiveBlocksPerMultiprocessor(w, sweep_split_kernel<S, 12>, 128, 0);
         case 16: return hipOccupancyMaxActiveBlocksPerMultiprocessor(w, sweep_split_kernel<S, 16>, 128, 0);
+        case 20: return hipOccupancyMaxActiveBlocksPerMultiprocessor(w, sweep_split_kernel<S, 20>, 128, 0);
         default: break;
       }
     }

@@ -30,7 +30,7 @@ constexpr int chunk_cells(int S, int T) {
 }
 // pipelined passes whose T levels two waves can share (sweep_split_kernel):
 // BDF2, where the carried states (5 per level) are what overflows 256 registers
-constexpr bool level_split_supported(int S, int T) { return S == 3 && (T == 8 || T == 12 || T == 16); }
+constexpr bool level_split_supported(int S, int T) { return S == 3 && (T == 8 || T == 12 || T == 16 || T == 20); }
 // rows per chunk of the level-split pass (16 rows with T/2 = 8 levels spill past 256 registers)
 #ifndef RT_CHUNK_SPLIT
 #define RT_CHUNK_SPLIT 8

@@ -52,7 +52,7 @@ struct rt_solver {
   int Tp = 0;                    // steps of the pass whose correction is pending
   int Sg = 1, Ls = 16;           // segments per line and cells per segment
   int seg_T = 0;                 // the time block the segments were sized for (0: none)
-  int level_waves = 1;           // pipelined BDF2 passes: 2 = levels shared by two waves (RTSN_LEVEL_WAVES=2)
+  int level_waves = 0;           // pipelined BDF2 passes: 0 auto (level_waves_of), 1 one wave, 2 levels shared by two
   int d_lo = 0, d_hi = 0;        // direction-pair shard [d_lo, d_hi) of the M/2 pairs (d_hi = 0: all)
   int M_full = 0;                // the configuration's M (p.M is the handle's own direction count)
   int device = 0, cus = 0;
@@ -93,6 +93,15 @@ struct rt_solver {
     if (stream) (void)hipStreamDestroy(stream);
   }
 };
+
+// Waves per segment of the pipelined pass: the caller's choice, or by default two waves
+// (sweep_split_kernel) where measured faster -- BDF2 at T = 20, whose one-wave kernel
+// needs 126 AGPRs beside 256 VGPRs (9% extra moves; split 8.29-8.31 vs 8.52-8.53 ms/step
+// on SL, profiles/r02b_split20.jsonl) -- and one wave otherwise (T = 16: 4% faster).
+static int level_waves_of(const rt_solver *s) {
+  if (s->level_waves) return s->level_waves;
+  return s->scheme == SCHEME_BDF2 && s->T == 20 ? 2 : 1;
+}
 
 // Chain positions of the pipelined schedule: the Sg segments of a line (both
 // halves in step), or 2 Sg when the mu > 0 lines continue the mu < 0 ones.
@@ -524,7 +533,7 @@ static hipError_t alloc_segments(rt_solver *h) {
 static rt_status resegment(rt_solver *h) {
   if (h->material || h->pending || h->Tpipe || h->seg_T == h->T) return RT_OK;
   int w = 0;
-  HIP_TRY(h, sweep_occupancy(h->scheme, h->T, h->level_waves, &w));
+  HIP_TRY(h, sweep_occupancy(h->scheme, h->T, level_waves_of(h), &w));
   if (const char *env = std::getenv("RTSN_WAVES_PER_CU")) w = std::atoi(env);  // experiments
   const int sg0 = h->Sg, ls0 = h->Ls;
   segment_lines(h, w);
@@ -647,7 +656,7 @@ static rt_status create_impl(const rt_params *pin, int g_lo, int g_hi, int d_lo,
     if (supported_time_block(std::atoi(t))) h->T = std::atoi(t);
   if (const char *lw = std::getenv("RTSN_LEVEL_WAVES"))  // experiments: only "1" or "2" are read
     if (!std::strcmp(lw, "1") || !std::strcmp(lw, "2")) h->level_waves = lw[0] - '0';
-  HIP_TRY(h, sweep_occupancy(h->scheme, h->T, h->level_waves, &waves_per_cu));
+  HIP_TRY(h, sweep_occupancy(h->scheme, h->T, level_waves_of(h), &waves_per_cu));
   // tuning knob for experiments: target resident waves per CU (segments per line follow)
   if (const char *w = std::getenv("RTSN_WAVES_PER_CU")) waves_per_cu = std::atoi(w);
   h->cus = prop.multiProcessorCount;
@@ -746,7 +755,7 @@ static SegArgs seg_args(rt_solver *s) {
   a.reflective = s->p.bc_left_indicator == 2;
   a.pending = s->pending ? 1 : 0;
   a.hd = 0.5 * (s->p.X / s->p.N);
-  a.level_waves = s->level_waves;
+  a.level_waves = level_waves_of(s);
   return a;
 }
 
@@ -1622,14 +1631,14 @@ extern "C" rt_status rt_get_time_block(rt_solver *s, int *steps_per_pass) {
 
 extern "C" rt_status rt_set_level_waves(rt_solver *s, int waves) {
   if (!s) return fail(nullptr, RT_ERR_ARG, "rt_set_level_waves: NULL handle");
-  if (waves != 1 && waves != 2) return fail(s, RT_ERR_PARAM, "rt_set_level_waves: 1 or 2");
+  if (waves < 0 || waves > 2) return fail(s, RT_ERR_PARAM, "rt_set_level_waves: 0 (auto), 1 or 2");
   s->level_waves = waves;  // segments stay as created: the schedule is exact for any segmentation
   return RT_OK;
 }
 
 extern "C" rt_status rt_get_level_waves(rt_solver *s, int *waves) {
   if (!s || !waves) return fail(s, RT_ERR_ARG, "rt_get_level_waves: bad argument");
-  *waves = s->level_waves;
+  *waves = level_waves_of(s);  // the effective choice for the current time block
   return RT_OK;
 }
 

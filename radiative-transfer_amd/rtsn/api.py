@@ -499,7 +499,8 @@ class Solver:
 
     @property
     def level_waves(self) -> int:
-        """Waves per segment of a pipelined BDF2 pass of 8/12/16 steps (rt_set_level_waves)."""
+        """Waves per segment of a pipelined BDF2 pass of 8/12/16/20 steps (rt_set_level_waves;
+        0 = auto: two at T = 20, one otherwise); reads the effective choice."""
         v = C.c_int()
         _check(lib().rt_get_level_waves(self._h, C.byref(v)), "rt_get_level_waves", self._h)
         return v.value

@@ -522,7 +522,22 @@ def test_headline_kernel_full_length(rtsn_mod, sl_pair_oracle, tb, steps, case):
     assert max(err.values()) <= TOL, err
 
 
-@pytest.mark.parametrize("tb", [8, 12, 16])
+def test_level_waves_auto(rtsn_mod):
+    """rt_set_level_waves 0 (the default): two waves at T = 20, one at other blocks."""
+    d = rtsn_mod.params_default()
+    with rtsn_mod.Solver(d) as s:
+        assert s.level_waves == 1
+        s.time_block = 20
+        assert s.level_waves == 2
+        s.level_waves = 1
+        assert s.level_waves == 1
+        s.level_waves = 0
+        assert s.level_waves == 2
+        s.time_block = 16
+        assert s.level_waves == 1
+
+
+@pytest.mark.parametrize("tb", [8, 12, 16, 20])
 @pytest.mark.parametrize("bc_left", [0, 2])
 def test_level_split_pass(rtsn_mod, oracle_mod, monkeypatch, tb, bc_left):
     """The level-split pipelined pass (sweep_split_kernel: the T levels of a BDF2 pass
