@@ -421,26 +421,33 @@ __global__ __launch_bounds__(64) void sweep_block_kernel(SegArgs a) {
 
 // ------------------------------------------------------------------------
 // Level-split pipelined pass: the same launch as sweep_block_kernel<S, T, 2>
-// with its T levels shared by two waves of one workgroup.  Wave 0 runs
-// levels [0, T/2) of chunk j and hands the chunk's level-(T/2 - 1) nodes to
-// wave 1 through LDS (three buffers, one barrier per chunk); wave 1 runs
-// levels [T/2, T) of an earlier chunk and stores it.  Each wave then holds
-// half the carried states (X), so the kernel fits 256 registers and a SIMD
-// runs two waves instead of one -- the FP64 issue rate of one wave with
-// ILP <= 16 is ~59 TF, of two ~62-65 TF (profiles/r01_fp64_peak.txt).  Same
-// arithmetic in the same order per (cell, level) as the one-wave kernel:
-// bitwise equal.  Measured on the SL pass at T = 16: 140.6 ms vs 134.6 ms for
-// the one-wave kernel, so it is opt-in (rt_set_level_waves).
+// with its T levels shared by KW waves of one workgroup (KW = 2 or 4), wave w
+// running levels [w T/KW, (w + 1) T/KW).  Wave 0 streams the rows in from HBM,
+// the last wave stores them, and each wave hands its chunk's nodes at its last
+// level to the next wave through LDS (two buffers per link, one barrier per
+// chunk interval): in interval I wave w computes chunk I - 2w from registers
+// while it refills them with chunk I - 2w + 1 (written by wave w - 1 in
+// interval I - 1) and writes chunk I - 2w into its outgoing buffer (I - 2w) & 1.
+// Same arithmetic in the same order per (cell, level) as the one-wave kernel:
+// bitwise equal.
+//   KW = 2: each wave holds half the carried states (X), so a SIMD runs two
+//     waves instead of one: at T = 20 (one-wave kernel: 126 AGPRs beside 256
+//     VGPRs) 8.29-8.31 vs 8.52-8.53 ms per step on SL, the default there; at
+//     T = 16 4% slower than one wave (140.6 vs 134.6 ms per pass).
+//   KW = 2, 4 in the pipeline's fill and drain: a launch with few active chain
+//     positions runs each segment on more waves, so the lines' traversal takes
+//     1/KW of the time while the chip would otherwise idle (rtsn_api.hip
+//     pipe_launch).
 // ------------------------------------------------------------------------
-template <int S, int TW, int C, bool FIRST, bool LAST>
+template <int S, int TW, int C, bool IN_HBM, bool OUT_HBM, bool LASTCH>
 __device__ __forceinline__ void split_chunk(const double *W, double (&ein)[C], double (&eout)[C],
                                             double (&X)[TW][SchemeDim<S>::K], bool head, double h_oi, double h_oo,
-                                            double2 *lds, __amdgpu_buffer_rsrc_t Rw,
+                                            const double2 *lin, double2 *lout, __amdgpu_buffer_rsrc_t Rw,
                                             __amdgpu_buffer_rsrc_t Rn, int voff, int row_bytes, int nv, int lane) {
   constexpr int K = SchemeDim<S>::K;
 #pragma unroll
   for (int c = 0; c < C; ++c) {
-    if (LAST && c >= nv) continue;  // wave-uniform: past the end of the segment
+    if (LASTCH && c >= nv) continue;  // wave-uniform: past the end of the segment
     double oi = ein[c], oo = eout[c];
     if (c == 0 && head) {  // reflective head cell, computed in the prologue
       oi = h_oi;
@@ -456,17 +463,17 @@ __device__ __forceinline__ void split_chunk(const double *W, double (&ein)[C], d
         oo = e;
       }
     }
-    if constexpr (FIRST) {  // hand the nodes to the second wave; refill from HBM
-      lds[c * 64 + lane] = make_double2(oi, oo);
-      if constexpr (!LAST) {
+    if constexpr (OUT_HBM)
+      row_store(Rw, voff, c * row_bytes, oi, oo);
+    else  // hand the nodes at this wave's last level to the next wave
+      lout[c * 64 + lane] = make_double2(oi, oo);
+    if constexpr (!LASTCH) {  // refill with the next chunk: from HBM, or from the previous wave
+      if constexpr (IN_HBM) {
         const double2 v = row_load(Rn, voff, c * row_bytes);
         ein[c] = v.x;
         eout[c] = v.y;
-      }
-    } else {  // store; refill from the next chunk's level-(TW - 1) nodes
-      row_store(Rw, voff, c * row_bytes, oi, oo);
-      if constexpr (!LAST) {
-        const double2 v = lds[c * 64 + lane];
+      } else {
+        const double2 v = lin[c * 64 + lane];
         ein[c] = v.x;
         eout[c] = v.y;
       }
@@ -474,17 +481,18 @@ __device__ __forceinline__ void split_chunk(const double *W, double (&ein)[C], d
   }
 }
 
-// One wave's role: FIRST = levels [0, T/2), else [T/2, T).  The two roles are
-// compile-time instantiation: with the role a runtime (wave-uniform) branch
-// inside one body the allocation measured ~340 registers, each role alone ~215.
-template <int S, int T, bool FIRST>
-__device__ __forceinline__ void split_role(const SegArgs &a, double2 (*hand)[split_chunk_cells() * 64], double2 *hhead) {
+// Wave w's role (compile time: with the role a runtime branch inside one body the
+// allocation measured ~340 registers, each role alone ~215).
+template <int S, int T, int KW, int w>
+__device__ __forceinline__ void split_role(const SegArgs &a, double2 (*hand)[2][split_chunk_cells() * 64],
+                                           double2 *hhead) {
   constexpr int K = SchemeDim<S>::K;
-  constexpr int TW = T / 2;
+  constexpr int TW = T / KW;
   constexpr int WN = map_count<S>();
   constexpr int C = split_chunk_cells();
+  constexpr bool IN = w == 0, OUT = w == KW - 1;
   const int lane = threadIdx.x & 63;
-  constexpr int t0 = FIRST ? 0 : TW;  // this wave's first level
+  constexpr int t0 = w * TW;  // this wave's first level
   const size_t stride = static_cast<size_t>(a.Lpad);
   int half, s, q, pos;
   if (a.reflective) {
@@ -542,13 +550,13 @@ __device__ __forceinline__ void split_role(const SegArgs &a, double2 (*hand)[spl
       for (int r = 0; r < K; ++r) X[t][r] = up[((t0 + t) * K + r) * stride];
   }
 
-  // ---- rows: the first wave streams them in, the second stores them ----
+  // ---- rows: wave 0 streams them in, the last wave stores them ----
   const int row_bytes = a.Lpad * static_cast<int>(sizeof(double2));
   const int voff = lane * static_cast<int>(sizeof(double2));
   const double2 *Eh = a.E + static_cast<size_t>(half) * a.Nrow * stride + q * 64;
   auto rows = [&](int k0) { return rows_rsrc<C>(Eh + static_cast<size_t>(k0) * stride, row_bytes); };
   double ein[C], eout[C];
-  if constexpr (FIRST) {
+  if constexpr (IN) {
     const __amdgpu_buffer_rsrc_t R0 = rows(k_begin);
 #pragma unroll
     for (int c = 0; c < C; ++c) {
@@ -560,18 +568,28 @@ __device__ __forceinline__ void split_role(const SegArgs &a, double2 (*hand)[spl
 #pragma unroll
     for (int c = 0; c < C; ++c) ein[c] = eout[c] = 0.0;
   }
-  // reflective head cell: levels [0, TW) on the loaded row, [TW, T) on their result
+  // reflective head cell: wave r runs its levels on wave r - 1's result, in turn
   double h_oi = 0.0, h_oo = 0.0;
-  if (refl_head) {  // workgroup-uniform: both waves reach the barrier
+  if (refl_head) {  // workgroup-uniform: every wave passes the KW - 1 barriers
     const double *lcp = a.lc + static_cast<size_t>(half) * LC_COUNT * stride + ell;
-    if constexpr (FIRST) {
+    if constexpr (IN) {
       h_oi = ein[0];
       h_oo = eout[0];
-      head_cell<S, TW>(lcp, stride, a.hd, b, X, h_oi, h_oo, 1.0);
-      hhead[lane] = make_double2(h_oi, h_oo);
     }
-    __syncthreads();
-    if constexpr (!FIRST) {
+#pragma unroll
+    for (int r = 0; r < KW - 1; ++r) {
+      if (r == w) {  // compile-time after unrolling
+        if constexpr (!IN) {
+          const double2 v = hhead[lane];
+          h_oi = v.x;
+          h_oo = v.y;
+        }
+        head_cell<S, TW>(lcp, stride, a.hd, b, X, h_oi, h_oo, 1.0);
+        hhead[lane] = make_double2(h_oi, h_oo);
+      }
+      __syncthreads();
+    }
+    if constexpr (OUT) {
       const double2 v = hhead[lane];
       h_oi = v.x;
       h_oo = v.y;
@@ -583,60 +601,61 @@ __device__ __forceinline__ void split_role(const SegArgs &a, double2 (*hand)[spl
 #pragma unroll
   for (int n = 0; n < WN; ++n) W[n] = a.map[(static_cast<size_t>(half) * WN + n) * stride + ell];
 
-  // Barrier interval j: the first wave runs chunk j and writes its nodes to
-  // hand[j % 3]; the second runs chunk j - 2 from registers while it refills
-  // them with chunk j - 1 (complete since the last barrier).  Each wave passes
-  // nch + 2 barriers (s_barrier counts waves, not program points).
-  auto store_aggregate = [&]() {
-    double *ag = a.aggs[slot] + half * half_stride + static_cast<size_t>(s) * seg_stride + ell;
-#pragma unroll
-    for (int t = 0; t < TW; ++t)
-#pragma unroll
-      for (int r = 0; r < K; ++r) ag[((t0 + t) * K + r) * stride] = X[t][r];
-  };
+  // ---- chunk intervals: nch + 2 (KW - 1) of them, one barrier after each, for every wave ----
   const int nch = (k_end - k_begin + C - 1) / C;
-  if constexpr (FIRST) {
-    int k0 = k_begin;
-    for (int jc = 0; jc + 1 < nch; ++jc, k0 += C) {
-      split_chunk<S, TW, C, true, false>(W, ein, eout, X, refl_head && jc == 0, h_oi, h_oo, hand[jc % 3], rows(k0),
-                                         rows(k0 + C), voff, row_bytes, C, lane);
-      __syncthreads();
-    }
-    split_chunk<S, TW, C, true, true>(W, ein, eout, X, refl_head && nch == 1, h_oi, h_oo, hand[(nch - 1) % 3],
-                                      rows(k0), rows(k0), voff, row_bytes, k_end - k0, lane);
-    store_aggregate();
-    __syncthreads();
-    __syncthreads();
-  } else {
-    __syncthreads();  // chunk 0 written
+  const double2 *lin = hand[w > 0 ? w - 1 : 0][0];  // (wave 0 reads HBM, the last wave writes it:
+  double2 *lout = hand[w < KW - 1 ? w : 0][0];       //  their unused link pointer is never touched)
+  constexpr int LB = split_chunk_cells() * 64;  // one buffer of a link
+  if constexpr (!IN) {
+    for (int I = 0; I < 2 * w - 1; ++I) __syncthreads();  // the previous waves fill the pipeline
+    // interval 2w - 1: chunk 0 of the previous wave (written in interval 2w - 2)
 #pragma unroll
     for (int c = 0; c < C; ++c) {
-      const double2 v = hand[0][c * 64 + lane];
+      const double2 v = lin[c * 64 + lane];
       ein[c] = v.x;
       eout[c] = v.y;
     }
-    __syncthreads();  // chunk 1 written (if any); hand[0] is read
-    int k0 = k_begin;
-    for (int jc = 0; jc + 1 < nch; ++jc, k0 += C) {
-      split_chunk<S, TW, C, false, false>(W, ein, eout, X, refl_head && jc == 0, h_oi, h_oo, hand[(jc + 1) % 3],
-                                          rows(k0), rows(k0), voff, row_bytes, C, lane);
-      __syncthreads();
-    }
-    split_chunk<S, TW, C, false, true>(W, ein, eout, X, refl_head && nch == 1, h_oi, h_oo, nullptr, rows(k0),
-                                       rows(k0), voff, row_bytes, k_end - k0, lane);
-    store_aggregate();
+    __syncthreads();
   }
+  int k0 = k_begin;
+  for (int m = 0; m + 1 < nch; ++m, k0 += C) {
+    split_chunk<S, TW, C, IN, OUT, false>(W, ein, eout, X, refl_head && m == 0, h_oi, h_oo, lin + ((m + 1) & 1) * LB,
+                                          lout + (m & 1) * LB, rows(k0), rows(k0 + C), voff, row_bytes, C, lane);
+    __syncthreads();
+  }
+  split_chunk<S, TW, C, IN, OUT, true>(W, ein, eout, X, refl_head && nch == 1, h_oi, h_oo, lin,
+                                       lout + ((nch - 1) & 1) * LB, rows(k0), rows(k0), voff, row_bytes, k_end - k0,
+                                       lane);
+  __syncthreads();
+  double *ag = a.aggs[slot] + half * half_stride + static_cast<size_t>(s) * seg_stride + ell;
+#pragma unroll
+  for (int t = 0; t < TW; ++t)
+#pragma unroll
+    for (int r = 0; r < K; ++r) ag[((t0 + t) * K + r) * stride] = X[t][r];
+  for (int I = 0; I < 2 * (KW - 1 - w); ++I) __syncthreads();  // the later waves drain it
 }
 
-template <int S, int T>
-__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2, 2))) void sweep_split_kernel(SegArgs a) {
-  static_assert(T % 2 == 0, "levels split evenly over two waves");
-  __shared__ double2 hand[3][split_chunk_cells() * 64];  // chunk nodes at level T/2 - 1, chunk jc in hand[jc % 3]
-  __shared__ double2 hhead[64];                          // reflective head cell at level T/2 - 1
-  if (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) == 0)
-    split_role<S, T, true>(a, hand, hhead);
-  else
-    split_role<S, T, false>(a, hand, hhead);
+template <int S, int T, int KW>
+__global__ __launch_bounds__(64 * KW) __attribute__((amdgpu_waves_per_eu(2, 2))) void sweep_split_kernel(SegArgs a) {
+  static_assert(T % KW == 0 && (KW == 2 || KW == 4), "levels split evenly over 2 or 4 waves");
+  __shared__ double2 hand[KW - 1][2][split_chunk_cells() * 64];  // link w: wave w -> w + 1, chunk m in [m & 1]
+  __shared__ double2 hhead[64];                                    // reflective head cell, wave to wave
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if constexpr (KW == 2) {
+    if (w == 0)
+      split_role<S, T, 2, 0>(a, hand, hhead);
+    else
+      split_role<S, T, 2, 1>(a, hand, hhead);
+  } else {
+    if (w == 0)
+      split_role<S, T, 4, 0>(a, hand, hhead);
+    else if (w == 1)
+      split_role<S, T, 4, 1>(a, hand, hhead);
+    else if (w == 2)
+      split_role<S, T, 4, 2>(a, hand, hhead);
+    else
+      split_role<S, T, 4, 3>(a, hand, hhead);
+  }
 }
 
 // ------------------------------------------------------------------------
@@ -1163,10 +1182,17 @@ static hipError_t launch_t(int mode, const SegArgs &a, int grid, hipStream_t st)
   if (mode == SWEEP_PIPELINED) {
     if constexpr (level_split_supported(S, T)) {
       if (a.level_waves == 2) {
-        hipLaunchKernelGGL((sweep_split_kernel<S, T>), dim3(grid), dim3(128), 0, st, a);
+        hipLaunchKernelGGL((sweep_split_kernel<S, T, 2>), dim3(grid), dim3(128), 0, st, a);
         return hipGetLastError();
       }
+      if constexpr (T % 4 == 0) {
+        if (a.level_waves == 4) {
+          hipLaunchKernelGGL((sweep_split_kernel<S, T, 4>), dim3(grid), dim3(256), 0, st, a);
+          return hipGetLastError();
+        }
+      }
     }
+    if (a.level_waves != 1) return hipErrorInvalidValue;
     hipLaunchKernelGGL((sweep_block_kernel<S, T, 2>), dim3(grid), dim3(64), 0, st, a);
     return hipGetLastError();
   }
@@ -1227,10 +1253,11 @@ static hipError_t occupancy_s(int T, int level_waves, int *w) {
   if constexpr (level_split_supported(S, 16)) {  // workgroups (segments) per CU of the level-split pass
     if (level_waves == 2) {
       switch (T) {
-        case 8: return hipOccupancyMaxActiveBlocksPerMultiprocessor(w, sweep_split_kernel<S, 8>, 128, 0);
-        case 12: return hipOccupancyMaxActiveBlocksPerMultiprocessor(w, sweep_split_kernel<S, 12>, 128, 0);
-        case 16: return hipOccupancyMaxActiveBlocksPerMultiprocessor(w, sweep_split_kernel<S, 16>, 128, 0);
-        case 20: return hipOccupancyMaxActiveBlocksPerMultiprocessor(w, sweep_split_kernel<S, 20>, 128, 0);
+        case 8: return hipOccupancyMaxActiveBlocksPerMultiprocessor(w, sweep_split_kernel<S, 8, 2>, 128, 0);
+        case 10: return hipOccupancyMaxActiveBlocksPerMultiprocessor(w, sweep_split_kernel<S, 10, 2>, 128, 0);
+        case 12: return hipOccupancyMaxActiveBlocksPerMultiprocessor(w, sweep_split_kernel<S, 12, 2>, 128, 0);
+        case 16: return hipOccupancyMaxActiveBlocksPerMultiprocessor(w, sweep_split_kernel<S, 16, 2>, 128, 0);
+        case 20: return hipOccupancyMaxActiveBlocksPerMultiprocessor(w, sweep_split_kernel<S, 20, 2>, 128, 0);
         default: break;
       }
     }

@@ -30,7 +30,7 @@ constexpr int chunk_cells(int S, int T) {
 }
 // pipelined passes whose T levels two waves can share (sweep_split_kernel):
 // BDF2, where the carried states (5 per level) are what overflows 256 registers
-constexpr bool level_split_supported(int S, int T) { return S == 3 && (T == 8 || T == 12 || T == 16 || T == 20); }
+constexpr bool level_split_supported(int S, int T) { return S == 3 && (T == 8 || T == 10 || T == 12 || T == 16 || T == 20); }
 // rows per chunk of the level-split pass (16 rows with T/2 = 8 levels spill past 256 registers)
 #ifndef RT_CHUNK_SPLIT
 #define RT_CHUNK_SPLIT 8
@@ -61,7 +61,7 @@ struct SegArgs {
   int reflective;             // bc_left == 2
   int pending;                // the stored state is provisional: apply the correction
   int pos_lo, npos, pass_lo;  // pipelined: active chain positions and the pass of the first
-  int level_waves;            // pipelined: 2 = T levels shared by two waves (sweep_split_kernel), else 1
+  int level_waves;            // pipelined: waves per segment, 1 (sweep_block_kernel) or 2, 4 (sweep_split_kernel)
   double hd;                  // dx / 2
   // material coupling (SWEEP_PASS, T = 1 only): per-cell emission B_g(T(x)),
   // [N][Gl] (g fastest), scaling the map constants stored for B = 1

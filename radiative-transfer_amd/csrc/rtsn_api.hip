@@ -98,9 +98,26 @@ struct rt_solver {
 // (sweep_split_kernel) where measured faster -- BDF2 at T = 20, whose one-wave kernel
 // needs 126 AGPRs beside 256 VGPRs (9% extra moves; split 8.29-8.31 vs 8.52-8.53 ms/step
 // on SL, profiles/r02b_split20.jsonl) -- and one wave otherwise (T = 16: 4% faster).
-static int level_waves_of(const rt_solver *s) {
+static int level_waves_of(const rt_solver *s, int T) {
   if (s->level_waves) return s->level_waves;
-  return s->scheme == SCHEME_BDF2 && s->T == 20 ? 2 : 1;
+  return s->scheme == SCHEME_BDF2 && T == 20 ? 2 : 1;
+}
+
+// Waves per segment of one pipelined launch of `grid` workgroups.  The segments are sized
+// so that a full launch (every chain position active) fills the chip; the pipeline's fill
+// and drain launches hold fewer positions, and with the default level_waves (0) their
+// segments are split over 2 or 4 waves (sweep_split_kernel) as long as the launch stays
+// within the full launch's wave count -- the lines are then traversed 2-4x faster while
+// the chip would otherwise idle (BDF2 time blocks the split kernel has: 8, 10, 12, 16, 20).
+static bool split_block(int T) { return T == 8 || T == 10 || T == 12 || T == 16 || T == 20; }
+
+static int fill_level_waves(const rt_solver *s, int grid) {
+  const int base = level_waves_of(s, s->Tpipe);
+  if (s->level_waves || s->scheme != SCHEME_BDF2 || !split_block(s->Tpipe)) return base;
+  const long long full = 2LL * s->Q * s->Sg * base;  // waves of a launch with every position active
+  int k = base;
+  while (k < 4 && s->Tpipe % (2 * k) == 0 && static_cast<long long>(grid) * 2 * k <= full) k *= 2;
+  return k;
 }
 
 // Chain positions of the pipelined schedule: the Sg segments of a line (both
@@ -533,7 +550,7 @@ static hipError_t alloc_segments(rt_solver *h) {
 static rt_status resegment(rt_solver *h) {
   if (h->material || h->pending || h->Tpipe || h->seg_T == h->T) return RT_OK;
   int w = 0;
-  HIP_TRY(h, sweep_occupancy(h->scheme, h->T, level_waves_of(h), &w));
+  HIP_TRY(h, sweep_occupancy(h->scheme, h->T, level_waves_of(h, h->T), &w));
   if (const char *env = std::getenv("RTSN_WAVES_PER_CU")) w = std::atoi(env);  // experiments
   const int sg0 = h->Sg, ls0 = h->Ls;
   segment_lines(h, w);
@@ -656,7 +673,7 @@ static rt_status create_impl(const rt_params *pin, int g_lo, int g_hi, int d_lo,
     if (supported_time_block(std::atoi(t))) h->T = std::atoi(t);
   if (const char *lw = std::getenv("RTSN_LEVEL_WAVES"))  // experiments: only "1" or "2" are read
     if (!std::strcmp(lw, "1") || !std::strcmp(lw, "2")) h->level_waves = lw[0] - '0';
-  HIP_TRY(h, sweep_occupancy(h->scheme, h->T, level_waves_of(h), &waves_per_cu));
+  HIP_TRY(h, sweep_occupancy(h->scheme, h->T, level_waves_of(h, h->T), &waves_per_cu));
   // tuning knob for experiments: target resident waves per CU (segments per line follow)
   if (const char *w = std::getenv("RTSN_WAVES_PER_CU")) waves_per_cu = std::atoi(w);
   h->cus = prop.multiProcessorCount;
@@ -755,7 +772,7 @@ static SegArgs seg_args(rt_solver *s) {
   a.reflective = s->p.bc_left_indicator == 2;
   a.pending = s->pending ? 1 : 0;
   a.hd = 0.5 * (s->p.X / s->p.N);
-  a.level_waves = level_waves_of(s);
+  a.level_waves = level_waves_of(s, s->T);
   return a;
 }
 
@@ -900,6 +917,7 @@ static rt_status pipe_launch(rt_solver *s) {
   a.npos = hi - lo + 1;
   a.pass_lo = static_cast<int>(((s->tau[lo] - s->pipe_base) / T) & 1);
   const int grid = (a.reflective ? 1 : 2) * a.npos * s->Q;
+  a.level_waves = fill_level_waves(s, grid);
   hipEvent_t e1;
   rt_status st = event_begin(s, &e1);
   if (st) return st;
@@ -1638,7 +1656,7 @@ extern "C" rt_status rt_set_level_waves(rt_solver *s, int waves) {
 
 extern "C" rt_status rt_get_level_waves(rt_solver *s, int *waves) {
   if (!s || !waves) return fail(s, RT_ERR_ARG, "rt_get_level_waves: bad argument");
-  *waves = level_waves_of(s);  // the effective choice for the current time block
+  *waves = level_waves_of(s, s->T);  // the effective choice for the current time block
   return RT_OK;
 }
 

@@ -541,7 +541,8 @@ def test_level_waves_auto(rtsn_mod):
 @pytest.mark.parametrize("bc_left", [0, 2])
 def test_level_split_pass(rtsn_mod, oracle_mod, monkeypatch, tb, bc_left):
     """The level-split pipelined pass (sweep_split_kernel: the T levels of a BDF2 pass
-    shared by two waves through LDS, opt-in for T = 8, 12, 16) is bitwise the
+    shared by two waves through LDS -- the default at T = 20 -- and by 2 or 4 waves in the
+    pipeline's fill and drain launches under the default level_waves 0) is bitwise the
     one-wave pass (rt_set_level_waves 1, and RTSN_LEVEL_WAVES=1 at creation, whose
     segment count follows the one-wave occupancy) -- same arithmetic per (cell, level)
     -- over 3 T + 1 steps (fill, steady state, drain, an aligned remainder), and matches
@@ -564,10 +565,14 @@ def test_level_split_pass(rtsn_mod, oracle_mod, monkeypatch, tb, bc_left):
     orc.set_ends(ends)
     orc.solve()
     out = {}
-    for env, lw in (("1", 1), ("2", 2), ("2", 1)):
-        monkeypatch.setenv("RTSN_LEVEL_WAVES", env)
+    for env, lw in (("1", 1), ("2", 2), ("2", 1), (None, 0)):
+        if env:
+            monkeypatch.setenv("RTSN_LEVEL_WAVES", env)
+        else:  # the default: fill and drain launches split over 2 or 4 waves (pipe_launch)
+            monkeypatch.delenv("RTSN_LEVEL_WAVES")
         with rtsn_mod.Solver(to_rt(p), g_lo=lo, g_hi=hi) as gpu:
-            assert gpu.level_waves == int(env)
+            if env:
+                assert gpu.level_waves == int(env)
             gpu.level_waves = lw
             with pytest.raises(rtsn_mod.RtError):
                 gpu.level_waves = 3
@@ -583,8 +588,8 @@ def test_level_split_pass(rtsn_mod, oracle_mod, monkeypatch, tb, bc_left):
                 gpu.set_ends(ends)
                 gpu.advance(tb + 3)
                 compare_all(gpu, orc, plus_vs_group=True)
-    monkeypatch.delenv("RTSN_LEVEL_WAVES")
     assert np.array_equal(out["2", 1], out["2", 2])
+    assert np.array_equal(out[None, 0], out["1", 1])
 
 
 @pytest.mark.parametrize("ts", [1, 2, 3])
