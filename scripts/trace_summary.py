@@ -7,7 +7,8 @@ The pipelined schedule's first and last launches (fill / drain) cover fewer
 segments than a steady-state pass, so the kernel's plain average over all
 dispatches is not the per-pass time bench.py reports.  Dispatches are
 grouped by (kernel, grid size); for each group: count, mean and median
-duration.  The full-grid group of the sweep kernel is the steady-state pass.
+duration.  The full-grid group of the sweep kernel (one-wave sweep_block_kernel or
+level-split sweep_split_kernel) with the most time is the steady-state pass.
 """
 import csv
 import json
@@ -30,7 +31,7 @@ def main():
     # (the material-coupled pass, `..., true>`, runs a larger grid but is not the headline)
     per_kernel = {}
     for r in rows:
-        if "sweep_block_kernel" in r["kernel"]:
+        if "sweep_block_kernel" in r["kernel"] or "sweep_split_kernel" in r["kernel"]:
             best = per_kernel.get(r["kernel"])
             if best is None or r["grid_threads"] > best["grid_threads"]:
                 per_kernel[r["kernel"]] = r
