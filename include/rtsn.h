@@ -199,10 +199,12 @@ rt_status rt_set_time_block(rt_solver *s, int steps_per_pass);
  * one pass apart, so each starts from its upwind neighbour's exact exit state
  * -- no cross-segment correction.  Steps are queued and launched as whole
  * passes; the pipeline fills over the first launches (one per segment) and
- * drains when a result is read (or rt_solve returns).  0: off -- every pass
- * moves all segments together (at most 4 steps) and corrects them in the
- * next pass; 1 (default): pipelined when an advance brings at least as many
- * passes as the pipeline is deep, else aligned; 2: always pipelined. */
+ * drains when a result is read (or rt_solve returns); those launches split
+ * their segments over 2-4 waves (BDF2).  0: off -- every pass moves all
+ * segments together (at most 4 steps) and corrects them in the next pass;
+ * 1 (default): pipelined when an advance brings enough whole passes (BDF2 with
+ * the split fill: at least 1/8 of the pipeline's depth; otherwise its depth),
+ * else aligned; 2: always pipelined. */
 rt_status rt_set_pipeline(rt_solver *s, int on);
 rt_status rt_get_pipeline(rt_solver *s, int *on);
 /* Schedule state: steps the chain head is ahead of the tail (0 = aligned),

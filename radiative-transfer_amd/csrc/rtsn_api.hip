@@ -927,6 +927,18 @@ static rt_status pipe_launch(rt_solver *s) {
   return RT_OK;
 }
 
+// rt_set_pipeline(1): the fewest whole passes an advance must bring for the pipelined
+// schedule.  A pipelined run of n passes over P chain positions takes P + n - 1 launches;
+// with the fill/drain launches split over 4 waves (fill_level_waves: BDF2 blocks with a
+// split kernel) a launch of at most P/4 positions costs a quarter of a pass, so from
+// n >= P/8 passes the run beats aligned passes (at most 4 steps each, the correction doubling
+// the FP64 work: 20.0 vs 8.3 ms per step on SL).  Without the split, n >= P.
+static int auto_pipeline_passes(const rt_solver *s) {
+  const int P = chain_positions(s);
+  if (s->scheme == SCHEME_BDF2 && !s->level_waves && split_block(s->T)) return std::max(1, (P + 7) / 8);
+  return P;
+}
+
 // Queue nsteps; launch whole passes while the chain head is behind.
 static rt_status pipe_advance(rt_solver *s, int nsteps) {
   s->queued += nsteps;
@@ -940,7 +952,7 @@ static rt_status pipe_advance(rt_solver *s, int nsteps) {
   const long long passes = s->queued / T;
   if (passes == 0) return RT_OK;
   if (!s->Tpipe) {
-    if (s->pipe == 1 && passes < chain_positions(s)) {
+    if (s->pipe == 1 && passes < auto_pipeline_passes(s)) {
       // too few passes to fill the pipeline (it would run its segments nearly one
       // at a time): aligned passes of at most kMaxAlignedBlock steps instead
       s->queued -= static_cast<int>(passes * T);
