@@ -60,11 +60,11 @@ import numpy as np  # noqa: E402
 
 METRIC = "cell·angle·group updates/sec (Sn sweep) + BDF2 steps/sec, llnl_slab_test"
 HBM_PEAK = 8.0e12
-SUPPORTED_TIME_BLOCKS = (1, 2, 3, 4, 5, 6, 7, 8, 10, 12, 16, 20)  # rt_set_time_block
+SUPPORTED_TIME_BLOCKS = (1, 2, 3, 4, 5, 6, 7, 8, 10, 12, 16, 20, 24, 32, 40)  # rt_set_time_block
 # the bench's choice for K timed steps: the first of these dividing K, fastest per step first
 # (SL pipelined, ms/step: T = 16 8.2-8.4, 20 8.7, 12 ~9.0, 10 8.9-9.0, 8 9.5, 4 12.3, 2 21;
 # profiles/r02a_windows.jsonl)
-TIME_BLOCK_PREFERENCE = (16, 20, 12, 10, 8, 7, 6, 5, 4, 3, 2, 1)
+TIME_BLOCK_PREFERENCE = (16, 20, 12, 10, 8, 7, 6, 5, 4, 3, 2, 1)  # 24, 32: only on request
 FP64_PEAK = 78.6e12  # MI355X FP64 vector spec (256 CU x 4 SIMD x 16 FMA lanes x 2 x 2.4 GHz); measured 71 TF: profiles/r01_fp64_peak.txt
 KAPPA_TABLE = REPO / "tests" / "golden" / "prm" / "llnl_slab_test_group_kappa_a.txt"
 
@@ -241,11 +241,15 @@ def load_traffic(variant: str, tb: int, algorithmic_bytes: float):
     return b if b and abs(b / algorithmic_bytes - 1.0) < 0.1 else None
 
 
-def choose_time_block(steps: int, cap: int = 0) -> int:
-    """Steps per pass for a timed region of exactly `steps` steps: the first block of
-    TIME_BLOCK_PREFERENCE (measured fastest per step first) that divides it, at most
-    `cap` when given (0: no cap)."""
-    return next(t for t in TIME_BLOCK_PREFERENCE if (not cap or t <= cap) and steps % t == 0)
+def choose_time_block(steps: int, forced: int = 0) -> int:
+    """Steps per pass for a timed region of exactly `steps` steps: `forced` when given
+    (it must divide `steps`), else the first block of TIME_BLOCK_PREFERENCE (measured
+    fastest per step first) that divides it."""
+    if forced:
+        if forced not in SUPPORTED_TIME_BLOCKS or steps % forced:
+            raise ValueError(f"--time-block {forced} must be a supported block dividing --steps {steps}")
+        return forced
+    return next(t for t in TIME_BLOCK_PREFERENCE if steps % t == 0)
 
 
 def warmup_steps(requested: int, fill: int, tb: int) -> int:
@@ -367,8 +371,8 @@ def run_rank(solver, p: dict, steps: int, warmup: int, world: int, device, shard
     # the pass the timed region runs, as rocprof names it: pipelined when the pipeline is
     # filled, level-split (two waves per segment) where the handle runs it (default: T = 20)
     if before["lag_steps"] > 0:
-        split = solver.level_waves == 2 and p.get("ts_method", 3) == 3 and tb in (8, 12, 16, 20)
-        kernel_name = f"sweep_split_kernel<3, {tb}>" if split else f"sweep_block_kernel<3, {tb}, 2, false>"
+        lw = solver.level_waves if p.get("ts_method", 3) == 3 else 1
+        kernel_name = f"sweep_split_kernel<3, {tb}, {lw}>" if lw > 1 else f"sweep_block_kernel<3, {tb}, 2, false>"
     else:
         kernel_name = f"sweep_block_kernel<3, {tb}, 0, false>"
     solver.set_profiling(True)
@@ -611,7 +615,7 @@ def main():
     ap.add_argument("--groups", type=int, default=128, help="groups per GPU (weak) or in total (strong)")
     ap.add_argument("--cells", type=int, default=1_000_000)
     ap.add_argument("--time-block", type=int, default=0,
-                    help="full steps fused per HBM pass (0: the library default)")
+                    help="full steps fused per HBM pass, dividing --steps (0: the fastest dividing it)")
     ap.add_argument("--schedule", choices=["pipelined", "aligned"], default="pipelined",
                     help="staggered segments (exact starts) or aligned segments with deferred correction")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -648,8 +652,8 @@ def main():
     if args.time_block:
         solver.time_block = args.time_block
     solver.pipeline = 1 if args.schedule == "pipelined" else 0  # 1: pipelined when the run fills it
-    # exactly K timed steps: the time block is the fastest supported one dividing K (at
-    # most --time-block when given); the handle re-sizes its segments for that block
+    # exactly K timed steps: the time block is --time-block, or the fastest supported one
+    # dividing K; the handle re-sizes its segments for that block
     steps = args.steps if args.steps > 0 else 2 * solver.time_block
     tb = choose_time_block(steps, args.time_block)
     solver.time_block = tb

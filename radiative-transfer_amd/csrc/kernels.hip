@@ -1181,7 +1181,7 @@ static hipError_t launch_t(int mode, const SegArgs &a, int grid, hipStream_t st)
   }
   if (mode == SWEEP_PIPELINED) {
     if constexpr (level_split_supported(S, T)) {
-      if (a.level_waves == 2) {
+      if (a.level_waves == 2 && T <= 20) {  // T = 24, 32: 12 or 16 levels per wave spill
         hipLaunchKernelGGL((sweep_split_kernel<S, T, 2>), dim3(grid), dim3(128), 0, st, a);
         return hipGetLastError();
       }
@@ -1193,8 +1193,11 @@ static hipError_t launch_t(int mode, const SegArgs &a, int grid, hipStream_t st)
       }
     }
     if (a.level_waves != 1) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((sweep_block_kernel<S, T, 2>), dim3(grid), dim3(64), 0, st, a);
-    return hipGetLastError();
+    if constexpr (one_wave_block(S, T)) {
+      hipLaunchKernelGGL((sweep_block_kernel<S, T, 2>), dim3(grid), dim3(64), 0, st, a);
+      return hipGetLastError();
+    }
+    return hipErrorInvalidValue;
   }
   if constexpr (T <= kMaxAlignedBlock) {
     if (mode == SWEEP_PASS)
@@ -1223,6 +1226,9 @@ static hipError_t launch_s(int T, int mode, const SegArgs &a, int grid, hipStrea
     case 12: return launch_t<S, 12>(mode, a, grid, st);
     case 16: return launch_t<S, 16>(mode, a, grid, st);
     case 20: return launch_t<S, 20>(mode, a, grid, st);
+    case 24: return launch_t<S, 24>(mode, a, grid, st);
+    case 32: return launch_t<S, 32>(mode, a, grid, st);
+    case 40: return launch_t<S, 40>(mode, a, grid, st);
     default: return hipErrorInvalidValue;
   }
 }
@@ -1261,6 +1267,18 @@ static hipError_t occupancy_s(int T, int level_waves, int *w) {
         default: break;
       }
     }
+    if (level_waves == 4) {
+      switch (T) {
+        case 8: return hipOccupancyMaxActiveBlocksPerMultiprocessor(w, sweep_split_kernel<S, 8, 4>, 256, 0);
+        case 12: return hipOccupancyMaxActiveBlocksPerMultiprocessor(w, sweep_split_kernel<S, 12, 4>, 256, 0);
+        case 16: return hipOccupancyMaxActiveBlocksPerMultiprocessor(w, sweep_split_kernel<S, 16, 4>, 256, 0);
+        case 20: return hipOccupancyMaxActiveBlocksPerMultiprocessor(w, sweep_split_kernel<S, 20, 4>, 256, 0);
+        case 24: return hipOccupancyMaxActiveBlocksPerMultiprocessor(w, sweep_split_kernel<S, 24, 4>, 256, 0);
+        case 32: return hipOccupancyMaxActiveBlocksPerMultiprocessor(w, sweep_split_kernel<S, 32, 4>, 256, 0);
+        case 40: return hipOccupancyMaxActiveBlocksPerMultiprocessor(w, sweep_split_kernel<S, 40, 4>, 256, 0);
+        default: break;
+      }
+    }
   }
   switch (T) {
     case 1: return hipOccupancyMaxActiveBlocksPerMultiprocessor(w, sweep_block_kernel<S, 1, 0>, 64, 0);
@@ -1275,6 +1293,15 @@ static hipError_t occupancy_s(int T, int level_waves, int *w) {
     case 12: return hipOccupancyMaxActiveBlocksPerMultiprocessor(w, sweep_block_kernel<S, 12, 2>, 64, 0);
     case 16: return hipOccupancyMaxActiveBlocksPerMultiprocessor(w, sweep_block_kernel<S, 16, 2>, 64, 0);
     case 20: return hipOccupancyMaxActiveBlocksPerMultiprocessor(w, sweep_block_kernel<S, 20, 2>, 64, 0);
+    case 24:
+      if constexpr (one_wave_block(S, 24)) return hipOccupancyMaxActiveBlocksPerMultiprocessor(w, sweep_block_kernel<S, 24, 2>, 64, 0);
+      return hipErrorInvalidValue;
+    case 32:
+      if constexpr (one_wave_block(S, 32)) return hipOccupancyMaxActiveBlocksPerMultiprocessor(w, sweep_block_kernel<S, 32, 2>, 64, 0);
+      return hipErrorInvalidValue;
+    case 40:
+      if constexpr (one_wave_block(S, 40)) return hipOccupancyMaxActiveBlocksPerMultiprocessor(w, sweep_block_kernel<S, 40, 2>, 64, 0);
+      return hipErrorInvalidValue;
     default: return hipErrorInvalidValue;
   }
 }

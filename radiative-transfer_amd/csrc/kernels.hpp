@@ -30,7 +30,12 @@ constexpr int chunk_cells(int S, int T) {
 }
 // pipelined passes whose T levels two waves can share (sweep_split_kernel):
 // BDF2, where the carried states (5 per level) are what overflows 256 registers
-constexpr bool level_split_supported(int S, int T) { return S == 3 && (T == 8 || T == 10 || T == 12 || T == 16 || T == 20); }
+constexpr bool level_split_supported(int S, int T) {
+  return S == 3 && (T == 8 || T == 10 || T == 12 || T == 16 || T == 20 || T == 24 || T == 32 || T == 40);
+}
+// pipelined passes with a one-wave kernel: all but BDF2 beyond 20 levels (its carried
+// states would spill; those run split over four waves)
+constexpr bool one_wave_block(int S, int T) { return S != 3 || T <= 20; }
 // rows per chunk of the level-split pass (16 rows with T/2 = 8 levels spill past 256 registers)
 #ifndef RT_CHUNK_SPLIT
 #define RT_CHUNK_SPLIT 8
@@ -39,7 +44,7 @@ constexpr int split_chunk_cells() { return RT_CHUNK_SPLIT; }
 constexpr int kXcds = 8;                                // gfx950: workgroups are dealt to 8 XCDs round-robin
 constexpr int kSweepTile = 64;                          // cells are padded to whole tiles of 64 rows
 
-constexpr int kMaxTimeBlock = 20;                       // full steps fused per pipelined pass (template range)
+constexpr int kMaxTimeBlock = 40;                       // full steps fused per pipelined pass (template range)
 constexpr int kMaxAlignedBlock = 4;                     // ... per aligned pass (carries a T K correction state)
 
 // Segment propagators of the T-level combined state (KC = T K, packed lower

@@ -98,9 +98,14 @@ struct rt_solver {
 // (sweep_split_kernel) where measured faster -- BDF2 at T = 20, whose one-wave kernel
 // needs 126 AGPRs beside 256 VGPRs (9% extra moves; split 8.29-8.31 vs 8.52-8.53 ms/step
 // on SL, profiles/r02b_split20.jsonl) -- and one wave otherwise (T = 16: 4% faster).
+static bool split_block(int T);
+
 static int level_waves_of(const rt_solver *s, int T) {
-  if (s->level_waves) return s->level_waves;
-  return s->scheme == SCHEME_BDF2 && T == 20 ? 2 : 1;
+  if (s->scheme != SCHEME_BDF2 || !split_block(T)) return 1;  // the split kernel is BDF2's
+  if (T > 20) return 4;                                         // one or two waves would spill
+  int lw = s->level_waves ? s->level_waves : (T == 20 ? 2 : 1);
+  if (lw == 4 && T % 4) lw = 2;
+  return lw;
 }
 
 // Waves per segment of one pipelined launch of `grid` workgroups.  The segments are sized
@@ -109,7 +114,9 @@ static int level_waves_of(const rt_solver *s, int T) {
 // segments are split over 2 or 4 waves (sweep_split_kernel) as long as the launch stays
 // within the full launch's wave count -- the lines are then traversed 2-4x faster while
 // the chip would otherwise idle (BDF2 time blocks the split kernel has: 8, 10, 12, 16, 20).
-static bool split_block(int T) { return T == 8 || T == 10 || T == 12 || T == 16 || T == 20; }
+static bool split_block(int T) {
+  return T == 8 || T == 10 || T == 12 || T == 16 || T == 20 || T == 24 || T == 32 || T == 40;
+}
 
 static int fill_level_waves(const rt_solver *s, int grid) {
   const int base = level_waves_of(s, s->Tpipe);
@@ -144,7 +151,9 @@ static rt_status fail(rt_solver *s, rt_status st, const std::string &msg) {
 static int default_time_block(int) { return 16; }
 
 // rt_set_time_block's domain: the instantiated sweep kernels (kernels.hip launch_s)
-static bool supported_time_block(int T) { return (T >= 1 && T <= 8) || T == 10 || T == 12 || T == 16 || T == 20; }
+static bool supported_time_block(int T) {
+  return (T >= 1 && T <= 8) || T == 10 || T == 12 || T == 16 || T == 20 || T == 24 || T == 32 || T == 40;
+}
 
 static int map_count_of(int scheme) {
   switch (scheme) {
@@ -672,7 +681,7 @@ static rt_status create_impl(const rt_params *pin, int g_lo, int g_hi, int d_lo,
   if (const char *t = std::getenv("RTSN_TIME_BLOCK"))  // experiments: the segment count follows
     if (supported_time_block(std::atoi(t))) h->T = std::atoi(t);
   if (const char *lw = std::getenv("RTSN_LEVEL_WAVES"))  // experiments: only "1" or "2" are read
-    if (!std::strcmp(lw, "1") || !std::strcmp(lw, "2")) h->level_waves = lw[0] - '0';
+    if (!std::strcmp(lw, "1") || !std::strcmp(lw, "2") || !std::strcmp(lw, "4")) h->level_waves = lw[0] - '0';
   HIP_TRY(h, sweep_occupancy(h->scheme, h->T, level_waves_of(h, h->T), &waves_per_cu));
   // tuning knob for experiments: target resident waves per CU (segments per line follow)
   if (const char *w = std::getenv("RTSN_WAVES_PER_CU")) waves_per_cu = std::atoi(w);
@@ -1647,7 +1656,7 @@ extern "C" rt_status rt_get_pipeline(rt_solver *s, int *on) {
 extern "C" rt_status rt_set_time_block(rt_solver *s, int steps_per_pass) {
   if (!s) return fail(nullptr, RT_ERR_ARG, "rt_set_time_block: NULL handle");
   if (!supported_time_block(steps_per_pass))
-    return fail(s, RT_ERR_ARG, "rt_set_time_block: steps per pass must be 1..8, 10, 12, 16 or 20");
+    return fail(s, RT_ERR_ARG, "rt_set_time_block: steps per pass must be 1..8, 10, 12, 16, 20, 24, 32 or 40");
   HIP_TRY(s, hipSetDevice(s->device));
   s->T = steps_per_pass;
   return resegment(s);  // now if the positions are aligned, else when they next are
@@ -1661,7 +1670,7 @@ extern "C" rt_status rt_get_time_block(rt_solver *s, int *steps_per_pass) {
 
 extern "C" rt_status rt_set_level_waves(rt_solver *s, int waves) {
   if (!s) return fail(nullptr, RT_ERR_ARG, "rt_set_level_waves: NULL handle");
-  if (waves < 0 || waves > 2) return fail(s, RT_ERR_PARAM, "rt_set_level_waves: 0 (auto), 1 or 2");
+  if (waves < 0 || waves > 4 || waves == 3) return fail(s, RT_ERR_PARAM, "rt_set_level_waves: 0 (auto), 1, 2 or 4");
   s->level_waves = waves;  // segments stay as created: the schedule is exact for any segmentation
   return RT_OK;
 }

@@ -229,7 +229,10 @@ def test_time_block_choice():
     assert bench.choose_time_block(2) == 2
     assert bench.choose_time_block(7) == 7
     assert bench.choose_time_block(11) == 1
-    assert bench.choose_time_block(20, cap=10) == 10
+    assert bench.choose_time_block(20, forced=10) == 10
+    assert bench.choose_time_block(64, forced=32) == 32
+    with pytest.raises(ValueError):
+        bench.choose_time_block(20, forced=16)
     for k in range(1, 200):
         t = bench.choose_time_block(k)
         assert k % t == 0 and t in bench.SUPPORTED_TIME_BLOCKS

@@ -191,6 +191,7 @@ def test_random_state_long_lines(rtsn_mod, oracle_mod, tb, steps, pipe):
 
 
 @pytest.mark.parametrize("ts,tb,steps", [(3, 12, 13), (3, 16, 17), (3, 20, 21), (3, 20, 43), (2, 20, 40),
+                                         (3, 24, 25), (3, 32, 33), (3, 32, 66), (3, 40, 41), (2, 32, 64), (1, 40, 80),
                                          (1, 20, 41), (3, 8, 16), (2, 16, 40), (1, 16, 40),
                                          (2, 12, 30), (1, 5, 11), (3, 10, 15), (3, 10, 20), (2, 10, 20), (1, 10, 30)])
 def test_large_time_blocks(rtsn_mod, oracle_mod, ts, tb, steps):
@@ -328,10 +329,10 @@ def test_pipeline_long_run_many_segments(rtsn_mod, oracle_mod, ts):
 def test_time_block_range(rtsn_mod):
     d = rtsn_mod.params_default()
     with rtsn_mod.Solver(d) as s:
-        for ok in (1, 4, 8, 10, 12, 16, 20):
+        for ok in (1, 4, 8, 10, 12, 16, 20, 24, 32, 40):
             s.time_block = ok
             assert s.time_block == ok
-        for bad in (0, 9, 13, 17, 21, 32, -1):
+        for bad in (0, 9, 13, 17, 21, 33, 48, -1):
             with pytest.raises(rtsn_mod.RtError) as e:
                 s.time_block = bad
             assert e.value.status == 8
@@ -448,8 +449,8 @@ def sl_pair_oracle(oracle_mod):
     """The headline kernel's workload at its full line length (verdict r01, item 1): the SL
     slab's grid, kappa table and N = 1e6 cells, M = 4, groups 126 (kappa set to the table's
     1e6: optically thick, tau = 4e5) and 127 (kappa 0.021: thin, tau = 0.008), V = 0 and
-    V = 5.994 with the v/c correction on; the oracle's state after 12, 18 and 22 BDF2 steps
-    (T + 2 for T = 10, 16, 20; 2 T + 2 for T = 10).  dt = 1e-7 (Courant number c mu dt / dx
+    V = 5.994 with the v/c correction on; the oracle's state after 12, 18, 22, 34 and 42 BDF2
+    steps (T + 2 for T = 10, 16, 20, 32, 40; 2 T + 2 for T = 10).  dt = 1e-7 (Courant number c mu dt / dx
     = 64: the upwind carry crosses segment after segment) and dt = 1e-9 (Courant 0.6).
     The three oracle runs go in parallel threads (ctypes releases the GIL)."""
     import sys
@@ -465,11 +466,11 @@ def sl_pair_oracle(oracle_mod):
         kap[126] = kap[0]
         p["group_kappa"] = kap
         q = dict(p, bc_left=0, bc_right=0, dx=p["X"] / p["N"], have_group_bounds=0, have_group_kappa=1,
-                 prm_found=1, max_timesteps=22)
+                 prm_found=1, max_timesteps=42)
         o = oracle_mod.OracleSolver(q, g_lo=126, g_hi=128)
         o.set_threads(2)
         snaps, done = {}, 0
-        for steps in (12, 18, 22):
+        for steps in (12, 18, 22, 34, 42):
             o.run_substeps(4 * done, 4 * (steps - done))
             done = steps
             mu, wt = o.quad()
@@ -482,10 +483,12 @@ def sl_pair_oracle(oracle_mod):
 
 
 @pytest.mark.parametrize("case", PAIR_CASES)
-@pytest.mark.parametrize("tb,steps", [(10, 12), (16, 18), (20, 22), (10, 22)])
+@pytest.mark.parametrize("tb,steps", [(10, 12), (16, 18), (20, 22), (10, 22), (32, 34), (40, 42)])
 def test_headline_kernel_full_length(rtsn_mod, sl_pair_oracle, tb, steps, case):
-    """sweep_block_kernel<3, T, 2> -- the pass the bench times -- on full-length SL lines
-    (N = 1e6 cut into ~500-1000 segments sized for the T-step kernel's occupancy) against
+    """The passes the bench times -- sweep_block_kernel<3, T, 2> at T = 10, 16 and the
+    level-split sweep_split_kernel<3, T, KW> at T = 20 (2 waves), 32 and 40 (4 waves) -- on
+    full-length SL lines (N = 1e6 cut into ~250-1000 segments sized for each kernel's
+    occupancy) against
     the oracle: the pipeline fills over every segment position, runs, drains, and an
     aligned 2-step remainder pass with its finalize follows.  psi, the node array, phi,
     phi_plus and F per group to 1e-10 of the group's scale; the group ends (one node sum
@@ -501,7 +504,7 @@ def test_headline_kernel_full_length(rtsn_mod, sl_pair_oracle, tb, steps, case):
         gpu.pipeline = 2
         gpu.time_block = tb
         _, segs = gpu.sweep_geometry()
-        assert segs >= 400
+        assert segs >= 200
         gpu.advance(steps)
         psi, ends = gpu.psi(), gpu.ends()
         phi_g, F_g, pp_g = gpu.moments()
