@@ -62,9 +62,11 @@ METRIC = "cell·angle·group updates/sec (Sn sweep) + BDF2 steps/sec, llnl_slab_
 HBM_PEAK = 8.0e12
 SUPPORTED_TIME_BLOCKS = (1, 2, 3, 4, 5, 6, 7, 8, 10, 12, 16, 20, 24, 32, 40)  # rt_set_time_block
 # the bench's choice for K timed steps: the first of these dividing K, fastest per step first
-# (SL pipelined, ms/step: T = 16 8.2-8.4, 20 8.7, 12 ~9.0, 10 8.9-9.0, 8 9.5, 4 12.3, 2 21;
-# profiles/r02a_windows.jsonl)
-TIME_BLOCK_PREFERENCE = (16, 20, 12, 10, 8, 7, 6, 5, 4, 3, 2, 1)  # 24, 32: only on request
+# (SL pipelined, same box, ms/step: T = 40 7.49-7.53, 32 7.69-7.75, 16 8.13-8.19, 20 8.22,
+# 24 8.26-8.29, 12 ~9.0, 10 8.9-9.0, 8 9.5, 4 12.3, 2 21; profiles/r02g_big_time_blocks.jsonl,
+# r02a_windows.jsonl)
+TIME_BLOCK_PREFERENCE = (40, 32, 16, 20, 24, 12, 10, 8, 7, 6, 5, 4, 3, 2, 1)
+DEFAULT_TIME_BLOCK = 40  # the default window: two passes of the fastest block
 FP64_PEAK = 78.6e12  # MI355X FP64 vector spec (256 CU x 4 SIMD x 16 FMA lanes x 2 x 2.4 GHz); measured 71 TF: profiles/r01_fp64_peak.txt
 KAPPA_TABLE = REPO / "tests" / "golden" / "prm" / "llnl_slab_test_group_kappa_a.txt"
 
@@ -606,8 +608,8 @@ def run_material(p: dict, info, world: int, device, local: int, steps: int, dirs
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    # defaults: the timed region is 2 steady-state passes (steps are rounded up to whole passes)
-    ap.add_argument("--steps", type=int, default=0, help="timed steps (default: two passes)")
+    # defaults: the timed region is 2 steady-state passes of the fastest block (T = 40)
+    ap.add_argument("--steps", type=int, default=0, help="timed steps (default: two passes of 40)")
     ap.add_argument("--warmup", type=int, default=-1,
                     help="untimed steps before timing, at least the pipeline fill (default: the fill)")
     ap.add_argument("--variant", choices=["v0", "corr"], default="v0")
@@ -654,7 +656,7 @@ def main():
     solver.pipeline = 1 if args.schedule == "pipelined" else 0  # 1: pipelined when the run fills it
     # exactly K timed steps: the time block is --time-block, or the fastest supported one
     # dividing K; the handle re-sizes its segments for that block
-    steps = args.steps if args.steps > 0 else 2 * solver.time_block
+    steps = args.steps if args.steps > 0 else 2 * (args.time_block or DEFAULT_TIME_BLOCK)
     tb = choose_time_block(steps, args.time_block)
     solver.time_block = tb
     # Warmup: at least W steps, and always whole passes that fill the pipeline (segments

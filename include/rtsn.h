@@ -189,9 +189,10 @@ rt_status rt_sweep_traffic(rt_solver *s, double *bytes_per_launch, double *updat
  * affine cell map (BDF2 28, CN 8, BE 6 FMAs per cell x line x step) times T
  * steps; the cross-segment correction is parallelisation overhead, not counted. */
 rt_status rt_sweep_flops(rt_solver *s, double *flops_per_launch);
-/* Time blocking: full steps advanced per pass over HBM: 1..8, 10, 12, 16 or 20
- * (default 16; aligned passes take at most 4).  Results do not depend on it
- * beyond rounding.  The segments of a line are re-sized for the new block's
+/* Time blocking: full steps advanced per pass over HBM: 1..8, 10, 12, 16, 20, 24,
+ * 32 or 40 (default 16; aligned passes take at most 4; BDF2 beyond 20 runs the
+ * level-split pass over four waves -- on SL T = 40 is the fastest per step, 7.5 vs
+ * 8.2 ms at T = 16).  Results do not depend on it beyond rounding.  The segments of a line are re-sized for the new block's
  * pipelined kernel (its occupancy) as soon as every segment is at the same time
  * with no correction outstanding (now, or before the next pass). */
 rt_status rt_set_time_block(rt_solver *s, int steps_per_pass);
@@ -211,13 +212,15 @@ rt_status rt_get_pipeline(rt_solver *s, int *on);
  * steps queued but not launched, whether a correction is pending; any NULL skipped. */
 rt_status rt_pipeline_state(rt_solver *s, long long *lag_steps, int *queued_steps, int *pending);
 rt_status rt_get_time_block(rt_solver *s, int *steps_per_pass);
-/* Waves per segment of a pipelined BDF2 pass of 8, 12, 16 or 20 steps: 1 runs all
- * levels in one wave; 2 shares them between two waves of a workgroup through LDS, so
- * a SIMD holds two waves instead of one; 0 (default) = 2 at T = 20 (its one-wave
- * kernel leans on AGPRs; the split one measured 2.7% faster on SL) and 1 otherwise (at
- * T = 16 one wave is 4% faster).  rt_get_level_waves reports the
- * effective choice for the current time block; RTSN_LEVEL_WAVES=1|2 at creation forces
- * one.  Bitwise-identical results.  Other passes always use one wave. */
+/* Waves per segment of a pipelined BDF2 pass of 8, 10, 12, 16 or 20 steps: 1 runs
+ * all levels in one wave; 2 (or 4, T divisible by 4) shares them between the waves of
+ * a workgroup through LDS; 0 (default) = 2 at T = 20 (its one-wave kernel leans on
+ * AGPRs; the split one measured 2.7% faster on SL), 1 otherwise (at T = 16 one wave is
+ * 4% faster), and with 0 the pipeline's fill and drain launches split
+ * further (up to 4 waves) while the chip would idle.  T = 24, 32, 40 always run 4
+ * waves.  rt_get_level_waves reports the effective choice for the current time block;
+ * RTSN_LEVEL_WAVES=1|2|4 at creation forces one.  Bitwise-identical results.  Other
+ * schemes always use one wave. */
 rt_status rt_set_level_waves(rt_solver *s, int waves);
 rt_status rt_get_level_waves(rt_solver *s, int *waves);
 /* Sweep geometry actually used: waves launched per step (one per line group

@@ -223,8 +223,10 @@ def test_time_block_choice():
     """bench.py: K timed steps run as whole passes of the fastest block dividing K."""
     import bench
     assert bench.choose_time_block(20) == 20        # the driver's window
-    assert bench.choose_time_block(32) == 16
-    assert bench.choose_time_block(80) == 16        # 16 before 20 when both divide
+    assert bench.choose_time_block(32) == 32
+    assert bench.choose_time_block(80) == 40
+    assert bench.choose_time_block(48) == 16        # 16 before 24 when both divide
+    assert bench.choose_time_block(60) == 20
     assert bench.choose_time_block(30) == 10
     assert bench.choose_time_block(2) == 2
     assert bench.choose_time_block(7) == 7
