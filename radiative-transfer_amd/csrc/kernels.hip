@@ -1181,9 +1181,11 @@ static hipError_t launch_t(int mode, const SegArgs &a, int grid, hipStream_t st)
   }
   if (mode == SWEEP_PIPELINED) {
     if constexpr (level_split_supported(S, T)) {
-      if (a.level_waves == 2 && T <= 20) {  // T = 24, 32: 12 or 16 levels per wave spill
-        hipLaunchKernelGGL((sweep_split_kernel<S, T, 2>), dim3(grid), dim3(128), 0, st, a);
-        return hipGetLastError();
+      if constexpr (T <= 20) {  // beyond, 12 or more levels per wave spill
+        if (a.level_waves == 2) {
+          hipLaunchKernelGGL((sweep_split_kernel<S, T, 2>), dim3(grid), dim3(128), 0, st, a);
+          return hipGetLastError();
+        }
       }
       if constexpr (T % 4 == 0) {
         if (a.level_waves == 4) {
