@@ -116,7 +116,8 @@ void rt_destroy(rt_solver *s);
 
 /* Solver::solve (solver.cpp:590-823): max_timesteps full steps (x4 substeps
  * for BDF2), preceded by computeEquilibriumSources when use_mg_equilib.
- * Synchronous. */
+ * Synchronous.  Unless rt_set_time_block was called, a BDF2 run of at least 80
+ * steps fuses 40 steps per pass (the fastest block; results equal to rounding). */
 rt_status rt_solve(rt_solver *s);
 /* Asynchronous: enqueue nsteps full steps on the handle's stream (with the
  * pipelined schedule, whole passes are launched now and a remainder of fewer

@@ -52,6 +52,7 @@ struct rt_solver {
   int Tp = 0;                    // steps of the pass whose correction is pending
   int Sg = 1, Ls = 16;           // segments per line and cells per segment
   int seg_T = 0;                 // the time block the segments were sized for (0: none)
+  bool T_set = false;            // the caller chose the time block (rt_set_time_block / RTSN_TIME_BLOCK)
   int level_waves = 0;           // pipelined BDF2 passes: 0 auto (level_waves_of), 1 one wave, 2 levels shared by two
   int d_lo = 0, d_hi = 0;        // direction-pair shard [d_lo, d_hi) of the M/2 pairs (d_hi = 0: all)
   int M_full = 0;                // the configuration's M (p.M is the handle's own direction count)
@@ -149,6 +150,7 @@ static rt_status fail(rt_solver *s, rt_status st, const std::string &msg) {
 // Measured on SL (pipelined schedule, profiles/): BDF2 43.0 / 21.7 / 14.5 / 12.3 /
 // 9.5 / 9.0 / 8.4 ms per step at T = 1 / 2 / 3 / 4 / 8 / 12 / 16.
 static int default_time_block(int) { return 16; }
+constexpr int kLongRunBlock = 40;  // rt_solve's block for runs of >= 2 such passes (BDF2)
 
 // rt_set_time_block's domain: the instantiated sweep kernels (kernels.hip launch_s)
 static bool supported_time_block(int T) {
@@ -679,7 +681,10 @@ static rt_status create_impl(const rt_params *pin, int g_lo, int g_hi, int d_lo,
   int waves_per_cu = 0;
   h->T = default_time_block(h->scheme);
   if (const char *t = std::getenv("RTSN_TIME_BLOCK"))  // experiments: the segment count follows
-    if (supported_time_block(std::atoi(t))) h->T = std::atoi(t);
+    if (supported_time_block(std::atoi(t))) {
+      h->T = std::atoi(t);
+      h->T_set = true;
+    }
   if (const char *lw = std::getenv("RTSN_LEVEL_WAVES"))  // experiments: only "1" or "2" are read
     if (!std::strcmp(lw, "1") || !std::strcmp(lw, "2") || !std::strcmp(lw, "4")) h->level_waves = lw[0] - '0';
   HIP_TRY(h, sweep_occupancy(h->scheme, h->T, level_waves_of(h, h->T), &waves_per_cu));
@@ -1025,8 +1030,17 @@ extern "C" rt_status rt_synchronize(rt_solver *s) {
   return RT_OK;
 }
 
+// rt_solve knows the run's length: unless the caller chose a block, a BDF2 run of at
+// least two T = 40 passes runs T = 40 (the fastest per step on SL: 7.5 vs 8.2 ms at 16,
+// DESIGN.md §8), shorter runs keep the default.
+static void solve_time_block(rt_solver *s) {
+  if (s->T_set || s->scheme != SCHEME_BDF2 || s->Tpipe || s->queued) return;
+  if (s->p.max_timesteps >= 2 * kLongRunBlock) s->T = kLongRunBlock;
+}
+
 extern "C" rt_status rt_solve(rt_solver *s) {
   if (!s) return fail(nullptr, RT_ERR_ARG, "rt_solve: NULL handle");
+  solve_time_block(s);
   rt_status st = rt_advance(s, s->p.max_timesteps);
   if (st) return st;
   if ((st = complete(s))) return st;
@@ -1659,6 +1673,7 @@ extern "C" rt_status rt_set_time_block(rt_solver *s, int steps_per_pass) {
     return fail(s, RT_ERR_ARG, "rt_set_time_block: steps per pass must be 1..8, 10, 12, 16, 20, 24, 32 or 40");
   HIP_TRY(s, hipSetDevice(s->device));
   s->T = steps_per_pass;
+  s->T_set = true;
   return resegment(s);  // now if the positions are aligned, else when they next are
 }
 
