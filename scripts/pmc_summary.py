@@ -22,8 +22,10 @@ def counters(d):
         for r in csv.DictReader(open(f)):
             name = r["Kernel_Name"]
             targs = name.replace(" ", "").split("(")[0].split("<")[-1].rstrip(">").split(",")
-            # a sweep pass <S, T, mode[, material]>: mode 0 aligned, 2 pipelined (1 = finalize)
-            if KERNEL in name and len(targs) >= 3 and targs[2] in ("0", "2") and "true" not in targs[3:]:
+            # a sweep pass: sweep_block_kernel<S, T, mode[, material]> with mode 0 aligned or 2
+            # pipelined (1 = finalize), or the level-split sweep_split_kernel<S, T, waves>
+            block = KERNEL in name and len(targs) >= 3 and targs[2] in ("0", "2") and "true" not in targs[3:]
+            if block or "sweep_split_kernel" in name:
                 out.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
     return out
 
