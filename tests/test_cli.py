@@ -327,3 +327,17 @@ def test_gray_binary(tmp_path):
     env = dict(os.environ, TRANSFER_DIR=str(tmp_path) + "/")
     r = subprocess.run([str(_bin("test_gray"))], cwd=run, capture_output=True, text=True, timeout=600, env=env)
     assert r.returncode == 0, r.stdout + r.stderr
+
+
+def test_transfer_ranks_fail_cleanly_without_gpu(tmp_path):
+    """RTSN_RANKS=n forks n ranks; when rank 0 cannot make the communicator id (here: no
+    GPU, ncclGetUniqueId needs one) it exits non-zero, the other ranks read end-of-file on
+    their pipe and exit too, and the parent returns the failure -- no rank is left waiting."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("the failure path needs a host without a GPU")
+    run = _run_tree(tmp_path)
+    r = subprocess.run([str(_bin("transfer")), "../prm/llnl_slab_test.prm"], cwd=run, capture_output=True, text=True,
+                       timeout=60, env=dict(os.environ, RTSN_RANKS="3"))
+    assert r.returncode != 0
+    assert "rt_comm_unique_id" in r.stderr

@@ -342,3 +342,13 @@ def test_direction_shard_plan():
     assert [bench.direction_shard("strong", 1, 6, 2, r) for r in range(2)] == [(0, 2), (2, 3)]
     with pytest.raises(ValueError):
         bench.direction_shard("strong", 1, 4, 4, 3)  # 2 pairs, 4 ranks
+
+
+def test_host_cpus_share(monkeypatch):
+    """bench.host_cpus: the CPU baseline's threads are the lease's share -- OMP_NUM_THREADS
+    where set, capped by the affinity (and the cgroup quota when there is one)."""
+    import bench
+    h = bench.host_cpus()
+    assert 1 <= h["threads"] <= h["affinity"] <= h["nproc"]
+    monkeypatch.setenv("OMP_NUM_THREADS", "1")
+    assert bench.host_cpus()["threads"] == 1
