@@ -97,6 +97,9 @@ enum SweepMode {
   SWEEP_PIPELINED = 2   // one launch of the staggered (pipelined) schedule
 };
 hipError_t launch_sweep(int scheme, int T, int mode, const SegArgs &a, int grid, hipStream_t st);
+// the level-split pipelined BDF2 pass (kernels_split.hip): T levels over `waves` waves
+hipError_t launch_split(int T, int waves, const SegArgs &a, int grid, hipStream_t st);
+hipError_t split_occupancy(int T, int waves, int *workgroups_per_cu);
 // segments resident per CU (workgroups of the pass: one wave, or two with level_waves 2)
 hipError_t sweep_occupancy(int scheme, int T, int level_waves, int *waves_per_cu);
 hipError_t coupled_occupancy(int scheme, int *waves_per_cu);  // the material-coupled pass (T = 1)

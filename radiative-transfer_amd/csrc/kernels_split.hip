@@ -1,0 +1,283 @@
+// kernels_split.hip -- the level-split pipelined pass (sweep_split_kernel): a BDF2
+// segment's T levels shared by 2 or 4 waves of a workgroup.  Its own translation unit
+// (the kernel is instantiated for 12 (T, waves) pairs) so it compiles beside kernels.hip.
+#include <hip/hip_runtime.h>
+
+#include "cell.hpp"
+#include "kernels.hpp"
+#include "sweep_device.hpp"
+
+namespace rtamd {
+
+// ------------------------------------------------------------------------
+// Level-split pipelined pass: the same launch as sweep_block_kernel<S, T, 2>
+// with its T levels shared by KW waves of one workgroup (KW = 2 or 4), wave w
+// running levels [w T/KW, (w + 1) T/KW).  Wave 0 streams the rows in from HBM,
+// the last wave stores them, and each wave hands its chunk's nodes at its last
+// level to the next wave through LDS (two buffers per link, one barrier per
+// chunk interval): in interval I wave w computes chunk I - 2w from registers
+// while it refills them with chunk I - 2w + 1 (written by wave w - 1 in
+// interval I - 1) and writes chunk I - 2w into its outgoing buffer (I - 2w) & 1.
+// Same arithmetic in the same order per (cell, level) as the one-wave kernel:
+// bitwise equal.
+//   KW = 2: each wave holds half the carried states (X), so a SIMD runs two
+//     waves instead of one: at T = 20 (one-wave kernel: 126 AGPRs beside 256
+//     VGPRs) 8.29-8.31 vs 8.52-8.53 ms per step on SL, the default there; at
+//     T = 16 4% slower than one wave (140.6 vs 134.6 ms per pass).
+//   KW = 2, 4 in the pipeline's fill and drain: a launch with few active chain
+//     positions runs each segment on more waves, so the lines' traversal takes
+//     1/KW of the time while the chip would otherwise idle (rtsn_api.hip
+//     pipe_launch).
+// ------------------------------------------------------------------------
+template <int S, int TW, int C, bool IN_HBM, bool OUT_HBM, bool LASTCH>
+__device__ __forceinline__ void split_chunk(const double *W, double (&ein)[C], double (&eout)[C],
+                                            double (&X)[TW][SchemeDim<S>::K], bool head, double h_oi, double h_oo,
+                                            const double2 *lin, double2 *lout, __amdgpu_buffer_rsrc_t Rw,
+                                            __amdgpu_buffer_rsrc_t Rn, int voff, int row_bytes, int nv, int lane) {
+  constexpr int K = SchemeDim<S>::K;
+#pragma unroll
+  for (int c = 0; c < C; ++c) {
+    if (LASTCH && c >= nv) continue;  // wave-uniform: past the end of the segment
+    double oi = ein[c], oo = eout[c];
+    if (c == 0 && head) {  // reflective head cell, computed in the prologue
+      oi = h_oi;
+      oo = h_oo;
+    } else {
+#pragma unroll
+      for (int t = 0; t < TW; ++t) {
+        double Xn[K], a, e;
+        map_apply<S, true>(W, X[t], oi, oo, Xn, a, e);
+#pragma unroll
+        for (int r = 0; r < K; ++r) X[t][r] = Xn[r];
+        oi = a;
+        oo = e;
+      }
+    }
+    if constexpr (OUT_HBM)
+      row_store(Rw, voff, c * row_bytes, oi, oo);
+    else  // hand the nodes at this wave's last level to the next wave
+      lout[c * 64 + lane] = make_double2(oi, oo);
+    if constexpr (!LASTCH) {  // refill with the next chunk: from HBM, or from the previous wave
+      if constexpr (IN_HBM) {
+        const double2 v = row_load(Rn, voff, c * row_bytes);
+        ein[c] = v.x;
+        eout[c] = v.y;
+      } else {
+        const double2 v = lin[c * 64 + lane];
+        ein[c] = v.x;
+        eout[c] = v.y;
+      }
+    }
+  }
+}
+
+// Wave w's role (compile time: with the role a runtime branch inside one body the
+// allocation measured ~340 registers, each role alone ~215).
+template <int S, int T, int KW, int w>
+__device__ __forceinline__ void split_role(const SegArgs &a, double2 (*hand)[2][split_chunk_cells() * 64],
+                                           double2 *hhead) {
+  constexpr int K = SchemeDim<S>::K;
+  constexpr int TW = T / KW;
+  constexpr int WN = map_count<S>();
+  constexpr int C = split_chunk_cells();
+  constexpr bool IN = w == 0, OUT = w == KW - 1;
+  const int lane = threadIdx.x & 63;
+  constexpr int t0 = w * TW;  // this wave's first level
+  const size_t stride = static_cast<size_t>(a.Lpad);
+  int half, s, q, pos;
+  if (a.reflective) {
+    pos = a.pos_lo + static_cast<int>(blockIdx.x) / a.Q;
+    q = static_cast<int>(blockIdx.x) % a.Q;
+    half = pos / a.Sg;
+    s = pos % a.Sg;
+  } else {
+    const int per_half = a.Q * a.npos;
+    half = static_cast<int>(blockIdx.x) / per_half;
+    const int rem = static_cast<int>(blockIdx.x) % per_half;
+    pos = a.pos_lo + rem / a.Q;
+    q = rem % a.Q;
+    s = pos;
+  }
+  const int slot = (a.pass_lo - (pos - a.pos_lo)) & 1;
+  const int ell = q * 64 + lane;
+  const bool neg = half == 0;
+  const int k_begin = s * a.Ls;
+  const int k_end = min(a.N, k_begin + a.Ls);
+  if (k_begin >= k_end) return;  // workgroup-uniform
+  const size_t seg_stride = static_cast<size_t>(T * K) * stride;
+  const size_t half_stride = static_cast<size_t>(a.Sg) * seg_stride;
+
+  // ---- inflow and carried state of this wave's levels ----
+  const bool head_seg = (s == 0);
+  double b[TW][4];
+  {
+    const double v = a.bdry[static_cast<size_t>(half) * stride + ell];
+#pragma unroll
+    for (int t = 0; t < TW; ++t) b[t][0] = b[t][1] = b[t][2] = b[t][3] = v;
+  }
+  const bool refl_head = head_seg && !neg && a.reflective;
+  if (refl_head) {  // solver.cpp:677-684, as in sweep_block_kernel (MODE 2)
+    const double *src = a.aggs[slot] + (a.Sg - 1) * seg_stride + ell;
+#pragma unroll
+    for (int t = 0; t < TW; ++t) {
+      if constexpr (S == SCHEME_BDF2) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) b[t][r] = src[((t0 + t) * K + 1 + r) * stride];
+      } else {
+        b[t][0] = b[t][1] = b[t][2] = b[t][3] = src[((t0 + t) * K + K - 1) * stride];
+      }
+    }
+  }
+  double X[TW][K];
+  if (head_seg) {
+#pragma unroll
+    for (int t = 0; t < TW; ++t) head_state<S>(b[t], X[t]);
+  } else {
+    const double *up = a.aggs[slot] + half * half_stride + (s - 1) * seg_stride + ell;
+#pragma unroll
+    for (int t = 0; t < TW; ++t)
+#pragma unroll
+      for (int r = 0; r < K; ++r) X[t][r] = up[((t0 + t) * K + r) * stride];
+  }
+
+  // ---- rows: wave 0 streams them in, the last wave stores them ----
+  const int row_bytes = a.Lpad * static_cast<int>(sizeof(double2));
+  const int voff = lane * static_cast<int>(sizeof(double2));
+  const double2 *Eh = a.E + static_cast<size_t>(half) * a.Nrow * stride + q * 64;
+  auto rows = [&](int k0) { return rows_rsrc<C>(Eh + static_cast<size_t>(k0) * stride, row_bytes); };
+  double ein[C], eout[C];
+  if constexpr (IN) {
+    const __amdgpu_buffer_rsrc_t R0 = rows(k_begin);
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      const double2 v = row_load(R0, voff, c * row_bytes);
+      ein[c] = v.x;
+      eout[c] = v.y;
+    }
+  } else {
+#pragma unroll
+    for (int c = 0; c < C; ++c) ein[c] = eout[c] = 0.0;
+  }
+  // reflective head cell: wave r runs its levels on wave r - 1's result, in turn
+  double h_oi = 0.0, h_oo = 0.0;
+  if (refl_head) {  // workgroup-uniform: every wave passes the KW - 1 barriers
+    const double *lcp = a.lc + static_cast<size_t>(half) * LC_COUNT * stride + ell;
+    if constexpr (IN) {
+      h_oi = ein[0];
+      h_oo = eout[0];
+    }
+#pragma unroll
+    for (int r = 0; r < KW - 1; ++r) {
+      if (r == w) {  // compile-time after unrolling
+        if constexpr (!IN) {
+          const double2 v = hhead[lane];
+          h_oi = v.x;
+          h_oo = v.y;
+        }
+        head_cell<S, TW>(lcp, stride, a.hd, b, X, h_oi, h_oo, 1.0);
+        hhead[lane] = make_double2(h_oi, h_oo);
+      }
+      __syncthreads();
+    }
+    if constexpr (OUT) {
+      const double2 v = hhead[lane];
+      h_oi = v.x;
+      h_oo = v.y;
+      head_cell<S, TW>(lcp, stride, a.hd, b, X, h_oi, h_oo, 1.0);
+    }
+  }
+
+  double W[WN];
+#pragma unroll
+  for (int n = 0; n < WN; ++n) W[n] = a.map[(static_cast<size_t>(half) * WN + n) * stride + ell];
+
+  // ---- chunk intervals: nch + 2 (KW - 1) of them, one barrier after each, for every wave ----
+  const int nch = (k_end - k_begin + C - 1) / C;
+  const double2 *lin = hand[w > 0 ? w - 1 : 0][0];  // (wave 0 reads HBM, the last wave writes it:
+  double2 *lout = hand[w < KW - 1 ? w : 0][0];       //  their unused link pointer is never touched)
+  constexpr int LB = split_chunk_cells() * 64;  // one buffer of a link
+  if constexpr (!IN) {
+    for (int I = 0; I < 2 * w - 1; ++I) __syncthreads();  // the previous waves fill the pipeline
+    // interval 2w - 1: chunk 0 of the previous wave (written in interval 2w - 2)
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      const double2 v = lin[c * 64 + lane];
+      ein[c] = v.x;
+      eout[c] = v.y;
+    }
+    __syncthreads();
+  }
+  int k0 = k_begin;
+  for (int m = 0; m + 1 < nch; ++m, k0 += C) {
+    split_chunk<S, TW, C, IN, OUT, false>(W, ein, eout, X, refl_head && m == 0, h_oi, h_oo, lin + ((m + 1) & 1) * LB,
+                                          lout + (m & 1) * LB, rows(k0), rows(k0 + C), voff, row_bytes, C, lane);
+    __syncthreads();
+  }
+  split_chunk<S, TW, C, IN, OUT, true>(W, ein, eout, X, refl_head && nch == 1, h_oi, h_oo, lin,
+                                       lout + ((nch - 1) & 1) * LB, rows(k0), rows(k0), voff, row_bytes, k_end - k0,
+                                       lane);
+  __syncthreads();
+  double *ag = a.aggs[slot] + half * half_stride + static_cast<size_t>(s) * seg_stride + ell;
+#pragma unroll
+  for (int t = 0; t < TW; ++t)
+#pragma unroll
+    for (int r = 0; r < K; ++r) ag[((t0 + t) * K + r) * stride] = X[t][r];
+  for (int I = 0; I < 2 * (KW - 1 - w); ++I) __syncthreads();  // the later waves drain it
+}
+
+template <int S, int T, int KW>
+__global__ __launch_bounds__(64 * KW) __attribute__((amdgpu_waves_per_eu(2, 2))) void sweep_split_kernel(SegArgs a) {
+  static_assert(T % KW == 0 && (KW == 2 || KW == 4), "levels split evenly over 2 or 4 waves");
+  __shared__ double2 hand[KW - 1][2][split_chunk_cells() * 64];  // link w: wave w -> w + 1, chunk m in [m & 1]
+  __shared__ double2 hhead[64];                                    // reflective head cell, wave to wave
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if constexpr (KW == 2) {
+    if (w == 0)
+      split_role<S, T, 2, 0>(a, hand, hhead);
+    else
+      split_role<S, T, 2, 1>(a, hand, hhead);
+  } else {
+    if (w == 0)
+      split_role<S, T, 4, 0>(a, hand, hhead);
+    else if (w == 1)
+      split_role<S, T, 4, 1>(a, hand, hhead);
+    else if (w == 2)
+      split_role<S, T, 4, 2>(a, hand, hhead);
+    else
+      split_role<S, T, 4, 3>(a, hand, hhead);
+  }
+}
+
+template <int T, int KW>
+static hipError_t launch_split_t(const SegArgs &a, int grid, hipStream_t st) {
+  hipLaunchKernelGGL((sweep_split_kernel<SCHEME_BDF2, T, KW>), dim3(grid), dim3(64 * KW), 0, st, a);
+  return hipGetLastError();
+}
+
+template <int T, int KW>
+static hipError_t occupancy_split_t(int *w) {
+  return hipOccupancyMaxActiveBlocksPerMultiprocessor(w, sweep_split_kernel<SCHEME_BDF2, T, KW>, 64 * KW, 0);
+}
+
+// (T, waves) pairs with a split kernel: 2 waves up to 20 levels (beyond, 12 or more
+// levels per wave spill), 4 waves for T divisible by 4 up to 40.
+#define RT_SPLIT_PAIRS(X) X(8, 2) X(10, 2) X(12, 2) X(16, 2) X(20, 2) \
+  X(8, 4) X(12, 4) X(16, 4) X(20, 4) X(24, 4) X(32, 4) X(40, 4)
+
+hipError_t launch_split(int T, int waves, const SegArgs &a, int grid, hipStream_t st) {
+#define RT_SPLIT_LAUNCH(t, k) \
+  if (T == t && waves == k) return launch_split_t<t, k>(a, grid, st);
+  RT_SPLIT_PAIRS(RT_SPLIT_LAUNCH)
+#undef RT_SPLIT_LAUNCH
+  return hipErrorInvalidValue;
+}
+
+hipError_t split_occupancy(int T, int waves, int *w) {
+#define RT_SPLIT_OCC(t, k) \
+  if (T == t && waves == k) return occupancy_split_t<t, k>(w);
+  RT_SPLIT_PAIRS(RT_SPLIT_OCC)
+#undef RT_SPLIT_OCC
+  return hipErrorInvalidValue;
+}
+
+}  // namespace rtamd
