@@ -787,11 +787,17 @@ __global__ void correction_power_kernel(const double *map, double *pow, int L, i
   for (int n = 0; n < tri_count(K); ++n) out[n * stride] = P[n];
 }
 
+// cells per LDS tile of the correction's sums (the tile bounds the waves a CU holds)
+#ifndef RT_PHI_CHUNK
+#define RT_PHI_CHUNK 16
+#endif
+constexpr int kPhiChunk = RT_PHI_CHUNK;
+
 template <int S>
 __global__ __launch_bounds__(64) void phi_correction_kernel(SegArgs a, int nsub, int Lsub, const double *pow) {
   constexpr int K = SchemeDim<S>::K;
   constexpr int WN = map_count<S>();
-  constexpr int C = 16;
+  constexpr int C = kPhiChunk;
   extern __shared__ double tile[];  // C rows of group_tile_row(H) (launch_phi_correction)
   const int lane = threadIdx.x;
   const size_t stride = static_cast<size_t>(a.Lpad);
@@ -1101,7 +1107,7 @@ hipError_t launch_correction_power(int scheme, const double *map, double *pow, i
 hipError_t launch_phi_correction(int scheme, const SegArgs &a, int nsub, int Lsub, const double *pow, hipStream_t st) {
   const long long pieces = (2LL * a.Sg * nsub + kXcds - 1) / kXcds * kXcds;
   const dim3 grid(static_cast<unsigned>(pieces * a.Q)), block(64);
-  const size_t lds = sizeof(double) * 16 * group_tile_row(a.H);
+  const size_t lds = sizeof(double) * kPhiChunk * group_tile_row(a.H);
   switch (scheme) {
     case SCHEME_BE: hipLaunchKernelGGL(phi_correction_kernel<SCHEME_BE>, grid, block, lds, st, a, nsub, Lsub, pow); break;
     case SCHEME_CN: hipLaunchKernelGGL(phi_correction_kernel<SCHEME_CN>, grid, block, lds, st, a, nsub, Lsub, pow); break;
