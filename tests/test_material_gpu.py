@@ -363,3 +363,18 @@ def test_material_stability_number(rtsn_mod, oracle_mod):
             got = s.material_enable(want / 3.0, T)
         assert got == pytest.approx(3.0, rel=1e-12)
         s.material_step(1)  # coupling is on
+
+
+@pytest.mark.parametrize("variant", ["v0", "corr"])
+def test_bench_material_leg(rtsn_mod, variant):
+    """bench.run_material for either SL variant (the corr variant's V = 5.994
+    with the correction on must not reach rt_material_enable): BE steps through the one-rank
+    rt_comm communicator, a finite T(x) and a stability number below 2."""
+    import torch
+    sys.path.insert(0, str(REPO))
+    import bench
+    p = bench.slab_params(8, variant, N=20000, M=8)
+    out = bench.run_material(p, (8, 0, 8), 1, torch.device("cuda", 0), 0, 2)
+    assert out["allreduce"].startswith("rt_comm_material_step")
+    assert out["state_finite"] and 0.0 < out["stability_number"] < 2.0
+    assert out["T_range_keV"][0] > 0.0
