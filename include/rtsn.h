@@ -132,6 +132,10 @@ rt_status rt_synchronize(rt_solver *s);
 void *rt_stream(rt_solver *s);
 
 /* ---- results (host buffers, reference layouts) ------------------------- */
+/* The host buffers may be pageable: psi / ends / moments move through two pinned
+ * staging buffers of the handle (one export chunk each, up to 2 x 512 MB for ends;
+ * allocated on the first transfer, freed by rt_destroy) with the host-side copy
+ * split over up to 16 threads -- about 49 GB/s D2H on the SL state. */
 rt_status rt_get_dims(rt_solver *s, int *M, int *G_local, int *N, int *g_lo, int *g_hi);
 rt_status rt_get_psi(rt_solver *s, double *psi);                /* psi_mat_ref */
 rt_status rt_get_ends(rt_solver *s, double *ends);              /* Solver::ends */
