@@ -116,9 +116,15 @@ void rt_destroy(rt_solver *s);
 
 /* Solver::solve (solver.cpp:590-823): max_timesteps full steps (x4 substeps
  * for BDF2), preceded by computeEquilibriumSources when use_mg_equilib.
- * Synchronous.  Unless rt_set_time_block was called, a BDF2 run of at least 80
- * steps fuses 40 steps per pass (the fastest block; results equal to rounding). */
+ * Synchronous.  Unless rt_set_time_block was called, a BDF2 run takes the time
+ * block rt_plan_time_block(3, max_timesteps) returns (results equal to rounding). */
 rt_status rt_solve(rt_solver *s);
+/* The time block rt_solve picks for a run of nsteps (host only, no handle): for BDF2
+ * the block of 40, 32, 20, 16, 10 or 8 steps with the least estimated whole-run time
+ * -- pipelined passes at the block's measured cost per step, its pipeline fill and
+ * drain, and the nsteps mod T remainder as aligned passes (about 2.5x the cost per
+ * step) -- e.g. 20 for 100 or 300 steps, 40 for 1000; the default block otherwise. */
+rt_status rt_plan_time_block(int ts_method, long long nsteps, int *steps_per_pass);
 /* Asynchronous: enqueue nsteps full steps on the handle's stream (with the
  * pipelined schedule, whole passes are launched now and a remainder of fewer
  * than T steps when the state is next read). */

@@ -158,7 +158,6 @@ static rt_status fail(rt_solver *s, rt_status st, const std::string &msg) {
 // Measured on SL (pipelined schedule, profiles/): BDF2 43.0 / 21.7 / 14.5 / 12.3 /
 // 9.5 / 9.0 / 8.4 ms per step at T = 1 / 2 / 3 / 4 / 8 / 12 / 16.
 static int default_time_block(int) { return 16; }
-constexpr int kLongRunBlock = 40;  // rt_solve's block for runs of >= 2 such passes (BDF2)
 
 // rt_set_time_block's domain: the instantiated sweep kernels (kernels.hip launch_s)
 static bool supported_time_block(int T) {
@@ -1039,12 +1038,49 @@ extern "C" rt_status rt_synchronize(rt_solver *s) {
   return RT_OK;
 }
 
-// rt_solve knows the run's length: unless the caller chose a block, a BDF2 run of at
-// least two T = 40 passes runs T = 40 (the fastest per step on SL: 7.5 vs 8.2 ms at 16,
-// DESIGN.md §8), shorter runs keep the default.
+// rt_solve knows the run's length.  Unless the caller chose a block, a BDF2 run takes the
+// block with the least estimated whole-run time: the pipelined passes at the block's steady
+// cost per step, plus its fill + drain (in passes of that block), plus the remainder of
+// n mod T steps, which runs as aligned passes of at most 4 steps with the cross-segment
+// correction.  Costs: SL, ms per step (profiles/r02g_big_time_blocks.jsonl)
+// and fill + drain from whole runs of 100 / 300 / 1000 steps (profiles/r02n_run_blocks_*);
+// only their ratios matter.  E.g. 100 steps: T = 20 (T = 40 would leave 20 aligned steps,
+// 1373 vs 1020 ms measured), 300: 20, 1000: 40.
+struct BlockCost {
+  int T;
+  double ms_per_step, fill_drain_passes;
+};
+constexpr BlockCost kBlockCosts[] = {{40, 7.5, 1.2}, {32, 7.7, 1.2}, {20, 8.3, 1.15},
+                                     {16, 8.15, 2.8}, {10, 9.0, 4.4}, {8, 9.5, 4.0}};
+constexpr double kAlignedMsPerStep = 20.0;
+
+static int plan_time_block(long long nsteps, int fallback) {
+  int best = fallback;
+  double best_ms = 0.0;
+  for (const BlockCost &c : kBlockCosts) {
+    const long long passes = nsteps / c.T, rem = nsteps % c.T;
+    if (passes == 0) continue;
+    const double ms = (nsteps - rem) * c.ms_per_step + c.fill_drain_passes * c.T * c.ms_per_step +
+                      rem * kAlignedMsPerStep;
+    if (best_ms == 0.0 || ms < best_ms) {
+      best = c.T;
+      best_ms = ms;
+    }
+  }
+  return best;
+}
+
+extern "C" rt_status rt_plan_time_block(int ts_method, long long nsteps, int *steps_per_pass) {
+  if (!steps_per_pass || nsteps < 0 || ts_method < 1 || ts_method > 3)
+    return fail(nullptr, RT_ERR_ARG, "rt_plan_time_block: bad argument");
+  *steps_per_pass = ts_method == SCHEME_BDF2 ? plan_time_block(nsteps, default_time_block(ts_method))
+                                             : default_time_block(ts_method);
+  return RT_OK;
+}
+
 static void solve_time_block(rt_solver *s) {
   if (s->T_set || s->scheme != SCHEME_BDF2 || s->Tpipe || s->queued) return;
-  if (s->p.max_timesteps >= 2 * kLongRunBlock) s->T = kLongRunBlock;
+  s->T = plan_time_block(s->p.max_timesteps, s->T);
 }
 
 extern "C" rt_status rt_solve(rt_solver *s) {

@@ -16,6 +16,7 @@ from .api import (  # noqa: F401
     exported_symbols,
     lib,
     params_default,
+    plan_time_block,
     planck_groups,
     quadrature,
 )

@@ -114,6 +114,7 @@ def lib():
         L.rt_get_pipeline.argtypes = [vp, C.POINTER(C.c_int)]
         L.rt_pipeline_state.argtypes = [vp, C.POINTER(C.c_longlong), C.POINTER(C.c_int), C.POINTER(C.c_int)]
         L.rt_get_time_block.argtypes = [vp, C.POINTER(C.c_int)]
+        L.rt_plan_time_block.argtypes = [C.c_int, C.c_longlong, C.POINTER(C.c_int)]
         L.rt_get_level_waves.argtypes = [vp, C.POINTER(C.c_int)]
         L.rt_material_enable.argtypes = [vp, C.c_double, dp]
         L.rt_material_sweep.argtypes = [vp, vp]
@@ -174,6 +175,13 @@ def quadrature(M: int):
     mu, wt = np.empty(M), np.empty(M)
     _check(lib().rt_quadrature(M, _dp(mu), _dp(wt)), "rt_quadrature")
     return mu, wt
+
+
+def plan_time_block(ts_method: int, nsteps: int) -> int:
+    """The time block rt_solve picks for a run of nsteps (rt_plan_time_block; host only)."""
+    t = C.c_int()
+    _check(lib().rt_plan_time_block(int(ts_method), int(nsteps), C.byref(t)), "rt_plan_time_block")
+    return t.value
 
 
 def planck_groups(T: float, e_edge):
@@ -499,8 +507,9 @@ class Solver:
 
     @property
     def level_waves(self) -> int:
-        """Waves per segment of a pipelined BDF2 pass of 8/12/16/20 steps (rt_set_level_waves;
-        0 = auto: two at T = 20, one otherwise); reads the effective choice."""
+        """Waves per segment of a pipelined BDF2 pass of 8/10/12/16/20/24/32/40 steps
+        (rt_set_level_waves; 0 = auto: one up to T = 16, two at T = 20, four above);
+        reads the effective choice."""
         v = C.c_int()
         _check(lib().rt_get_level_waves(self._h, C.byref(v)), "rt_get_level_waves", self._h)
         return v.value

@@ -183,3 +183,22 @@ def test_direction_shard_argument_checks(rtsn_mod):
     with pytest.raises(rtsn_mod.RtError) as e:
         rtsn_mod.Solver(p, d_lo=1, d_hi=3)
     assert e.value.status == 6  # RT_ERR_DEVICE
+
+
+def test_plan_time_block(rtsn_mod):
+    """rt_solve's run-length-aware block (rt_plan_time_block): the measured whole-run times
+    on SL (profiles/r02n_run_blocks_*) -- 100 steps: T = 20 1020 ms vs T = 40 1373 ms (20
+    aligned remainder steps); 300: 20; 1000: 40 -- and whole multiples of the block win."""
+    plan = rtsn_mod.plan_time_block
+    assert plan(3, 100) == 20
+    assert plan(3, 300) == 20
+    assert plan(3, 1000) == 40
+    assert plan(3, 4000) == 40
+    assert plan(3, 96) == 32
+    assert plan(3, 2) == 16  # no whole pass of any block: the default, run as aligned passes
+    for n in range(8, 2000, 7):  # always a pipelined block with at least one whole pass
+        T = plan(3, n)
+        assert T in (8, 10, 16, 20, 32, 40) and n // T >= 1
+    assert plan(1, 1000) == 16 and plan(2, 1000) == 16  # BE / CN keep the default
+    with pytest.raises(rtsn_mod.RtError):
+        plan(4, 10)
