@@ -693,7 +693,7 @@ static rt_status create_impl(const rt_params *pin, int g_lo, int g_hi, int d_lo,
       h->T = std::atoi(t);
       h->T_set = true;
     }
-  if (const char *lw = std::getenv("RTSN_LEVEL_WAVES"))  // experiments: only "1" or "2" are read
+  if (const char *lw = std::getenv("RTSN_LEVEL_WAVES"))  // experiments: only "1", "2" or "4" are read
     if (!std::strcmp(lw, "1") || !std::strcmp(lw, "2") || !std::strcmp(lw, "4")) h->level_waves = lw[0] - '0';
   HIP_TRY(h, sweep_occupancy(h->scheme, h->T, level_waves_of(h, h->T), &waves_per_cu));
   // tuning knob for experiments: target resident waves per CU (segments per line follow)
