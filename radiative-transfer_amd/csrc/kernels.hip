@@ -857,6 +857,93 @@ __global__ __launch_bounds__(64) void phi_correction_kernel(SegArgs a, int nsub,
   }
 }
 
+// The correction's share for BE, in closed form.  BE carries one scalar per line, and the
+// map's linear part sends it to Z' = a Z with d = (d_in + d_out)/2 = (a + b)/2 Z (a, b
+// line constants), so at cell m of a segment (m = 0 at its head) the line adds
+//   w (a + b)/2 z a^m,   z the segment's incoming correction state (yseg).
+// Instead of walking each line cell by cell and reducing over the group's lines per
+// cell, lanes run over cells: wave w of a workgroup owns group g = 8 gb + w, keeps
+// p_i = a_i^m for its H <= 32 lines in registers (a_i^(m0 + lane) by binary powering,
+// then times a_i^64 per 64-cell chunk) and sums c_i p_i; the 8 waves' rows go through
+// LDS to [x][g] stores of 8 consecutive groups.  2 FP64 operations per cell and line
+// against the walk's map application plus an LDS tile reduction.
+constexpr int kGeoLines = 32;   // lines per group and half held in registers (H <= 32)
+constexpr int kGeoWaves = 8;    // groups (waves) per workgroup
+constexpr int kGeoRange = 2048; // cells per workgroup (32 chunks of 64)
+
+__device__ __forceinline__ double pow_u(double x, unsigned e) {
+  double r = 1.0;
+  for (; e; e >>= 1) {
+    if (e & 1) r *= x;
+    x *= x;
+  }
+  return r;
+}
+
+__global__ __launch_bounds__(64 * kGeoWaves) void phi_correction_be_kernel(SegArgs a, int ranges, int gblocks) {
+  constexpr int WN = map_count<SCHEME_BE>();
+  __shared__ double uni[kGeoWaves][4][kGeoLines];  // per wave: c_i, a_i, a_i^64, a_i^m0
+  __shared__ double tile[64][kGeoWaves + 1];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const size_t stride = static_cast<size_t>(a.Lpad);
+  int b = blockIdx.x;
+  const int gb = b % gblocks;
+  b /= gblocks;
+  const int r = b % ranges;
+  b /= ranges;
+  const int s = 1 + b % (a.Sg - 1), half = b / (a.Sg - 1);  // segment 0 starts exact
+  const bool neg = half == 0;
+  const int k_seg = s * a.Ls, seg_len = min(a.Ls, a.N - k_seg);
+  const int m0 = r * kGeoRange, m_end = min(seg_len, m0 + kGeoRange);
+  if (m0 >= m_end) return;  // workgroup-uniform
+  const int g = gb * kGeoWaves + w, H = a.H;
+  const bool gv = g < a.Gl;  // wave-uniform
+  if (gv && lane < H) {
+    const int ell = g * H + lane;
+    double W[WN];
+#pragma unroll
+    for (int n = 0; n < WN; ++n) W[n] = a.map[(static_cast<size_t>(half) * WN + n) * stride + ell];
+    double one[1] = {1.0}, zn[1], di, dd;
+    map_apply<SCHEME_BE, false>(W, one, 0.0, 0.0, zn, di, dd);  // zn = dd = a, di = b
+    const double z = a.yseg[(static_cast<size_t>(half) * (a.Sg + 1) + s) * stride + ell];
+    const double wl = a.wt[neg ? H - 1 - lane : H + lane];
+    uni[w][0][lane] = wl * (0.5 * (di + dd)) * z;
+    uni[w][1][lane] = zn[0];
+    uni[w][2][lane] = pow_u(zn[0], 64);
+    uni[w][3][lane] = pow_u(zn[0], static_cast<unsigned>(m0));
+  }
+  __syncthreads();
+  double c[kGeoLines], a64[kGeoLines], p[kGeoLines];
+#pragma unroll
+  for (int i = 0; i < kGeoLines; ++i) {
+    c[i] = 0.0;
+    a64[i] = 0.0;
+    p[i] = 0.0;
+    if (gv && i < H) {  // wave-uniform
+      c[i] = uni[w][0][i];
+      a64[i] = uni[w][2][i];
+      p[i] = uni[w][3][i] * pow_u(uni[w][1][i], static_cast<unsigned>(lane));  // a_i^(m0 + lane)
+    }
+  }
+  const int t_cell = threadIdx.x / kGeoWaves, t_g = threadIdx.x % kGeoWaves, t_gg = gb * kGeoWaves + t_g;
+  for (int m = m0; m < m_end; m += 64) {
+    double acc = 0.0;
+#pragma unroll
+    for (int i = 0; i < kGeoLines; ++i) {
+      acc = fma(c[i], p[i], acc);
+      p[i] *= a64[i];
+    }
+    tile[lane][w] = acc;
+    __syncthreads();
+    // 512 threads store 64 cells x 8 groups: each cell's 8 groups are one 64-byte run
+    if (t_gg < a.Gl && m + t_cell < m_end) {
+      const int k = k_seg + m + t_cell;
+      a.phic[(static_cast<size_t>(half) * a.N + (neg ? a.N - 1 - k : k)) * a.Gl + t_gg] = tile[t_cell][t_g];
+    }
+    __syncthreads();
+  }
+}
+
 // q(x) = sum_g sigma_g (phi_g(x) - W B_g(x)), phi the sum of nparts arrays
 // [part][x][g] (the fused halves and their corrections, or one full phi):
 // one wave per cell, lanes over groups, then a butterfly over the wave
@@ -1113,6 +1200,17 @@ hipError_t launch_phi_correction(int scheme, const SegArgs &a, int nsub, int Lsu
     case SCHEME_CN: hipLaunchKernelGGL(phi_correction_kernel<SCHEME_CN>, grid, block, lds, st, a, nsub, Lsub, pow); break;
     default: hipLaunchKernelGGL(phi_correction_kernel<SCHEME_BDF2>, grid, block, lds, st, a, nsub, Lsub, pow); break;
   }
+  return hipGetLastError();
+}
+
+bool phi_correction_be_supported(const SegArgs &a) { return a.H >= 1 && a.H <= kGeoLines && a.Sg > 1; }
+
+hipError_t launch_phi_correction_be(const SegArgs &a, hipStream_t st) {
+  if (!phi_correction_be_supported(a)) return hipErrorInvalidValue;
+  const int ranges = (a.Ls + kGeoRange - 1) / kGeoRange, gblocks = (a.Gl + kGeoWaves - 1) / kGeoWaves;
+  const long long blocks = 2LL * (a.Sg - 1) * ranges * gblocks;
+  hipLaunchKernelGGL(phi_correction_be_kernel, dim3(static_cast<unsigned>(blocks)), dim3(64 * kGeoWaves), 0, st, a,
+                     ranges, gblocks);
   return hipGetLastError();
 }
 
