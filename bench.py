@@ -165,8 +165,9 @@ def reference_config_timings(rate_steps: int = 1000) -> dict:
         against the oracle's (max per-group relative difference); for llnl_slab_test also
         the oracle with the reference's literal per-cell half_ends copy (solver.cpp:733,
         quadratic in the state size);
-      * as a rate: `rate_steps` BDF2 steps of the same configuration (handle created and
-        warmed outside the timer; advance + finish + device sync timed), GPU BDF2 steps/s
+      * as a rate: `rate_steps` BDF2 steps of the same configuration at the time block
+        rt_solve would pick (rt_plan_time_block; handle created and warmed outside the
+        timer; advance + finish + device sync timed), GPU BDF2 steps/s
         and updates/s beside the oracle's on one core over the same steps, with the
         number of sweep passes (HIP event pairs) the GPU ran -- the metric's named config,
         llnl_slab_test, among them."""
@@ -201,10 +202,12 @@ def reference_config_timings(rate_steps: int = 1000) -> dict:
         params = dict(ph.params, max_timesteps=rate_steps)
         upd_step = (4.0 if q["ts_method"] == 3 else 1.0) * q["M"] * q["G"] * q["N"]
         with rtsn.Solver(params) as s:  # warm: kernels loaded, equilibrium sources built
-            s.advance(16)
+            s.time_block = rtsn.plan_time_block(q["ts_method"], rate_steps)
+            s.advance(2 * s.time_block)
             s.finish()
             s.synchronize()
         with rtsn.Solver(params) as s:
+            s.time_block = rtsn.plan_time_block(q["ts_method"], rate_steps)  # rt_solve's choice
             s.set_profiling(True)
             s.synchronize()
             t0 = time.perf_counter()
