@@ -607,6 +607,26 @@ __global__ void group_absorption_kernel(const double *phi, const double *sigma, 
   }
 }
 
+// compute_balance's absorption and emission sums (solver.cpp:262-272) per group, in the
+// reference's order -- sequential over cells, one lane per group (phi row-major [c][g]:
+// a wave's loads of one cell are contiguous) -- with the host loop's arithmetic
+// (ab += (rho kappa phi) dx contracted to one FMA, sr += src).
+__global__ void balance_sums_kernel(const double *phi, const double *rk, const double *src, double dx, double *ab,
+                                    double *sr, int Gl, int N) {
+  const int g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= Gl) return;
+  const double r = rk[g], q = src[g];
+  double a = 0.0, e = 0.0;
+  const double *col = phi + g;
+#pragma unroll 8
+  for (int c = 0; c < N; ++c) {
+    a = fma(r * col[static_cast<size_t>(c) * Gl], dx, a);
+    e += q;
+  }
+  ab[g] = a;
+  sr[g] = e;
+}
+
 // ------------------------------------------------------------------------
 // Material coupling: Planck group integrals per cell, exchange term, T update
 // ------------------------------------------------------------------------
@@ -1165,6 +1185,12 @@ hipError_t launch_finite_scan(const double2 *E, int *flag, const Geometry &g, hi
 hipError_t launch_boundary_rows(const double2 *E, double2 *rows, const Geometry &g, hipStream_t st) {
   hipLaunchKernelGGL(boundary_rows_kernel, dim3(grid_for(static_cast<size_t>(4) * g.Lpad, 256)), dim3(256), 0, st, E,
                      rows, g.N, g.Nrow, g.Lpad);
+  return hipGetLastError();
+}
+
+hipError_t launch_balance_sums(const double *phi, const double *rk, const double *src, double dx, double *ab,
+                               double *sr, int Gl, int N, hipStream_t st) {
+  hipLaunchKernelGGL(balance_sums_kernel, dim3((Gl + 63) / 64), dim3(64), 0, st, phi, rk, src, dx, ab, sr, Gl, N);
   return hipGetLastError();
 }
 

@@ -1584,34 +1584,46 @@ extern "C" rt_status rt_get_group_ends(rt_solver *s, double *left, double *right
   return RT_OK;
 }
 
+// compute_balance's absorption and emission sums per group (solver.cpp:262-272) on the
+// device from the moments kernel's phi (N x Gl, g fastest): sequential in c per group
+// in the reference's order and association, one lane per group (balance_sums_kernel).
+static rt_status balance_sums(rt_solver *s, std::vector<double> &ab, std::vector<double> &sr) {
+  if (rt_status st = compute_moments(s)) return st;
+  const int N = s->p.N, Gl = s->Gl;
+  const double ac = phys::kRadA * phys::kLight, dx = s->p.X / N;
+  std::vector<double> host(4 * static_cast<size_t>(Gl));  // rk, src | ab, sr
+  for (int gl = 0; gl < Gl; ++gl) {
+    host[gl] = s->gt.rho[s->g_lo + gl] * s->gt.kappa[s->g_lo + gl];
+    host[Gl + gl] = host[gl] * ac * std::pow(s->p.T, 4) * dx;
+  }
+  double *d = nullptr;
+  HIP_TRY(s, hipMalloc(reinterpret_cast<void **>(&d), sizeof(double) * host.size()));
+  hipError_t e = hipMemcpyAsync(d, host.data(), sizeof(double) * 2 * Gl, hipMemcpyHostToDevice, s->stream);
+  if (e == hipSuccess)
+    e = launch_balance_sums(static_cast<const double *>(s->mom.p), d, d + Gl, dx, d + 2 * Gl, d + 3 * Gl, Gl, N,
+                            s->stream);
+  if (e == hipSuccess)
+    e = hipMemcpyAsync(host.data() + 2 * Gl, d + 2 * Gl, sizeof(double) * 2 * Gl, hipMemcpyDeviceToHost, s->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
+  (void)hipStreamSynchronize(s->stream);
+  (void)hipFree(d);
+  if (e != hipSuccess) return fail(s, RT_ERR_DEVICE, std::string("balance sums: ") + hipGetErrorString(e));
+  ab.assign(host.begin() + 2 * Gl, host.begin() + 3 * Gl);
+  sr.assign(host.begin() + 3 * Gl, host.end());
+  return RT_OK;
+}
+
 extern "C" rt_status rt_get_balance_terms(rt_solver *s, double *balance, double *sources_out, double *sinks_out) {
   if (!s) return fail(s, RT_ERR_ARG, "rt_get_balance_terms: NULL handle");
   if (s->d_hi > 0)  // its emission/absorption terms need phi over all directions
     return fail(s, RT_ERR_PARAM, "rt_get_balance_terms: a direction shard holds part of phi; sum the shards' "
                                  "moments and group ends, then balance on the totals");
   HIP_TRY(s, hipSetDevice(s->device));
-  const int N = s->p.N, Gl = s->Gl;
-  std::vector<double> phi(static_cast<size_t>(Gl) * N);
-  rt_status st = rt_get_moments(s, phi.data(), nullptr, nullptr);
+  const int Gl = s->Gl;
+  std::vector<double> ab, sr, rows;
+  rt_status st = balance_sums(s, ab, sr);
   if (st) return st;
-  std::vector<double> rows;
   if ((st = fetch_rows(s, rows))) return st;
-  const double ac = phys::kRadA * phys::kLight, dx = s->p.X / N;
-  // absorption and source sums: sequential in c per group in the reference's order and
-  // association (:262-272), with the group loop innermost so phi (N x Gl, g fastest) is
-  // read contiguously
-  std::vector<double> rk(Gl), src(Gl), ab(Gl, 0.), sr(Gl, 0.);
-  for (int gl = 0; gl < Gl; ++gl) {
-    rk[gl] = s->gt.rho[s->g_lo + gl] * s->gt.kappa[s->g_lo + gl];
-    src[gl] = rk[gl] * ac * std::pow(s->p.T, 4) * dx;
-  }
-  for (int c = 0; c < N; ++c) {
-    const double *row = phi.data() + static_cast<size_t>(c) * Gl;
-    for (int gl = 0; gl < Gl; ++gl) {
-      ab[gl] += rk[gl] * row[gl] * dx;
-      sr[gl] += src[gl];
-    }
-  }
   for (int gl = 0; gl < Gl; ++gl) {  // solver.cpp:240-284
     double jhm = 0., jhp = 0., jNm = 0., jNp = 0.;
     for (int i = 0; i < s->p.M; ++i) {
@@ -1640,25 +1652,11 @@ extern "C" rt_status rt_get_balance_partials(rt_solver *s, double *inflow, doubl
                                              double *emission) {
   if (!s) return fail(nullptr, RT_ERR_ARG, "rt_get_balance_partials: NULL handle");
   HIP_TRY(s, hipSetDevice(s->device));
-  const int N = s->p.N, Gl = s->Gl;
-  std::vector<double> phi(static_cast<size_t>(Gl) * N);
-  rt_status st = rt_get_moments(s, phi.data(), nullptr, nullptr);
+  const int Gl = s->Gl;
+  std::vector<double> ab, sr, rows;
+  rt_status st = balance_sums(s, ab, sr);
   if (st) return st;
-  std::vector<double> rows;
   if ((st = fetch_rows(s, rows))) return st;
-  const double ac = phys::kRadA * phys::kLight, dx = s->p.X / N;
-  std::vector<double> rk(Gl), src(Gl), ab(Gl, 0.), sr(Gl, 0.);
-  for (int gl = 0; gl < Gl; ++gl) {
-    rk[gl] = s->gt.rho[s->g_lo + gl] * s->gt.kappa[s->g_lo + gl];
-    src[gl] = rk[gl] * ac * std::pow(s->p.T, 4) * dx;
-  }
-  for (int c = 0; c < N; ++c) {
-    const double *row = phi.data() + static_cast<size_t>(c) * Gl;
-    for (int gl = 0; gl < Gl; ++gl) {
-      ab[gl] += rk[gl] * row[gl] * dx;
-      sr[gl] += src[gl];
-    }
-  }
   for (int gl = 0; gl < Gl; ++gl) {
     double jin = 0., jout = 0.;
     for (int i = 0; i < s->p.M; ++i) {
