@@ -877,16 +877,22 @@ __global__ __launch_bounds__(64) void phi_correction_kernel(SegArgs a, int nsub,
   }
 }
 
-// The correction's share for BE, in closed form.  BE carries one scalar per line, and the
-// map's linear part sends it to Z' = a Z with d = (d_in + d_out)/2 = (a + b)/2 Z (a, b
-// line constants), so at cell m of a segment (m = 0 at its head) the line adds
-//   w (a + b)/2 z a^m,   z the segment's incoming correction state (yseg).
+// The correction's share for BE and CN, in closed form.  The map's linear part moves the
+// correction state Z with no data delta (d_in = d_out = 0): BE carries one scalar, and
+// CN's first component is the copied d_out = 0 after one cell, so from the second cell of
+// a segment on both carry one live scalar y with y' = lambda y and the cell's share
+// (d_in + d_out)/2 = mu y (lambda, mu: the map's linear part on the unit live component).
+// At cell m of a segment the line adds
+//   m = 0:  w f,                       f = (d_in + d_out)/2 of Z = z (the segment's
+//                                      incoming correction state, yseg)
+//   m >= 1: w mu y1 lambda^(m-1),      y1 = the live component after cell 0
 // Instead of walking each line cell by cell and reducing over the group's lines per
 // cell, lanes run over cells: wave w of a workgroup owns group g = 8 gb + w, keeps
-// p_i = a_i^m for its H <= 32 lines in registers (a_i^(m0 + lane) by binary powering,
-// then times a_i^64 per 64-cell chunk) and sums c_i p_i; the 8 waves' rows go through
-// LDS to [x][g] stores of 8 consecutive groups.  2 FP64 operations per cell and line
-// against the walk's map application plus an LDS tile reduction.
+// p_i = lambda_i^(m-1) for its H <= 32 lines in registers (by binary powering at the
+// workgroup's start, then times lambda_i^64 per 64-cell chunk) and sums c_i p_i; the 8
+// waves' rows go through LDS to [x][g] stores of 8 consecutive groups.  2 FP64
+// operations per cell and line against the walk's map application plus an LDS tile
+// reduction.
 constexpr int kGeoLines = 32;   // lines per group and half held in registers (H <= 32)
 constexpr int kGeoWaves = 8;    // groups (waves) per workgroup
 constexpr int kGeoRange = 2048; // cells per workgroup (32 chunks of 64)
@@ -900,9 +906,13 @@ __device__ __forceinline__ double pow_u(double x, unsigned e) {
   return r;
 }
 
-__global__ __launch_bounds__(64 * kGeoWaves) void phi_correction_be_kernel(SegArgs a, int ranges, int gblocks) {
-  constexpr int WN = map_count<SCHEME_BE>();
-  __shared__ double uni[kGeoWaves][4][kGeoLines];  // per wave: c_i, a_i, a_i^64, a_i^m0
+template <int S>
+__global__ __launch_bounds__(64 * kGeoWaves) void phi_correction_geo_kernel(SegArgs a, int ranges, int gblocks) {
+  static_assert(S == SCHEME_BE || S == SCHEME_CN, "one live scalar after the first cell");
+  constexpr int K = SchemeDim<S>::K;
+  constexpr int WN = map_count<S>();
+  // per wave and line: w mu y1, lambda, lambda^64, lambda^e0 (e0 = m0 - 1, or 0), w f
+  __shared__ double uni[kGeoWaves][5][kGeoLines];
   __shared__ double tile[64][kGeoWaves + 1];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const size_t stride = static_cast<size_t>(a.Lpad);
@@ -923,17 +933,26 @@ __global__ __launch_bounds__(64 * kGeoWaves) void phi_correction_be_kernel(SegAr
     double W[WN];
 #pragma unroll
     for (int n = 0; n < WN; ++n) W[n] = a.map[(static_cast<size_t>(half) * WN + n) * stride + ell];
-    double one[1] = {1.0}, zn[1], di, dd;
-    map_apply<SCHEME_BE, false>(W, one, 0.0, 0.0, zn, di, dd);  // zn = dd = a, di = b
-    const double z = a.yseg[(static_cast<size_t>(half) * (a.Sg + 1) + s) * stride + ell];
+    double z[K], zn[K], di, dd, u[K], un[K], ui, ud;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      z[k] = a.yseg[((static_cast<size_t>(half) * (a.Sg + 1) + s) * K + k) * stride + ell];
+      u[k] = k == K - 1 ? 1.0 : 0.0;
+    }
+    map_apply<S, false>(W, z, 0.0, 0.0, zn, di, dd);  // cell 0
+    map_apply<S, false>(W, u, 0.0, 0.0, un, ui, ud);  // the live component's propagator
     const double wl = a.wt[neg ? H - 1 - lane : H + lane];
-    uni[w][0][lane] = wl * (0.5 * (di + dd)) * z;
-    uni[w][1][lane] = zn[0];
-    uni[w][2][lane] = pow_u(zn[0], 64);
-    uni[w][3][lane] = pow_u(zn[0], static_cast<unsigned>(m0));
+    const double lam = un[K - 1];
+    uni[w][0][lane] = wl * (0.5 * (ui + ud)) * zn[K - 1];
+    uni[w][1][lane] = lam;
+    uni[w][2][lane] = pow_u(lam, 64);
+    uni[w][3][lane] = pow_u(lam, static_cast<unsigned>(m0 > 0 ? m0 - 1 : 0));
+    uni[w][4][lane] = wl * (0.5 * (di + dd));
   }
   __syncthreads();
   double c[kGeoLines], a64[kGeoLines], p[kGeoLines];
+  double f0 = 0.0;  // cell 0 of the segment (m0 = 0, lane 0): the sum of w f over the lines
+  const unsigned el = static_cast<unsigned>(m0 > 0 ? lane : (lane > 0 ? lane - 1 : 0));
 #pragma unroll
   for (int i = 0; i < kGeoLines; ++i) {
     c[i] = 0.0;
@@ -942,7 +961,8 @@ __global__ __launch_bounds__(64 * kGeoWaves) void phi_correction_be_kernel(SegAr
     if (gv && i < H) {  // wave-uniform
       c[i] = uni[w][0][i];
       a64[i] = uni[w][2][i];
-      p[i] = uni[w][3][i] * pow_u(uni[w][1][i], static_cast<unsigned>(lane));  // a_i^(m0 + lane)
+      p[i] = uni[w][3][i] * pow_u(uni[w][1][i], el);  // lambda_i^(m0 + lane - 1)
+      f0 += uni[w][4][i];
     }
   }
   const int t_cell = threadIdx.x / kGeoWaves, t_g = threadIdx.x % kGeoWaves, t_gg = gb * kGeoWaves + t_g;
@@ -952,6 +972,12 @@ __global__ __launch_bounds__(64 * kGeoWaves) void phi_correction_be_kernel(SegAr
     for (int i = 0; i < kGeoLines; ++i) {
       acc = fma(c[i], p[i], acc);
       p[i] *= a64[i];
+    }
+    if (m == 0 && lane == 0) {  // cell 0 (its Z is the incoming state itself); cell 64 next
+      acc = f0;
+#pragma unroll
+      for (int i = 0; i < kGeoLines; ++i)
+        if (gv && i < H) p[i] = pow_u(uni[w][1][i], 63);
     }
     tile[lane][w] = acc;
     __syncthreads();
@@ -1229,14 +1255,18 @@ hipError_t launch_phi_correction(int scheme, const SegArgs &a, int nsub, int Lsu
   return hipGetLastError();
 }
 
-bool phi_correction_be_supported(const SegArgs &a) { return a.H >= 1 && a.H <= kGeoLines && a.Sg > 1; }
+bool phi_correction_geo_supported(int scheme, const SegArgs &a) {
+  return (scheme == SCHEME_BE || scheme == SCHEME_CN) && a.H >= 1 && a.H <= kGeoLines && a.Sg > 1;
+}
 
-hipError_t launch_phi_correction_be(const SegArgs &a, hipStream_t st) {
-  if (!phi_correction_be_supported(a)) return hipErrorInvalidValue;
+hipError_t launch_phi_correction_geo(int scheme, const SegArgs &a, hipStream_t st) {
+  if (!phi_correction_geo_supported(scheme, a)) return hipErrorInvalidValue;
   const int ranges = (a.Ls + kGeoRange - 1) / kGeoRange, gblocks = (a.Gl + kGeoWaves - 1) / kGeoWaves;
-  const long long blocks = 2LL * (a.Sg - 1) * ranges * gblocks;
-  hipLaunchKernelGGL(phi_correction_be_kernel, dim3(static_cast<unsigned>(blocks)), dim3(64 * kGeoWaves), 0, st, a,
-                     ranges, gblocks);
+  const dim3 grid(static_cast<unsigned>(2LL * (a.Sg - 1) * ranges * gblocks)), block(64 * kGeoWaves);
+  if (scheme == SCHEME_BE)
+    hipLaunchKernelGGL(phi_correction_geo_kernel<SCHEME_BE>, grid, block, 0, st, a, ranges, gblocks);
+  else
+    hipLaunchKernelGGL(phi_correction_geo_kernel<SCHEME_CN>, grid, block, 0, st, a, ranges, gblocks);
   return hipGetLastError();
 }
 

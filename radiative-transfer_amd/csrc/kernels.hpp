@@ -138,9 +138,9 @@ hipError_t launch_planck_cells(const PlanckCells &pc, const double *T, double *B
 // pow^j applied to the segment's correction state, pow = A^Lsub (launch_correction_power)
 hipError_t launch_phi_correction(int scheme, const SegArgs &a, int nsub, int Lsub, const double *pow, hipStream_t st);
 // pow[half][K (K + 1) / 2][Lpad] = A^L, A the map's linear X -> X' block (lower triangular)
-// BE: the correction's share in closed form (lanes over cells, H <= 32 lines per group-half)
-bool phi_correction_be_supported(const SegArgs &a);
-hipError_t launch_phi_correction_be(const SegArgs &a, hipStream_t st);
+// BE, CN: the correction's share in closed form (lanes over cells, H <= 32 lines per group-half)
+bool phi_correction_geo_supported(int scheme, const SegArgs &a);
+hipError_t launch_phi_correction_geo(int scheme, const SegArgs &a, hipStream_t st);
 hipError_t launch_correction_power(int scheme, const double *map, double *pow, int L, int Lpad, hipStream_t st);
 // q(x) = sum_g sigma_g (phi_g(x) - W B_g(x)) over the handle's groups, phi the
 // sum of nparts [N][Gl] arrays at phi (the fused parts, or one full phi)

@@ -1235,11 +1235,11 @@ extern "C" rt_status rt_material_sweep(rt_solver *s, double *d_q) {
       a.H = s->H;
       a.phic = static_cast<double *>(s->phi_part.p) + 2 * static_cast<size_t>(s->p.N) * s->Gl;
       a.wt = static_cast<const double *>(s->muwt.p) + s->p.M;
-      // BE: closed form, lanes over cells (phi_correction_be_kernel); RTSN_PHI_WALK=1 keeps
-      // the walk for comparison
+      // BE, CN: closed form, lanes over cells (phi_correction_geo_kernel); RTSN_PHI_WALK=1
+      // keeps the walk for comparison
       const char *walk = std::getenv("RTSN_PHI_WALK");
-      if (s->scheme == SCHEME_BE && phi_correction_be_supported(a) && !(walk && !std::strcmp(walk, "1"))) {
-        HIP_TRY(s, launch_phi_correction_be(a, s->stream));
+      if (phi_correction_geo_supported(s->scheme, a) && !(walk && !std::strcmp(walk, "1"))) {
+        HIP_TRY(s, launch_phi_correction_geo(s->scheme, a, s->stream));
         HIP_TRY(s, launch_material_q(static_cast<const double *>(s->phi_part.p), 4, B, sig, s->wsum, q, s->Gl,
                                      s->p.N, s->stream));
         return RT_OK;

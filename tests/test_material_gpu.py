@@ -143,13 +143,15 @@ def test_coupled_long_lines_llnl_groups(rtsn_mod, oracle_mod, ts):
         compare(gpu, orc)
 
 
+@pytest.mark.parametrize("ts", [1, 2])
 @pytest.mark.parametrize("M,bc_left,waves", [(64, 0, "1"), (64, 2, "1"), (16, 1, "2"), (8, 2, "")])
-def test_be_correction_closed_form(rtsn_mod, oracle_mod, monkeypatch, M, bc_left, waves):
-    """BE: the correction's share in closed form (phi_correction_be_kernel: lanes over cells,
-    a^m by powers) against the oracle and against the cell-by-cell walk (RTSN_PHI_WALK=1),
-    on 50k-cell lines in segments longer than a workgroup's 2048-cell range (few waves per
-    CU -> few, long segments; "" keeps the default segmentation: short segments)."""
-    p = params(oracle_mod, ts=1, dt=1e-3, M=M, G=6, N=50000, bc_left=bc_left, bc_right=0)
+def test_be_correction_closed_form(rtsn_mod, oracle_mod, monkeypatch, M, bc_left, waves, ts):
+    """BE and CN: the correction's share in closed form (phi_correction_geo_kernel: lanes over
+    cells, the live scalar's propagator by powers) against the oracle and against the
+    cell-by-cell walk (RTSN_PHI_WALK=1), on 50k-cell lines in segments longer than a
+    workgroup's 2048-cell range (few waves per CU -> few, long segments; "" keeps the
+    default segmentation: short segments)."""
+    p = params(oracle_mod, ts=ts, dt=1e-3, M=M, G=6, N=50000, bc_left=bc_left, bc_right=0)
     p["psi_source"] = np.linspace(0.5, 2.0, M * p["G"]).reshape(M, p["G"])
     if waves:
         monkeypatch.setenv("RTSN_WAVES_PER_CU", waves)
