@@ -1386,7 +1386,8 @@ static void parallel_copy(double *dst, const double *src, size_t n) {
 constexpr size_t kStagedPiece = size_t(1) << 21;  // 16 MB
 static rt_status staged_d2h(rt_solver *s, double *host, const double *dev, size_t count) {
   if (rt_status st = ensure_staging(s, sizeof(double) * std::min(count, kStagedPiece))) return st;
-  const size_t piece = std::min(kStagedPiece, s->staging_bytes / sizeof(double));
+  size_t piece = std::min(kStagedPiece, s->staging_bytes / sizeof(double));
+  if (const char *env = std::getenv("RTSN_EXPORT_CHUNK")) piece = std::min(piece, size_t(std::max(1L, std::atol(env))));  // tests
   hipError_t e = hipSuccess;
   size_t k = 0, prev = 0, prev_n = 0;
   for (size_t o = 0; o < count && e == hipSuccess; o += piece, ++k) {
