@@ -238,11 +238,15 @@ __host__ __device__ constexpr int map_count() {
 // Apply the map (CONST: with the affine constants; otherwise its linear part).
 // cs scales the constants: the material-coupled sweep stores them for B = 1
 // and passes the cell's B_g(T(x)) (with the correction off they are linear in
-// the source); 1.0 elsewhere, which the compiler folds away.
-template <int S, bool CONST>
+// the source); 1.0 elsewhere, which the compiler folds away.  For the correction
+// walks, which move a state with no data delta: NODATA skips the din/dout columns
+// (both 0.0; fma(w, 0.0, acc) is not folded by the compiler), ZERO0 also skips X[0]
+// (0.0 after one cell where row 0 copies dout: CN, BDF2) -- the same values.
+template <int S, bool CONST, bool NODATA = false, bool ZERO0 = false>
 __host__ __device__ __forceinline__ void map_apply(const double *W, const double *X, double din, double dout,
                                                    double *Xn, double &oin, double &oout, double cs = 1.0) {
   constexpr int K = SchemeDim<S>::K;
+  static_assert(!ZERO0 || (NODATA && map_copy_row0<S>()), "X[0] vanishes only where row 0 copies a zero dout");
 #pragma unroll
   for (int r = 0; r <= K; ++r) {
     if (map_copy_row0<S>() && r == 0) {
@@ -253,6 +257,7 @@ __host__ __device__ __forceinline__ void map_apply(const double *W, const double
 #pragma unroll
     for (int c = 0; c < K + 2; ++c) {
       if (!map_dep<S>(r, c)) continue;
+      if ((NODATA && c >= K) || (ZERO0 && c == 0)) continue;
       const double u = c < K ? X[c] : (c == K ? din : dout);
       acc = fma(W[map_slot<S>(r, c)], u, acc);
     }

@@ -106,7 +106,10 @@ __device__ __forceinline__ void sweep_chunk(const double *W, double (&ein)[C], d
 #pragma unroll
       for (int t = 0; t < T; ++t) {
         double Zn[K], a, e;
-        map_apply<S, false>(W, Z[t], di, dd, Zn, a, e);
+        if (t == 0)  // zero data delta at level 0 (resolved at compile time once unrolled)
+          map_apply<S, false, true>(W, Z[t], di, dd, Zn, a, e);
+        else
+          map_apply<S, false>(W, Z[t], di, dd, Zn, a, e);
 #pragma unroll
         for (int r = 0; r < K; ++r) Z[t][r] = Zn[r];
         di = a;
@@ -607,21 +610,40 @@ __global__ void group_absorption_kernel(const double *phi, const double *sigma, 
   }
 }
 
-// compute_balance's absorption and emission sums (solver.cpp:262-272) per group, in the
-// reference's order -- sequential over cells, one lane per group (phi row-major [c][g]:
-// a wave's loads of one cell are contiguous) -- with the host loop's arithmetic
-// (ab += (rho kappa phi) dx contracted to one FMA, sr += src).
-__global__ void balance_sums_kernel(const double *phi, const double *rk, const double *src, double dx, double *ab,
-                                    double *sr, int Gl, int N) {
-  const int g = blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= Gl) return;
+// compute_balance's absorption and emission sums (solver.cpp:262-272) per group:
+// ab = sum_c (rho kappa phi_c) dx, sr = sum_c src.  The reference adds sequentially over
+// the N cells; here kBalanceParts contiguous cell ranges are summed sequentially (one
+// lane per (range, group): a wave's loads of one cell are contiguous), then the ranges'
+// partial sums in range order -- a two-level sum, so the result differs from the
+// reference's by rounding only (the balance is compared at 1e-9; one lane per group
+// over 1e6 cells took 62 ms on SL, latency-bound on its loads).
+constexpr int kBalanceParts = 512;
+
+__global__ void balance_partials_kernel(const double *phi, const double *rk, const double *src, double dx,
+                                        double *part, int Gl, int N) {
+  const long long t = static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (t >= static_cast<long long>(kBalanceParts) * Gl) return;
+  const int g = static_cast<int>(t % Gl), rp = static_cast<int>(t / Gl);
+  const int c0 = static_cast<int>(static_cast<long long>(N) * rp / kBalanceParts);
+  const int c1 = static_cast<int>(static_cast<long long>(N) * (rp + 1) / kBalanceParts);
   const double r = rk[g], q = src[g];
   double a = 0.0, e = 0.0;
   const double *col = phi + g;
-#pragma unroll 8
-  for (int c = 0; c < N; ++c) {
+  for (int c = c0; c < c1; ++c) {
     a = fma(r * col[static_cast<size_t>(c) * Gl], dx, a);
     e += q;
+  }
+  part[(static_cast<size_t>(rp) * Gl + g) * 2] = a;
+  part[(static_cast<size_t>(rp) * Gl + g) * 2 + 1] = e;
+}
+
+__global__ void balance_sums_kernel(const double *part, double *ab, double *sr, int Gl) {
+  const int g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= Gl) return;
+  double a = 0.0, e = 0.0;
+  for (int rp = 0; rp < kBalanceParts; ++rp) {
+    a += part[(static_cast<size_t>(rp) * Gl + g) * 2];
+    e += part[(static_cast<size_t>(rp) * Gl + g) * 2 + 1];
   }
   ab[g] = a;
   sr[g] = e;
@@ -860,6 +882,17 @@ __global__ __launch_bounds__(64) void phi_correction_kernel(SegArgs a, int nsub,
   const int ip = ell % a.H;
   const double wl = a.wt[neg ? a.H - 1 - ip : a.H + ip];
   double *dst = a.phic + static_cast<size_t>(half) * a.N * a.Gl;
+  // CN / BDF2: row 0 copies d_out = 0, so X[0] is 0 after the segment's first cell (and at
+  // every sub-segment start): that cell runs the full linear map, the rest skip column 0
+  constexpr bool Z0 = map_copy_row0<S>();
+  double d_first = 0.0;
+  if (Z0 && j == 0) {
+    double Zn[K], di, dd;
+    map_apply<S, false, true>(W, Z, 0.0, 0.0, Zn, di, dd);
+#pragma unroll
+    for (int r = 0; r < K; ++r) Z[r] = Zn[r];
+    d_first = 0.5 * (di + dd);
+  }
   for (int k0 = k_begin; k0 < k_end; k0 += C) {
     const int nv = min(C, k_end - k0);
     double d[C];
@@ -867,8 +900,12 @@ __global__ __launch_bounds__(64) void phi_correction_kernel(SegArgs a, int nsub,
     for (int c = 0; c < C; ++c) {
       d[c] = 0.0;
       if (c >= nv) continue;  // wave-uniform
+      if (Z0 && j == 0 && c == 0 && k0 == k_begin) {  // wave-uniform: done above
+        d[c] = d_first;
+        continue;
+      }
       double Zn[K], di, dd;
-      map_apply<S, false>(W, Z, 0.0, 0.0, Zn, di, dd);
+      map_apply<S, false, true, Z0>(W, Z, 0.0, 0.0, Zn, di, dd);
 #pragma unroll
       for (int r = 0; r < K; ++r) Z[r] = Zn[r];
       d[c] = 0.5 * (di + dd);
@@ -1214,9 +1251,14 @@ hipError_t launch_boundary_rows(const double2 *E, double2 *rows, const Geometry 
   return hipGetLastError();
 }
 
-hipError_t launch_balance_sums(const double *phi, const double *rk, const double *src, double dx, double *ab,
-                               double *sr, int Gl, int N, hipStream_t st) {
-  hipLaunchKernelGGL(balance_sums_kernel, dim3((Gl + 63) / 64), dim3(64), 0, st, phi, rk, src, dx, ab, sr, Gl, N);
+size_t balance_scratch_doubles(int Gl) { return static_cast<size_t>(kBalanceParts) * Gl * 2; }
+
+hipError_t launch_balance_sums(const double *phi, const double *rk, const double *src, double dx, double *part,
+                               double *ab, double *sr, int Gl, int N, hipStream_t st) {
+  const long long lanes = static_cast<long long>(kBalanceParts) * Gl;
+  hipLaunchKernelGGL(balance_partials_kernel, dim3(static_cast<unsigned>((lanes + 255) / 256)), dim3(256), 0, st, phi,
+                     rk, src, dx, part, Gl, N);
+  hipLaunchKernelGGL(balance_sums_kernel, dim3((Gl + 63) / 64), dim3(64), 0, st, part, ab, sr, Gl);
   return hipGetLastError();
 }
 

@@ -114,9 +114,11 @@ hipError_t launch_moments(const double2 *E, const double *mu, const double *wt, 
 hipError_t launch_boundary_rows(const double2 *E, double2 *rows, const Geometry &g, hipStream_t st);
 // *flag |= 1 if any node of the N real rows of either half is not finite (flag zeroed by the caller)
 hipError_t launch_finite_scan(const double2 *E, int *flag, const Geometry &g, hipStream_t st);
-// per group: ab = sum_c (rk phi) dx, sr = sum_c src, sequential in c (compute_balance)
-hipError_t launch_balance_sums(const double *phi, const double *rk, const double *src, double dx, double *ab,
-                               double *sr, int Gl, int N, hipStream_t st);
+// per group: ab = sum_c (rk phi) dx, sr = sum_c src (compute_balance), as a two-level sum
+// over contiguous cell ranges; part: balance_scratch_doubles(Gl) doubles of scratch
+size_t balance_scratch_doubles(int Gl);
+hipError_t launch_balance_sums(const double *phi, const double *rk, const double *src, double dx, double *part,
+                               double *ab, double *sr, int Gl, int N, hipStream_t st);
 hipError_t launch_group_absorption(const double *phi, const double *sigma, double *out, const Geometry &g,
                                    hipStream_t st);
 

@@ -1586,8 +1586,8 @@ extern "C" rt_status rt_get_group_ends(rt_solver *s, double *left, double *right
 }
 
 // compute_balance's absorption and emission sums per group (solver.cpp:262-272) on the
-// device from the moments kernel's phi (N x Gl, g fastest): sequential in c per group
-// in the reference's order and association, one lane per group (balance_sums_kernel).
+// device from the moments kernel's phi (N x Gl, g fastest): sequential within contiguous
+// cell ranges, then over the ranges (balance_partials_kernel, balance_sums_kernel).
 static rt_status balance_sums(rt_solver *s, std::vector<double> &ab, std::vector<double> &sr) {
   if (rt_status st = compute_moments(s)) return st;
   const int N = s->p.N, Gl = s->Gl;
@@ -1598,11 +1598,11 @@ static rt_status balance_sums(rt_solver *s, std::vector<double> &ab, std::vector
     host[Gl + gl] = host[gl] * ac * std::pow(s->p.T, 4) * dx;
   }
   double *d = nullptr;
-  HIP_TRY(s, hipMalloc(reinterpret_cast<void **>(&d), sizeof(double) * host.size()));
+  HIP_TRY(s, hipMalloc(reinterpret_cast<void **>(&d), sizeof(double) * (host.size() + balance_scratch_doubles(Gl))));
   hipError_t e = hipMemcpyAsync(d, host.data(), sizeof(double) * 2 * Gl, hipMemcpyHostToDevice, s->stream);
   if (e == hipSuccess)
-    e = launch_balance_sums(static_cast<const double *>(s->mom.p), d, d + Gl, dx, d + 2 * Gl, d + 3 * Gl, Gl, N,
-                            s->stream);
+    e = launch_balance_sums(static_cast<const double *>(s->mom.p), d, d + Gl, dx, d + host.size(), d + 2 * Gl,
+                            d + 3 * Gl, Gl, N, s->stream);
   if (e == hipSuccess)
     e = hipMemcpyAsync(host.data() + 2 * Gl, d + 2 * Gl, sizeof(double) * 2 * Gl, hipMemcpyDeviceToHost, s->stream);
   if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
