@@ -7,6 +7,10 @@
 #include "kernels.hpp"
 #include "sweep_device.hpp"
 
+#ifndef RT_SPLIT_BIAS
+#define RT_SPLIT_BIAS 0
+#endif
+
 namespace rtamd {
 
 // ------------------------------------------------------------------------
@@ -77,12 +81,15 @@ template <int S, int T, int KW, int w>
 __device__ __forceinline__ void split_role(const SegArgs &a, double2 (*hand)[2][split_chunk_cells() * 64],
                                            double2 *hhead) {
   constexpr int K = SchemeDim<S>::K;
-  constexpr int TW = T / KW;
+  // levels [t0, t0 + TW); two waves: RT_SPLIT_BIAS levels moved from wave 0 (which also
+  // streams the rows in) to wave 1 (timing experiments; 0 = even)
+  constexpr int bias = KW == 2 ? RT_SPLIT_BIAS : 0;
+  constexpr int TW = T / KW + (w == 0 ? -bias : (w == 1 ? bias : 0));
   constexpr int WN = map_count<S>();
   constexpr int C = split_chunk_cells();
   constexpr bool IN = w == 0, OUT = w == KW - 1;
   const int lane = threadIdx.x & 63;
-  constexpr int t0 = w * TW;  // this wave's first level
+  constexpr int t0 = w * (T / KW) - (w == 1 ? bias : 0);  // this wave's first level
   const size_t stride = static_cast<size_t>(a.Lpad);
   int half, s, q, pos;
   if (a.reflective) {
