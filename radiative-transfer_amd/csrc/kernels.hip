@@ -30,6 +30,7 @@
 // second launch after a fold of the mu < 0 exit states (MODE 0).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
 
 #include "cell.hpp"
@@ -1027,6 +1028,232 @@ __global__ __launch_bounds__(64 * kGeoWaves) void phi_correction_geo_kernel(SegA
   }
 }
 
+// The correction's share for BDF2 (any scheme whose map copies a zero d_out into X[0]),
+// lanes over cells.  After a segment's cell 0 the correction state lives in the KL = K-1
+// components X[1..K-1] and moves by the lower-triangular A (the map's linear part on
+// them); the share of cell m >= 1 is b A^(m-1) Z1 (b: (d_in + d_out)/2 on a unit
+// component, Z1 the state after cell 0).  corr_rows_kernel tabulates per line the row
+// vectors R_j = b A^j (j < 64) and A^64 once per handle; phi_correction_rows_kernel gives
+// lane j of a 64-cell chunk starting at cell m the share R_j . v with v = w A^(m-1) Z1
+// (one vector per line, broadcast through LDS, advanced by A^64 per chunk): KL FMAs per
+// cell and line, no walk along the segment and no per-cell reduction across lanes.
+constexpr int kRowsRep = 1;                // cells per lane and chunk (v read once for them)
+constexpr int kRowsLen = 64 * kRowsRep;    // R_j per line: one per cell of a chunk
+constexpr int kRowsLines = 16;             // lines per wave (R_j of each held in registers)
+constexpr int kRowsWaves = 8;              // waves per workgroup
+constexpr int kRowsSquarings = 6;          // A^kRowsLen = A^(2^6)
+static_assert(kRowsLen == 1 << kRowsSquarings, "chunk length");
+
+template <int S>
+__global__ void corr_rows_kernel(const double *map, double *rows, double *a64, int Lpad) {
+  constexpr int K = SchemeDim<S>::K, KL = K - 1, WN = map_count<S>();
+  static_assert(map_copy_row0<S>(), "X[0] is the copied zero d_out after one cell");
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= 2 * Lpad) return;
+  const int half = idx / Lpad, ell = idx % Lpad;
+  const size_t stride = static_cast<size_t>(Lpad);
+  double W[WN];
+#pragma unroll
+  for (int n = 0; n < WN; ++n) W[n] = map[(static_cast<size_t>(half) * WN + n) * stride + ell];
+  double A[tri_count(KL)], b[KL];
+#pragma unroll
+  for (int c = 0; c < KL; ++c) {  // live component c = X[c + 1]
+    double e[K], Zn[K], di, dd;
+#pragma unroll
+    for (int r = 0; r < K; ++r) e[r] = r == c + 1 ? 1.0 : 0.0;
+    map_apply<S, false, true>(W, e, 0.0, 0.0, Zn, di, dd);
+#pragma unroll
+    for (int r = c; r < KL; ++r) A[tri(r, c)] = Zn[r + 1];
+    b[c] = 0.5 * (di + dd);
+  }
+  double *out = rows + (static_cast<size_t>(half) * stride + ell) * KL * kRowsLen;
+  for (int j = 0; j < kRowsLen; ++j) {  // R_j, then R_{j+1} = R_j A
+#pragma unroll
+    for (int c = 0; c < KL; ++c) out[c * kRowsLen + j] = b[c];
+    double Rn[KL];
+#pragma unroll
+    for (int c = 0; c < KL; ++c) {
+      double acc = 0.0;
+#pragma unroll
+      for (int r = c; r < KL; ++r) acc = fma(b[r], A[tri(r, c)], acc);
+      Rn[c] = acc;
+    }
+#pragma unroll
+    for (int c = 0; c < KL; ++c) b[c] = Rn[c];
+  }
+#pragma unroll
+  for (int sq = 0; sq < kRowsSquarings; ++sq) {  // A^kRowsLen by squaring
+    double Rm[tri_count(KL)];
+#pragma unroll
+    for (int r = 0; r < KL; ++r)
+#pragma unroll
+      for (int c = 0; c <= r; ++c) {
+        double acc = 0.0;
+#pragma unroll
+        for (int m = c; m <= r; ++m) acc = fma(A[tri(r, m)], A[tri(m, c)], acc);
+        Rm[tri(r, c)] = acc;
+      }
+#pragma unroll
+    for (int n = 0; n < tri_count(KL); ++n) A[n] = Rm[n];
+  }
+#pragma unroll
+  for (int n = 0; n < tri_count(KL); ++n) a64[(static_cast<size_t>(half) * tri_count(KL) + n) * stride + ell] = A[n];
+}
+
+template <int KL>
+__device__ __forceinline__ void tri_apply(const double (&P)[tri_count(KL)], double (&v)[KL]) {
+#pragma unroll
+  for (int r = KL - 1; r >= 0; --r) {  // in place, rows from the bottom (lower triangular)
+    double acc = 0.0;
+#pragma unroll
+    for (int m = 0; m <= r; ++m) acc = fma(P[tri(r, m)], v[m], acc);
+    v[r] = acc;
+  }
+}
+
+// grid: [half][segment 1..Sg-1][cell range][block of 8 groups].  The workgroup takes its 8
+// groups in rounds of gpw = 8 / wpg groups: wave w takes group w / wpg of the round, lines
+// (w % wpg) * 8 .. +8 of it (wpg = ceil(H / 8) <= 4); lane j of a chunk starting at cell m
+// gives cells m + j + 64 c (c < kRowsRep) with R_(j + 64 c); each chunk's sums leave as
+// runs of gpw groups per cell.
+// Range r covers cells 1 + r * kRowsRange .. (r + 1) * kRowsRange; range 0 also cell 0.
+constexpr int kRowsRange = 8192;
+
+template <int S>
+__global__ __launch_bounds__(64 * kRowsWaves) void phi_correction_rows_kernel(SegArgs a, int ranges, int gblocks,
+                                                                              int wpg, const double *rows,
+                                                                              const double *a64) {
+  constexpr int K = SchemeDim<S>::K, KL = K - 1, WN = map_count<S>(), LW = kRowsLines, NG = kRowsWaves;
+  __shared__ double vsh[kRowsWaves][LW][KL];
+  __shared__ double fsh[kRowsWaves][LW];
+  __shared__ double tile[kRowsLen][kRowsWaves + 1];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const size_t stride = static_cast<size_t>(a.Lpad);
+  int b = blockIdx.x;
+  const int gb = b % gblocks;
+  b /= gblocks;
+  const int r = b % ranges;
+  b /= ranges;
+  const int s = 1 + b % (a.Sg - 1), half = b / (a.Sg - 1);
+  const bool neg = half == 0;
+  const int k_seg = s * a.Ls, seg_len = min(a.Ls, a.N - k_seg);
+  const int base = r * kRowsRange, c0 = base + 1, c_end = min(seg_len, c0 + kRowsRange);
+  const int gpw = kRowsWaves / wpg, H = a.H, rounds = (NG + gpw - 1) / gpw;
+  const int i0 = (w % wpg) * LW, nl = min(LW, H - i0);
+  const int t_cell = threadIdx.x / kRowsWaves, t_g = threadIdx.x % kRowsWaves;
+  constexpr int kCellsPerPass = 64;  // the 512 threads store 64 cells x 8 groups per pass
+  auto cell_index = [&](int m, int gl) {
+    const int k = k_seg + m;
+    return (static_cast<size_t>(half) * a.N + (neg ? a.N - 1 - k : k)) * a.Gl + gb * NG + gl;
+  };
+  for (int round = 0; round < rounds; ++round) {
+    const int gloc = round * gpw + w / wpg, g = gb * NG + gloc;
+    const bool gv = w < gpw * wpg && gloc < NG && g < a.Gl;  // wave-uniform
+    double v[KL], P[tri_count(KL)];
+#pragma unroll
+    for (int c = 0; c < KL; ++c) v[c] = 0.0;
+#pragma unroll
+    for (int n = 0; n < tri_count(KL); ++n) P[n] = 0.0;
+    double f = 0.0;
+    if (gv && lane < nl) {
+      const int ell = g * H + i0 + lane;
+      double W[WN], z[K], Z1[K], di, dd;
+#pragma unroll
+      for (int n = 0; n < WN; ++n) W[n] = a.map[(static_cast<size_t>(half) * WN + n) * stride + ell];
+#pragma unroll
+      for (int k = 0; k < K; ++k)
+        z[k] = a.yseg[((static_cast<size_t>(half) * (a.Sg + 1) + s) * K + k) * stride + ell];
+      map_apply<S, false, true>(W, z, 0.0, 0.0, Z1, di, dd);  // cell 0 (its share from z itself)
+      const double wl = a.wt[neg ? H - 1 - i0 - lane : H + i0 + lane];
+      f = wl * (0.5 * (di + dd));
+#pragma unroll
+      for (int c = 0; c < KL; ++c) v[c] = Z1[c + 1];
+#pragma unroll
+      for (int n = 0; n < tri_count(KL); ++n)
+        P[n] = a64[(static_cast<size_t>(half) * tri_count(KL) + n) * stride + ell];
+      // v = A^(c0 - 1) Z1 = (A^L)^(base / L) Z1 (L = kRowsLen), binary powering of A^L
+      double Q[tri_count(KL)];
+#pragma unroll
+      for (int n = 0; n < tri_count(KL); ++n) Q[n] = P[n];
+      for (unsigned e = static_cast<unsigned>(base / kRowsLen); e; e >>= 1) {
+        if (e & 1) tri_apply<KL>(Q, v);
+        if (e > 1) {
+          double Rm[tri_count(KL)];
+#pragma unroll
+          for (int rr = 0; rr < KL; ++rr)
+#pragma unroll
+            for (int c = 0; c <= rr; ++c) {
+              double acc = 0.0;
+#pragma unroll
+              for (int m = c; m <= rr; ++m) acc = fma(Q[tri(rr, m)], Q[tri(m, c)], acc);
+              Rm[tri(rr, c)] = acc;
+            }
+#pragma unroll
+          for (int n = 0; n < tri_count(KL); ++n) Q[n] = Rm[n];
+        }
+      }
+#pragma unroll
+      for (int c = 0; c < KL; ++c) v[c] *= wl;
+    }
+    if (lane < LW) {
+      fsh[w][lane] = f;
+#pragma unroll
+      for (int c = 0; c < KL; ++c) vsh[w][lane][c] = v[c];
+    }
+    double R[kRowsRep][LW][KL];  // R_(lane + 64 c) of each of the wave's lines (0 for absent lines)
+#pragma unroll
+    for (int cc = 0; cc < kRowsRep; ++cc)
+#pragma unroll
+      for (int i = 0; i < LW; ++i)
+#pragma unroll
+        for (int c = 0; c < KL; ++c) {
+          R[cc][i][c] = 0.0;
+          if (gv && i < nl)  // wave-uniform
+            R[cc][i][c] =
+                rows[((static_cast<size_t>(half) * stride + g * H + i0 + i) * KL + c) * kRowsLen + 64 * cc + lane];
+        }
+    __syncthreads();
+    const bool t_store = t_g < gpw && round * gpw + t_g < NG && gb * NG + round * gpw + t_g < a.Gl;
+    if (r == 0 && t_cell == 0 && t_store) {  // cell 0 of the segment
+      double acc = 0.0;
+      for (int p = 0; p < wpg; ++p)
+        for (int i = 0; i < LW; ++i) acc += fsh[t_g * wpg + p][i];
+      a.phic[cell_index(0, round * gpw + t_g)] = acc;
+    }
+    for (int m = c0; m < c_end; m += kRowsLen) {
+      double acc[kRowsRep];
+#pragma unroll
+      for (int cc = 0; cc < kRowsRep; ++cc) acc[cc] = 0.0;
+#pragma unroll
+      for (int i = 0; i < LW; ++i)
+#pragma unroll
+        for (int c = 0; c < KL; ++c) {
+          const double vv = vsh[w][i][c];
+#pragma unroll
+          for (int cc = 0; cc < kRowsRep; ++cc) acc[cc] = fma(R[cc][i][c], vv, acc[cc]);
+        }
+#pragma unroll
+      for (int cc = 0; cc < kRowsRep; ++cc) tile[64 * cc + lane][w] = acc[cc];
+      __syncthreads();
+#pragma unroll
+      for (int cc = 0; cc < kRowsLen / kCellsPerPass; ++cc) {
+        const int mc = cc * kCellsPerPass + t_cell;
+        if (t_store && m + mc < c_end) {
+          double sum = tile[mc][t_g * wpg];
+          for (int p = 1; p < wpg; ++p) sum += tile[mc][t_g * wpg + p];
+          a.phic[cell_index(m + mc, round * gpw + t_g)] = sum;
+        }
+      }
+      if (lane < LW) {  // next chunk: v = A^kRowsLen v
+        tri_apply<KL>(P, v);
+#pragma unroll
+        for (int c = 0; c < KL; ++c) vsh[w][lane][c] = v[c];
+      }
+      __syncthreads();
+    }
+  }
+}
+
 // q(x) = sum_g sigma_g (phi_g(x) - W B_g(x)), phi the sum of nparts arrays
 // [part][x][g] (the fused halves and their corrections, or one full phi):
 // one wave per cell, lanes over groups, then a butterfly over the wave
@@ -1309,6 +1536,35 @@ hipError_t launch_phi_correction_geo(int scheme, const SegArgs &a, hipStream_t s
     hipLaunchKernelGGL(phi_correction_geo_kernel<SCHEME_BE>, grid, block, 0, st, a, ranges, gblocks);
   else
     hipLaunchKernelGGL(phi_correction_geo_kernel<SCHEME_CN>, grid, block, 0, st, a, ranges, gblocks);
+  return hipGetLastError();
+}
+
+bool phi_correction_rows_supported(int scheme, const SegArgs &a) {
+  return scheme == SCHEME_BDF2 && a.H >= 1 && a.H <= kGeoLines && a.Sg > 1;
+}
+
+size_t corr_rows_doubles(int scheme, int Lpad) {
+  const int KL = (scheme == SCHEME_BDF2 ? SchemeDim<SCHEME_BDF2>::K : 1) - 1;
+  return 2ULL * Lpad * (static_cast<size_t>(KL) * kRowsLen + tri_count(KL));
+}
+
+hipError_t launch_corr_rows(int scheme, const double *map, double *rows, int Lpad, hipStream_t st) {
+  if (scheme != SCHEME_BDF2) return hipErrorInvalidValue;
+  constexpr int KL = SchemeDim<SCHEME_BDF2>::K - 1;
+  double *a64 = rows + 2ULL * Lpad * KL * kRowsLen;
+  hipLaunchKernelGGL(corr_rows_kernel<SCHEME_BDF2>, dim3((2 * Lpad + 255) / 256), dim3(256), 0, st, map, rows, a64,
+                     Lpad);
+  return hipGetLastError();
+}
+
+hipError_t launch_phi_correction_rows(int scheme, const SegArgs &a, const double *rows, hipStream_t st) {
+  if (!phi_correction_rows_supported(scheme, a)) return hipErrorInvalidValue;
+  constexpr int KL = SchemeDim<SCHEME_BDF2>::K - 1;
+  const int wpg = (a.H + kRowsLines - 1) / kRowsLines;
+  const int ranges = std::max(1, (a.Ls - 1 + kRowsRange - 1) / kRowsRange), gblocks = (a.Gl + kRowsWaves - 1) / kRowsWaves;
+  const dim3 grid(static_cast<unsigned>(2LL * (a.Sg - 1) * ranges * gblocks)), block(64 * kRowsWaves);
+  const double *a64 = rows + 2ULL * a.Lpad * KL * kRowsLen;
+  hipLaunchKernelGGL(phi_correction_rows_kernel<SCHEME_BDF2>, grid, block, 0, st, a, ranges, gblocks, wpg, rows, a64);
   return hipGetLastError();
 }
 

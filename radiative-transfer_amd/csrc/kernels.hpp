@@ -143,6 +143,12 @@ hipError_t launch_phi_correction(int scheme, const SegArgs &a, int nsub, int Lsu
 // BE, CN: the correction's share in closed form (lanes over cells, H <= 32 lines per group-half)
 bool phi_correction_geo_supported(int scheme, const SegArgs &a);
 hipError_t launch_phi_correction_geo(int scheme, const SegArgs &a, hipStream_t st);
+// BDF2: the correction's share by tabulated rows b A^j (lanes over cells, H <= 32);
+// launch_corr_rows fills the table (corr_rows_doubles) once per handle from the map
+bool phi_correction_rows_supported(int scheme, const SegArgs &a);
+size_t corr_rows_doubles(int scheme, int Lpad);
+hipError_t launch_corr_rows(int scheme, const double *map, double *rows, int Lpad, hipStream_t st);
+hipError_t launch_phi_correction_rows(int scheme, const SegArgs &a, const double *rows, hipStream_t st);
 hipError_t launch_correction_power(int scheme, const double *map, double *pow, int L, int Lpad, hipStream_t st);
 // q(x) = sum_g sigma_g (phi_g(x) - W B_g(x)) over the handle's groups, phi the
 // sum of nparts [N][Gl] arrays at phi (the fused parts, or one full phi)

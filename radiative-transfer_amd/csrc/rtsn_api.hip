@@ -78,6 +78,7 @@ struct rt_solver {
   DeviceBuf Tcell, Bcell, qbuf, edges, map_unit, lc_unit, phi_part;
   DeviceBuf corr_pow;            // A^Lsub per line for phi_correction_kernel's sub-segments
   int corr_pow_L = 0;            // the Lsub it holds (0: none)
+  DeviceBuf corr_rows;           // BDF2: rows b A^j and A^64 per line (phi_correction_rows_kernel)
   bool phi_fused = false;        // angular sums fused into the coupled pass (M/2 divides 64)
   PlanckCells pc{};
   // profiling
@@ -1240,6 +1241,18 @@ extern "C" rt_status rt_material_sweep(rt_solver *s, double *d_q) {
       const char *walk = std::getenv("RTSN_PHI_WALK");
       if (phi_correction_geo_supported(s->scheme, a) && !(walk && !std::strcmp(walk, "1"))) {
         HIP_TRY(s, launch_phi_correction_geo(s->scheme, a, s->stream));
+        HIP_TRY(s, launch_material_q(static_cast<const double *>(s->phi_part.p), 4, B, sig, s->wsum, q, s->Gl,
+                                     s->p.N, s->stream));
+        return RT_OK;
+      }
+      // BDF2: closed form by tabulated rows (phi_correction_rows_kernel)
+      if (phi_correction_rows_supported(s->scheme, a) && !(walk && !std::strcmp(walk, "1"))) {
+        if (!s->corr_rows.p) {
+          HIP_TRY(s, dalloc(s->corr_rows, sizeof(double) * corr_rows_doubles(s->scheme, s->Lpad)));
+          HIP_TRY(s, launch_corr_rows(s->scheme, static_cast<const double *>(s->map.p),
+                                      static_cast<double *>(s->corr_rows.p), s->Lpad, s->stream));
+        }
+        HIP_TRY(s, launch_phi_correction_rows(s->scheme, a, static_cast<const double *>(s->corr_rows.p), s->stream));
         HIP_TRY(s, launch_material_q(static_cast<const double *>(s->phi_part.p), 4, B, sig, s->wsum, q, s->Gl,
                                      s->p.N, s->stream));
         return RT_OK;

@@ -170,6 +170,32 @@ def test_be_correction_closed_form(rtsn_mod, oracle_mod, monkeypatch, M, bc_left
         assert per_group_rel(phi_geo, walk.moments()[0], 0) <= 1e-12
 
 
+@pytest.mark.parametrize("M,bc_left,waves", [(64, 0, "1"), (64, 2, "1"), (32, 1, "2"), (16, 2, ""), (8, 0, "1")])
+def test_bdf2_correction_rows(rtsn_mod, oracle_mod, monkeypatch, M, bc_left, waves):
+    """BDF2: the correction's share by tabulated rows b A^j (phi_correction_rows_kernel: lanes
+    over cells, A^64 per 64-cell chunk) against the oracle and against the cell-by-cell walk
+    (RTSN_PHI_WALK=1), on 50k-cell lines: segments longer than a workgroup's 2048-cell range
+    (few waves per CU) and short ones (""); H = 32 (two waves per group), 16, 8, 4 lines.
+    dt = 1e-6 keeps the coupled BDF2 run bounded (at 1e-4 the oracle's T goes negative)."""
+    p = params(oracle_mod, ts=3, dt=1e-6, M=M, G=6, N=50000, bc_left=bc_left, bc_right=0)
+    p["psi_source"] = np.linspace(0.5, 2.0, M * p["G"]).reshape(M, p["G"])
+    if waves:
+        monkeypatch.setenv("RTSN_WAVES_PER_CU", waves)
+    T0 = t_profile(p["N"], 0.5, 1.5)
+    gpu, orc = run_pair(rtsn_mod, oracle_mod, p, 3, rho_cv=5.0, T0=T0)
+    with gpu:
+        compare(gpu, orc)
+        T_rows, phi_rows = gpu.temperature(), gpu.moments()[0]
+    monkeypatch.setenv("RTSN_PHI_WALK", "1")
+    with rtsn_mod.Solver(to_rt(p)) as walk:
+        walk.material_enable(5.0, T0)
+        for _ in range(3):
+            walk.material_sweep()
+            walk.material_update()
+        np.testing.assert_allclose(T_rows, walk.temperature(), rtol=1e-13)
+        assert per_group_rel(phi_rows, walk.moments()[0], 0) <= 1e-12
+
+
 def test_backward_euler_energy_on_device(rtsn_mod, oracle_mod):
     from test_material import net_outflow, total_energy
     p = params(oracle_mod, ts=1, M=8, G=6, N=300, bc_left=2, bc_right=0)
