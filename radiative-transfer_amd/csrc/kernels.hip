@@ -1042,6 +1042,7 @@ constexpr int kRowsLen = 64 * kRowsRep;    // R_j per line: one per cell of a ch
 constexpr int kRowsLines = 16;             // lines per wave (R_j of each held in registers)
 constexpr int kRowsWaves = 8;              // waves per workgroup
 constexpr int kRowsSquarings = 6;          // A^kRowsLen = A^(2^6)
+constexpr int kRowsBatch = 4;              // chunks per barrier round (their v staged together)
 static_assert(kRowsLen == 1 << kRowsSquarings, "chunk length");
 
 template <int S>
@@ -1124,9 +1125,10 @@ __global__ __launch_bounds__(64 * kRowsWaves) void phi_correction_rows_kernel(Se
                                                                               int wpg, const double *rows,
                                                                               const double *a64) {
   constexpr int K = SchemeDim<S>::K, KL = K - 1, WN = map_count<S>(), LW = kRowsLines, NG = kRowsWaves;
-  __shared__ double vsh[kRowsWaves][LW][KL];
+  constexpr int NB = kRowsBatch;
+  __shared__ double vsh[kRowsWaves][NB][LW][KL];  // v of the round's NB chunks
   __shared__ double fsh[kRowsWaves][LW];
-  __shared__ double tile[kRowsLen][kRowsWaves + 1];
+  __shared__ double tile[NB * kRowsLen][kRowsWaves + 1];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const size_t stride = static_cast<size_t>(a.Lpad);
   int b = blockIdx.x;
@@ -1198,7 +1200,13 @@ __global__ __launch_bounds__(64 * kRowsWaves) void phi_correction_rows_kernel(Se
     if (lane < LW) {
       fsh[w][lane] = f;
 #pragma unroll
-      for (int c = 0; c < KL; ++c) vsh[w][lane][c] = v[c];
+      for (int c = 0; c < KL; ++c) vsh[w][0][lane][c] = v[c];
+#pragma unroll
+      for (int qb = 1; qb < NB; ++qb) {
+        tri_apply<KL>(P, v);
+#pragma unroll
+        for (int c = 0; c < KL; ++c) vsh[w][qb][lane][c] = v[c];
+      }
     }
     double R[kRowsRep][LW][KL];  // R_(lane + 64 c) of each of the wave's lines (0 for absent lines)
 #pragma unroll
@@ -1220,23 +1228,26 @@ __global__ __launch_bounds__(64 * kRowsWaves) void phi_correction_rows_kernel(Se
         for (int i = 0; i < LW; ++i) acc += fsh[t_g * wpg + p][i];
       a.phic[cell_index(0, round * gpw + t_g)] = acc;
     }
-    for (int m = c0; m < c_end; m += kRowsLen) {
-      double acc[kRowsRep];
+    for (int m = c0; m < c_end; m += NB * kRowsLen) {
 #pragma unroll
-      for (int cc = 0; cc < kRowsRep; ++cc) acc[cc] = 0.0;
+      for (int qb = 0; qb < NB; ++qb) {
+        double acc[kRowsRep];
 #pragma unroll
-      for (int i = 0; i < LW; ++i)
+        for (int cc = 0; cc < kRowsRep; ++cc) acc[cc] = 0.0;
 #pragma unroll
-        for (int c = 0; c < KL; ++c) {
-          const double vv = vsh[w][i][c];
+        for (int i = 0; i < LW; ++i)
 #pragma unroll
-          for (int cc = 0; cc < kRowsRep; ++cc) acc[cc] = fma(R[cc][i][c], vv, acc[cc]);
-        }
+          for (int c = 0; c < KL; ++c) {
+            const double vv = vsh[w][qb][i][c];
 #pragma unroll
-      for (int cc = 0; cc < kRowsRep; ++cc) tile[64 * cc + lane][w] = acc[cc];
+            for (int cc = 0; cc < kRowsRep; ++cc) acc[cc] = fma(R[cc][i][c], vv, acc[cc]);
+          }
+#pragma unroll
+        for (int cc = 0; cc < kRowsRep; ++cc) tile[qb * kRowsLen + 64 * cc + lane][w] = acc[cc];
+      }
       __syncthreads();
 #pragma unroll
-      for (int cc = 0; cc < kRowsLen / kCellsPerPass; ++cc) {
+      for (int cc = 0; cc < NB * kRowsLen / kCellsPerPass; ++cc) {
         const int mc = cc * kCellsPerPass + t_cell;
         if (t_store && m + mc < c_end) {
           double sum = tile[mc][t_g * wpg];
@@ -1244,10 +1255,13 @@ __global__ __launch_bounds__(64 * kRowsWaves) void phi_correction_rows_kernel(Se
           a.phic[cell_index(m + mc, round * gpw + t_g)] = sum;
         }
       }
-      if (lane < LW) {  // next chunk: v = A^kRowsLen v
-        tri_apply<KL>(P, v);
+      if (lane < LW) {  // the next round's chunks: v = A^kRowsLen v, NB times
 #pragma unroll
-        for (int c = 0; c < KL; ++c) vsh[w][lane][c] = v[c];
+        for (int qb = 0; qb < NB; ++qb) {
+          tri_apply<KL>(P, v);
+#pragma unroll
+          for (int c = 0; c < KL; ++c) vsh[w][qb][lane][c] = v[c];
+        }
       }
       __syncthreads();
     }
