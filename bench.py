@@ -58,7 +58,11 @@ sys.path.insert(0, str(REPO / "radiative-transfer_amd"))
 
 import numpy as np  # noqa: E402
 
-METRIC = "cell·angle·group updates/sec (Sn sweep) + BDF2 steps/sec, llnl_slab_test"
+# BASELINE.json's metric, named on the workload the headline value is measured on: the SL
+# slab (the north_star's 1e6-cell x S64 x 128-group slab); the metric's named
+# config, llnl_slab_test, is timed on the same run under the top-level "llnl_slab_test" key
+METRIC = ("cell·angle·group updates/sec (Sn sweep) + BDF2 steps/sec, SL slab (N=1e6 x S64 x 128 groups); "
+          "llnl_slab_test rate under 'llnl_slab_test'")
 HBM_PEAK = 8.0e12
 SUPPORTED_TIME_BLOCKS = (1, 2, 3, 4, 5, 6, 7, 8, 10, 12, 16, 20, 24, 32, 40)  # rt_set_time_block
 # the bench's choice for K timed steps: the first of these dividing K, fastest per step first
@@ -157,6 +161,67 @@ REFERENCE_CONFIGS = ("single_group.prm", "multi_group_equilibrium.prm", "llnl_sl
                      "llnl_slab_test_uncapped.prm")
 
 
+def gpu_rate(params: dict, ts_method: int, rate_steps: int = 1000) -> dict:
+    """rate_steps steps of a configuration on the GPU as rt_solve runs them -- the short-line
+    wavefront (one launch per advance) where the lines fit a wave, else the segment
+    pipeline at the time block rt_solve would pick (rt_plan_time_block) -- the handle
+    created and warmed outside the timer, advance + finish + device sync timed: BDF2
+    steps/s and cell-angle-group updates/s, with the number of sweep launches (HIP event
+    pairs) that ran."""
+    import rtsn
+    params = dict(params, max_timesteps=rate_steps)
+    upd_step = (4.0 if ts_method == 3 else 1.0) * params["M"] * params["G"] * params["N"]
+
+    def schedule(s):  # rt_solve's choice
+        if not s.wavefront_state()["active"]:
+            s.time_block = rtsn.plan_time_block(ts_method, rate_steps)
+
+    with rtsn.Solver(params) as s:  # warm: kernels loaded, equilibrium sources built
+        schedule(s)
+        s.advance(2 * s.time_block)
+        s.finish()
+        s.synchronize()
+    with rtsn.Solver(params) as s:
+        schedule(s)
+        path = "wavefront" if s.wavefront_state()["active"] else "segments"
+        s.set_profiling(True)
+        s.synchronize()
+        t0 = time.perf_counter()
+        s.advance(rate_steps)
+        s.finish()
+        s.synchronize()
+        gpu_s = time.perf_counter() - t0
+        passes = s.sweep_time()[1]
+        s.set_profiling(False)
+        finite = s.state_finite()
+        tb = s.time_block
+    return {"steps": rate_steps, "bdf2_steps_per_s": rate_steps / gpu_s, "updates_per_s": upd_step * rate_steps / gpu_s,
+            "ms": 1e3 * gpu_s, "sweep_passes": passes, "path": path,
+            "time_block": None if path == "wavefront" else tb, "state_finite": finite}
+
+
+def llnl_slab_test_rate(ref_configs=None, rate_steps: int = 1000) -> dict:
+    """BASELINE.json's named config, prm/llnl_slab_test.prm (M = 2, G = 124 tabulated groups,
+    N = 50), as a rate over rate_steps BDF2 steps on the GPU -- from reference_config when
+    it ran (with the oracle beside it), else measured here (GPU only)."""
+    import rtsn
+    cfg = "prm/llnl_slab_test.prm (M=2, G=124 tabulated bounds/kappa, N=50, BDF2 dt=1e-3)"
+    if ref_configs and "llnl_slab_test.prm" in ref_configs:
+        r = ref_configs["llnl_slab_test.prm"]
+        rate = r["rate"]
+        return {"config": cfg, "steps": rate["steps"], "bdf2_steps_per_s": rate["gpu_bdf2_steps_per_s"],
+                "updates_per_s": rate["gpu_updates_per_s"], "ms": rate["gpu_ms"], "path": rate["path"],
+                "time_block": rate["time_block"],
+                "sweep_passes": rate["gpu_sweep_passes"], "state_finite": rate["state_finite"],
+                "cpu_bdf2_steps_per_s": rate["cpu_bdf2_steps_per_s"], "cpu": rate["cpu"],
+                "prm_length_end_to_end_ms": r["gpu_end_to_end_ms"], "prm_length_cpu_ms": r["cpu_ms"],
+                "phi_max_rel_diff_vs_oracle": r["phi_max_rel_diff"]}
+    pdir = REPO / "tests" / "golden" / "prm"
+    ph = rtsn.ParameterHandler(pdir / "llnl_slab_test.prm", table_dir=str(pdir) + "/")
+    g = gpu_rate(ph.params, 3, rate_steps)
+    return dict({"config": cfg}, **g)
+
+
 def reference_config_timings(rate_steps: int = 1000) -> dict:
     """BASELINE.json's small configs (the reference's own .prm files, SURVEY §8(d) SG, EQ,
     LL, LL-uncapped):
@@ -201,33 +266,16 @@ def reference_config_timings(rate_steps: int = 1000) -> dict:
         # the rate over rate_steps BDF2 steps
         params = dict(ph.params, max_timesteps=rate_steps)
         upd_step = (4.0 if q["ts_method"] == 3 else 1.0) * q["M"] * q["G"] * q["N"]
-        with rtsn.Solver(params) as s:  # warm: kernels loaded, equilibrium sources built
-            s.time_block = rtsn.plan_time_block(q["ts_method"], rate_steps)
-            s.advance(2 * s.time_block)
-            s.finish()
-            s.synchronize()
-        with rtsn.Solver(params) as s:
-            s.time_block = rtsn.plan_time_block(q["ts_method"], rate_steps)  # rt_solve's choice
-            s.set_profiling(True)
-            s.synchronize()
-            t0 = time.perf_counter()
-            s.advance(rate_steps)
-            s.finish()
-            s.synchronize()
-            gpu_s = time.perf_counter() - t0
-            passes = s.sweep_time()[1]
-            s.set_profiling(False)
-            finite = s.state_finite()
-            tb = s.time_block
+        g = gpu_rate(params, q["ts_method"], rate_steps)
         o = oracle.OracleSolver(dict(q, max_timesteps=rate_steps))
         t0 = time.perf_counter()
         o.solve()
         cpu_s = time.perf_counter() - t0
-        r["rate"] = {"steps": rate_steps, "gpu_bdf2_steps_per_s": rate_steps / gpu_s,
-                     "cpu_bdf2_steps_per_s": rate_steps / cpu_s, "gpu_updates_per_s": upd_step * rate_steps / gpu_s,
-                     "cpu_updates_per_s": upd_step * rate_steps / cpu_s, "gpu_ms": 1e3 * gpu_s, "cpu_ms": 1e3 * cpu_s,
-                     "gpu_sweep_passes": passes, "time_block": tb, "state_finite": finite,
-                     "cpu": "oracle, 1 thread, the reference's loop order"}
+        r["rate"] = {"steps": rate_steps, "gpu_bdf2_steps_per_s": g["bdf2_steps_per_s"],
+                     "cpu_bdf2_steps_per_s": rate_steps / cpu_s, "gpu_updates_per_s": g["updates_per_s"],
+                     "cpu_updates_per_s": upd_step * rate_steps / cpu_s, "gpu_ms": g["ms"], "cpu_ms": 1e3 * cpu_s,
+                     "gpu_sweep_passes": g["sweep_passes"], "path": g["path"], "time_block": g["time_block"],
+                     "state_finite": g["state_finite"], "cpu": "oracle, 1 thread, the reference's loop order"}
         out[name] = r
     return out
 
@@ -299,23 +347,41 @@ def make_solver(p: dict, local: int, info, dirs):
     return rtsn.Solver(p, device=local, g_lo=info[1], g_hi=info[2])
 
 
-def gather_results(solver, N: int, world: int, shard_info, shards, device, dirs=None):
+def gather_results(solver, N: int, world: int, shard_info, shards, device, dirs=None, timings=None):
     """All-gather of the per-rank result blocks (RCCL on the GPU box, gloo in
     the CPU tests): returns {"phi", "F", "phi_plus"} as (N, G_total) tensors and
-    {"left", "right", "balance"} as (G_total,) tensors."""
+    {"left", "right", "balance"} as (G_total,) tensors.  timings (a dict) receives the
+    wall time of each step in ms, every step synchronised: alloc (the device buffers),
+    moments (rt_get_moments_device: the moments kernel and the copy out), group_ends,
+    balance (both reuse the moments of the same state), collective (the all-gathers),
+    assemble (the per-rank blocks into the (N, G) arrays)."""
     import torch
     import torch.distributed as dist
+
+    t = timings if timings is not None else {}
+    clock = [time.perf_counter()]
+
+    def mark(name):
+        solver.synchronize()
+        if device.type == "cuda":
+            torch.cuda.synchronize(device)
+        now = time.perf_counter()
+        t[name] = t.get(name, 0.0) + 1e3 * (now - clock[0])
+        clock[0] = now
 
     G_total, g_lo, g_hi = shard_info
     if dirs:  # direction shards: every rank holds partial sums over its directions of all groups
         mom = torch.empty(3, N * G_total, dtype=torch.float64, device=device)
+        mark("alloc")
         solver.moments_device(mom[0], mom[1], mom[2])
+        mark("moments")
         left, right = solver.compute_group_ends()
-        solver.synchronize()
         ends = torch.as_tensor(np.stack([left, right]), device=device)
+        mark("group_ends")
         if world > 1:
             dist.all_reduce(mom)
             dist.all_reduce(ends)
+        mark("collective")
         fields = mom.view(3, N, G_total)
         nan = torch.full((G_total,), float("nan"), dtype=torch.float64, device=device)
         return {"phi": fields[0], "F": fields[1], "phi_plus": fields[2],
@@ -323,24 +389,34 @@ def gather_results(solver, N: int, world: int, shard_info, shards, device, dirs=
     shards = shards or [(g_lo, g_hi)]
     Gl = g_hi - g_lo
     Gmax = max(hi - lo for lo, hi in shards)
-    block = torch.zeros(3, N, Gmax, dtype=torch.float64, device=device)
-    mom = torch.empty(3, N * Gl, dtype=torch.float64, device=device)
+    # the rank's wire block [3][N][Gmax]: the moments land in it directly when this shard
+    # is the largest, else in its first Gl columns
+    block = (torch.empty if Gl == Gmax else torch.zeros)(3, N, Gmax, dtype=torch.float64, device=device)
+    mom = block.view(3, N * Gmax) if Gl == Gmax else torch.empty(3, N * Gl, dtype=torch.float64, device=device)
+    mark("alloc")
     solver.moments_device(mom[0], mom[1], mom[2])
+    mark("moments")
     left, right = solver.compute_group_ends()
+    mark("group_ends")
     bal = solver.compute_balance()
-    solver.synchronize()
-    block[:, :, :Gl] = mom.view(3, N, Gl)
+    mark("balance")
+    if Gl != Gmax:
+        block[:, :, :Gl] = mom.view(3, N, Gl)
     small = torch.zeros(3, Gmax, dtype=torch.float64, device=device)
     small[:, :Gl] = torch.as_tensor(np.stack([left, right, bal]), device=device)
-    if world > 1:
-        big = [torch.empty_like(block) for _ in range(world)]
-        dist.all_gather(big, block)
-        sm = [torch.empty_like(small) for _ in range(world)]
-        dist.all_gather(sm, small)
-    else:
-        big, sm = [block], [small]
+    if world == 1:  # one shard: the block is the result
+        mark("assemble")
+        return {"phi": block[0], "F": block[1], "phi_plus": block[2],
+                "left": small[0], "right": small[1], "balance": small[2]}
+    big = [torch.empty_like(block) for _ in range(world)]
+    sm = [torch.empty_like(small) for _ in range(world)]
+    mark("alloc")
+    dist.all_gather(big, block)
+    dist.all_gather(sm, small)
+    mark("collective")
     fields = torch.cat([big[r][:, :, :hi - lo] for r, (lo, hi) in enumerate(shards)], dim=2)
     scal = torch.cat([sm[r][:, :hi - lo] for r, (lo, hi) in enumerate(shards)], dim=1)
+    mark("assemble")
     return {"phi": fields[0], "F": fields[1], "phi_plus": fields[2],
             "left": scal[0], "right": scal[1], "balance": scal[2]}
 
@@ -419,7 +495,9 @@ def run_rank(solver, p: dict, steps: int, warmup: int, world: int, device, shard
     # fastest) and its group ends and balance, assembled into the reference's (N, G)
     # / (G) arrays on every rank; ragged shards are padded to the largest
     t2 = time.perf_counter()
-    gathered = gather_results(solver, p["N"], world, shard_info, scaling_shards, device, dirs) if gather else None
+    gather_steps = {}
+    gathered = (gather_results(solver, p["N"], world, shard_info, scaling_shards, device, dirs, gather_steps)
+                if gather else None)
     gather_ms = 1e3 * (time.perf_counter() - t2)
 
     t = torch.tensor([wall, kern_ms / max(nlaunch, 1)], dtype=torch.float64, device=device)
@@ -501,7 +579,8 @@ def run_rank(solver, p: dict, steps: int, warmup: int, world: int, device, shard
         "bytes_per_update": b_upd, "frac": value / world * b_upd / HBM_PEAK, "target": 0.5}
     if gather:
         line["gather"] = {"fields": "phi, F, phi_plus (N x G) + left/right ends, balance (G)",
-                          "bytes_per_rank": 8 * 3 * p["N"] * (g_hi - g_lo), "ms": gather_ms}
+                          "bytes_per_rank": 8 * 3 * p["N"] * (g_hi - g_lo), "ms": gather_ms,
+                          "steps_ms": {k: round(v, 3) for k, v in gather_steps.items()}}
     return line, absorb, gathered
 
 
@@ -604,6 +683,7 @@ def run_material(p: dict, info, world: int, device, local: int, steps: int, dirs
                     "emission, q(x) all-reduce over ranks, T update",
             "ts_method": 1, "steps": steps, "warmup": 1, "ms_per_step": 1e3 * wall / steps,
             "updates_per_s": upd / wall, "allreduce_bytes_per_step": 8 * q["N"], "allreduce": path,
+            "rccl": rtsn.comm_version(),  # the RCCL rt_comm ran on (the process's librccl.so.1)
             "stability_number": number, "rho_cv": 1.0, "T_range_keV": [float(T.min()), float(T.max())],
             "state_finite": bool(np.isfinite(T).all())}
 
@@ -693,6 +773,8 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(args.variant)
         line["reference_config"] = reference_config_timings()
+    if rank == 0:
+        line["llnl_slab_test"] = llnl_slab_test_rate(line.get("reference_config"))
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:

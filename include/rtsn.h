@@ -223,6 +223,18 @@ rt_status rt_get_pipeline(rt_solver *s, int *on);
  * steps queued but not launched, whether a correction is pending; any NULL skipped. */
 rt_status rt_pipeline_state(rt_solver *s, long long *lag_steps, int *queued_steps, int *pending);
 rt_status rt_get_time_block(rt_solver *s, int *steps_per_pass);
+/* Short lines: a wavefront over (cell, time level) with lanes over cells -- a line (with the
+ * reflective left boundary: a mu < 0 line and its mirror) in one wave, C cells per lane in
+ * registers, every step of an advance in one launch (up to 65536 steps per launch), the
+ * upwind recurrence carried lane to lane by a DPP shift each tick: for lines of up to
+ * 64 C cells (reflective: 32 C), C = 1, 2, 4 or 8.  Results are bitwise those of the
+ * pipelined segment schedule.  mode 0: off; 1 (default): used when the line fits and the
+ * caller set neither a time block (rt_set_time_block) nor a schedule (rt_set_pipeline);
+ * 2: used whenever the line fits.  RTSN_WAVEFRONT=0|2 at creation sets 0 or 2. */
+rt_status rt_set_wavefront(rt_solver *s, int mode);
+/* *mode as set; *active: the next rt_advance takes the wavefront; *cells_per_lane: C for
+ * this handle's lines (0: too long for a wave).  Any NULL skipped. */
+rt_status rt_get_wavefront(rt_solver *s, int *mode, int *active, int *cells_per_lane);
 /* Waves per segment of a pipelined BDF2 pass of 8, 10, 12, 16 or 20 steps: 1 runs
  * all levels in one wave; 2 (or 4, T divisible by 4) shares them between the waves of
  * a workgroup through LDS; 0 (default) = 2 at T = 20 (its one-wave kernel leans on
@@ -319,6 +331,48 @@ rt_status rt_comm_allreduce_absorption(rt_comm *c, rt_solver *s, double *d_out);
  * update -- stream-ordered, no host synchronisation; every rank ends with the same T(x). */
 rt_status rt_comm_material_step(rt_comm *c, rt_solver *s, int nsteps);
 const char *rt_comm_last_error(rt_comm *c);
+/* The RCCL this library's collectives run on (host only, no device call): ncclGetVersion
+ * (e.g. 22707 for 2.27.7) and the file the process resolved ncclGetVersion from.  librtsn
+ * links librccl.so.1; a process that loaded another library of that name first (torch's
+ * bundled RCCL, when torch is imported before librtsn) runs rt_comm on that one -- the same
+ * RCCL as torch.distributed's process group in that process.  path may be NULL. */
+rt_status rt_comm_version(int *version, char *path, size_t path_len);
+
+/* ---- multi-GPU: host-side layout of the gathered shard blocks ----------------------
+ * The placement steps of the rt_comm gathers as host functions (no device calls, valid
+ * without a GPU) for callers that run their own collectives (MPI, torch.distributed, ...).
+ * rt_comm_* runs exactly these copy plans on the device (hipMemcpy2DAsync).  A shard is
+ * groups [g_lo, g_hi) and direction pairs [d_lo, d_hi) of the M/2 of a (G, M, N)
+ * configuration (rt_get_shard, rt_get_dims); the ranks' shards must be group shards
+ * tiling [0, G) in rank order or direction shards tiling [0, M/2) over all groups
+ * (else RT_ERR_PARAM).  Wire blocks are padded to the largest shard's Gmax groups. */
+typedef struct {
+  int G, M;         /* the configuration's groups and directions */
+  int g_lo, g_hi;   /* the shard's groups */
+  int d_lo, d_hi;   /* its direction pairs of the M/2 (all: 0, M/2) */
+  int N;            /* cells */
+  int reserved;     /* 0 */
+} rt_shard;
+/* *mode: 0 group shards, 1 direction shards; *max_groups: Gmax.  Any NULL skipped. */
+rt_status rt_layout_mode(const rt_shard *shards, int nranks, int *mode, int *max_groups);
+/* rank's phi, F, phi_plus (local: 3 arrays of N x G_local back to back, g fastest, as
+ * rt_get_moments_device writes them) -> its wire block [3][N][Gmax], padding zeroed */
+rt_status rt_layout_pack_moments(const rt_shard *shards, int nranks, int rank, const double *local, double *block);
+/* gathered: group shards the all-gather of every rank's block [rank][3][N][Gmax];
+ * direction shards their sum [3][N][Gmax] -> phi, F, phi_plus (G x N, g + G c); NULL skipped */
+rt_status rt_layout_unpack_moments(const rt_shard *shards, int nranks, const double *gathered, double *phi,
+                                   double *F, double *phi_plus);
+/* k per-group vectors (G_local each) -> the rank's block [k][Gmax]; in[j] NULL leaves zeros */
+rt_status rt_layout_pack_vectors(const rt_shard *shards, int nranks, int rank, int k, const double *const *in,
+                                 double *block);
+/* gathered [rank][k][Gmax] (group shards) or their sum [k][Gmax] (direction shards) -> k
+ * vectors of G; out[j] NULL skipped */
+rt_status rt_layout_unpack_vectors(const rt_shard *shards, int nranks, int k, const double *gathered,
+                                   double *const *out);
+/* one shard's psi (M_l, G_local, N) as rt_get_psi returns it -> its entries of the (M, G, N) psi */
+rt_status rt_layout_place_psi(const rt_shard *shard, const double *block, double *psi);
+/* one shard's psi_source rows (M_l x G, as rt_get_psi_source returns them) -> its rows of (M x G) */
+rt_status rt_layout_place_psi_source(const rt_shard *shard, const double *rows, double *psi_source);
 
 const char *rt_status_string(rt_status st);
 /* Last error message recorded on the handle (or the global one for s == NULL). */

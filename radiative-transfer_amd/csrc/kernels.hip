@@ -1114,7 +1114,8 @@ __device__ __forceinline__ void tri_apply(const double (&P)[tri_count(KL)], doub
 
 // grid: [half][segment 1..Sg-1][cell range][block of 8 groups].  The workgroup takes its 8
 // groups in rounds of gpw = 8 / wpg groups: wave w takes group w / wpg of the round, lines
-// (w % wpg) * 8 .. +8 of it (wpg = ceil(H / 8) <= 4); lane j of a chunk starting at cell m
+// (w % wpg) * 16 .. +16 of it (LW = kRowsLines = 16, wpg = ceil(H / 16) <= 2 for H <= 32);
+// lane j of a chunk starting at cell m
 // gives cells m + j + 64 c (c < kRowsRep) with R_(j + 64 c); each chunk's sums leave as
 // runs of gpw groups per cell.
 // Range r covers cells 1 + r * kRowsRange .. (r + 1) * kRowsRange; range 0 also cell 0.
@@ -1265,6 +1266,9 @@ __global__ __launch_bounds__(64 * kRowsWaves) void phi_correction_rows_kernel(Se
       }
       __syncthreads();
     }
+    // the next round rewrites fsh / vsh: a range with no chunk (c0 >= c_end, e.g. range 0 of a
+    // one-cell last segment) has passed no barrier since the cell-0 sum read fsh above
+    __syncthreads();
   }
 }
 

@@ -1,0 +1,169 @@
+// kernels_wave.hip -- short lines: a wavefront over (cell, time level), lanes over cells,
+// every step of an advance in one launch (wavefront_kernel).
+//
+// The segment pipeline (kernels.hip) parallelises a line over segments that hand their
+// exit states from one launch to the next, so a line's traversal costs a launch per
+// segment and time block -- for the reference's own configurations (llnl_slab_test: 50
+// cells, single_group / multi_group_equilibrium: 100) that is microseconds of dependent
+// latency per step on a handful of workgroups.  Here a line (or, with the reflective left
+// boundary, a mu < 0 line followed by its mu > 0 mirror) lives in ONE wave: lane j holds
+// C consecutive cells of the chain in registers and, at tick tau, runs time level
+// t = tau - j of its cells -- the upwind recurrence x_{k+1} = A x_k + b_k of every level is
+// carried across lanes by one DPP lane shift of the carried state per tick (wave_shr:1), so
+// level t of lane j starts from lane j - 1's exit state of the same level, produced one tick
+// earlier.  n steps of an L-lane chain take n + L - 1 ticks of C cell maps each; the state
+// is read once and written once per launch.
+//
+// Same arithmetic per (cell, level) as the pipelined segment pass (the per-line affine map
+// of cell.hpp, exact carries; the reflective mu > 0 head cell by the reference's algebra
+// with the mirror's per-substep outflows, sweep_device.hpp head_cell): bitwise equal to it.
+#include <hip/hip_runtime.h>
+
+#include "cell.hpp"
+#include "kernels.hpp"
+
+namespace rtamd {
+
+// DPP wave_shr:1 (gfx9 family): lane l receives lane l - 1's value, lane 0 receives 0
+__device__ __forceinline__ double lane_shift_up(double v) {
+  const unsigned long long b = __builtin_bit_cast(unsigned long long, v);
+  const int lo = __builtin_amdgcn_update_dpp(0, static_cast<int>(b & 0xffffffffu), 0x138, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, static_cast<int>(b >> 32), 0x138, 0xf, 0xf, false);
+  return __builtin_bit_cast(double, (static_cast<unsigned long long>(static_cast<unsigned int>(hi)) << 32) |
+                                        static_cast<unsigned int>(lo));
+}
+
+// grid: one wave per line (mu < 0 lines then mu > 0 lines, ell < H Gl) -- or, reflective,
+// one wave per line pair ell (lanes [0, Lw) the mu < 0 line, [Lw, 2 Lw) its mirror).
+// Lw = lanes per line = ceil(N / C).  nsteps full steps from the stored state.
+template <int S, int C>
+__global__ __launch_bounds__(64) void wavefront_kernel(SegArgs a, int nsteps, int Lw) {
+  constexpr int K = SchemeDim<S>::K, WN = map_count<S>();
+  const int lane = threadIdx.x;
+  const bool pair = a.reflective != 0;
+  const int nl = a.H * a.Gl;
+  int half, ell, j;
+  if (pair) {
+    ell = blockIdx.x;
+    half = lane < Lw ? 0 : 1;
+    j = lane - half * Lw;
+  } else {
+    half = static_cast<int>(blockIdx.x) / nl;
+    ell = static_cast<int>(blockIdx.x) % nl;
+    j = lane;
+  }
+  const int used = pair ? 2 * Lw : Lw;  // lanes holding cells; the chain's lane index is `lane`
+  const bool real = lane < used;
+  const size_t stride = static_cast<size_t>(a.Lpad);
+  double2 *Eh = a.E + static_cast<size_t>(half) * a.Nrow * stride + ell;
+
+  double ein[C], eout[C];
+#pragma unroll
+  for (int c = 0; c < C; ++c) {
+    const int k = j * C + c;
+    ein[c] = eout[c] = 0.0;
+    if (real && k < a.N) {
+      const double2 v = Eh[static_cast<size_t>(k) * stride];
+      ein[c] = v.x;
+      eout[c] = v.y;
+    }
+  }
+  double W[WN];
+#pragma unroll
+  for (int n = 0; n < WN; ++n) W[n] = a.map[(static_cast<size_t>(half) * WN + n) * stride + ell];
+  const double bv = a.bdry[static_cast<size_t>(half) * stride + ell];
+  const bool head = j == 0;
+  const bool refl_head = pair && half == 1 && head;  // one lane of a pair wave
+  LineConst L{};
+  if (refl_head) {
+    const double *lcp = a.lc + static_cast<size_t>(half) * LC_COUNT * stride + ell;
+#pragma unroll
+    for (int n = 0; n < LC_COUNT; ++n) L.c[n] = lcp[n * stride];
+  }
+
+  double X[K];
+#pragma unroll
+  for (int r = 0; r < K; ++r) X[r] = 0.0;
+  const int ticks = nsteps + used - 1;
+  for (int tick = 0; tick < ticks; ++tick) {
+    double Xin[K];
+#pragma unroll
+    for (int r = 0; r < K; ++r) Xin[r] = lane_shift_up(X[r]);  // lane - 1's exit state of this level
+    const int t = tick - lane;
+    if (!real || t < 0 || t >= nsteps) continue;
+    double b[4] = {bv, bv, bv, bv};
+    if (head) {
+      if (refl_head) {  // solver.cpp:677-684: the mirror's outflow after each substep of this step
+        if constexpr (S == SCHEME_BDF2) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) b[r] = Xin[1 + r];
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) b[r] = Xin[K - 1];
+        }
+      }
+      head_state<S>(b, Xin);
+    }
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      if (j * C + c >= a.N) break;  // the chain's padding cells carry X through
+      if (c == 0 && refl_head) {    // reflective head: the reference's algebra, distinct inflows
+        double oi, oo;
+        cell_step_maybe_head<S>(L, a.hd, false, ein[0], eout[0], Xin, true, b[3], oi, oo);
+        ein[0] = oi;
+        eout[0] = oo;
+        continue;
+      }
+      double Xn[K], oi, oo;
+      map_apply<S, true>(W, Xin, ein[c], eout[c], Xn, oi, oo);
+#pragma unroll
+      for (int r = 0; r < K; ++r) Xin[r] = Xn[r];
+      ein[c] = oi;
+      eout[c] = oo;
+    }
+#pragma unroll
+    for (int r = 0; r < K; ++r) X[r] = Xin[r];
+  }
+#pragma unroll
+  for (int c = 0; c < C; ++c) {
+    const int k = j * C + c;
+    if (real && k < a.N) Eh[static_cast<size_t>(k) * stride] = make_double2(ein[c], eout[c]);
+  }
+}
+
+template <int S>
+static hipError_t launch_wave_s(int C, const SegArgs &a, int nsteps, int Lw, int grid, hipStream_t st) {
+  switch (C) {
+#define RT_WAVE_CASE(c) \
+  case c: hipLaunchKernelGGL((wavefront_kernel<S, c>), dim3(grid), dim3(64), 0, st, a, nsteps, Lw); break;
+    RT_WAVE_CASE(1) RT_WAVE_CASE(2) RT_WAVE_CASE(4) RT_WAVE_CASE(8)
+#undef RT_WAVE_CASE
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+int wavefront_cells_per_lane(int N, bool reflective) {
+  const int lanes = reflective ? 32 : 64;
+  const int c = (N + lanes - 1) / lanes;
+  for (int C : {1, 2, 4, 8})
+    if (c <= C) return C;
+  return 0;  // too long: the segment pipeline
+}
+
+hipError_t launch_wavefront(int scheme, const SegArgs &a, int nsteps, hipStream_t st) {
+  const bool pair = a.reflective != 0;
+  const int C = wavefront_cells_per_lane(a.N, pair);
+  const int nl = a.H * a.Gl;
+  if (C == 0 || nl <= 0 || nsteps < 0) return hipErrorInvalidValue;
+  if (nsteps == 0) return hipSuccess;
+  const int Lw = (a.N + C - 1) / C;
+  const int grid = pair ? nl : 2 * nl;
+  switch (scheme) {
+    case SCHEME_BE: return launch_wave_s<SCHEME_BE>(C, a, nsteps, Lw, grid, st);
+    case SCHEME_CN: return launch_wave_s<SCHEME_CN>(C, a, nsteps, Lw, grid, st);
+    default: return launch_wave_s<SCHEME_BDF2>(C, a, nsteps, Lw, grid, st);
+  }
+}
+
+}  // namespace rtamd

@@ -64,9 +64,14 @@ struct rt_solver {
   bool prop_ready[kMaxAlignedBlock + 1] = {};
   int agg_cur = 0;               // aggregates of the last pass live in agg[agg_cur ^ 1]
   bool pending = false;          // E holds provisional segments (correction outstanding)
+  // every launch that writes E bumps state_version; the moments kernel's phi, F, phi_plus
+  // in `mom` are reused by every read-out (moments, balance, absorption) of the same state
+  unsigned long long state_version = 1, mom_version = 0;
   // pipelined schedule (rt_set_pipeline): chain positions (segments; half 0 then
   // half 1 when the left boundary is reflective) at staggered time levels
   int pipe = 1;                  // 0 off, 1 auto (runs long enough to fill), 2 always
+  bool pipe_set = false;         // the caller chose the schedule (rt_set_pipeline)
+  int wave = 1;                  // short lines, one launch per advance (rt_set_wavefront): 0 off, 1 auto, 2 on
   std::vector<long long> tau;    // full steps completed per chain position
   long long target = 0;          // full steps every position must reach
   long long pipe_base = 0;       // tau of every position when the pipeline started
@@ -694,6 +699,8 @@ static rt_status create_impl(const rt_params *pin, int g_lo, int g_hi, int d_lo,
       h->T = std::atoi(t);
       h->T_set = true;
     }
+  if (const char *wv = std::getenv("RTSN_WAVEFRONT"))  // experiments: "0" off, "2" on for every short line
+    if (!std::strcmp(wv, "0") || !std::strcmp(wv, "2")) h->wave = wv[0] - '0';
   if (const char *lw = std::getenv("RTSN_LEVEL_WAVES"))  // experiments: only "1", "2" or "4" are read
     if (!std::strcmp(lw, "1") || !std::strcmp(lw, "2") || !std::strcmp(lw, "4")) h->level_waves = lw[0] - '0';
   HIP_TRY(h, sweep_occupancy(h->scheme, h->T, level_waves_of(h, h->T), &waves_per_cu));
@@ -730,6 +737,7 @@ static rt_status create_impl(const rt_params *pin, int g_lo, int g_hi, int d_lo,
   if ((st = upload_inflow(h))) return st;
   HIP_TRY(h, launch_init_state(static_cast<double2 *>(h->E.p), static_cast<const double *>(h->lineB.p), geometry(h),
                                h->stream));
+  ++h->state_version;
 
   HIP_TRY(h, hipStreamSynchronize(h->stream));
   *out = s.release();
@@ -828,6 +836,7 @@ static rt_status apply_correction(rt_solver *s) {
   if (st) return st;
   SegArgs a = seg_args(s);
   HIP_TRY(s, launch_sweep(s->scheme, s->Tp, SWEEP_FINALIZE, a, 2 * s->Q * s->Sg, s->stream));
+  ++s->state_version;
   s->pending = false;
   return RT_OK;
 }
@@ -886,6 +895,7 @@ static rt_status enqueue_pass(rt_solver *s, int T, bool coupled = false) {
     HIP_TRY(s, launch_sweep(s->scheme, T, SWEEP_PASS, a, 2 * per_half, s->stream));
   }
   if ((st = event_end(s, e1))) return st;
+  ++s->state_version;
   s->pending = s->Sg > 1;
   s->Tp = T;
   s->agg_cur ^= 1;
@@ -945,6 +955,7 @@ static rt_status pipe_launch(rt_solver *s) {
   rt_status st = event_begin(s, &e1);
   if (st) return st;
   HIP_TRY(s, launch_sweep(s->scheme, T, SWEEP_PIPELINED, a, grid, s->stream));
+  ++s->state_version;
   if ((st = event_end(s, e1))) return st;
   for (int c = lo; c <= hi; ++c) s->tau[c] += T;
   return RT_OK;
@@ -1017,6 +1028,37 @@ static rt_status finalize(rt_solver *s) {
   return apply_correction(s);
 }
 
+// Short lines (kernels_wave.hip): every step of an advance in one launch per chunk of
+// steps, lanes over cells -- by default (rt_set_wavefront 1) when the line fits a wave and
+// the caller chose neither a time block nor a schedule, always with rt_set_wavefront 2.
+static bool use_wavefront(const rt_solver *s) {
+  if (s->material || s->wave == 0) return false;
+  if (wavefront_cells_per_lane(s->p.N, s->p.bc_left_indicator == 2) == 0) return false;
+  return s->wave == 2 || (!s->T_set && !s->pipe_set);
+}
+
+constexpr int kWaveMaxSteps = 1 << 16;  // steps per wavefront launch (bounds one launch's length)
+
+static rt_status wave_advance(rt_solver *s, int nsteps) {
+  if (rt_status st = finalize(s)) return st;  // the stored state exact at the requested time
+  SegArgs a = seg_args(s);
+  a.Gl = s->Gl;
+  a.H = s->H;
+  while (nsteps > 0) {
+    const int m = std::min(nsteps, kWaveMaxSteps);
+    hipEvent_t e1;
+    rt_status st = event_begin(s, &e1);
+    if (st) return st;
+    HIP_TRY(s, launch_wavefront(s->scheme, a, m, s->stream));
+    if ((st = event_end(s, e1))) return st;
+    ++s->state_version;
+    for (long long &t : s->tau) t += m;
+    s->target += m;
+    nsteps -= m;
+  }
+  return RT_OK;
+}
+
 extern "C" rt_status rt_advance(rt_solver *s, int nsteps) {
   if (!s || nsteps < 0) return fail(s, RT_ERR_ARG, "rt_advance: bad argument");
   if (s->material) return fail(s, RT_ERR_STATE, "material coupling is on: step with rt_material_step / rt_material_sweep");
@@ -1024,6 +1066,7 @@ extern "C" rt_status rt_advance(rt_solver *s, int nsteps) {
   rt_status st = check_validation(s);
   if (st) return st;
   if ((st = ensure_equilibrium(s))) return st;
+  if (use_wavefront(s)) return wave_advance(s, nsteps);
   return s->pipe ? pipe_advance(s, nsteps) : enqueue_steps(s, nsteps);
 }
 
@@ -1505,6 +1548,7 @@ extern "C" rt_status rt_set_ends(rt_solver *s, const double *ends) {
   }
   (void)hipStreamSynchronize(s->stream);  // d is freed below
   (void)hipFree(d);
+  ++s->state_version;
   if (e != hipSuccess)  // some chunks may hold the new cells, the rest the old ones
     return fail(s, RT_ERR_DEVICE, std::string("rt_set_ends: ") + hipGetErrorString(e) +
                                       " (the handle's state is undefined: load it again or destroy the handle)");
@@ -1514,12 +1558,14 @@ extern "C" rt_status rt_set_ends(rt_solver *s, const double *ends) {
 
 static rt_status compute_moments(rt_solver *s) {
   if (rt_status st = finalize(s)) return st;
+  if (s->mom_version == s->state_version) return RT_OK;  // `mom` holds this state's moments
   const Geometry g = geometry(s);
   const size_t GN = static_cast<size_t>(s->Gl) * s->p.N;
   double *m = static_cast<double *>(s->mom.p);
   const double *muwt = static_cast<const double *>(s->muwt.p);
   HIP_TRY(s, launch_moments(static_cast<const double2 *>(s->E.p), muwt, muwt + s->p.M, m, m + GN, m + 2 * GN, g,
                             s->stream));
+  s->mom_version = s->state_version;
   return RT_OK;
 }
 
@@ -1798,6 +1844,22 @@ extern "C" rt_status rt_set_pipeline(rt_solver *s, int on) {
     if (rt_status st = complete(s)) return st;  // leave the positions aligned
   }
   s->pipe = on;
+  s->pipe_set = true;
+  return RT_OK;
+}
+
+extern "C" rt_status rt_set_wavefront(rt_solver *s, int mode) {
+  if (!s) return fail(nullptr, RT_ERR_ARG, "rt_set_wavefront: NULL handle");
+  if (mode < 0 || mode > 2) return fail(s, RT_ERR_ARG, "rt_set_wavefront: 0 (off), 1 (auto) or 2 (on)");
+  s->wave = mode;
+  return RT_OK;
+}
+
+extern "C" rt_status rt_get_wavefront(rt_solver *s, int *mode, int *active, int *cells_per_lane) {
+  if (!s) return fail(nullptr, RT_ERR_ARG, "rt_get_wavefront: NULL handle");
+  if (mode) *mode = s->wave;
+  if (active) *active = use_wavefront(s) ? 1 : 0;
+  if (cells_per_lane) *cells_per_lane = wavefront_cells_per_lane(s->p.N, s->p.bc_left_indicator == 2);
   return RT_OK;
 }
 

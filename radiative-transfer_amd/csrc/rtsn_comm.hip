@@ -11,7 +11,10 @@
 // largest shard so the counts agree):
 //   moments  [3][N][Gmax]   (phi, F, phi_plus; g fastest, as rt_get_moments_device)
 //   vectors  [k][Gmax]      (group ends, balance terms)
-// and the assembly into the (G, N) / (G) arrays is a strided copy per rank.
+// and the assembly into the (G, N) / (G) arrays is the copy plans of comm_layout.cpp --
+// host code shared with the rt_layout_* entry points, which the CPU tests check at world
+// sizes 2, 3 and 8 -- run here with hipMemcpy2DAsync (device blocks) or on the host.
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -22,6 +25,9 @@
 #include <vector>
 
 #include "../../include/rtsn.h"
+#include "comm_layout.hpp"
+
+namespace layout = rtamd::layout;
 
 struct rt_comm {
   ncclComm_t nc = nullptr;
@@ -73,92 +79,70 @@ struct Scratch {
   }
 };
 
-struct Shard {
-  int G, M, g_lo, g_hi, d_lo, d_hi, N, Gl;
-};
-
-// Every rank's shard, and how the shards tile the problem: 0 = group shards covering
-// [0, G) in rank order (all directions each), 1 = direction shards covering [0, M/2) in
-// rank order over the same groups.
-rt_status all_shards(rt_comm *c, rt_solver *s, std::vector<Shard> &out, int &mode) {
-  Shard me{};
-  RT_TRY(c, s, rt_get_shard(s, &me.G, &me.M, &me.g_lo, &me.g_hi, &me.d_lo, &me.d_hi));
-  RT_TRY(c, s, rt_get_dims(s, nullptr, &me.Gl, &me.N, nullptr, nullptr));
+// Every rank's shard, and how the shards tile the problem (layout::shard_mode): 0 = group
+// shards covering [0, G) in rank order (all directions each), 1 = direction shards covering
+// [0, M/2) in rank order over the same groups.
+rt_status all_shards(rt_comm *c, rt_solver *s, std::vector<rt_shard> &out, int &mode) {
+  rt_shard me{};
+  int G_total = 0, M_total = 0;
+  RT_TRY(c, s, rt_get_shard(s, &G_total, &M_total, &me.g_lo, &me.g_hi, &me.d_lo, &me.d_hi));
+  RT_TRY(c, s, rt_get_dims(s, nullptr, nullptr, &me.N, nullptr, nullptr));
+  me.G = G_total;
+  me.M = M_total;
   hipStream_t st = static_cast<hipStream_t>(rt_stream(s));
-  constexpr int kInts = sizeof(Shard) / sizeof(int);
+  constexpr int kInts = sizeof(rt_shard) / sizeof(int);
+  static_assert(sizeof(rt_shard) == kInts * sizeof(int), "rt_shard is ints only");
   Scratch buf;
   buf.st = st;
   HC_TRY(c, hipMalloc(&buf.p, sizeof(int) * kInts * (c->nranks + 1)));
   int *d = static_cast<int *>(buf.p);
-  HC_TRY(c, hipMemcpyAsync(d, &me, sizeof(Shard), hipMemcpyHostToDevice, st));
+  HC_TRY(c, hipMemcpyAsync(d, &me, sizeof(rt_shard), hipMemcpyHostToDevice, st));
   NC_TRY(c, ncclAllGather(d, d + kInts, kInts, ncclInt32, c->nc, st));
   out.resize(c->nranks);
-  HC_TRY(c, hipMemcpyAsync(out.data(), d + kInts, sizeof(Shard) * c->nranks, hipMemcpyDeviceToHost, st));
+  HC_TRY(c, hipMemcpyAsync(out.data(), d + kInts, sizeof(rt_shard) * c->nranks, hipMemcpyDeviceToHost, st));
   HC_TRY(c, hipStreamSynchronize(st));
-  const int H = me.M / 2;
-  bool groups = true, dirs = true;
-  for (int r = 0; r < c->nranks; ++r) {
-    const Shard &a = out[r];
-    if (a.G != me.G || a.M != me.M || a.N != me.N) return cfail(c, RT_ERR_PARAM, "ranks hold different configurations");
-    groups = groups && a.d_lo == 0 && a.d_hi == H && a.g_lo == (r ? out[r - 1].g_hi : 0);
-    dirs = dirs && a.g_lo == me.g_lo && a.g_hi == me.g_hi && a.d_lo == (r ? out[r - 1].d_hi : 0);
-  }
-  groups = groups && out.back().g_hi == me.G;
-  dirs = dirs && out.back().d_hi == H && me.g_lo == 0 && me.g_hi == me.G;
-  if (groups) {
-    mode = 0;
-  } else if (dirs) {
-    mode = 1;
-  } else {
+  mode = layout::shard_mode(out.data(), c->nranks);
+  if (mode < 0)
     return cfail(c, RT_ERR_PARAM, "shards must be group shards tiling [0, G) or direction shards tiling [0, M/2), "
-                                  "in rank order");
-  }
+                                  "in rank order, of one configuration");
   return RT_OK;
 }
 
-int max_groups(const std::vector<Shard> &sh) {
-  int m = 0;
-  for (const Shard &a : sh) m = std::max(m, a.g_hi - a.g_lo);
-  return m;
+// A copy plan between device buffers, or from a device buffer to host memory.
+rt_status run_plan(rt_comm *c, const std::vector<layout::Copy2D> &plan, const double *src, double *dst,
+                   hipMemcpyKind kind, hipStream_t st) {
+  for (const layout::Copy2D &p : plan)
+    HC_TRY(c, hipMemcpy2DAsync(dst + p.dst, sizeof(double) * p.dpitch, src + p.src, sizeof(double) * p.spitch,
+                               sizeof(double) * p.width, p.height, kind, st));
+  return RT_OK;
 }
 
 // k host vectors of this rank's Gl groups -> all G groups on every rank: gathered (mode 0)
 // or summed (mode 1).  in[j] / out[j] may be NULL (out NULL: not wanted).
-rt_status combine_vectors(rt_comm *c, rt_solver *s, const std::vector<Shard> &sh, int mode,
+rt_status combine_vectors(rt_comm *c, rt_solver *s, const std::vector<rt_shard> &sh, int mode,
                           const std::vector<const double *> &in, const std::vector<double *> &out) {
-  const int k = static_cast<int>(in.size()), G = sh[0].G, Gl = sh[c->rank].Gl, Gm = max_groups(sh);
+  const int k = static_cast<int>(in.size()), n = c->nranks, Gm = layout::max_groups(sh.data(), n);
   hipStream_t st = static_cast<hipStream_t>(rt_stream(s));
-  std::vector<double> block(static_cast<size_t>(k) * Gm, 0.0);
+  const size_t cnt = static_cast<size_t>(k) * Gm;
+  std::vector<double> block(cnt, 0.0);
   for (int j = 0; j < k; ++j)
-    if (in[j]) std::copy(in[j], in[j] + Gl, block.begin() + static_cast<size_t>(j) * Gm);
+    if (in[j]) layout::apply(layout::vectors_pack(sh.data(), n, c->rank, k, j), in[j], block.data());
   Scratch buf;
   buf.st = st;
-  const size_t cnt = static_cast<size_t>(k) * Gm;
-  HC_TRY(c, hipMalloc(&buf.p, sizeof(double) * cnt * (c->nranks + 1)));
+  HC_TRY(c, hipMalloc(&buf.p, sizeof(double) * cnt * (n + 1)));
   double *d = static_cast<double *>(buf.p);
   HC_TRY(c, hipMemcpyAsync(d, block.data(), sizeof(double) * cnt, hipMemcpyHostToDevice, st));
-  std::vector<double> all;
+  std::vector<double> all(mode == 0 ? cnt * n : cnt);
   if (mode == 0) {
     NC_TRY(c, ncclAllGather(d, d + cnt, cnt, ncclFloat64, c->nc, st));
-    all.resize(cnt * c->nranks);
     HC_TRY(c, hipMemcpyAsync(all.data(), d + cnt, sizeof(double) * all.size(), hipMemcpyDeviceToHost, st));
   } else {
     NC_TRY(c, ncclAllReduce(d, d, cnt, ncclFloat64, ncclSum, c->nc, st));
-    all.resize(cnt);
     HC_TRY(c, hipMemcpyAsync(all.data(), d, sizeof(double) * cnt, hipMemcpyDeviceToHost, st));
   }
   HC_TRY(c, hipStreamSynchronize(st));
-  for (int j = 0; j < k; ++j) {
-    if (!out[j]) continue;
-    if (mode == 1) {
-      std::copy(all.begin() + static_cast<size_t>(j) * Gm, all.begin() + static_cast<size_t>(j) * Gm + G, out[j]);
-      continue;
-    }
-    for (int r = 0; r < c->nranks; ++r) {
-      const double *src = all.data() + cnt * r + static_cast<size_t>(j) * Gm;
-      std::copy(src, src + sh[r].Gl, out[j] + sh[r].g_lo);
-    }
-  }
+  for (int j = 0; j < k; ++j)
+    if (out[j]) layout::apply(layout::vectors_unpack(sh.data(), n, k, j), all.data(), out[j]);
   return RT_OK;
 }
 
@@ -208,45 +192,44 @@ extern "C" const char *rt_comm_last_error(rt_comm *c) { return c ? c->err.c_str(
 extern "C" rt_status rt_comm_gather_moments(rt_comm *c, rt_solver *s, double *phi, double *F, double *phi_plus) {
   if (!c || !s) return cfail(c, RT_ERR_ARG, "rt_comm_gather_moments: NULL argument");
   HC_TRY(c, hipSetDevice(c->device));
-  std::vector<Shard> sh;
+  std::vector<rt_shard> sh;
   int mode = 0;
   if (rt_status st = all_shards(c, s, sh, mode)) return st;
-  const Shard &me = sh[c->rank];
-  const int N = me.N, G = me.G, Gm = max_groups(sh);
+  const int n = c->nranks;
+  const rt_shard &me = sh[c->rank];
+  const int N = me.N, Gl = layout::groups_of(me), Gm = layout::max_groups(sh.data(), n);
   const size_t blk = static_cast<size_t>(N) * Gm;  // one field of one rank, padded
   hipStream_t st = static_cast<hipStream_t>(rt_stream(s));
   Scratch buf;
   buf.st = st;
-  HC_TRY(c, hipMalloc(&buf.p, sizeof(double) * 3 * blk * (mode == 0 ? c->nranks + 1 : 1)));
+  HC_TRY(c, hipMalloc(&buf.p, sizeof(double) * 3 * blk * (mode == 0 ? n + 1 : 1)));
   double *d = static_cast<double *>(buf.p);
-  if (me.Gl == Gm) {
+  if (Gl == Gm) {  // the local arrays are the wire block (layout::moments_pack is one contiguous copy)
     RT_TRY(c, s, rt_get_moments_device(s, d, d + blk, d + 2 * blk));
   } else {  // a short shard: its (N, Gl) blocks into the padded (N, Gm) rows
     Scratch tmp;
     tmp.st = st;
-    const size_t gn = static_cast<size_t>(N) * me.Gl;
+    const size_t gn = static_cast<size_t>(N) * Gl;
     HC_TRY(c, hipMalloc(&tmp.p, sizeof(double) * 3 * gn));
     double *t = static_cast<double *>(tmp.p);
     RT_TRY(c, s, rt_get_moments_device(s, t, t + gn, t + 2 * gn));
     HC_TRY(c, hipMemsetAsync(d, 0, sizeof(double) * 3 * blk, st));
-    for (int k = 0; k < 3; ++k)
-      HC_TRY(c, hipMemcpy2DAsync(d + k * blk, sizeof(double) * Gm, t + k * gn, sizeof(double) * me.Gl,
-                                 sizeof(double) * me.Gl, N, hipMemcpyDeviceToDevice, st));
+    if (rt_status e = run_plan(c, layout::moments_pack(sh.data(), n, c->rank), t, d, hipMemcpyDeviceToDevice, st))
+      return e;
   }
   double *want[3] = {phi, F, phi_plus};
+  const double *gathered = d;
   if (mode == 1) {  // every rank holds partial sums over its directions of all G groups
     NC_TRY(c, ncclAllReduce(d, d, 3 * blk, ncclFloat64, ncclSum, c->nc, st));
-    for (int k = 0; k < 3; ++k)
-      if (want[k]) HC_TRY(c, hipMemcpyAsync(want[k], d + k * blk, sizeof(double) * blk, hipMemcpyDeviceToHost, st));
   } else {
-    double *all = d + 3 * blk;  // [rank][3][N][Gm]
-    NC_TRY(c, ncclAllGather(d, all, 3 * blk, ncclFloat64, c->nc, st));
-    for (int r = 0; r < c->nranks; ++r)
-      for (int k = 0; k < 3; ++k)
-        if (want[k] && sh[r].Gl > 0)
-          HC_TRY(c, hipMemcpy2DAsync(want[k] + sh[r].g_lo, sizeof(double) * G, all + (3 * r + k) * blk,
-                                     sizeof(double) * Gm, sizeof(double) * sh[r].Gl, N, hipMemcpyDeviceToHost, st));
+    NC_TRY(c, ncclAllGather(d, d + 3 * blk, 3 * blk, ncclFloat64, c->nc, st));  // [rank][3][N][Gm]
+    gathered = d + 3 * blk;
   }
+  for (int k = 0; k < 3; ++k)
+    if (want[k])
+      if (rt_status e = run_plan(c, layout::moments_unpack(sh.data(), n, k), gathered, want[k],
+                                 hipMemcpyDeviceToHost, st))
+        return e;
   HC_TRY(c, hipStreamSynchronize(st));
   return RT_OK;
 }
@@ -254,10 +237,10 @@ extern "C" rt_status rt_comm_gather_moments(rt_comm *c, rt_solver *s, double *ph
 extern "C" rt_status rt_comm_gather_group_ends(rt_comm *c, rt_solver *s, double *left, double *right) {
   if (!c || !s) return cfail(c, RT_ERR_ARG, "rt_comm_gather_group_ends: NULL argument");
   HC_TRY(c, hipSetDevice(c->device));
-  std::vector<Shard> sh;
+  std::vector<rt_shard> sh;
   int mode = 0;
   if (rt_status st = all_shards(c, s, sh, mode)) return st;
-  const int Gl = sh[c->rank].Gl;
+  const int Gl = layout::groups_of(sh[c->rank]);
   std::vector<double> l(Gl), r(Gl);
   RT_TRY(c, s, rt_get_group_ends(s, l.data(), r.data()));
   return combine_vectors(c, s, sh, mode, {l.data(), r.data()}, {left, right});
@@ -267,10 +250,10 @@ extern "C" rt_status rt_comm_gather_balance(rt_comm *c, rt_solver *s, double *ba
                                             double *sinks) {
   if (!c || !s) return cfail(c, RT_ERR_ARG, "rt_comm_gather_balance: NULL argument");
   HC_TRY(c, hipSetDevice(c->device));
-  std::vector<Shard> sh;
+  std::vector<rt_shard> sh;
   int mode = 0;
   if (rt_status st = all_shards(c, s, sh, mode)) return st;
-  const int G = sh[0].G, Gl = sh[c->rank].Gl;
+  const int G = sh[0].G, Gl = layout::groups_of(sh[c->rank]);
   if (mode == 0) {  // each shard's own terms, exactly as one handle computes them
     std::vector<double> b(Gl), so(Gl), si(Gl);
     RT_TRY(c, s, rt_get_balance_terms(s, b.data(), so.data(), si.data()));
@@ -293,18 +276,18 @@ extern "C" rt_status rt_comm_gather_psi(rt_comm *c, rt_solver *s, int root, doub
   if (!c || !s || root < 0 || root >= c->nranks || (c->rank == root && !psi))
     return cfail(c, RT_ERR_ARG, "rt_comm_gather_psi: bad argument");
   HC_TRY(c, hipSetDevice(c->device));
-  std::vector<Shard> sh;
+  std::vector<rt_shard> sh;
   int mode = 0;
   if (rt_status st = all_shards(c, s, sh, mode)) return st;
-  const Shard &me = sh[c->rank];
-  const int N = me.N, G = me.G, M = me.M, H = M / 2;
-  auto Ml = [&](const Shard &a) { return 2 * (a.d_hi - a.d_lo); };  // directions a shard holds
-  auto block = [&](const Shard &a) { return static_cast<size_t>(Ml(a)) * a.Gl * N; };
+  const rt_shard &me = sh[c->rank];
+  auto block = [&](const rt_shard &a) {  // (M_l, Gl, N): i + M_l (g + Gl c)
+    return static_cast<size_t>(layout::dirs_of(a)) * layout::groups_of(a) * a.N;
+  };
   size_t big = 0;
-  for (const Shard &a : sh) big = std::max(big, block(a));
+  for (const rt_shard &a : sh) big = std::max(big, block(a));
   hipStream_t st = static_cast<hipStream_t>(rt_stream(s));
   std::vector<double> mine(block(me));
-  RT_TRY(c, s, rt_get_psi(s, mine.data()));  // (Ml, Gl, N): i + Ml (g + Gl c)
+  RT_TRY(c, s, rt_get_psi(s, mine.data()));
   Scratch buf;
   buf.st = st;
   HC_TRY(c, hipMalloc(&buf.p, sizeof(double) * big * (c->rank == root ? 2 : 1)));
@@ -317,25 +300,12 @@ extern "C" rt_status rt_comm_gather_psi(rt_comm *c, rt_solver *s, int root, doub
   }
   double *rx = d + big;
   for (int r = 0; r < c->nranks; ++r) {
-    const Shard &a = sh[r];
     const double *src = d;
     if (r != root) {  // one rank's block at a time through the receive buffer
-      NC_TRY(c, ncclRecv(rx, block(a), ncclFloat64, r, c->nc, st));
+      NC_TRY(c, ncclRecv(rx, block(sh[r]), ncclFloat64, r, c->nc, st));
       src = rx;
     }
-    const int ml = Ml(a), n = a.d_hi - a.d_lo;
-    // rows (g, c) of the shard's block hold its directions i' in [H - d_hi, H - d_lo) then
-    // [H + d_lo, H + d_hi): two strided copies into the (M, G, N) rows i + M (g + G c)
-    const size_t rows = static_cast<size_t>(a.Gl) * N;
-    if (mode == 0) {  // all directions, groups [g_lo, g_hi): one contiguous run of M Gl per cell
-      HC_TRY(c, hipMemcpy2DAsync(psi + static_cast<size_t>(M) * a.g_lo, sizeof(double) * M * G, src,
-                                 sizeof(double) * M * a.Gl, sizeof(double) * M * a.Gl, N, hipMemcpyDeviceToHost, st));
-    } else {
-      HC_TRY(c, hipMemcpy2DAsync(psi + (H - a.d_hi), sizeof(double) * M, src, sizeof(double) * ml, sizeof(double) * n,
-                                 rows, hipMemcpyDeviceToHost, st));
-      HC_TRY(c, hipMemcpy2DAsync(psi + (H + a.d_lo), sizeof(double) * M, src + n, sizeof(double) * ml,
-                                 sizeof(double) * n, rows, hipMemcpyDeviceToHost, st));
-    }
+    if (rt_status e = run_plan(c, layout::psi_place(sh[r]), src, psi, hipMemcpyDeviceToHost, st)) return e;
     HC_TRY(c, hipStreamSynchronize(st));  // rx is reused by the next rank
   }
   return RT_OK;
@@ -344,18 +314,17 @@ extern "C" rt_status rt_comm_gather_psi(rt_comm *c, rt_solver *s, int root, doub
 extern "C" rt_status rt_comm_gather_psi_source(rt_comm *c, rt_solver *s, double *out) {
   if (!c || !s || !out) return cfail(c, RT_ERR_ARG, "rt_comm_gather_psi_source: bad argument");
   HC_TRY(c, hipSetDevice(c->device));
-  std::vector<Shard> sh;
+  std::vector<rt_shard> sh;
   int mode = 0;
   if (rt_status st = all_shards(c, s, sh, mode)) return st;
-  const Shard &me = sh[c->rank];
-  const int G = me.G, M = me.M, H = M / 2;
+  const int G = sh[0].G;
   if (mode == 0) {  // every group shard holds all M x G rows (the table covers all groups)
     RT_TRY(c, s, rt_get_psi_source(s, out));
     return RT_OK;
   }
   // direction shards: rows m of the shard's (M_l, G) table, ascending mu, into the (M, G) table
   int Hm = 0;
-  for (const Shard &a : sh) Hm = std::max(Hm, a.d_hi - a.d_lo);
+  for (const rt_shard &a : sh) Hm = std::max(Hm, a.d_hi - a.d_lo);
   const size_t cnt = static_cast<size_t>(2) * Hm * G;
   std::vector<double> mine(cnt, 0.0);
   RT_TRY(c, s, rt_get_psi_source(s, mine.data()));
@@ -369,15 +338,7 @@ extern "C" rt_status rt_comm_gather_psi_source(rt_comm *c, rt_solver *s, double 
   std::vector<double> all(cnt * c->nranks);
   HC_TRY(c, hipMemcpyAsync(all.data(), d + cnt, sizeof(double) * all.size(), hipMemcpyDeviceToHost, st));
   HC_TRY(c, hipStreamSynchronize(st));
-  for (int r = 0; r < c->nranks; ++r) {
-    const Shard &a = sh[r];
-    const int n = a.d_hi - a.d_lo;
-    const double *src = all.data() + cnt * r;
-    for (int k = 0; k < 2 * n; ++k) {  // shard row k -> global direction (see rt_create_direction_shard)
-      const int i = k < n ? H - a.d_hi + k : H + a.d_lo + (k - n);
-      std::copy(src + static_cast<size_t>(k) * G, src + static_cast<size_t>(k + 1) * G, out + static_cast<size_t>(i) * G);
-    }
-  }
+  for (int r = 0; r < c->nranks; ++r) layout::apply(layout::psi_source_place(sh[r]), all.data() + cnt * r, out);
   return RT_OK;
 }
 
@@ -410,6 +371,18 @@ extern "C" rt_status rt_comm_material_step(rt_comm *c, rt_solver *s, int nsteps)
     RT_TRY(c, s, rt_material_sweep(s, c->q));
     NC_TRY(c, ncclAllReduce(c->q, c->q, N, ncclFloat64, ncclSum, c->nc, st));
     RT_TRY(c, s, rt_material_update(s, c->q));
+  }
+  return RT_OK;
+}
+
+extern "C" rt_status rt_comm_version(int *version, char *path, size_t path_len) {
+  if (!version) return cfail(nullptr, RT_ERR_ARG, "rt_comm_version: NULL version");
+  NC_TRY(nullptr, ncclGetVersion(version));
+  if (path && path_len) {
+    Dl_info info{};
+    const char *f = dladdr(reinterpret_cast<void *>(&ncclGetVersion), &info) && info.dli_fname ? info.dli_fname : "";
+    std::strncpy(path, f, path_len - 1);
+    path[path_len - 1] = '\0';
   }
   return RT_OK;
 }

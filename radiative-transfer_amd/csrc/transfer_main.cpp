@@ -15,6 +15,9 @@
 #include <sys/wait.h>
 #include <unistd.h>
 
+#include <cerrno>
+#include <csignal>
+
 #include <cstdlib>
 #include <iostream>
 #include <string>
@@ -52,12 +55,19 @@ bool read_all(int fd, char *p, size_t n) {
   return true;
 }
 
-// Parent: fork the ranks and wait for them (returns main's exit code: 0 when every rank
+// Parent: fork the ranks and reap them (returns main's exit code: 0 when every rank
 // succeeded).  Child: returns -1 with *rs filled in.  All pipes exist before the first
 // fork; rank 0 makes the communicator id and writes it into the pipe of every rank > 0.
+// A rank that fails after the hand-off (no device, a bad .prm, ...) would leave the others
+// blocked in ncclCommInitRank or a collective: the parent reaps whichever rank ends first
+// and, on the first failure, stops the rest (SIGTERM, SIGKILL after a grace period).
+// Fault injection (tests): RTSN_FAULT_STALL_RANK=r makes rank r block right after the fork,
+// standing in for a rank stuck in a collective.
 int spawn_ranks(int n, RankSetup *rs) {
   const char *base = std::getenv("RTSN_DEVICE_BASE");
   const int dev0 = base ? std::atoi(base) : 0;
+  const char *stall = std::getenv("RTSN_FAULT_STALL_RANK");
+  const int stall_rank = stall ? std::atoi(stall) : -1;
   std::vector<int> rd(n, -1), wr(n, -1);
   for (int r = 1; r < n; ++r) {
     int fds[2];
@@ -69,7 +79,11 @@ int spawn_ranks(int n, RankSetup *rs) {
   std::vector<pid_t> kids;
   for (int r = 0; r < n; ++r) {
     const pid_t pid = fork();
-    if (pid < 0) return 1;
+    if (pid < 0) {
+      for (pid_t k : kids) kill(k, SIGKILL);
+      for (pid_t k : kids) waitpid(k, nullptr, 0);
+      return 1;
+    }
     if (pid > 0) {
       kids.push_back(pid);
       continue;
@@ -81,6 +95,8 @@ int spawn_ranks(int n, RankSetup *rs) {
       if (q != r) close(rd[q]);
       if (r != 0) close(wr[q]);
     }
+    if (r == stall_rank)
+      for (;;) pause();
     if (r == 0) {
       const bool ok = rt_comm_unique_id(rs->comm_id) == RT_OK;
       if (!ok) std::cerr << "rt_comm_unique_id: " << rt_comm_last_error(nullptr) << std::endl;
@@ -101,14 +117,44 @@ int spawn_ranks(int n, RankSetup *rs) {
     close(wr[q]);
   }
   int code = 0;
-  for (pid_t k : kids) {
+  size_t live = kids.size();
+  auto forget = [&](pid_t k) {
+    for (pid_t &x : kids)
+      if (x == k) x = 0;
+  };
+  while (live) {
     int st = 0;
-    if (waitpid(k, &st, 0) < 0) {
-      code = 1;
-    } else if (!WIFEXITED(st) || WEXITSTATUS(st)) {
-      const int c = WIFEXITED(st) ? WEXITSTATUS(st) : 128 + WTERMSIG(st);
-      if (!code) code = c;
+    const pid_t k = waitpid(-1, &st, 0);
+    if (k < 0) {
+      if (errno == EINTR) continue;
+      code = code ? code : 1;
+      break;
     }
+    bool known = false;
+    for (pid_t x : kids) known = known || x == k;
+    if (!known) continue;
+    forget(k);
+    --live;
+    if (WIFEXITED(st) && WEXITSTATUS(st) == 0) continue;
+    if (!code) code = WIFEXITED(st) ? WEXITSTATUS(st) : 128 + WTERMSIG(st);
+    // first failure: the remaining ranks cannot complete their collectives
+    for (pid_t x : kids)
+      if (x) kill(x, SIGTERM);
+    for (int tick = 0; tick < 50 && live; ++tick) {  // 5 s grace, then SIGKILL
+      for (pid_t &x : kids)
+        if (x && waitpid(x, nullptr, WNOHANG) == x) {
+          x = 0;
+          --live;
+        }
+      if (live) usleep(100000);
+    }
+    for (pid_t &x : kids)
+      if (x) {
+        kill(x, SIGKILL);
+        waitpid(x, nullptr, 0);
+        x = 0;
+        --live;
+      }
   }
   return code;
 }

@@ -8,11 +8,13 @@ fallback in this package.
 """
 from .api import (  # noqa: F401
     Comm,
+    Layout,
     LIB_PATH,
     ParameterHandler,
     RtError,
     Solver,
     build,
+    comm_version,
     exported_symbols,
     lib,
     params_default,

@@ -43,6 +43,10 @@ class rt_params(C.Structure):
     ]
 
 
+class rt_shard(C.Structure):
+    _fields_ = [(f, C.c_int) for f in ("G", "M", "g_lo", "g_hi", "d_lo", "d_hi", "N", "reserved")]
+
+
 _SCALARS = [f for f, _ in rt_params._fields_ if f not in ("psi_source", "group_bounds", "group_kappa")]
 
 
@@ -116,6 +120,8 @@ def lib():
         L.rt_get_time_block.argtypes = [vp, C.POINTER(C.c_int)]
         L.rt_plan_time_block.argtypes = [C.c_int, C.c_longlong, C.POINTER(C.c_int)]
         L.rt_get_level_waves.argtypes = [vp, C.POINTER(C.c_int)]
+        L.rt_set_wavefront.argtypes = [vp, C.c_int]
+        L.rt_get_wavefront.argtypes = [vp, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)]
         L.rt_material_enable.argtypes = [vp, C.c_double, dp]
         L.rt_material_sweep.argtypes = [vp, vp]
         L.rt_material_update.argtypes = [vp, vp]
@@ -137,6 +143,15 @@ def lib():
         L.rt_comm_gather_psi_source.argtypes = [vp, vp, dp]
         L.rt_comm_allreduce_absorption.argtypes = [vp, vp, vp]
         L.rt_comm_material_step.argtypes = [vp, vp, C.c_int]
+        L.rt_comm_version.argtypes = [C.POINTER(C.c_int), C.c_char_p, C.c_size_t]
+        sp = C.POINTER(rt_shard)
+        L.rt_layout_mode.argtypes = [sp, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int)]
+        L.rt_layout_pack_moments.argtypes = [sp, C.c_int, C.c_int, dp, dp]
+        L.rt_layout_unpack_moments.argtypes = [sp, C.c_int, dp, dp, dp, dp]
+        L.rt_layout_pack_vectors.argtypes = [sp, C.c_int, C.c_int, C.c_int, C.POINTER(dp), dp]
+        L.rt_layout_unpack_vectors.argtypes = [sp, C.c_int, C.c_int, dp, C.POINTER(dp)]
+        L.rt_layout_place_psi.argtypes = [sp, dp, dp]
+        L.rt_layout_place_psi_source.argtypes = [sp, dp, dp]
         L.rt_comm_last_error.argtypes = [vp]
         L.rt_comm_last_error.restype = C.c_char_p
         L.rt_status_string.argtypes = [C.c_int]
@@ -529,6 +544,24 @@ class Solver:
     def pipeline(self, mode):
         _check(lib().rt_set_pipeline(self._h, int(mode)), "rt_set_pipeline", self._h)
 
+    @property
+    def wavefront(self) -> int:
+        """Short lines in one launch per advance, lanes over cells (rt_set_wavefront): 0 off,
+        1 auto (the line fits and the caller chose neither time block nor schedule), 2 on."""
+        v = C.c_int()
+        _check(lib().rt_get_wavefront(self._h, C.byref(v), None, None), "rt_get_wavefront", self._h)
+        return v.value
+
+    @wavefront.setter
+    def wavefront(self, mode):
+        _check(lib().rt_set_wavefront(self._h, int(mode)), "rt_set_wavefront", self._h)
+
+    def wavefront_state(self) -> dict:
+        """{"mode", "active" (the next advance takes the wavefront), "cells_per_lane" (0: too long)}."""
+        m, a, c = C.c_int(), C.c_int(), C.c_int()
+        _check(lib().rt_get_wavefront(self._h, C.byref(m), C.byref(a), C.byref(c)), "rt_get_wavefront", self._h)
+        return {"mode": m.value, "active": bool(a.value), "cells_per_lane": c.value}
+
     def pipeline_state(self) -> dict:
         """{"lag_steps", "queued_steps", "pending"} (rt_pipeline_state)."""
         lag, q, pend = C.c_longlong(), C.c_int(), C.c_int()
@@ -645,3 +678,82 @@ class Comm:
     def material_step(self, solver: "Solver", nsteps: int = 1):
         """nsteps coupled steps with one all-reduce of q(x) per step on the handle's stream."""
         self._check(lib().rt_comm_material_step(self._h, solver._h, int(nsteps)), "rt_comm_material_step")
+
+
+def comm_version() -> dict:
+    """rt_comm_version: the RCCL the library's collectives run on -- ncclGetVersion's code
+    and version string, and the librccl file the process resolved it from."""
+    v = C.c_int()
+    path = C.create_string_buffer(4096)
+    _check(lib().rt_comm_version(C.byref(v), path, len(path)), "rt_comm_version")
+    code = v.value
+    major, rest = divmod(code, 10000)
+    minor, patch = divmod(rest, 100)
+    return {"code": code, "version": f"{major}.{minor}.{patch}", "path": path.value.decode(errors="replace")}
+
+
+class Layout:
+    """Host-side layout of the gathered shard blocks (include/rtsn.h rt_layout_*): the copy
+    plans the rt_comm gathers run on the device, on numpy arrays.  shards: one dict (or
+    tuple) per rank with G, M, g_lo, g_hi, d_lo, d_hi, N."""
+
+    def __init__(self, shards):
+        n = len(shards)
+        self.n = n
+        arr = (rt_shard * n)()
+        for r, sh in enumerate(shards):
+            if not isinstance(sh, dict):
+                sh = dict(zip(("G", "M", "g_lo", "g_hi", "d_lo", "d_hi", "N"), sh))
+            for f in ("G", "M", "g_lo", "g_hi", "d_lo", "d_hi", "N"):
+                setattr(arr[r], f, int(sh[f]))
+            arr[r].reserved = 0
+        self._sh = arr
+        mode, gm = C.c_int(), C.c_int()
+        st = lib().rt_layout_mode(arr, n, C.byref(mode), C.byref(gm))
+        self.mode, self.max_groups = mode.value, gm.value
+        _check(st, "rt_layout_mode")
+        self.G, self.M, self.N = arr[0].G, arr[0].M, arr[0].N
+
+    def shard(self, r: int) -> rt_shard:
+        return self._sh[r]
+
+    def pack_moments(self, rank: int, phi, F, phi_plus) -> np.ndarray:
+        """rank's (N, G_local) fields (g fastest) -> its wire block (3, N, Gmax)."""
+        local = np.ascontiguousarray(np.stack([phi, F, phi_plus]), dtype=np.float64)
+        block = np.empty((3, self.N, self.max_groups))
+        _check(lib().rt_layout_pack_moments(self._sh, self.n, rank, _dp(local), _dp(block)), "rt_layout_pack_moments")
+        return block
+
+    def unpack_moments(self, gathered: np.ndarray):
+        """gathered wire blocks -> phi, F, phi_plus as (N, G) arrays (g fastest)."""
+        g = np.ascontiguousarray(gathered, dtype=np.float64)
+        out = [np.empty((self.N, self.G)) for _ in range(3)]
+        _check(lib().rt_layout_unpack_moments(self._sh, self.n, _dp(g), *[_dp(a) for a in out]),
+               "rt_layout_unpack_moments")
+        return out
+
+    def pack_vectors(self, rank: int, vecs) -> np.ndarray:
+        vecs = [np.ascontiguousarray(v, dtype=np.float64) for v in vecs]
+        ptrs = (C.POINTER(C.c_double) * len(vecs))(*[_dp(v) for v in vecs])
+        block = np.empty((len(vecs), self.max_groups))
+        _check(lib().rt_layout_pack_vectors(self._sh, self.n, rank, len(vecs), ptrs, _dp(block)),
+               "rt_layout_pack_vectors")
+        return block
+
+    def unpack_vectors(self, k: int, gathered: np.ndarray):
+        g = np.ascontiguousarray(gathered, dtype=np.float64)
+        out = [np.empty(self.G) for _ in range(k)]
+        ptrs = (C.POINTER(C.c_double) * k)(*[_dp(v) for v in out])
+        _check(lib().rt_layout_unpack_vectors(self._sh, self.n, k, _dp(g), ptrs), "rt_layout_unpack_vectors")
+        return out
+
+    def place_psi(self, rank: int, block: np.ndarray, psi_flat: np.ndarray):
+        """rank's psi (as rt_get_psi's flat ColMajor (M_l, G_l, N) buffer) into psi_flat
+        (the (M, G, N) ColMajor buffer, i + M (g + G c))."""
+        b = np.ascontiguousarray(block, dtype=np.float64)
+        _check(lib().rt_layout_place_psi(C.byref(self._sh[rank]), _dp(b), _dp(psi_flat)), "rt_layout_place_psi")
+
+    def place_psi_source(self, rank: int, rows: np.ndarray, table: np.ndarray):
+        r = np.ascontiguousarray(rows, dtype=np.float64)
+        _check(lib().rt_layout_place_psi_source(C.byref(self._sh[rank]), _dp(r), _dp(table)),
+               "rt_layout_place_psi_source")

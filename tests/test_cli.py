@@ -341,3 +341,37 @@ def test_transfer_ranks_fail_cleanly_without_gpu(tmp_path):
                        timeout=60, env=dict(os.environ, RTSN_RANKS="3"))
     assert r.returncode != 0
     assert "rt_comm_unique_id" in r.stderr
+
+
+def test_transfer_ranks_stop_survivors_on_failure(tmp_path):
+    """A rank that fails after the fork must not leave the others blocked (in
+    ncclCommInitRank or a collective) with the parent waiting on them: the parent reaps
+    whichever rank ends first and stops the rest.  RTSN_FAULT_STALL_RANK=2 makes rank 2
+    block right after the fork; rank 0 fails (no GPU here, so no communicator id) and the
+    run must still end, non-zero, well within the timeout."""
+    import time
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("the failure path needs a host without a GPU")
+    run = _run_tree(tmp_path)
+    t0 = time.perf_counter()
+    r = subprocess.run([str(_bin("transfer")), "../prm/llnl_slab_test.prm"], cwd=run, capture_output=True, text=True,
+                       timeout=60, env=dict(os.environ, RTSN_RANKS="3", RTSN_FAULT_STALL_RANK="2"))
+    assert r.returncode != 0
+    assert time.perf_counter() - t0 < 30
+
+
+@pytest.mark.gpu
+def test_transfer_ranks_missing_device_fails_cleanly(tmp_path):
+    """RTSN_RANKS=2 on a one-GPU box: rank 1's device (RTSN_DEVICE_BASE + 1) does not exist,
+    so its rt_create_from_params fails after the id hand-off while rank 0 waits in
+    ncclCommInitRank for it.  The parent stops rank 0 and returns the failure instead of
+    hanging."""
+    import torch
+    if torch.cuda.device_count() != 1:
+        pytest.skip("needs exactly one visible GPU")
+    run = _run_tree(tmp_path)
+    r = subprocess.run([str(_bin("transfer")), "../prm/llnl_slab_test.prm"], cwd=run, capture_output=True, text=True,
+                       timeout=90, env=dict(os.environ, RTSN_RANKS="2", RTSN_QUIET="1"))
+    assert r.returncode != 0
+    assert "rt_create_from_params" in r.stderr

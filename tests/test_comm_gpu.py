@@ -82,3 +82,15 @@ def test_shards_must_tile(rtsn_mod, oracle_mod, comm):
         with pytest.raises(rtsn_mod.RtError) as e:
             comm.gather_moments(s)
         assert e.value.status == 3
+
+
+def test_comm_version_is_the_loaded_rccl(rtsn_mod, comm):
+    """rt_comm_version names the RCCL the communicator runs on: the librccl.so.1 this
+    process resolved (torch imports first, so its bundled RCCL -- the one torch.distributed
+    uses -- serves librtsn too), with a 2.x version code."""
+    import os
+    v = rtsn_mod.comm_version()
+    assert v["code"] >= 20000 and v["version"].startswith("2.")
+    assert os.path.exists(v["path"]) and "rccl" in os.path.basename(v["path"])
+    loaded = [l.split()[-1] for l in open("/proc/self/maps") if "librccl" in l]
+    assert os.path.realpath(v["path"]) in {os.path.realpath(x) for x in loaded}

@@ -646,28 +646,39 @@ def test_direction_shards(rtsn_mod, oracle_mod, ts, bc_left, bc_right):
         assert np.allclose(a, b, rtol=1e-13, atol=0.0), (a, b)
 
 
-def test_full_size_sl_properties(rtsn_mod):
+@pytest.mark.parametrize("shard_tb", [16, 20])
+def test_full_size_sl_properties(rtsn_mod, shard_tb):
     """BASELINE.json's headline workload at its full size -- SL, N = 1e6 cells x S64 x 128
     groups, BDF2 -- through size-independent properties (the oracle covers one of its
-    groups at full line length, test_full_length_sl_line): 48 steps pipelined at T = 16
-    (fill, 3 passes, drain) with dt = 1e-7 so the state stays finite, then
-    (1) a second run is bitwise identical (determinism), (2) the two 64-group shards an
-    N = 2 run would own give the full run's groups bitwise (groups are independent),
-    (3) the aligned schedule (segments corrected across passes, T = 4) agrees to 1e-12
-    per group, (4) every node is finite."""
+    groups at full line length, test_full_length_sl_line, and the timed kernels with several
+    line groups per half, test_timed_kernels_multi_line_group): 80 steps pipelined with
+    dt = 1e-7 so the state stays finite, at every block the bench and rt_solve
+    time -- T = 16 (sweep_block_kernel<3,16,2>), T = 20 (the driver's window:
+    sweep_split_kernel<3,20,2>, two waves per segment), the same T = 20 on one wave
+    (rt_set_level_waves 1: sweep_block_kernel<3,20,2>) and T = 40 (sweep_split_kernel<3,40,4>,
+    rt_solve's block for 1000 steps) -- with the segments re-sized for each kernel.  Then
+    (1) a second run is bitwise identical (determinism), (2) all four blocks give bitwise
+    the same phi, F and phi_plus (the pipelined schedule starts every segment from its
+    upwind neighbour's exact exit state, so the arithmetic per line is independent of T,
+    the segmentation and the level split), (3) the two 64-group shards an N = 2 run would
+    own give the full run's groups bitwise (groups are independent), at block shard_tb,
+    (4) the aligned schedule (segments corrected across passes, T = 4) agrees to 1e-12 per
+    group, (5) every node is finite."""
     import sys
     import torch
     sys.path.insert(0, str(REPO))
     import bench
     p = bench.slab_params(128, "v0")
     p["dt"] = 1e-7
-    N, steps = p["N"], 48
+    N, steps = p["N"], 80
 
-    def run(g_lo=0, g_hi=0, pipe=2):
+    def run(g_lo=0, g_hi=0, pipe=2, tb=16, lw=0, kernel=None):
         with rtsn_mod.Solver(p, g_lo=g_lo, g_hi=g_hi) as s:
             s.pipeline = pipe
-            if pipe == 0:
-                s.time_block = 4
+            s.time_block = tb if pipe else 4
+            if pipe:
+                s.level_waves = lw
+                assert s.level_waves == {16: 1, 20: lw or 2, 40: 4}[tb]
             s.advance(steps)
             s.finish()
             out = [torch.empty(N * s.G, dtype=torch.float64, device="cuda") for _ in range(3)]
@@ -676,13 +687,20 @@ def test_full_size_sl_properties(rtsn_mod):
             assert s.state_finite()
             return [t.view(N, s.G) for t in out]
 
-    full = run()
-    again = run()
+    full = run(tb=shard_tb)
+    again = run(tb=shard_tb)
     for a, b in zip(full, again):
         assert torch.equal(a, b)
     del again
+    for tb, lw in ((16, 0), (20, 0), (20, 1), (40, 0)):
+        if tb == shard_tb and lw == 0:
+            continue
+        other = run(tb=tb, lw=lw)
+        for a, b in zip(other, full):
+            assert torch.equal(a, b), (tb, lw)
+        del other
     for lo, hi in ((0, 64), (64, 128)):
-        part = run(lo, hi)
+        part = run(lo, hi, tb=shard_tb)
         for a, b in zip(part, full):
             assert torch.equal(a, b[:, lo:hi])
         del part
@@ -690,3 +708,115 @@ def test_full_size_sl_properties(rtsn_mod):
     phi, phi_a = full[0], aligned[0]
     err = ((phi_a - phi).abs().amax(dim=0) / phi.abs().amax(dim=0)).max().item()
     assert err <= 1e-12, err
+
+
+# The timed kernels with several 64-line groups per half (verdict r02, item 1): the
+# workgroup -> (half, segment, line group q) decode of sweep_split_kernel (kernels_split.hip
+# split_role: ell = q * 64 + lane) and sweep_block_kernel, reflective (one chain of 2 Sg
+# positions) and not (two chains), with the last line group partly padding.
+MLG_CASES = {
+    # id: (dt, random initial state, bc_left, (g_lo, g_hi), N, oracle snapshots)
+    "q2-vacuum-random": (1e-9, True, 0, (30, 50), 20000, (22, 42, 82)),
+    "q2-reflective-random": (1e-9, True, 2, (30, 50), 20000, (22, 42, 82)),
+    "q2-vacuum-carry": (1e-7, False, 0, (30, 50), 20000, (22, 42)),
+    "q2-reflective-carry": (1e-7, False, 2, (30, 50), 20000, (22, 42)),
+    "q3-reflective-random": (1e-9, True, 2, (20, 60), 8000, (22, 42, 82)),
+}
+
+
+def _mlg_params(oracle_mod, case):
+    dt, _, bc_left, (lo, hi), N, snaps = MLG_CASES[case]
+    p = load(oracle_mod, "llnl_slab_test.prm", N=N, M=8, dt=dt, use_correction=1, V=5.994, bc_left=bc_left,
+             bc_right=0, max_timesteps=max(snaps))
+    p["dx"] = p["X"] / p["N"]
+    p["psi_source"] = np.linspace(0.5, 2.0, p["M"] * p["G"]).reshape(p["M"], p["G"])
+    return p
+
+
+@pytest.fixture(scope="module")
+def mlg_oracle(oracle_mod):
+    """The oracle's state at each snapshot of every MLG case (runs in parallel threads:
+    ctypes releases the GIL); the random initial state (seeded) is returned with it."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    def run(case):
+        dt, rnd, _, (lo, hi), N, snaps = MLG_CASES[case]
+        p = _mlg_params(oracle_mod, case)
+        o = oracle_mod.OracleSolver(p, g_lo=lo, g_hi=hi)
+        o.set_threads(3)
+        o.set_parallel_copies(True)
+        ends = None
+        if rnd:
+            B = o.groups()["B"][lo:hi]
+            rng = np.random.default_rng(SEED + hi + 3 * p["bc_left"])
+            ends = B[None, :, None, None] * rng.uniform(0.5, 1.5, size=(p["M"], hi - lo, N, 2))
+            o.set_ends(ends)
+        out, done = {}, 0
+        for n in snaps:
+            o.run_substeps(4 * done, 4 * (n - done))
+            done = n
+            mu, wt = o.quad()
+            out[n] = {"psi": o.psi(), "ends": o.ends(), "moments": o.moments(), "group_ends": o.group_ends(),
+                      "mu": mu, "wt": wt, "de": o.groups()["de_ave"][lo:hi]}
+        return p, ends, out
+
+    with ThreadPoolExecutor(len(MLG_CASES)) as ex:
+        return dict(zip(MLG_CASES, ex.map(run, MLG_CASES)))
+
+
+@pytest.mark.parametrize("case", list(MLG_CASES))
+@pytest.mark.parametrize("tb,steps", [(20, 22), (20, 42), (40, 42), (40, 82)])
+def test_timed_kernels_multi_line_group(rtsn_mod, mlg_oracle, case, tb, steps):
+    """sweep_split_kernel<3,20,2> (the driver's T = 20 pass) and <3,40,4> (rt_solve's block for
+    1000-step runs), with their 4-wave fill and drain launches, on M = 8 lines of 20 or 40
+    groups: 80 or 160 lines per half, i.e. Q = 2 or 3 line groups of 64 per half, the last
+    one partly padding; hundreds of segments per line; T + 2 and 2 T + 2 steps (fill, run,
+    drain, then a 2-step aligned remainder).  psi, the node array, phi, phi_plus and F per
+    group to 1e-10 of the group's scale, and the group ends (relative at dt = 1e-9; against
+    the group's node scale at dt = 1e-7, where the reference's BDF2 grows the interior,
+    test_headline_kernel_full_length).  At T = 20 the one-wave pass (rt_set_level_waves 1,
+    sweep_block_kernel<3,20,2>) gives bitwise the same node array over 2 T steps."""
+    dt, rnd, bc_left, (lo, hi), N, snaps = MLG_CASES[case]
+    if steps not in snaps:
+        pytest.skip("no oracle snapshot at this length for this case")
+    p, ends0, ref_all = mlg_oracle[case]
+    ref = ref_all[steps]
+    rp = to_rt(p)
+    with rtsn_mod.Solver(rp, g_lo=lo, g_hi=hi) as gpu:
+        gpu.pipeline = 2
+        gpu.time_block = tb
+        assert gpu.level_waves == (2 if tb == 20 else 4)
+        wg, segs = gpu.sweep_geometry()
+        assert segs >= 100
+        if ends0 is not None:
+            gpu.set_ends(ends0)
+        gpu.advance(steps)
+        psi, ends = gpu.psi(), gpu.ends()
+        phi_g, F_g, pp_g = gpu.moments()
+        l_g, r_g = gpu.compute_group_ends()
+    err = {"psi": per_group_rel(psi, ref["psi"], 1), "node array": per_group_rel(ends, ref["ends"], 1)}
+    phi_o, F_o, pp_o = ref["moments"]
+    err["phi"] = per_group_rel(phi_g, phi_o, 0)
+    err["phi_plus"] = per_group_rel(pp_g, pp_o, 0)
+    err["F"] = flux_rel(F_g, F_o, ref["psi"], ref["mu"], ref["wt"])
+    l_o, r_o = ref["group_ends"]
+    if dt < 1e-8:
+        scale_l, scale_r = np.abs(l_o), np.abs(r_o)
+    else:
+        node_scale = np.abs(ref["ends"]).max(axis=(0, 2, 3)) * (p["M"] // 2) / (ref["de"] * 299.792458)
+        scale_l = scale_r = node_scale
+    err["left_ends"] = float(np.max(np.abs(l_g - l_o) / scale_l))
+    err["right_ends"] = float(np.max(np.abs(r_g - r_o) / scale_r))
+    assert max(err.values()) <= TOL, err
+    if tb == 20 and steps == 42:  # 2 T steps (no remainder): one wave vs two, bitwise
+        out = []
+        for lw in (1, 2):
+            with rtsn_mod.Solver(rp, g_lo=lo, g_hi=hi) as gpu:
+                gpu.pipeline = 2
+                gpu.time_block = 20
+                gpu.level_waves = lw
+                if ends0 is not None:
+                    gpu.set_ends(ends0)
+                gpu.advance(40)
+                out.append(gpu.ends())
+        assert np.array_equal(out[0], out[1])

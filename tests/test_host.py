@@ -202,3 +202,42 @@ def test_plan_time_block(rtsn_mod):
     assert plan(1, 1000) == 16 and plan(2, 1000) == 16  # BE / CN keep the default
     with pytest.raises(rtsn_mod.RtError):
         plan(4, 10)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["llnl_slab_test.prm", "single_group.prm", "multi_group_equilibrium.prm"])
+def test_c_client_solves_against_oracle(oracle_mod, tmp_path, name):
+    """The boundary from C, on the GPU: tests/c_abi/abi_solve.c (C99, links librtsn.so only)
+    runs rt_create(.prm) + rt_solve and reads psi, phi, F, phi_plus, the group ends,
+    balance and e_ave through the host getters in the reference's ColMajor layouts; every
+    array against the oracle (the reference's algorithm) per group to 1e-10, F against its
+    summands' scale, e_ave exactly."""
+    import subprocess
+    from parity import flux_rel, per_group_rel
+    exe = tmp_path / "abi_solve"
+    subprocess.run(["gcc", "-std=c99", "-Wall", "-Wextra", "-Werror", "-pedantic", f"-I{REPO / 'include'}",
+                    str(REPO / "tests" / "c_abi" / "abi_solve.c"), "-o", str(exe), f"-L{LIB.parent}", "-lrtsn",
+                    f"-Wl,-rpath,{LIB.parent}"], check=True)
+    out = tmp_path / "out.bin"
+    prm = REPO / "tests" / "golden" / "prm"
+    r = subprocess.run([str(exe), str(prm / name), str(prm) + "/", str(out)], capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, (r.returncode, r.stdout, r.stderr)
+    o = oracle_mod.OracleSolver(oracle_mod.parse_prm(prm / name, table_dir=prm))
+    o.solve()
+    M, G, N = (int(x.split("=")[1]) for x in r.stdout.split())
+    a = np.fromfile(out)
+    MGN, GN = M * G * N, G * N
+    psi = a[:MGN].reshape(N, G, M).transpose(2, 1, 0)  # ColMajor (M, G, N)
+    phi, F, pp = (a[MGN + k * GN:MGN + (k + 1) * GN].reshape(N, G).T for k in range(3))
+    rest = a[MGN + 3 * GN:]
+    left, right, bal, e_ave = (rest[k * G:(k + 1) * G] for k in range(4))
+    mu, wt = o.quad()
+    phi_o, F_o, pp_o = o.moments()
+    assert per_group_rel(psi, o.psi(), 1) <= 1e-10
+    assert per_group_rel(phi, phi_o, 0) <= 1e-10 and per_group_rel(pp, pp_o, 0) <= 1e-10
+    assert flux_rel(F, F_o, o.psi(), mu, wt) <= 1e-10
+    l_o, r_o = o.group_ends()
+    assert np.allclose(left, l_o, rtol=1e-10, atol=0) and np.allclose(right, r_o, rtol=1e-10, atol=0)
+    assert np.allclose(bal, o.balance(), rtol=1e-9, atol=1e-12)
+    assert np.array_equal(e_ave, o.groups()["e_ave"])

@@ -1,0 +1,156 @@
+"""The multi-rank assembly of the RCCL gathers, on the CPU (verdict r02, item 3).
+
+rtsn_comm.hip moves every rank's block through RCCL and then places it into the
+reference's result arrays (main.cc:88-133: psi (M, G, N), phi / F / phi_plus (G, N),
+psi_source (M x G), per-group vectors) with copy plans built by host code
+(csrc/comm_layout.cpp) -- the same plans the C ABI's rt_layout_* functions run on host
+memory.  Here they run through the ABI at world sizes 2, 3 and 8 on ragged group shards
+(124 groups over 8, and the rt::Solver split), an empty shard, and direction-pair shards
+with uneven pair counts, with each rank's block cut from ONE oracle run of the whole
+configuration: the assembled arrays must equal that run's arrays bitwise (the layouts
+only copy; where direction shards sum -- RCCL's all-reduce -- the test sums the blocks
+in rank order and the placement of that sum must be exact).
+"""
+import numpy as np
+import pytest
+
+from conftest import PRM_DIR
+from parity import flux_rel, per_group_rel
+
+N_CELLS = 37
+
+
+@pytest.fixture(scope="module")
+def full(oracle_mod):
+    """One oracle run of llnl_slab_test's 124 groups (M = 8, or M = 16 for 8 direction
+    shards) with a reflective left boundary and a psi_source table, a few BDF2 steps."""
+    out = {}
+    for M in (8, 16):
+        p = oracle_mod.parse_prm(PRM_DIR / "llnl_slab_test.prm", table_dir=PRM_DIR)
+        p.update(N=N_CELLS, M=M, max_timesteps=3, bc_left=2, bc_right=1, dt=1e-6)
+        p["dx"] = p["X"] / p["N"]
+        p["psi_source"] = np.linspace(0.5, 2.0, M * p["G"]).reshape(M, p["G"])
+        o = oracle_mod.OracleSolver(p)
+        o.solve()
+        mu, wt = o.quad()
+        out[M] = {"p": p, "psi": o.psi(), "moments": o.moments(), "ends": o.group_ends(), "balance": o.balance(),
+                  "psi_source": o.psi_source(), "mu": mu, "wt": wt}
+    return out
+
+
+def _group_shards(G, n, kind):
+    if kind == "solver":  # rt::Solver(..., Ranks): groups [r G / n, (r + 1) G / n)
+        return [(r * G // n, (r + 1) * G // n) for r in range(n)]
+    if kind == "ceil":  # bench.shard: ceil(G / n) per rank, the last ones short
+        per = -(-G // n)
+        return [(min(G, r * per), min(G, (r + 1) * per)) for r in range(n)]
+    raise ValueError(kind)
+
+
+def _flat_psi(psi):
+    """(M, G, N) array -> rt_get_psi's flat ColMajor buffer (i + M (g + G c))."""
+    return np.ascontiguousarray(np.asarray(psi).transpose(2, 1, 0)).ravel()
+
+
+GROUP_LAYOUTS = [(2, "solver"), (3, "solver"), (8, "solver"), (8, "ceil"), (3, "empty")]
+
+
+@pytest.mark.parametrize("n,kind", GROUP_LAYOUTS)
+def test_group_shard_assembly(rtsn_mod, full, n, kind):
+    f = full[8]
+    M, G, N = 8, f["p"]["G"], N_CELLS
+    H = M // 2
+    ranges = [(0, 60), (60, 60), (60, G)] if kind == "empty" else _group_shards(G, n, kind)
+    shards = [dict(G=G, M=M, g_lo=lo, g_hi=hi, d_lo=0, d_hi=H, N=N) for lo, hi in ranges]
+    lay = rtsn_mod.Layout(shards)
+    assert lay.mode == 0 and lay.max_groups == max(hi - lo for lo, hi in ranges)
+    phi, F, pp = (np.asarray(a) for a in f["moments"])  # (G, N)
+    # moments: each rank packs its (N, Gl) columns, the all-gather stacks the blocks
+    blocks = [lay.pack_moments(r, phi[lo:hi].T, F[lo:hi].T, pp[lo:hi].T) for r, (lo, hi) in enumerate(ranges)]
+    for b, (lo, hi) in zip(blocks, ranges):  # padding is zero
+        assert not b[:, :, hi - lo:].any()
+    got = lay.unpack_moments(np.stack(blocks))
+    for a, want in zip(got, (phi, F, pp)):
+        assert np.array_equal(a, want.T)
+    # per-group vectors: group ends and balance
+    left, right = f["ends"]
+    vecs = (left, right, f["balance"])
+    vb = [lay.pack_vectors(r, [v[lo:hi] for v in vecs]) for r, (lo, hi) in enumerate(ranges)]
+    for a, want in zip(lay.unpack_vectors(3, np.stack(vb)), vecs):
+        assert np.array_equal(a, want)
+    # psi: every rank's (M, Gl, N) block placed into one (M, G, N) buffer
+    psi = np.asarray(f["psi"])
+    out = np.full(M * G * N, np.nan)
+    for r, (lo, hi) in enumerate(ranges):
+        if hi > lo:
+            lay.place_psi(r, _flat_psi(psi[:, lo:hi]), out)
+    assert np.array_equal(out, _flat_psi(psi))
+    # psi_source: a group shard holds all M x G rows
+    table = np.full(M * G, np.nan)
+    lay.place_psi_source(0, np.asarray(f["psi_source"]).ravel(), table)
+    assert np.array_equal(table, np.asarray(f["psi_source"]).ravel())
+
+
+@pytest.mark.parametrize("M,n", [(8, 2), (8, 3), (16, 8), (16, 3)])
+def test_direction_shard_assembly(rtsn_mod, full, M, n):
+    f = full[M]
+    G, N, H = f["p"]["G"], N_CELLS, M // 2
+    pairs = [(r * H // n, (r + 1) * H // n) for r in range(n)]  # rt::Solver's split: uneven when n does not divide H
+    shards = [dict(G=G, M=M, g_lo=0, g_hi=G, d_lo=lo, d_hi=hi, N=N) for lo, hi in pairs]
+    lay = rtsn_mod.Layout(shards)
+    assert lay.mode == 1
+    psi, mu, wt = np.asarray(f["psi"]), f["mu"], f["wt"]
+    dirs = [list(range(H - hi, H - lo)) + list(range(H + lo, H + hi)) for lo, hi in pairs]
+    # moments: each shard's partial sums over its directions; RCCL's all-reduce sums the blocks
+    blocks = []
+    for r, idx in enumerate(dirs):
+        w, m = wt[idx], mu[idx]
+        part = [np.einsum("i,igc->gc", w, psi[idx]), np.einsum("i,igc->gc", m * w, psi[idx]),
+                np.einsum("i,igc->gc", np.where(m > 0, w, 0.0), psi[idx])]
+        blocks.append(lay.pack_moments(r, *(a.T for a in part)))
+    total = blocks[0].copy()
+    for b in blocks[1:]:
+        total += b
+    for k, a in enumerate(lay.unpack_moments(total)):
+        assert np.array_equal(a, total[k])
+    # against one handle's sums: the reference's sequential sum over i, regrouped by shard
+    phi, F, pp = lay.unpack_moments(total)
+    phi_o, F_o, pp_o = f["moments"]
+    assert per_group_rel(phi.T, phi_o, 0) <= 1e-13 and per_group_rel(pp.T, pp_o, 0) <= 1e-13
+    assert flux_rel(F.T, F_o, psi, mu, wt) <= 1e-13  # F cancels: against its summands' scale
+    # psi: every shard's rows (ascending mu) placed into the (M, G, N) buffer
+    out = np.full(M * G * N, np.nan)
+    for r, idx in enumerate(dirs):
+        lay.place_psi(r, _flat_psi(psi[idx]), out)
+    assert np.array_equal(out, _flat_psi(psi))
+    # psi_source rows: the shard's table rows in ascending mu
+    src = np.asarray(f["psi_source"])
+    table = np.full(M * G, np.nan)
+    for r, idx in enumerate(dirs):
+        lay.place_psi_source(r, src[idx].ravel(), table)
+    assert np.array_equal(table, src.ravel())
+    # per-group vectors: summed partials placed as they are
+    vb = [lay.pack_vectors(r, [np.full(G, r + 1.0), np.arange(G, dtype=float) * (r + 1)]) for r in range(n)]
+    s = sum(vb)
+    for j, a in enumerate(lay.unpack_vectors(2, s)):
+        assert np.array_equal(a, s[j])
+
+
+@pytest.mark.parametrize("shards", [
+    [(0, 60, 0, 4), (70, 124, 0, 4)],           # a gap between group shards
+    [(60, 124, 0, 4), (0, 60, 0, 4)],           # not in rank order
+    [(0, 124, 0, 2), (0, 124, 1, 4)],           # overlapping direction pairs
+    [(0, 124, 0, 2), (0, 100, 2, 4)],           # direction shards over different groups
+    [(0, 62, 0, 2), (62, 124, 2, 4)],           # neither tiling
+])
+def test_layout_rejects_bad_tilings(rtsn_mod, shards):
+    with pytest.raises(rtsn_mod.RtError):
+        rtsn_mod.Layout([dict(G=124, M=8, g_lo=a, g_hi=b, d_lo=c, d_hi=d, N=5) for a, b, c, d in shards])
+
+
+def test_comm_version_host_only(rtsn_mod):
+    """rt_comm_version needs no device: the RCCL version librtsn's collectives resolve to and
+    the library file it comes from (torch's bundled librccl when torch loaded one first)."""
+    v = rtsn_mod.comm_version()
+    assert v["code"] >= 20000 and v["version"].startswith("2.")
+    assert "rccl" in v["path"]

@@ -1,0 +1,110 @@
+"""The short-line wavefront (kernels_wave.hip wavefront_kernel; include/rtsn.h
+rt_set_wavefront): lanes over cells, every step of an advance in one launch.
+
+Same arithmetic per (cell, level) as the pipelined segment pass -- the per-line affine map
+with exact carries, the reflective mu > 0 head by the reference's algebra -- so its node
+array must equal the pipelined schedule's BITWISE (the segment kernels are pinned to the
+oracle by test_gpu_parity.py), for every scheme, boundary pair and line length around the
+lane-count edges (C = 1, 2, 4, 8 cells per lane; 32 lanes per line when reflective); and
+through the reference's own configurations it runs by default (rt_solve with no block or
+schedule chosen), which test_gpu_parity.test_reference_configs checks against the oracle.
+"""
+import numpy as np
+import pytest
+
+from conftest import PRM_DIR, SEED
+from parity import per_group_rel
+
+pytestmark = pytest.mark.gpu
+
+LENGTHS = [1, 5, 31, 32, 33, 50, 64, 65, 100, 128, 129, 255, 256, 257, 512]
+
+
+def _params(oracle_mod, N, ts, bc_left, bc_right, M=6, V=5.994, dt=1e-6):
+    p = oracle_mod.parse_prm(PRM_DIR / "llnl_slab_test.prm", table_dir=PRM_DIR)
+    p.update(N=N, M=M, ts_method=ts, bc_left=bc_left, bc_right=bc_right, use_correction=1, V=V, dt=dt)
+    p["dx"] = p["X"] / p["N"]
+    p["psi_source"] = np.linspace(0.5, 2.0, M * p["G"]).reshape(M, p["G"])
+    q = dict(p, bc_left_indicator=bc_left, bc_right_indicator=bc_right)
+    return p, q
+
+
+def _random_ends(q, lo, hi, B, seed):
+    rng = np.random.default_rng(seed)
+    return B[None, :, None, None] * rng.uniform(0.5, 1.5, size=(q["M"], hi - lo, q["N"], 2))
+
+
+@pytest.mark.parametrize("N", LENGTHS)
+@pytest.mark.parametrize("ts", [1, 2, 3])
+@pytest.mark.parametrize("bc_left,bc_right", [(0, 0), (1, 1), (2, 1), (2, 0), (0, 2)])
+def test_wavefront_bitwise_pipelined(rtsn_mod, oracle_mod, N, ts, bc_left, bc_right):
+    """7 steps from a random state on 10 groups x 6 directions: the wavefront's node array
+    equals the pipelined segment schedule's (T = 1, every segment exact) bitwise."""
+    lo, hi, steps = 40, 50, 7
+    p, q = _params(oracle_mod, N, ts, bc_left, bc_right)
+    B = oracle_mod.OracleSolver(p, g_lo=lo, g_hi=hi).groups()["B"][lo:hi]
+    ends0 = _random_ends(q, lo, hi, B, SEED + N + 7 * ts + 3 * bc_left + bc_right)
+    out = {}
+    for wave in (2, 0):
+        with rtsn_mod.Solver(q, g_lo=lo, g_hi=hi) as s:
+            s.wavefront = wave
+            if wave == 0:
+                s.pipeline = 2
+                s.time_block = 1
+            st = s.wavefront_state()
+            fits = st["cells_per_lane"] > 0
+            assert st["active"] == (wave == 2 and fits)
+            s.set_ends(ends0)
+            s.advance(steps)
+            out[wave] = s.ends()
+    assert fits == (N <= (256 if bc_left == 2 else 512))
+    assert np.array_equal(out[2], out[0])
+
+
+@pytest.mark.parametrize("ts", [1, 3])
+def test_wavefront_oracle_and_default(rtsn_mod, oracle_mod, ts):
+    """llnl_slab_test's geometry (M = 2, 124 groups, N = 50) but reflective on the left and
+    40 steps: the default handle takes the wavefront (nothing chosen), matches the oracle
+    to 1e-10 per group; choosing a time block or a schedule turns it off."""
+    p, q = _params(oracle_mod, 50, ts, 2, 1, M=2, dt=1e-4)
+    p["max_timesteps"] = q["max_timesteps"] = 40
+    orc = oracle_mod.OracleSolver(p)
+    orc.solve()
+    with rtsn_mod.Solver(q) as s:
+        assert s.wavefront_state() == {"mode": 1, "active": True, "cells_per_lane": 2}
+        s.solve()
+        assert per_group_rel(s.psi(), orc.psi(), 1) <= 1e-10
+        assert per_group_rel(s.ends(), orc.ends(), 1) <= 1e-10
+    with rtsn_mod.Solver(q) as s:
+        s.time_block = 4
+        assert not s.wavefront_state()["active"]
+    with rtsn_mod.Solver(q) as s:
+        s.pipeline = 1
+        assert not s.wavefront_state()["active"]
+        s.wavefront = 2
+        assert s.wavefront_state()["active"]
+
+
+def test_wavefront_long_advance_chunks(rtsn_mod, oracle_mod):
+    """An advance longer than one launch's 65536 steps runs in chunks: 70000 BE steps of a
+    tiny slab equal 7 x 10000 and the segment schedule's aligned passes (one segment: exact)."""
+    p, q = _params(oracle_mod, 8, 1, 2, 1, M=2, V=0.0, dt=1e-6)
+    q["G"] = 1
+    q["group_bounds"] = None
+    q["group_kappa"] = None
+    q["psi_source"] = np.full((2, 1), 0.7)
+    res = []
+    for mode in ("one", "chunks", "segments"):
+        with rtsn_mod.Solver(q) as s:
+            if mode == "segments":
+                s.wavefront = 0
+                s.pipeline = 0
+                s.time_block = 4
+                assert s.sweep_geometry()[1] == 1
+            else:
+                assert s.wavefront_state()["active"]
+            for n in ([70000] if mode != "chunks" else [10000] * 7):
+                s.advance(n)
+            res.append(s.ends())
+    assert np.array_equal(res[0], res[1])
+    assert np.array_equal(res[0], res[2])
