@@ -787,7 +787,7 @@ def test_timed_kernels_multi_line_group(rtsn_mod, mlg_oracle, case, tb, steps):
         gpu.time_block = tb
         assert gpu.level_waves == (2 if tb == 20 else 4)
         wg, segs = gpu.sweep_geometry()
-        assert segs >= 100
+        assert segs >= 50
         if ends0 is not None:
             gpu.set_ends(ends0)
         gpu.advance(steps)

@@ -58,7 +58,8 @@ def test_wavefront_bitwise_pipelined(rtsn_mod, oracle_mod, N, ts, bc_left, bc_ri
             s.advance(steps)
             out[wave] = s.ends()
     assert fits == (N <= (256 if bc_left == 2 else 512))
-    assert np.array_equal(out[2], out[0])
+    if fits:  # (too long: both handles ran segment schedules of their own choosing)
+        assert np.array_equal(out[2], out[0])
 
 
 @pytest.mark.parametrize("ts", [1, 3])
