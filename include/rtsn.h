@@ -116,14 +116,21 @@ void rt_destroy(rt_solver *s);
 
 /* Solver::solve (solver.cpp:590-823): max_timesteps full steps (x4 substeps
  * for BDF2), preceded by computeEquilibriumSources when use_mg_equilib.
- * Synchronous.  Unless rt_set_time_block was called, a BDF2 run takes the time
- * block rt_plan_time_block(3, max_timesteps) returns (results equal to rounding). */
+ * Synchronous.  Short lines take the wavefront (rt_set_wavefront); a BDF2 run of longer
+ * lines whose caller chose no time block, waves per segment or segmentation takes the
+ * schedule rt_plan_schedule returns (results equal to rounding). */
 rt_status rt_solve(rt_solver *s);
-/* The time block rt_solve picks for a run of nsteps (host only, no handle): for BDF2
- * the block of 40, 32, 20, 16, 10 or 8 steps with the least estimated whole-run time
- * -- pipelined passes at the block's measured cost per step, its pipeline fill and
- * drain, and the nsteps mod T remainder as aligned passes (about 2.5x the cost per
- * step) -- e.g. 20 for 100 or 300 steps, 40 for 1000; the default block otherwise. */
+/* The pipelined schedule rt_solve picks for a BDF2 run of nsteps on this handle's lines:
+ * the time block (8..40 steps), waves per segment (4) and segments sized for wgs_per_cu
+ * workgroups per CU (4..32) with the least estimated whole-run time -- a model of the run
+ * as P = n / T passes over the chain of segments (fill ramp, plateau, drain ramp; each
+ * launch in rounds of the resident workgroups) plus the n mod T remainder as aligned
+ * passes -- and that estimate.  Host arithmetic only; any NULL skipped. */
+rt_status rt_plan_schedule(rt_solver *s, long long nsteps, int *steps_per_pass, int *level_waves, int *wgs_per_cu,
+                           double *estimated_ms);
+/* The time block rt_plan_schedule picks on the SL slab's geometry (N = 1e6 cells, S64, 128
+ * groups, 256 CUs) for a BDF2 run of nsteps (host only, no handle), e.g. 20 for 100 or 300
+ * steps, 40 for 1000; the default block for BE / CN. */
 rt_status rt_plan_time_block(int ts_method, long long nsteps, int *steps_per_pass);
 /* Asynchronous: enqueue nsteps full steps on the handle's stream (with the
  * pipelined schedule, whole passes are launched now and a remainder of fewer
@@ -245,6 +252,14 @@ rt_status rt_get_wavefront(rt_solver *s, int *mode, int *active, int *cells_per_
  * RTSN_LEVEL_WAVES=1|2|4 at creation forces one.  Bitwise-identical results.  Other
  * schemes always use one wave. */
 rt_status rt_set_level_waves(rt_solver *s, int waves);
+/* Segments per line: sized so a pipelined launch with every segment active holds
+ * wgs_per_cu workgroups per CU (1..64), or 0 (default) for the pass kernel's occupancy.
+ * More segments than resident workgroups shorten the pipeline's fill and drain (the line
+ * traversal per launch) at a small cost per segment: a 1000-step run of a 16-group SL
+ * shard 1270 -> 1017 ms at 16 per CU (profiles/r03g_grid16.jsonl).  Applied now if the
+ * positions are aligned, else before the next pass; results bitwise independent of it in
+ * the pipelined schedule. */
+rt_status rt_set_segmentation(rt_solver *s, int wgs_per_cu);
 rt_status rt_get_level_waves(rt_solver *s, int *waves);
 /* Sweep geometry actually used: waves launched per step (one per line group
  * and segment) and segments per line. */

@@ -52,8 +52,13 @@ struct rt_solver {
   int Tp = 0;                    // steps of the pass whose correction is pending
   int Sg = 1, Ls = 16;           // segments per line and cells per segment
   int seg_T = 0;                 // the time block the segments were sized for (0: none)
+  int seg_w = 0;                 // ... and the workgroups per CU they were sized for
   bool T_set = false;            // the caller chose the time block (rt_set_time_block / RTSN_TIME_BLOCK)
   int level_waves = 0;           // pipelined BDF2 passes: 0 auto (level_waves_of), 1 one wave, 2 levels shared by two
+  bool lw_set = false;           // the caller chose the waves per segment (rt_set_level_waves)
+  int seg_wgs = 0;               // segments sized for this many workgroups per CU (0: the pass's occupancy)
+  bool seg_set = false;          // the caller chose the segmentation (rt_set_segmentation)
+  bool planned = false;          // rt_solve planned the schedule (plan_schedule): pipelined from one pass
   int d_lo = 0, d_hi = 0;        // direction-pair shard [d_lo, d_hi) of the M/2 pairs (d_hi = 0: all)
   int M_full = 0;                // the configuration's M (p.M is the handle's own direction count)
   int device = 0, cus = 0;
@@ -535,7 +540,7 @@ static Geometry geometry(const rt_solver *s) { return Geometry{s->p.M, s->Gl, s-
 // Segments per line: enough waves (2 Q Sg) to fill the chip at the sweep
 // kernel's occupancy, Ls a multiple of the register chunk.
 static void segment_lines(rt_solver *h, int waves_per_cu) {
-  waves_per_cu = std::max(1, std::min(waves_per_cu, 32));
+  waves_per_cu = std::max(1, std::min(waves_per_cu, 64));
   const long long target = static_cast<long long>(h->cus) * waves_per_cu;
   long long sg = std::max<long long>(1, target / (2LL * h->Q));
   const long long max_sg = (h->p.N + kSweepCells - 1) / kSweepCells;
@@ -571,18 +576,32 @@ static hipError_t alloc_segments(rt_solver *h) {
 // depend on the segmentation, only the aggregates and propagators do.  Called by
 // rt_set_time_block and again before the next pipelined or aligned pass, so a handle
 // always runs its passes with segments for the time block it runs.
+static rt_status segment_target(rt_solver *h, int *w_out);
+
 static rt_status resegment(rt_solver *h) {
-  if (h->material || h->pending || h->Tpipe || h->seg_T == h->T) return RT_OK;
+  if (h->material || h->pending || h->Tpipe) return RT_OK;
   int w = 0;
-  HIP_TRY(h, sweep_occupancy(h->scheme, h->T, level_waves_of(h, h->T), &w));
-  if (const char *env = std::getenv("RTSN_WAVES_PER_CU")) w = std::atoi(env);  // experiments
+  if (rt_status st = segment_target(h, &w)) return st;
+  if (h->seg_T == h->T && h->seg_w == w) return RT_OK;
   const int sg0 = h->Sg, ls0 = h->Ls;
   segment_lines(h, w);
   h->seg_T = h->T;
+  h->seg_w = w;
   if (h->Sg == sg0 && h->Ls == ls0) return RT_OK;
   if (2LL * h->Q * h->Sg >= (1LL << 31)) return fail(h, RT_ERR_PARAM, "too many lines for one handle: shard the groups");
   HIP_TRY(h, alloc_segments(h));
   h->tau.assign(chain_positions(h), h->target);  // every position at the same, requested time
+  return RT_OK;
+}
+
+// Workgroups per CU the segments of the current time block are sized for: the caller's
+// (rt_set_segmentation, or the schedule rt_solve planned), else the pipelined pass's
+// occupancy (RTSN_WAVES_PER_CU overrides, for experiments).
+static rt_status segment_target(rt_solver *h, int *w_out) {
+  int w = h->seg_wgs;
+  if (!w) HIP_TRY(h, sweep_occupancy(h->scheme, h->T, level_waves_of(h, h->T), &w));
+  if (const char *env = std::getenv("RTSN_WAVES_PER_CU")) w = std::atoi(env);  // experiments
+  *w_out = std::max(1, std::min(w, 64));
   return RT_OK;
 }
 
@@ -703,12 +722,11 @@ static rt_status create_impl(const rt_params *pin, int g_lo, int g_hi, int d_lo,
     if (!std::strcmp(wv, "0") || !std::strcmp(wv, "2")) h->wave = wv[0] - '0';
   if (const char *lw = std::getenv("RTSN_LEVEL_WAVES"))  // experiments: only "1", "2" or "4" are read
     if (!std::strcmp(lw, "1") || !std::strcmp(lw, "2") || !std::strcmp(lw, "4")) h->level_waves = lw[0] - '0';
-  HIP_TRY(h, sweep_occupancy(h->scheme, h->T, level_waves_of(h, h->T), &waves_per_cu));
-  // tuning knob for experiments: target resident waves per CU (segments per line follow)
-  if (const char *w = std::getenv("RTSN_WAVES_PER_CU")) waves_per_cu = std::atoi(w);
   h->cus = prop.multiProcessorCount;
+  if ((st = segment_target(h, &waves_per_cu))) return st;
   segment_lines(h, waves_per_cu);
   h->seg_T = h->T;
+  h->seg_w = waves_per_cu;
   if (2LL * h->Q * h->Sg >= (1LL << 31)) return fail(nullptr, RT_ERR_PARAM, "too many lines for one handle: shard the groups");
   // a chunk's rows are addressed through one buffer descriptor with 32-bit offsets
   if (16LL * 16 * h->Lpad >= (1LL << 31)) return fail(nullptr, RT_ERR_PARAM, "too many lines per row: shard the groups");
@@ -969,6 +987,7 @@ static rt_status pipe_launch(rt_solver *s) {
 // the FP64 work: 20.0 vs 8.3 ms per step on SL).  Without the split, n >= P.
 static int auto_pipeline_passes(const rt_solver *s) {
   const int P = chain_positions(s);
+  if (s->planned) return 1;  // the planned schedule's model is the pipelined run
   if (s->scheme == SCHEME_BDF2 && !s->level_waves && split_block(s->T)) return std::max(1, (P + 7) / 8);
   return P;
 }
@@ -1082,49 +1101,131 @@ extern "C" rt_status rt_synchronize(rt_solver *s) {
   return RT_OK;
 }
 
-// rt_solve knows the run's length.  Unless the caller chose a block, a BDF2 run takes the
-// block with the least estimated whole-run time: the pipelined passes at the block's steady
-// cost per step, plus its fill + drain (in passes of that block), plus the remainder of
-// n mod T steps, which runs as aligned passes of at most 4 steps with the cross-segment
-// correction.  Costs: SL, ms per step (profiles/r02g_big_time_blocks.jsonl)
-// and fill + drain from whole runs of 100 / 300 / 1000 steps (profiles/r02n_run_blocks_*);
-// only their ratios matter.  E.g. 100 steps: T = 20 (T = 40 would leave 20 aligned steps,
-// 1373 vs 1020 ms measured), 300: 20, 1000: 40.
-struct BlockCost {
-  int T;
-  double ms_per_step, fill_drain_passes;
+// rt_solve knows the run's length.  Unless the caller chose the schedule (time block, waves
+// per segment, segmentation), a BDF2 run takes the pipelined schedule with the least
+// estimated whole-run time (plan_schedule): time block T of 8-40 steps, four waves per
+// segment (sweep_split_kernel<3, T, 4>, every launch of the run) and segments sized for w of
+// 4-32 workgroups per CU.  The model (fitted to the whole-run grids
+// profiles/r03[efg]_grid*.jsonl): a run of n steps is P = n / T passes over a chain of C
+// segment positions, launched as P + C - 1 launches whose active positions form a band
+// (ramp up, plateau of min(P, C), ramp down); a launch of W workgroups runs in rounds of
+// the resident 2 per CU, a round's time is one segment's Ls x T / 4 cell-levels per wave at
+// the per-level cost of its block (t_T, a wave alone on its SIMD slightly faster: x 0.96)
+// times the waves per SIMD beyond one.  n mod T steps more run as aligned passes with the
+// cross-segment correction (~2.5 steps' cost each and a fixed ~0.1 s: propagators, folds),
+// so a candidate without a remainder wins unless another is estimated >5% faster.
+struct RunGeom {
+  long long N;
+  int M, Gl, cus;
+  bool reflective;
 };
-constexpr BlockCost kBlockCosts[] = {{40, 7.5, 1.2}, {32, 7.7, 1.2}, {20, 8.3, 1.15},
-                                     {16, 8.15, 2.8}, {10, 9.0, 4.4}, {8, 9.5, 4.0}};
-constexpr double kAlignedMsPerStep = 20.0;
 
-static int plan_time_block(long long nsteps, int fallback) {
-  int best = fallback;
-  double best_ms = 0.0;
-  for (const BlockCost &c : kBlockCosts) {
-    const long long passes = nsteps / c.T, rem = nsteps % c.T;
-    if (passes == 0) continue;
-    const double ms = (nsteps - rem) * c.ms_per_step + c.fill_drain_passes * c.T * c.ms_per_step +
-                      rem * kAlignedMsPerStep;
-    if (best_ms == 0.0 || ms < best_ms) {
-      best = c.T;
-      best_ms = ms;
-    }
+static double level_ns(int T) {  // per cell-level and wave, a SIMD's issue shared by its waves
+  switch (T) {
+    case 8: return 78.0;
+    case 12: return 74.0;
+    case 16: return 74.0;
+    case 20: return 66.0;
+    case 24: return 62.0;
+    case 32: return 59.4;
+    default: return 58.4;  // 40
   }
-  return best;
+}
+
+static void model_segments(const RunGeom &g, int w, long long *Sg, long long *Ls) {
+  const long long Q = (static_cast<long long>(g.M / 2) * g.Gl + 63) / 64;
+  long long sg = std::max<long long>(1, static_cast<long long>(g.cus) * w / (2 * Q));
+  sg = std::min(sg, (g.N + kSweepCells - 1) / kSweepCells);
+  long long ls = (g.N + sg - 1) / sg;
+  ls = (ls + kSweepCells - 1) / kSweepCells * kSweepCells;
+  *Ls = ls;
+  *Sg = (g.N + ls - 1) / ls;
+}
+
+static double run_ms_model(const RunGeom &g, long long n, int T, int w) {
+  constexpr int kw = 4, occ = 2;
+  long long Sg, Ls;
+  model_segments(g, w, &Sg, &Ls);
+  const long long Q = (static_cast<long long>(g.M / 2) * g.Gl + 63) / 64;
+  const long long C = g.reflective ? 2 * Sg : Sg, R = g.reflective ? Q : 2 * Q;
+  const long long P = n / T, rem = n % T;
+  if (P == 0) return 1e300;
+  const double tf = level_ns(T) * 1e-9, tl = 0.96 * tf, unit = static_cast<double>(Ls) * T / kw;
+  const long long S = static_cast<long long>(occ) * g.cus;
+  auto launch = [&](long long a) {  // seconds
+    const long long W = a * R, full = W / S, part = W % S;
+    double t = full * unit * tf * (static_cast<double>(S) * kw / (4.0 * g.cus));
+    if (part) {
+      const double wps = static_cast<double>(part) * kw / (4.0 * g.cus);
+      t += unit * (wps <= 1.0 ? tl : tf * wps);
+    }
+    return t + 5e-6;  // + launch
+  };
+  const long long m = std::min(P, C);
+  double s = 0.0;
+  for (long long a = 1; a < m; ++a) s += 2.0 * launch(a);  // fill and drain ramps
+  s += static_cast<double>(std::max(P, C) - m + 1) * launch(m);
+  if (rem) {
+    const double step = static_cast<double>(R) * g.N * tf / (4.0 * g.cus);  // one step, every line, full load
+    s += rem * 2.5 * step + 0.1;
+  }
+  return 1e3 * s;
+}
+
+struct Schedule {
+  int T = 0, w = 0;
+  double ms = 0.0;
+};
+
+static Schedule plan_schedule(const RunGeom &g, long long nsteps) {
+  static const int kBlocks[] = {40, 32, 24, 20, 16, 12, 8}, kWgs[] = {4, 8, 16, 32};
+  Schedule best, exact;
+  for (int T : kBlocks)
+    for (int w : kWgs) {
+      const double ms = run_ms_model(g, nsteps, T, w);
+      if (ms >= 1e300) continue;
+      if (!best.T || ms < best.ms) best = {T, w, ms};
+      if (nsteps % T == 0 && (!exact.T || ms < exact.ms)) exact = {T, w, ms};
+    }
+  return exact.T && exact.ms <= 1.05 * best.ms ? exact : best;
+}
+
+static RunGeom run_geom(const rt_solver *s) {
+  return RunGeom{s->p.N, s->p.M, s->Gl, s->cus, s->p.bc_left_indicator == 2};
 }
 
 extern "C" rt_status rt_plan_time_block(int ts_method, long long nsteps, int *steps_per_pass) {
   if (!steps_per_pass || nsteps < 0 || ts_method < 1 || ts_method > 3)
     return fail(nullptr, RT_ERR_ARG, "rt_plan_time_block: bad argument");
-  *steps_per_pass = ts_method == SCHEME_BDF2 ? plan_time_block(nsteps, default_time_block(ts_method))
-                                             : default_time_block(ts_method);
+  *steps_per_pass = default_time_block(ts_method);
+  if (ts_method == SCHEME_BDF2) {  // the SL slab's geometry on one MI355X: N = 1e6, S64, 128 groups, 256 CUs
+    const Schedule sc = plan_schedule(RunGeom{1000000, 64, 128, 256, false}, nsteps);
+    if (sc.T) *steps_per_pass = sc.T;
+  }
+  return RT_OK;
+}
+
+extern "C" rt_status rt_plan_schedule(rt_solver *s, long long nsteps, int *steps_per_pass, int *level_waves,
+                                      int *wgs_per_cu, double *estimated_ms) {
+  if (!s || nsteps < 0) return fail(s, RT_ERR_ARG, "rt_plan_schedule: bad argument");
+  Schedule sc;
+  if (s->scheme == SCHEME_BDF2) sc = plan_schedule(run_geom(s), nsteps);
+  if (steps_per_pass) *steps_per_pass = sc.T ? sc.T : s->T;
+  if (level_waves) *level_waves = sc.T ? 4 : s->level_waves;
+  if (wgs_per_cu) *wgs_per_cu = sc.T ? sc.w : s->seg_wgs;
+  if (estimated_ms) *estimated_ms = sc.T ? sc.ms : 0.0;
   return RT_OK;
 }
 
 static void solve_time_block(rt_solver *s) {
-  if (s->T_set || s->scheme != SCHEME_BDF2 || s->Tpipe || s->queued) return;
-  s->T = plan_time_block(s->p.max_timesteps, s->T);
+  if (s->scheme != SCHEME_BDF2 || s->Tpipe || s->queued || use_wavefront(s)) return;
+  if (s->T_set || s->lw_set || s->seg_set) return;  // the caller chose (part of) the schedule
+  const Schedule sc = plan_schedule(run_geom(s), s->p.max_timesteps);
+  if (!sc.T) return;
+  s->T = sc.T;
+  s->level_waves = 4;
+  s->seg_wgs = sc.w;
+  s->planned = true;
 }
 
 extern "C" rt_status rt_solve(rt_solver *s) {
@@ -1216,6 +1317,7 @@ extern "C" rt_status rt_material_enable(rt_solver *s, double rho_cv, const doubl
     const int sg0 = s->Sg;
     segment_lines(s, w);
     s->seg_T = 0;  // sized for the coupled pass
+    s->seg_w = 0;
     if (s->Sg != sg0) {
       if (2LL * s->Q * s->Sg >= (1LL << 31)) return fail(s, RT_ERR_PARAM, "too many segments");
       HIP_TRY(s, alloc_segments(s));
@@ -1845,6 +1947,7 @@ extern "C" rt_status rt_set_pipeline(rt_solver *s, int on) {
   }
   s->pipe = on;
   s->pipe_set = true;
+  s->planned = false;
   return RT_OK;
 }
 
@@ -1884,6 +1987,7 @@ extern "C" rt_status rt_set_time_block(rt_solver *s, int steps_per_pass) {
   HIP_TRY(s, hipSetDevice(s->device));
   s->T = steps_per_pass;
   s->T_set = true;
+  s->planned = false;
   return resegment(s);  // now if the positions are aligned, else when they next are
 }
 
@@ -1896,8 +2000,21 @@ extern "C" rt_status rt_get_time_block(rt_solver *s, int *steps_per_pass) {
 extern "C" rt_status rt_set_level_waves(rt_solver *s, int waves) {
   if (!s) return fail(nullptr, RT_ERR_ARG, "rt_set_level_waves: NULL handle");
   if (waves < 0 || waves > 4 || waves == 3) return fail(s, RT_ERR_PARAM, "rt_set_level_waves: 0 (auto), 1, 2 or 4");
-  s->level_waves = waves;  // segments stay as created: the schedule is exact for any segmentation
+  s->level_waves = waves;  // segments re-sized for its occupancy before the next pass (the schedule is exact
+  s->lw_set = true;        // for any segmentation)
+  s->planned = false;
+  if (rt_status st = resegment(s)) return st;
   return RT_OK;
+}
+
+extern "C" rt_status rt_set_segmentation(rt_solver *s, int wgs_per_cu) {
+  if (!s) return fail(nullptr, RT_ERR_ARG, "rt_set_segmentation: NULL handle");
+  if (wgs_per_cu < 0 || wgs_per_cu > 64) return fail(s, RT_ERR_ARG, "rt_set_segmentation: 0 (occupancy) .. 64");
+  HIP_TRY(s, hipSetDevice(s->device));
+  s->seg_wgs = wgs_per_cu;
+  s->seg_set = true;
+  s->planned = false;
+  return resegment(s);  // now if the positions are aligned, else before the next pass
 }
 
 extern "C" rt_status rt_get_level_waves(rt_solver *s, int *waves) {

@@ -119,6 +119,9 @@ def lib():
         L.rt_pipeline_state.argtypes = [vp, C.POINTER(C.c_longlong), C.POINTER(C.c_int), C.POINTER(C.c_int)]
         L.rt_get_time_block.argtypes = [vp, C.POINTER(C.c_int)]
         L.rt_plan_time_block.argtypes = [C.c_int, C.c_longlong, C.POINTER(C.c_int)]
+        L.rt_plan_schedule.argtypes = [vp, C.c_longlong, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int),
+                                       dp]
+        L.rt_set_segmentation.argtypes = [vp, C.c_int]
         L.rt_get_level_waves.argtypes = [vp, C.POINTER(C.c_int)]
         L.rt_set_wavefront.argtypes = [vp, C.c_int]
         L.rt_get_wavefront.argtypes = [vp, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)]
@@ -561,6 +564,18 @@ class Solver:
         m, a, c = C.c_int(), C.c_int(), C.c_int()
         _check(lib().rt_get_wavefront(self._h, C.byref(m), C.byref(a), C.byref(c)), "rt_get_wavefront", self._h)
         return {"mode": m.value, "active": bool(a.value), "cells_per_lane": c.value}
+
+    def plan_schedule(self, nsteps: int) -> dict:
+        """rt_plan_schedule: the pipelined BDF2 schedule rt_solve picks for nsteps on this
+        handle -- {"time_block", "level_waves", "wgs_per_cu", "estimated_ms"}."""
+        T, lw, w, ms = C.c_int(), C.c_int(), C.c_int(), C.c_double()
+        _check(lib().rt_plan_schedule(self._h, int(nsteps), C.byref(T), C.byref(lw), C.byref(w), C.byref(ms)),
+               "rt_plan_schedule", self._h)
+        return {"time_block": T.value, "level_waves": lw.value, "wgs_per_cu": w.value, "estimated_ms": ms.value}
+
+    def set_segmentation(self, wgs_per_cu: int):
+        """rt_set_segmentation: segments sized for wgs_per_cu workgroups per CU (0: occupancy)."""
+        _check(lib().rt_set_segmentation(self._h, int(wgs_per_cu)), "rt_set_segmentation", self._h)
 
     def pipeline_state(self) -> dict:
         """{"lag_steps", "queued_steps", "pending"} (rt_pipeline_state)."""
