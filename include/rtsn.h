@@ -129,8 +129,8 @@ rt_status rt_solve(rt_solver *s);
 rt_status rt_plan_schedule(rt_solver *s, long long nsteps, int *steps_per_pass, int *level_waves, int *wgs_per_cu,
                            double *estimated_ms);
 /* The time block rt_plan_schedule picks on the SL slab's geometry (N = 1e6 cells, S64, 128
- * groups, 256 CUs) for a BDF2 run of nsteps (host only, no handle), e.g. 20 for 100 or 300
- * steps, 40 for 1000; the default block for BE / CN. */
+ * groups, 256 CUs) for a BDF2 run of nsteps (host only, no handle), e.g. 20 for 300 steps,
+ * 40 for 1000; the default block for BE / CN. */
 rt_status rt_plan_time_block(int ts_method, long long nsteps, int *steps_per_pass);
 /* Asynchronous: enqueue nsteps full steps on the handle's stream (with the
  * pipelined schedule, whole passes are launched now and a remainder of fewer

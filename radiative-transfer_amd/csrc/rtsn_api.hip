@@ -1105,15 +1105,14 @@ extern "C" rt_status rt_synchronize(rt_solver *s) {
 // per segment, segmentation), a BDF2 run takes the pipelined schedule with the least
 // estimated whole-run time (plan_schedule): time block T of 8-40 steps, four waves per
 // segment (sweep_split_kernel<3, T, 4>, every launch of the run) and segments sized for w of
-// 4-32 workgroups per CU.  The model (fitted to the whole-run grids
-// profiles/r03[efg]_grid*.jsonl): a run of n steps is P = n / T passes over a chain of C
-// segment positions, launched as P + C - 1 launches whose active positions form a band
-// (ramp up, plateau of min(P, C), ramp down); a launch of W workgroups runs in rounds of
-// the resident 2 per CU, a round's time is one segment's Ls x T / 4 cell-levels per wave at
-// the per-level cost of its block (t_T, a wave alone on its SIMD slightly faster: x 0.96)
-// times the waves per SIMD beyond one.  n mod T steps more run as aligned passes with the
-// cross-segment correction (~2.5 steps' cost each and a fixed ~0.1 s: propagators, folds),
-// so a candidate without a remainder wins unless another is estimated >5% faster.
+// 4-32 workgroups per CU.  The model (fitted to the finite-state whole-run
+// grids profiles/r03l_grid{16,128}.jsonl: mean error 3%): a run of n steps is P = n / T
+// passes over a chain of C segment positions, launched as P + C - 1 launches whose active
+// positions form a band (ramp up, plateau of min(P, C), ramp down); a launch of W workgroups
+// runs in rounds of the resident 2 per CU, and a round's time is one segment's Ls x T / 4
+// cell-levels per wave at the per-level cost of its block (t_T) times the workgroups the
+// busiest CU holds (ceil(W / CUs): a wave per SIMD each).  n mod T steps more run as aligned
+// passes with the cross-segment correction (~3 steps' cost each, ~30 ms of folds).
 struct RunGeom {
   long long N;
   int M, Gl, cus;
@@ -1122,13 +1121,12 @@ struct RunGeom {
 
 static double level_ns(int T) {  // per cell-level and wave, a SIMD's issue shared by its waves
   switch (T) {
-    case 8: return 78.0;
-    case 12: return 74.0;
-    case 16: return 74.0;
-    case 20: return 66.0;
-    case 24: return 62.0;
-    case 32: return 59.4;
-    default: return 58.4;  // 40
+    case 8: return 76.7;
+    case 16: return 71.0;
+    case 20: return 67.6;
+    case 24: return 70.4;
+    case 32: return 66.7;
+    default: return 64.7;  // 40
   }
 }
 
@@ -1150,14 +1148,14 @@ static double run_ms_model(const RunGeom &g, long long n, int T, int w) {
   const long long C = g.reflective ? 2 * Sg : Sg, R = g.reflective ? Q : 2 * Q;
   const long long P = n / T, rem = n % T;
   if (P == 0) return 1e300;
-  const double tf = level_ns(T) * 1e-9, tl = 0.96 * tf, unit = static_cast<double>(Ls) * T / kw;
+  const double tf = level_ns(T) * 1e-9, tl = 0.99 * tf, unit = static_cast<double>(Ls) * T / kw;
   const long long S = static_cast<long long>(occ) * g.cus;
   auto launch = [&](long long a) {  // seconds
     const long long W = a * R, full = W / S, part = W % S;
-    double t = full * unit * tf * (static_cast<double>(S) * kw / (4.0 * g.cus));
+    double t = full * unit * tf * occ;
     if (part) {
-      const double wps = static_cast<double>(part) * kw / (4.0 * g.cus);
-      t += unit * (wps <= 1.0 ? tl : tf * wps);
+      const long long per_cu = (part + g.cus - 1) / g.cus;  // workgroups on the busiest CU
+      t += unit * (per_cu <= 1 ? tl : tf * per_cu);
     }
     return t + 5e-6;  // + launch
   };
@@ -1167,7 +1165,7 @@ static double run_ms_model(const RunGeom &g, long long n, int T, int w) {
   s += static_cast<double>(std::max(P, C) - m + 1) * launch(m);
   if (rem) {
     const double step = static_cast<double>(R) * g.N * tf / (4.0 * g.cus);  // one step, every line, full load
-    s += rem * 2.5 * step + 0.1;
+    s += rem * 3.0 * step + 0.03;
   }
   return 1e3 * s;
 }
@@ -1178,16 +1176,14 @@ struct Schedule {
 };
 
 static Schedule plan_schedule(const RunGeom &g, long long nsteps) {
-  static const int kBlocks[] = {40, 32, 24, 20, 16, 12, 8}, kWgs[] = {4, 8, 16, 32};
-  Schedule best, exact;
+  static const int kBlocks[] = {40, 32, 24, 20, 16, 8}, kWgs[] = {4, 8, 16, 32};
+  Schedule best;
   for (int T : kBlocks)
     for (int w : kWgs) {
       const double ms = run_ms_model(g, nsteps, T, w);
-      if (ms >= 1e300) continue;
-      if (!best.T || ms < best.ms) best = {T, w, ms};
-      if (nsteps % T == 0 && (!exact.T || ms < exact.ms)) exact = {T, w, ms};
+      if (ms < 1e300 && (!best.T || ms < best.ms)) best = {T, w, ms};
     }
-  return exact.T && exact.ms <= 1.05 * best.ms ? exact : best;
+  return best;
 }
 
 static RunGeom run_geom(const rt_solver *s) {
