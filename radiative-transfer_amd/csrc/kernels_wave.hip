@@ -24,26 +24,31 @@
 
 namespace rtamd {
 
-// DPP wave_shr:1 (gfx9 family): lane l receives lane l - 1's value, lane 0 receives 0
-__device__ __forceinline__ double lane_shift_up(double v) {
+// DPP wave_shr:1 (gfx9 family): lane l receives lane l - 1's value; lane 0 has no source and
+// keeps `old` -- the chain head's inflow state, loop-carried in the same registers, so the
+// head needs no per-tick select or copy.
+__device__ __forceinline__ double lane_shift_up(double old, double v) {
   const unsigned long long b = __builtin_bit_cast(unsigned long long, v);
-  const int lo = __builtin_amdgcn_update_dpp(0, static_cast<int>(b & 0xffffffffu), 0x138, 0xf, 0xf, false);
-  const int hi = __builtin_amdgcn_update_dpp(0, static_cast<int>(b >> 32), 0x138, 0xf, 0xf, false);
+  const unsigned long long o = __builtin_bit_cast(unsigned long long, old);
+  const int lo = __builtin_amdgcn_update_dpp(static_cast<int>(o & 0xffffffffu), static_cast<int>(b & 0xffffffffu),
+                                             0x138, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(static_cast<int>(o >> 32), static_cast<int>(b >> 32), 0x138, 0xf, 0xf,
+                                             false);
   return __builtin_bit_cast(double, (static_cast<unsigned long long>(static_cast<unsigned int>(hi)) << 32) |
                                         static_cast<unsigned int>(lo));
 }
 
-// grid: one wave per line (mu < 0 lines then mu > 0 lines, ell < H Gl) -- or, reflective,
-// one wave per line pair ell (lanes [0, Lw) the mu < 0 line, [Lw, 2 Lw) its mirror).
-// Lw = lanes per line = ceil(N / C).  nsteps full steps from the stored state.
-template <int S, int C>
+// grid: one wave per line (mu < 0 lines then mu > 0 lines, ell < H Gl) -- or, PAIR (the
+// reflective left boundary), one wave per line pair ell (lanes [0, Lw) the mu < 0 line,
+// [Lw, 2 Lw) its mirror).  Lw = lanes per line = ceil(N / C) <= 64 (PAIR: 32).  nsteps full
+// steps from the stored state.
+template <int S, int C, bool PAIR>
 __global__ __launch_bounds__(64) void wavefront_kernel(SegArgs a, int nsteps, int Lw) {
   constexpr int K = SchemeDim<S>::K, WN = map_count<S>();
   const int lane = threadIdx.x;
-  const bool pair = a.reflective != 0;
   const int nl = a.H * a.Gl;
   int half, ell, j;
-  if (pair) {
+  if (PAIR) {
     ell = blockIdx.x;
     half = lane < Lw ? 0 : 1;
     j = lane - half * Lw;
@@ -52,7 +57,7 @@ __global__ __launch_bounds__(64) void wavefront_kernel(SegArgs a, int nsteps, in
     ell = static_cast<int>(blockIdx.x) % nl;
     j = lane;
   }
-  const int used = pair ? 2 * Lw : Lw;  // lanes holding cells; the chain's lane index is `lane`
+  const int used = PAIR ? 2 * Lw : Lw;  // lanes holding cells; the chain's lane index is `lane`
   const bool real = lane < used;
   const size_t stride = static_cast<size_t>(a.Lpad);
   double2 *Eh = a.E + static_cast<size_t>(half) * a.Nrow * stride + ell;
@@ -70,10 +75,13 @@ __global__ __launch_bounds__(64) void wavefront_kernel(SegArgs a, int nsteps, in
   }
   double W[WN];
 #pragma unroll
-  for (int n = 0; n < WN; ++n) W[n] = a.map[(static_cast<size_t>(half) * WN + n) * stride + ell];
-  const double bv = a.bdry[static_cast<size_t>(half) * stride + ell];
-  const bool head = j == 0;
-  const bool refl_head = pair && half == 1 && head;  // one lane of a pair wave
+  for (int n = 0; n < WN; ++n) {
+    W[n] = a.map[(static_cast<size_t>(half) * WN + n) * stride + ell];
+    // a wave-uniform line map would live in SGPRs, and gfx9's one scalar operand per VALU op
+    // then costs an accumulator copy per row and cell: keep it in VGPRs
+    asm volatile("" : "+v"(W[n]));
+  }
+  const bool refl_head = PAIR && half == 1 && j == 0;  // one lane of a pair wave
   LineConst L{};
   if (refl_head) {
     const double *lcp = a.lc + static_cast<size_t>(half) * LC_COUNT * stride + ell;
@@ -81,48 +89,49 @@ __global__ __launch_bounds__(64) void wavefront_kernel(SegArgs a, int nsteps, in
     for (int n = 0; n < LC_COUNT; ++n) L.c[n] = lcp[n * stride];
   }
 
-  double X[K];
+  // Xin: the state each lane receives at its tick -- lane - 1's exit state of the same level;
+  // lane 0's stays the chain head's inflow state (solver.cpp:695-697), the mu < 0 line's
+  // with PAIR.  Every lane runs its cells every tick (no divergent branch, no register
+  // shuffling at a join); only lanes at a level in [0, nsteps) commit their nodes, and
+  // an idle lane's exit state only ever reaches idle lanes.
+  double Xin[K], X[K];
+  {
+    const double bv = a.bdry[static_cast<size_t>(PAIR ? 0 : half) * stride + ell];
+    const double b[4] = {bv, bv, bv, bv};
+    head_state<S>(b, Xin);
 #pragma unroll
-  for (int r = 0; r < K; ++r) X[r] = 0.0;
+    for (int r = 0; r < K; ++r) X[r] = Xin[r];
+  }
   const int ticks = nsteps + used - 1;
   for (int tick = 0; tick < ticks; ++tick) {
-    double Xin[K];
 #pragma unroll
-    for (int r = 0; r < K; ++r) Xin[r] = lane_shift_up(X[r]);  // lane - 1's exit state of this level
+    for (int r = 0; r < K; ++r) Xin[r] = lane_shift_up(Xin[r], X[r]);
     const int t = tick - lane;
-    if (!real || t < 0 || t >= nsteps) continue;
-    double b[4] = {bv, bv, bv, bv};
-    if (head) {
-      if (refl_head) {  // solver.cpp:677-684: the mirror's outflow after each substep of this step
-        if constexpr (S == SCHEME_BDF2) {
+    const bool active = real && t >= 0 && t < nsteps;
 #pragma unroll
-          for (int r = 0; r < 4; ++r) b[r] = Xin[1 + r];
-        } else {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) b[r] = Xin[K - 1];
-        }
-      }
-      head_state<S>(b, Xin);
+    for (int r = 0; r < K; ++r) X[r] = Xin[r];
+    if (PAIR && refl_head) {
+      // solver.cpp:677-684: the mirror's outflow after each substep is the inflow b of the
+      // same substep; head_state(b) differs from the received state in component 0 only
+      if constexpr (S == SCHEME_BDF2) X[0] = X[2];
+      if constexpr (S == SCHEME_CN) X[0] = X[1];
     }
 #pragma unroll
     for (int c = 0; c < C; ++c) {
-      if (j * C + c >= a.N) break;  // the chain's padding cells carry X through
-      if (c == 0 && refl_head) {    // reflective head: the reference's algebra, distinct inflows
-        double oi, oo;
-        cell_step_maybe_head<S>(L, a.hd, false, ein[0], eout[0], Xin, true, b[3], oi, oo);
-        ein[0] = oi;
-        eout[0] = oo;
-        continue;
-      }
       double Xn[K], oi, oo;
-      map_apply<S, true>(W, Xin, ein[c], eout[c], Xn, oi, oo);
+      if (PAIR && c == 0 && refl_head) {  // reflective head: the reference's algebra, distinct inflows
+        cell_step_maybe_head<S>(L, a.hd, false, ein[0], eout[0], X, true, X[K - 1], oi, oo);
 #pragma unroll
-      for (int r = 0; r < K; ++r) Xin[r] = Xn[r];
-      ein[c] = oi;
-      eout[c] = oo;
+        for (int r = 0; r < K; ++r) Xn[r] = X[r];
+      } else {
+        map_apply<S, true>(W, X, ein[c], eout[c], Xn, oi, oo);
+      }
+      if (C > 1 && j * C + c >= a.N) continue;  // the chain's padding cells carry X through
+#pragma unroll
+      for (int r = 0; r < K; ++r) X[r] = Xn[r];
+      ein[c] = active ? oi : ein[c];
+      eout[c] = active ? oo : eout[c];
     }
-#pragma unroll
-    for (int r = 0; r < K; ++r) X[r] = Xin[r];
   }
 #pragma unroll
   for (int c = 0; c < C; ++c) {
@@ -131,11 +140,11 @@ __global__ __launch_bounds__(64) void wavefront_kernel(SegArgs a, int nsteps, in
   }
 }
 
-template <int S>
+template <int S, bool PAIR>
 static hipError_t launch_wave_s(int C, const SegArgs &a, int nsteps, int Lw, int grid, hipStream_t st) {
   switch (C) {
 #define RT_WAVE_CASE(c) \
-  case c: hipLaunchKernelGGL((wavefront_kernel<S, c>), dim3(grid), dim3(64), 0, st, a, nsteps, Lw); break;
+  case c: hipLaunchKernelGGL((wavefront_kernel<S, c, PAIR>), dim3(grid), dim3(64), 0, st, a, nsteps, Lw); break;
     RT_WAVE_CASE(1) RT_WAVE_CASE(2) RT_WAVE_CASE(4) RT_WAVE_CASE(8)
 #undef RT_WAVE_CASE
     default: return hipErrorInvalidValue;
@@ -143,6 +152,7 @@ static hipError_t launch_wave_s(int C, const SegArgs &a, int nsteps, int Lw, int
   return hipGetLastError();
 }
 
+// lanes of a chain: 64, a reflective pair 2 x 32
 int wavefront_cells_per_lane(int N, bool reflective) {
   const int lanes = reflective ? 32 : 64;
   const int c = (N + lanes - 1) / lanes;
@@ -160,9 +170,15 @@ hipError_t launch_wavefront(int scheme, const SegArgs &a, int nsteps, hipStream_
   const int Lw = (a.N + C - 1) / C;
   const int grid = pair ? nl : 2 * nl;
   switch (scheme) {
-    case SCHEME_BE: return launch_wave_s<SCHEME_BE>(C, a, nsteps, Lw, grid, st);
-    case SCHEME_CN: return launch_wave_s<SCHEME_CN>(C, a, nsteps, Lw, grid, st);
-    default: return launch_wave_s<SCHEME_BDF2>(C, a, nsteps, Lw, grid, st);
+    case SCHEME_BE:
+      return pair ? launch_wave_s<SCHEME_BE, true>(C, a, nsteps, Lw, grid, st)
+                  : launch_wave_s<SCHEME_BE, false>(C, a, nsteps, Lw, grid, st);
+    case SCHEME_CN:
+      return pair ? launch_wave_s<SCHEME_CN, true>(C, a, nsteps, Lw, grid, st)
+                  : launch_wave_s<SCHEME_CN, false>(C, a, nsteps, Lw, grid, st);
+    default:
+      return pair ? launch_wave_s<SCHEME_BDF2, true>(C, a, nsteps, Lw, grid, st)
+                  : launch_wave_s<SCHEME_BDF2, false>(C, a, nsteps, Lw, grid, st);
   }
 }
 

@@ -5,7 +5,7 @@ Same arithmetic per (cell, level) as the pipelined segment pass -- the per-line 
 with exact carries, the reflective mu > 0 head by the reference's algebra -- so its node
 array must equal the pipelined schedule's BITWISE (the segment kernels are pinned to the
 oracle by test_gpu_parity.py), for every scheme, boundary pair and line length around the
-lane-count edges (C = 1, 2, 4, 8 cells per lane; 32 lanes per line when reflective); and
+lane-count edges (C = 1, 2, 4, 8 cells per lane on 64 lanes, 32 per line when reflective); and
 through the reference's own configurations it runs by default (rt_solve with no block or
 schedule chosen), which test_gpu_parity.test_reference_configs checks against the oracle.
 """
@@ -17,7 +17,7 @@ from parity import per_group_rel
 
 pytestmark = pytest.mark.gpu
 
-LENGTHS = [1, 5, 31, 32, 33, 50, 64, 65, 100, 128, 129, 255, 256, 257, 512]
+LENGTHS = [1, 5, 31, 32, 33, 50, 63, 64, 65, 100, 127, 128, 129, 255, 256, 257, 511, 512, 513]
 
 
 def _params(oracle_mod, N, ts, bc_left, bc_right, M=6, V=5.994, dt=1e-6):
@@ -57,7 +57,7 @@ def test_wavefront_bitwise_pipelined(rtsn_mod, oracle_mod, N, ts, bc_left, bc_ri
             s.set_ends(ends0)
             s.advance(steps)
             out[wave] = s.ends()
-    assert fits == (N <= (256 if bc_left == 2 else 512))
+    assert fits == (N <= (256 if bc_left == 2 else 512))  # 32 / 64 lanes x 8 cells
     if fits:  # (too long: both handles ran segment schedules of their own choosing)
         assert np.array_equal(out[2], out[0])
 
