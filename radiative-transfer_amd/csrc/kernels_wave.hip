@@ -19,6 +19,8 @@
 // with the mirror's per-substep outflows, sweep_device.hpp head_cell): bitwise equal to it.
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "cell.hpp"
 #include "kernels.hpp"
 
@@ -102,36 +104,57 @@ __global__ __launch_bounds__(64) void wavefront_kernel(SegArgs a, int nsteps, in
 #pragma unroll
     for (int r = 0; r < K; ++r) X[r] = Xin[r];
   }
-  const int ticks = nsteps + used - 1;
-  for (int tick = 0; tick < ticks; ++tick) {
+  // ticks [used - 1, nsteps) have every lane of the chain at a level in [0, nsteps): that
+  // stretch (all but the chain's fill and drain) runs without the commit masks
+  const auto run = [&](int tick0, int tick1, auto masked) {
+    const auto body = [&](int tick) {
 #pragma unroll
-    for (int r = 0; r < K; ++r) Xin[r] = lane_shift_up(Xin[r], X[r]);
-    const int t = tick - lane;
-    const bool active = real && t >= 0 && t < nsteps;
-#pragma unroll
-    for (int r = 0; r < K; ++r) X[r] = Xin[r];
-    if (PAIR && refl_head) {
-      // solver.cpp:677-684: the mirror's outflow after each substep is the inflow b of the
-      // same substep; head_state(b) differs from the received state in component 0 only
-      if constexpr (S == SCHEME_BDF2) X[0] = X[2];
-      if constexpr (S == SCHEME_CN) X[0] = X[1];
-    }
-#pragma unroll
-    for (int c = 0; c < C; ++c) {
-      double Xn[K], oi, oo;
-      if (PAIR && c == 0 && refl_head) {  // reflective head: the reference's algebra, distinct inflows
-        cell_step_maybe_head<S>(L, a.hd, false, ein[0], eout[0], X, true, X[K - 1], oi, oo);
-#pragma unroll
-        for (int r = 0; r < K; ++r) Xn[r] = X[r];
-      } else {
-        map_apply<S, true>(W, X, ein[c], eout[c], Xn, oi, oo);
+      for (int r = 0; r < K; ++r) Xin[r] = lane_shift_up(Xin[r], X[r]);
+      bool active = true;
+      if constexpr (decltype(masked)::value) {
+        const int t = tick - lane;
+        active = real && t >= 0 && t < nsteps;
       }
-      if (C > 1 && j * C + c >= a.N) continue;  // the chain's padding cells carry X through
 #pragma unroll
-      for (int r = 0; r < K; ++r) X[r] = Xn[r];
-      ein[c] = active ? oi : ein[c];
-      eout[c] = active ? oo : eout[c];
+      for (int r = 0; r < K; ++r) X[r] = Xin[r];
+      if (PAIR && refl_head) {
+        // solver.cpp:677-684: the mirror's outflow after each substep is the inflow b of the
+        // same substep; head_state(b) differs from the received state in component 0 only
+        if constexpr (S == SCHEME_BDF2) X[0] = X[2];
+        if constexpr (S == SCHEME_CN) X[0] = X[1];
+      }
+#pragma unroll
+      for (int c = 0; c < C; ++c) {
+        double Xn[K], oi, oo;
+        if (PAIR && c == 0 && refl_head) {  // reflective head: the reference's algebra, distinct inflows
+          cell_step_maybe_head<S>(L, a.hd, false, ein[0], eout[0], X, true, X[K - 1], oi, oo);
+#pragma unroll
+          for (int r = 0; r < K; ++r) Xn[r] = X[r];
+        } else {
+          map_apply<S, true>(W, X, ein[c], eout[c], Xn, oi, oo);
+        }
+        if (C > 1 && j * C + c >= a.N) continue;  // the chain's padding cells carry X through
+#pragma unroll
+        for (int r = 0; r < K; ++r) X[r] = Xn[r];
+        ein[c] = active ? oi : ein[c];
+        eout[c] = active ? oo : eout[c];
+      }
+    };
+    // two ticks per iteration: the loop-carried renames of X, ein and eout then cancel
+    int tick = tick0;
+    for (; tick + 1 < tick1; tick += 2) {
+      body(tick);
+      body(tick + 1);
     }
+    if (tick < tick1) body(tick);
+  };
+  const int ticks = nsteps + used - 1;
+  if (nsteps > used - 1) {
+    run(0, used - 1, std::true_type{});
+    run(used - 1, nsteps, std::false_type{});
+    run(nsteps, ticks, std::true_type{});
+  } else {
+    run(0, ticks, std::true_type{});
   }
 #pragma unroll
   for (int c = 0; c < C; ++c) {
