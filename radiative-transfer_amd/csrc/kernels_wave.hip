@@ -77,12 +77,12 @@ __global__ __launch_bounds__(64) void wavefront_kernel(SegArgs a, int nsteps, in
   }
   double W[WN];
 #pragma unroll
-  for (int n = 0; n < WN; ++n) {
-    W[n] = a.map[(static_cast<size_t>(half) * WN + n) * stride + ell];
-    // a wave-uniform line map would live in SGPRs, and gfx9's one scalar operand per VALU op
-    // then costs an accumulator copy per row and cell: keep it in VGPRs
-    asm volatile("" : "+v"(W[n]));
-  }
+  for (int n = 0; n < WN; ++n) W[n] = a.map[(static_cast<size_t>(half) * WN + n) * stride + ell];
+  // a wave-uniform line map would live in SGPRs, and gfx9's one scalar operand per VALU op
+  // then costs an accumulator copy per row and cell: keep it in VGPRs (after all the loads
+  // are issued, so that they are in flight together)
+#pragma unroll
+  for (int n = 0; n < WN; ++n) asm volatile("" : "+v"(W[n]));
   const bool refl_head = PAIR && half == 1 && j == 0;  // one lane of a pair wave
   LineConst L{};
   if (refl_head) {
