@@ -371,7 +371,8 @@ typedef struct {
 /* *mode: 0 group shards, 1 direction shards; *max_groups: Gmax.  Any NULL skipped. */
 rt_status rt_layout_mode(const rt_shard *shards, int nranks, int *mode, int *max_groups);
 /* rank's phi, F, phi_plus (local: 3 arrays of N x G_local back to back, g fastest, as
- * rt_get_moments_device writes them) -> its wire block [3][N][Gmax], padding zeroed */
+ * rt_get_moments_device writes them; NULL for an empty shard) -> its wire block
+ * [3][N][Gmax], padding zeroed */
 rt_status rt_layout_pack_moments(const rt_shard *shards, int nranks, int rank, const double *local, double *block);
 /* gathered: group shards the all-gather of every rank's block [rank][3][N][Gmax];
  * direction shards their sum [3][N][Gmax] -> phi, F, phi_plus (G x N, g + G c); NULL skipped */

@@ -140,8 +140,9 @@ extern "C" rt_status rt_layout_mode(const rt_shard *shards, int nranks, int *mod
 
 extern "C" rt_status rt_layout_pack_moments(const rt_shard *shards, int nranks, int rank, const double *local,
                                             double *block) {
-  if (!shards || nranks < 1 || rank < 0 || rank >= nranks || !local || !block) return RT_ERR_ARG;
+  if (!shards || nranks < 1 || rank < 0 || rank >= nranks || !block) return RT_ERR_ARG;
   if (shard_mode(shards, nranks) < 0) return RT_ERR_PARAM;
+  if (!local && groups_of(shards[rank]) > 0) return RT_ERR_ARG;  // an empty shard has no local arrays
   std::fill(block, block + 3 * static_cast<size_t>(shards[0].N) * max_groups(shards, nranks), 0.0);
   apply(moments_pack(shards, nranks, rank), local, block);
   return RT_OK;
