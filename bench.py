@@ -9,11 +9,16 @@ Workload (SURVEY.md §8(d) "SL"): 1D slab X = 0.4 cm, N = 1e6 cells, S64
 Gauss-Legendre (M = 64), 128 energy groups per GPU on a log grid 0.001-30 keV
 with kappa_g resampled from the LLNL capped table, rho = 1, T = 1 keV, BDF2
 (ts_method = 3), vacuum boundaries; V = 0 (variant v0) or V = 5.994 with the
-v/c correction (variant corr).  dt = 1e-7 (--dt): at SURVEY's dt = 1e-3 the
+v/c correction (variant corr).  dt = 1e-9 (--dt): at SURVEY's dt = 1e-3 the
 reference's BDF2 (const_B from the full dt, solver.cpp:501) overflows the state
 to inf within the pipeline fill, and inf arithmetic runs ~4% faster than the
 finite state (interleaved A/B, profiles/r03c_ab_finite.jsonl), so the headline
-is timed on the finite one and dt = 1e-3 is a side leg (overflow_control).  A "step" is one full BDF2
+is timed on a finite one and dt = 1e-3 is a side leg (overflow_control).  The
+state stays finite for 200-400 steps at dt = 1e-7, 1200-1400 at 1e-8 and more
+than 4000 at 1e-9 (profiles/r03j_finite_horizon.jsonl); the fill grows as the
+groups per GPU shrink (160 steps at 128 groups, 1280 at the 16 of an 8-GPU
+run), so every N runs the same dt = 1e-9, whose timing equals dt = 1e-7's
+(profiles/r03k_window_ab.jsonl).  A "step" is one full BDF2
 step (4 substeps) of every cell x angle x group of the GPU's groups, i.e.
 4 M G N cell-angle-group updates, computed in fp64 by the fused HIP sweep.
 State is resident in HBM before timing.
@@ -116,7 +121,7 @@ def host_cpus() -> dict:
     return info
 
 
-def cpu_baseline(variant: str, dt: float = 1e-7) -> dict:
+def cpu_baseline(variant: str, dt: float = 1e-9) -> dict:
     """The C oracle (the reference's algorithm restated, solver.cpp loop order, gcc -O3) on
     a bounded sample of the SL workload -- all 64 angles, N = 200000 cells, 1 BDF2 step --
     on the lease's CPU share (host_cpus):
@@ -594,9 +599,9 @@ def side_leg(p: dict, info, world: int, device, local: int, scaling: str, tb: in
     it): the state is created fresh, the pipeline filled untimed, then two passes timed
     exactly as the headline.  Used for (a) the HBM-bound T = 1 pass (one HBM round trip
     of the state per BDF2 step: the north_star's HBM-roofline view of the sweep), (b)
-    the finite-state control (dt = 1e-7: the reference's BDF2 stays bounded, so the
-    timing of the headline -- whose state overflows, DESIGN.md §5 -- is shown to be
-    data-independent) and (c) the other SL variant (v/c correction on / inactive)."""
+    the overflow control (dt = 1e-3, SURVEY's step: the reference's BDF2 overflows the
+    state to inf, which runs ~4% faster -- not the headline) and (c) the
+    other SL variant (v/c correction on / inactive)."""
     import rtsn
     with make_solver(p, local, info, dirs) as s:
         s.time_block = tb
@@ -706,9 +711,11 @@ def main():
     ap.add_argument("--cells", type=int, default=1_000_000)
     # SURVEY §8(d)'s SL names dt = 1e-3, at which the reference's BDF2 (const_B from the full dt,
     # solver.cpp:501) overflows the slab's state to inf within the pipeline fill; the headline is
-    # timed on a finite state (dt = 1e-7), which runs ~4% slower than the overflowed one on the
-    # same box (profiles/r03c_ab_finite.jsonl); dt = 1e-3 is the side leg "overflow_control"
-    ap.add_argument("--dt", type=float, default=1e-7, help="time step of the SL slab (default 1e-7: finite state)")
+    # timed on a finite state, which runs ~4% slower than the overflowed one on the same box
+    # (profiles/r03c_ab_finite.jsonl); dt = 1e-3 is the side leg "overflow_control".  1e-9 keeps
+    # the state finite through the longest fill (1280 steps for the 16 groups of an 8-GPU run)
+    ap.add_argument("--dt", type=float, default=1e-9,
+                    help="time step of the SL slab (default 1e-9: finite state at every GPU count)")
     ap.add_argument("--time-block", type=int, default=0,
                     help="full steps fused per HBM pass, dividing --steps (0: the fastest dividing it)")
     ap.add_argument("--schedule", choices=["pipelined", "aligned"], default="pipelined",
@@ -774,7 +781,7 @@ def main():
                                                        "BDF2 overflows the state to inf within the fill: not the "
                                                        "headline (inf arithmetic runs ~4% faster)", dirs)
         other = "corr" if args.variant == "v0" else "v0"
-        # dt = 1e-9: with the v/c correction on, the reference's BDF2 overflows the SL state
+        # at most 1e-9: with the v/c correction on, the reference's BDF2 overflows the SL state
         # within the fill already at dt = 1e-7 (profiles/r03o_bench.json)
         line[f"variant_{other}"] = side_leg(dict(slab_params(info[0], other, N=args.cells), variant=other,
                                                  dt=min(args.dt, 1e-9)), info,
