@@ -43,8 +43,11 @@ __device__ __forceinline__ double lane_shift_up(double old, double v) {
 // grid: one wave per line (mu < 0 lines then mu > 0 lines, ell < H Gl) -- or, PAIR (the
 // reflective left boundary), one wave per line pair ell (lanes [0, Lw) the mu < 0 line,
 // [Lw, 2 Lw) its mirror).  Lw = lanes per line = ceil(N / C) <= 64 (PAIR: 32).  nsteps full
-// steps from the stored state.
-template <int S, int C, bool PAIR>
+// steps from the stored state.  Padding cells (the last lane of a line holds N mod C real
+// cells) feed nothing real -- except, with PAIR and N mod C != 0 (PAD), those of the mu < 0
+// line, whose exit state is the mirror head's inflow: there they pass X through by a select
+// (a per-lane branch would make every tick divergent).
+template <int S, int C, bool PAIR, bool PAD>
 __global__ __launch_bounds__(64) void wavefront_kernel(SegArgs a, int nsteps, int Lw) {
   constexpr int K = SchemeDim<S>::K, WN = map_count<S>();
   const int lane = threadIdx.x;
@@ -104,12 +107,27 @@ __global__ __launch_bounds__(64) void wavefront_kernel(SegArgs a, int nsteps, in
 #pragma unroll
     for (int r = 0; r < K; ++r) X[r] = Xin[r];
   }
-  // ticks [used - 1, nsteps) have every lane of the chain at a level in [0, nsteps): that
-  // stretch (all but the chain's fill and drain) runs without the commit masks
+  // ticks [used, nsteps) have every lane of the chain at a level in [1, nsteps): that
+  // stretch (all but the chain's fill and drain) runs without the commit masks, and there
+  // component 0 of the received state (the upwind cell's node before level t, which the
+  // map copies from dout) is not shifted in: it is the upwind cell's output node of level
+  // t - 1, which this lane received one tick earlier as component K - 1 (CN, BDF2; the
+  // chain head's inflow state has equal components) -- one DPP lane shift fewer per tick
   const auto run = [&](int tick0, int tick1, auto masked) {
     const auto body = [&](int tick) {
+      if constexpr (K > 1 && !decltype(masked)::value) {
+        // the shift of component K - 1 keeps Xin[0] as its `old` (lane 0: the head's
+        // inflow state, all of whose components are equal), so the two registers trade
+        // roles each tick and two ticks per iteration need no copy
+        const double x0 = Xin[K - 1];
+        Xin[K - 1] = lane_shift_up(Xin[0], X[K - 1]);
 #pragma unroll
-      for (int r = 0; r < K; ++r) Xin[r] = lane_shift_up(Xin[r], X[r]);
+        for (int r = 1; r < K - 1; ++r) Xin[r] = lane_shift_up(Xin[r], X[r]);
+        Xin[0] = x0;
+      } else {
+#pragma unroll
+        for (int r = 0; r < K; ++r) Xin[r] = lane_shift_up(Xin[r], X[r]);
+      }
       bool active = true;
       if constexpr (decltype(masked)::value) {
         const int t = tick - lane;
@@ -133,9 +151,14 @@ __global__ __launch_bounds__(64) void wavefront_kernel(SegArgs a, int nsteps, in
         } else {
           map_apply<S, true>(W, X, ein[c], eout[c], Xn, oi, oo);
         }
-        if (C > 1 && j * C + c >= a.N) continue;  // the chain's padding cells carry X through
+        if constexpr (PAD) {
+          const bool pad = j * C + c >= a.N;
 #pragma unroll
-        for (int r = 0; r < K; ++r) X[r] = Xn[r];
+          for (int r = 0; r < K; ++r) X[r] = pad ? X[r] : Xn[r];
+        } else {
+#pragma unroll
+          for (int r = 0; r < K; ++r) X[r] = Xn[r];
+        }
         ein[c] = active ? oi : ein[c];
         eout[c] = active ? oo : eout[c];
       }
@@ -149,9 +172,9 @@ __global__ __launch_bounds__(64) void wavefront_kernel(SegArgs a, int nsteps, in
     if (tick < tick1) body(tick);
   };
   const int ticks = nsteps + used - 1;
-  if (nsteps > used - 1) {
-    run(0, used - 1, std::true_type{});
-    run(used - 1, nsteps, std::false_type{});
+  if (nsteps > used) {
+    run(0, used, std::true_type{});
+    run(used, nsteps, std::false_type{});
     run(nsteps, ticks, std::true_type{});
   } else {
     run(0, ticks, std::true_type{});
@@ -165,9 +188,16 @@ __global__ __launch_bounds__(64) void wavefront_kernel(SegArgs a, int nsteps, in
 
 template <int S, bool PAIR>
 static hipError_t launch_wave_s(int C, const SegArgs &a, int nsteps, int Lw, int grid, hipStream_t st) {
+  const bool pad = PAIR && a.N % C != 0;
   switch (C) {
-#define RT_WAVE_CASE(c) \
-  case c: hipLaunchKernelGGL((wavefront_kernel<S, c, PAIR>), dim3(grid), dim3(64), 0, st, a, nsteps, Lw); break;
+#define RT_WAVE_CASE(c)                                                                                      \
+  case c:                                                                                                    \
+    if (pad)                                                                                                 \
+      hipLaunchKernelGGL((wavefront_kernel<S, c, PAIR, PAIR && (c > 1)>), dim3(grid), dim3(64), 0, st, a, nsteps, \
+                         Lw);                                                                                \
+    else                                                                                                     \
+      hipLaunchKernelGGL((wavefront_kernel<S, c, PAIR, false>), dim3(grid), dim3(64), 0, st, a, nsteps, Lw); \
+    break;
     RT_WAVE_CASE(1) RT_WAVE_CASE(2) RT_WAVE_CASE(4) RT_WAVE_CASE(8)
 #undef RT_WAVE_CASE
     default: return hipErrorInvalidValue;

@@ -62,6 +62,34 @@ def test_wavefront_bitwise_pipelined(rtsn_mod, oracle_mod, N, ts, bc_left, bc_ri
         assert np.array_equal(out[2], out[0])
 
 
+@pytest.mark.parametrize("N", [1, 33, 64, 100, 129, 255, 256, 512])
+@pytest.mark.parametrize("ts", [1, 2, 3])
+@pytest.mark.parametrize("bc_left,bc_right", [(0, 0), (2, 1), (1, 1)])
+def test_wavefront_bitwise_pipelined_long(rtsn_mod, oracle_mod, N, ts, bc_left, bc_right):
+    """As above for 150 steps, more than a chain has lanes: the ticks between the chain's fill
+    and drain (every lane at a level in [1, n)) run unmasked and take component 0 of the
+    carried state from the previous tick instead of a lane shift -- bitwise the pipelined
+    schedule still (dt = 1e-9 keeps the reference's BDF2 finite over the run)."""
+    lo, hi, steps = 40, 44, 150
+    p, q = _params(oracle_mod, N, ts, bc_left, bc_right, dt=1e-9)
+    B = oracle_mod.OracleSolver(p, g_lo=lo, g_hi=hi).groups()["B"][lo:hi]
+    ends0 = _random_ends(q, lo, hi, B, SEED + 3 * N + 11 * ts + 5 * bc_left + bc_right)
+    out = {}
+    for wave in (2, 0):
+        with rtsn_mod.Solver(q, g_lo=lo, g_hi=hi) as s:
+            s.wavefront = wave
+            if wave == 0:
+                s.pipeline = 2
+                s.time_block = 1
+            fits = s.wavefront_state()["cells_per_lane"] > 0
+            s.set_ends(ends0)
+            s.advance(steps)
+            out[wave] = s.ends()
+    if fits:
+        assert np.isfinite(out[0]).all()
+        assert np.array_equal(out[2], out[0])
+
+
 @pytest.mark.parametrize("ts", [1, 3])
 def test_wavefront_oracle_and_default(rtsn_mod, oracle_mod, ts):
     """llnl_slab_test's geometry (M = 2, 124 groups, N = 50) but reflective on the left and
