@@ -10,6 +10,9 @@
 #ifndef RT_SPLIT_BIAS
 #define RT_SPLIT_BIAS 0
 #endif
+#ifndef RT_SPLIT_PIN_LOADS
+#define RT_SPLIT_PIN_LOADS 1
+#endif
 
 namespace rtamd {
 
@@ -61,16 +64,34 @@ __device__ __forceinline__ void split_chunk(const double *W, double (&ein)[C], d
       row_store(Rw, voff, c * row_bytes, oi, oo);
     else  // hand the nodes at this wave's last level to the next wave
       lout[c * 64 + lane] = make_double2(oi, oo);
-    if constexpr (!LASTCH) {  // refill with the next chunk: from HBM, or from the previous wave
-      if constexpr (IN_HBM) {
+    if constexpr (IN_HBM) {
+#if RT_SPLIT_PIN_LOADS
+      // refill from HBM one cell late: row c - 1 with the next chunk's (row C - 1 of THIS
+      // chunk at cell 0).  The upwind node of cell c - 1 (row c - 1's e_out) is the carried
+      // state's component 0 until cell c's first level, so an earlier load could not reuse
+      // its registers: the allocator copied the loaded rows at the loop head, whose wait for
+      // the chunk's last loads, issued just before, stalled every chunk's start
+      const bool load = LASTCH ? (c == 0 && C - 1 < nv) : true;
+      if (load) {
+        const int rr = c == 0 ? C - 1 : c - 1;
+        const double2 v = row_load(c == 0 ? Rw : Rn, voff, rr * row_bytes);
+        ein[rr] = v.x;
+        eout[rr] = v.y;
+      }
+      // each load after its cell's FMAs (left alone, the scheduler sinks them to the end)
+      __builtin_amdgcn_sched_group_barrier(0x002, TW * 28, 0);  // VALU
+      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);        // VMEM read
+#else
+      if constexpr (!LASTCH) {
         const double2 v = row_load(Rn, voff, c * row_bytes);
         ein[c] = v.x;
         eout[c] = v.y;
-      } else {
-        const double2 v = lin[c * 64 + lane];
-        ein[c] = v.x;
-        eout[c] = v.y;
       }
+#endif
+    } else if constexpr (!LASTCH) {  // refill with the next chunk from the previous wave
+      const double2 v = lin[c * 64 + lane];
+      ein[c] = v.x;
+      eout[c] = v.y;
     }
   }
 }
@@ -156,8 +177,9 @@ __device__ __forceinline__ void split_role(const SegArgs &a, double2 (*hand)[2][
   if constexpr (IN) {
     const __amdgpu_buffer_rsrc_t R0 = rows(k_begin);
 #pragma unroll
-    for (int c = 0; c < C; ++c) {
-      const double2 v = row_load(R0, voff, c * row_bytes);
+    for (int c = 0; c < C; ++c) {  // (RT_SPLIT_PIN_LOADS: row C - 1 by the first chunk's cell 0)
+      const double2 v =
+          (c + 1 < C || !RT_SPLIT_PIN_LOADS) ? row_load(R0, voff, c * row_bytes) : make_double2(0.0, 0.0);
       ein[c] = v.x;
       eout[c] = v.y;
     }
@@ -197,6 +219,13 @@ __device__ __forceinline__ void split_role(const SegArgs &a, double2 (*hand)[2][
   double W[WN];
 #pragma unroll
   for (int n = 0; n < WN; ++n) W[n] = a.map[(static_cast<size_t>(half) * WN + n) * stride + ell];
+#if RT_SPLIT_PIN_LOADS
+  // every prologue load (map, carried states, chunk 0) complete before the chunks start:
+  // the wait-count pass merges the loop's entry into its head, and a map load still
+  // pending there made EVERY chunk start wait for all loads in flight (vmcnt(0)) -- the
+  // next chunk's rows, issued just before
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0) expcnt(7) lgkmcnt(15)
+#endif
 
   // ---- chunk intervals: nch + 2 (KW - 1) of them, one barrier after each, for every wave ----
   const int nch = (k_end - k_begin + C - 1) / C;
