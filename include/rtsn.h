@@ -112,6 +112,10 @@ rt_status rt_create_from_params(const rt_params *p, int g_lo, int g_hi, int devi
  * bitwise that of a full handle. */
 rt_status rt_create_direction_shard(const rt_params *p, int g_lo, int g_hi, int d_lo, int d_hi, int device,
                                     rt_solver **out);
+/* ~Solver.  Waits for the handle's queued work, then returns its device buffers (up to
+ * 64 MB each), pinned staging, stream and events to a process-wide cache that the next
+ * rt_create* on the device draws from (RTSN_POOL_MB, default 512, caps it; 0 frees
+ * everything at once, as before); a failed device allocation empties the cache first. */
 void rt_destroy(rt_solver *s);
 
 /* Solver::solve (solver.cpp:590-823): max_timesteps full steps (x4 substeps

@@ -8,9 +8,12 @@
 #include <cstdlib>
 #include <cstring>
 #include <limits>
+#include <map>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <thread>
+#include <tuple>
 #include <vector>
 
 #include "../../include/rtsn.h"
@@ -25,14 +28,159 @@ namespace {
 
 thread_local std::string g_last_error;
 
+// ---------------------------------------------------------------------------
+// Handle resource cache.  A handle's lifetime allocates ~20 device buffers, two pinned
+// staging buffers, a stream and events, and hipFree / hipHostFree synchronise the device:
+// together ~1 ms per Solver(ph) ... ~Solver() pair on the box, more than the reference's
+// own configurations take to solve (llnl_slab_test's 2 steps: 21 us).  rt_destroy (and
+// the getters' temporaries) hand them to this process-wide cache -- blocks of at most
+// kPoolMaxBlock, RTSN_POOL_MB in all (default 512; 0 turns the cache off), only after the
+// owning stream is idle -- and the next allocation of the same kind, device and size class
+// takes them back.  A failed device allocation empties that device's cache and retries.
+// The cache is never destroyed (no HIP call after the runtime's teardown at exit).
+// ---------------------------------------------------------------------------
+constexpr size_t kPoolMaxBlock = size_t(64) << 20;
+
+class ResourcePool {
+ public:
+  static ResourcePool &get() {
+    static ResourcePool *pool = new ResourcePool();
+    return *pool;
+  }
+  // device (host = false) or pinned host (host = true) memory: *cap receives the block's size
+  hipError_t alloc(bool host, size_t bytes, void **out, size_t *cap) {
+    const size_t want = round(bytes);
+    int dev = 0;
+    if (!host) (void)hipGetDevice(&dev);
+    if (cap_ && want <= kPoolMaxBlock) {
+      std::lock_guard<std::mutex> lk(m_);
+      auto it = blocks_.lower_bound(std::make_tuple(host, host ? 0 : dev, want));
+      if (it != blocks_.end() && std::get<0>(it->first) == host && std::get<1>(it->first) == (host ? 0 : dev) &&
+          std::get<2>(it->first) <= 2 * want) {  // the smallest cached block that fits, if not twice too big
+        *cap = std::get<2>(it->first);
+        *out = it->second;
+        cached_ -= *cap;
+        blocks_.erase(it);
+        return hipSuccess;
+      }
+    }
+    *cap = want;
+    hipError_t e = host ? hipHostMalloc(out, want, hipHostMallocDefault) : hipMalloc(out, want);
+    if (e != hipSuccess) {  // memory held by the cache first
+      (void)hipGetLastError();
+      trim(host, dev);
+      e = host ? hipHostMalloc(out, want, hipHostMallocDefault) : hipMalloc(out, want);
+    }
+    return e;
+  }
+  // p must not be in use by any queued work (its stream synchronised)
+  void release(bool host, void *p, size_t cap, int dev) {
+    if (!p) return;
+    if (cap_ && cap <= kPoolMaxBlock) {
+      std::lock_guard<std::mutex> lk(m_);
+      if (cached_ + cap <= cap_) {
+        blocks_.emplace(std::make_tuple(host, host ? 0 : dev, cap), p);
+        cached_ += cap;
+        return;
+      }
+    }
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    if (!host && cur != dev) (void)hipSetDevice(dev);
+    (void)(host ? hipHostFree(p) : hipFree(p));
+    if (!host && cur != dev) (void)hipSetDevice(cur);
+  }
+  hipError_t stream(hipStream_t *out) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (cap_) {
+      std::lock_guard<std::mutex> lk(m_);
+      for (size_t i = 0; i < streams_.size(); ++i)
+        if (streams_[i].first == dev) {
+          *out = streams_[i].second;
+          streams_.erase(streams_.begin() + static_cast<long>(i));
+          return hipSuccess;
+        }
+    }
+    return hipStreamCreateWithFlags(out, hipStreamNonBlocking);
+  }
+  void release_stream(hipStream_t st, int dev) {  // st idle
+    if (!st) return;
+    if (cap_) {
+      std::lock_guard<std::mutex> lk(m_);
+      if (streams_.size() < 64) {
+        streams_.emplace_back(dev, st);
+        return;
+      }
+    }
+    (void)hipStreamDestroy(st);
+  }
+  hipError_t event(bool timing, hipEvent_t *out) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (cap_) {
+      std::lock_guard<std::mutex> lk(m_);
+      auto it = events_.find(std::make_pair(dev, timing));
+      if (it != events_.end()) {
+        *out = it->second;
+        events_.erase(it);
+        return hipSuccess;
+      }
+    }
+    return timing ? hipEventCreate(out) : hipEventCreateWithFlags(out, hipEventDisableTiming);
+  }
+  void release_event(hipEvent_t ev, bool timing, int dev) {
+    if (!ev) return;
+    if (cap_) {
+      std::lock_guard<std::mutex> lk(m_);
+      if (events_.size() < 4096) {
+        events_.emplace(std::make_pair(dev, timing), ev);
+        return;
+      }
+    }
+    (void)hipEventDestroy(ev);
+  }
+
+ private:
+  ResourcePool() {
+    cap_ = size_t(512) << 20;
+    if (const char *env = std::getenv("RTSN_POOL_MB")) cap_ = static_cast<size_t>(std::max(0L, std::atol(env))) << 20;
+  }
+  static size_t round(size_t bytes) {  // size classes: 256 B up to 64 KiB, then 64 KiB
+    const size_t q = bytes <= (size_t(64) << 10) ? 256 : (size_t(64) << 10);
+    return (std::max<size_t>(bytes, 16) + q - 1) / q * q;
+  }
+  void trim(bool host, int dev) {
+    std::lock_guard<std::mutex> lk(m_);
+    for (auto it = blocks_.begin(); it != blocks_.end();) {
+      if (std::get<0>(it->first) == host && (host || std::get<1>(it->first) == dev)) {
+        (void)(host ? hipHostFree(it->second) : hipFree(it->second));
+        cached_ -= std::get<2>(it->first);
+        it = blocks_.erase(it);
+      } else {
+        ++it;
+      }
+    }
+  }
+  std::mutex m_;
+  size_t cap_ = 0, cached_ = 0;
+  std::multimap<std::tuple<bool, int, size_t>, void *> blocks_;  // (pinned host, device, size) -> block
+  std::vector<std::pair<int, hipStream_t>> streams_;
+  std::multimap<std::pair<int, bool>, hipEvent_t> events_;      // (device, timing) -> event
+};
+
 struct DeviceBuf {
   void *p = nullptr;
-  size_t bytes = 0;
+  size_t bytes = 0, cap = 0;
+  int dev = 0;
   DeviceBuf() = default;
   DeviceBuf(const DeviceBuf &) = delete;  // owns p
   DeviceBuf &operator=(const DeviceBuf &) = delete;
-  ~DeviceBuf() {
-    if (p) (void)hipFree(p);
+  ~DeviceBuf() { reset(); }
+  void reset() {  // the owner's stream must be idle
+    ResourcePool::get().release(false, p, cap, dev);
+    p = nullptr;
+    bytes = cap = 0;
   }
 };
 
@@ -99,18 +247,18 @@ struct rt_solver {
   long long launches = 0, profiled = 0;
   // chunked host transfers (rt_get_psi / rt_get_ends / rt_set_ends): pinned staging
   void *staging[2] = {nullptr, nullptr};
-  size_t staging_bytes = 0;
+  size_t staging_bytes = 0, staging_cap[2] = {0, 0};
   hipEvent_t staging_ev[2] = {nullptr, nullptr};
   std::string err;
 
-  ~rt_solver() {
+  ~rt_solver() {  // everything goes back to the resource cache once the stream is idle
+    (void)hipSetDevice(device);
     if (stream) (void)hipStreamSynchronize(stream);  // no kernel may outlive the buffers it uses
-    for (void *h : staging)
-      if (h) (void)hipHostFree(h);
-    for (hipEvent_t e : staging_ev)
-      if (e) (void)hipEventDestroy(e);
-    for (hipEvent_t e : ev_pool) (void)hipEventDestroy(e);
-    if (stream) (void)hipStreamDestroy(stream);
+    ResourcePool &pool = ResourcePool::get();
+    for (int k = 0; k < 2; ++k) pool.release(true, staging[k], staging_cap[k], 0);
+    for (hipEvent_t e : staging_ev) pool.release_event(e, false, device);
+    for (hipEvent_t e : ev_pool) pool.release_event(e, true, device);
+    pool.release_stream(stream, device);
   }
 };
 
@@ -183,9 +331,10 @@ static int map_count_of(int scheme) {
   }
 }
 
-static hipError_t dalloc(DeviceBuf &b, size_t bytes) {
+static hipError_t dalloc(DeviceBuf &b, size_t bytes) {  // b empty
   b.bytes = bytes;
-  return hipMalloc(&b.p, bytes ? bytes : 16);
+  (void)hipGetDevice(&b.dev);
+  return ResourcePool::get().alloc(false, bytes, &b.p, &b.cap);
 }
 
 // ---------------------------------------------------------------------------
@@ -556,11 +705,8 @@ static void segment_lines(rt_solver *h, int waves_per_cu) {
 static hipError_t alloc_segments(rt_solver *h) {
   const size_t Lp = h->Lpad;
   const int K = h->K;
-  for (DeviceBuf *b : {&h->agg[0], &h->agg[1], &h->yseg})
-    if (b->p) {
-      (void)hipFree(b->p);
-      b->p = nullptr;
-    }
+  if (h->agg[0].p || h->agg[1].p || h->yseg.p) (void)hipStreamSynchronize(h->stream);  // before the cache may hand them out
+  for (DeviceBuf *b : {&h->agg[0], &h->agg[1], &h->yseg}) b->reset();
   hipError_t e = dalloc(h->agg[0], sizeof(double) * 2 * h->Sg * kMaxTimeBlock * K * Lp);
   if (!e) e = dalloc(h->agg[1], sizeof(double) * 2 * h->Sg * kMaxTimeBlock * K * Lp);
   if (!e) e = dalloc(h->yseg, sizeof(double) * 2 * (h->Sg + 1) * kMaxAlignedBlock * K * Lp);
@@ -707,8 +853,8 @@ static rt_status create_impl(const rt_params *pin, int g_lo, int g_hi, int d_lo,
   HIP_TRY(h, hipGetDeviceProperties(&prop, device));
   if (std::string(prop.gcnArchName).find("gfx950") == std::string::npos)
     return fail(nullptr, RT_ERR_DEVICE, std::string("librtsn is built for gfx950, device is ") + prop.gcnArchName);
-  HIP_TRY(h, hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
-  for (hipEvent_t &ev : h->staging_ev) HIP_TRY(h, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+  HIP_TRY(h, ResourcePool::get().stream(&h->stream));
+  for (hipEvent_t &ev : h->staging_ev) HIP_TRY(h, ResourcePool::get().event(false, &ev));
 
   // segments: enough waves to fill the chip (occupancy x CUs), Ls a multiple of the chunk
   int waves_per_cu = 0;
@@ -1509,14 +1655,15 @@ static int chunk_cells(const rt_solver *s) {
 // copy of chunk i overlaps the device's export + DMA of chunk i + 1.
 static rt_status ensure_staging(rt_solver *s, size_t bytes) {
   if (s->staging_bytes >= bytes) return RT_OK;
-  for (void *&h : s->staging)
-    if (h) {
-      (void)hipHostFree(h);
-      h = nullptr;
-    }
+  (void)hipStreamSynchronize(s->stream);  // no transfer may still use the old pair
+  for (int k = 0; k < 2; ++k) {
+    ResourcePool::get().release(true, s->staging[k], s->staging_cap[k], 0);
+    s->staging[k] = nullptr;
+    s->staging_cap[k] = 0;
+  }
   s->staging_bytes = 0;
-  for (void *&h : s->staging) HIP_TRY(s, hipHostMalloc(&h, bytes, hipHostMallocDefault));
-  s->staging_bytes = bytes;
+  for (int k = 0; k < 2; ++k) HIP_TRY(s, ResourcePool::get().alloc(true, bytes, &s->staging[k], &s->staging_cap[k]));
+  s->staging_bytes = std::min(s->staging_cap[0], s->staging_cap[1]);
   return RT_OK;
 }
 
@@ -1570,8 +1717,9 @@ static rt_status export_chunks(rt_solver *s, int nodes, double *host, F &&launch
   const int cc = chunk_cells(s);
   const size_t cap = static_cast<size_t>(nodes) * MG * cc;  // doubles per chunk
   if (rt_status st = ensure_staging(s, sizeof(double) * cap)) return st;
-  double *d = nullptr;
-  HIP_TRY(s, hipMalloc(reinterpret_cast<void **>(&d), sizeof(double) * cap));
+  DeviceBuf dbuf;
+  HIP_TRY(s, dalloc(dbuf, sizeof(double) * cap));
+  double *d = static_cast<double *>(dbuf.p);
   hipError_t e = hipSuccess;
   int prev_c0 = -1, prev_nc = 0, k = 0;
   auto drain = [&](int c0, int nc, const double *h) {  // staging -> caller, node blocks MGN apart
@@ -1596,8 +1744,8 @@ static rt_status export_chunks(rt_solver *s, int nodes, double *host, F &&launch
     e = hipEventSynchronize(s->staging_ev[(k - 1) & 1]);
     if (e == hipSuccess) drain(prev_c0, prev_nc, static_cast<const double *>(s->staging[(k - 1) & 1]));
   }
-  (void)hipStreamSynchronize(s->stream);  // d is freed below
-  (void)hipFree(d);
+  (void)hipStreamSynchronize(s->stream);  // d is released below
+  dbuf.reset();
   if (e != hipSuccess) return fail(s, RT_ERR_DEVICE, std::string("result transfer: ") + hipGetErrorString(e));
   return RT_OK;
 }
@@ -1630,8 +1778,9 @@ extern "C" rt_status rt_set_ends(rt_solver *s, const double *ends) {
   const size_t MG = static_cast<size_t>(g.M) * g.Gl, MGN = MG * g.N;
   const int cc = chunk_cells(s);
   if (rt_status st = ensure_staging(s, sizeof(double) * 2 * MG * cc)) return st;
-  double *d = nullptr;
-  HIP_TRY(s, hipMalloc(reinterpret_cast<void **>(&d), sizeof(double) * 2 * MG * cc));
+  DeviceBuf dbuf;
+  HIP_TRY(s, dalloc(dbuf, sizeof(double) * 2 * MG * cc));
+  double *d = static_cast<double *>(dbuf.p);
   hipError_t e = hipSuccess;
   int k = 0;
   for (int c0 = 0; c0 < g.N && e == hipSuccess; c0 += cc, ++k) {
@@ -1644,8 +1793,8 @@ extern "C" rt_status rt_set_ends(rt_solver *s, const double *ends) {
     if (e == hipSuccess) e = hipEventRecord(s->staging_ev[k & 1], s->stream);
     if (e == hipSuccess) e = launch_import_ends(static_cast<double2 *>(s->E.p), d, g, c0, nc, s->stream);
   }
-  (void)hipStreamSynchronize(s->stream);  // d is freed below
-  (void)hipFree(d);
+  (void)hipStreamSynchronize(s->stream);  // d is released below
+  dbuf.reset();
   ++s->state_version;
   if (e != hipSuccess)  // some chunks may hold the new cells, the rest the old ones
     return fail(s, RT_ERR_DEVICE, std::string("rt_set_ends: ") + hipGetErrorString(e) +
@@ -1754,8 +1903,9 @@ static rt_status balance_sums(rt_solver *s, std::vector<double> &ab, std::vector
     host[gl] = s->gt.rho[s->g_lo + gl] * s->gt.kappa[s->g_lo + gl];
     host[Gl + gl] = host[gl] * ac * std::pow(s->p.T, 4) * dx;
   }
-  double *d = nullptr;
-  HIP_TRY(s, hipMalloc(reinterpret_cast<void **>(&d), sizeof(double) * (host.size() + balance_scratch_doubles(Gl))));
+  DeviceBuf dbuf;
+  HIP_TRY(s, dalloc(dbuf, sizeof(double) * (host.size() + balance_scratch_doubles(Gl))));
+  double *d = static_cast<double *>(dbuf.p);
   hipError_t e = hipMemcpyAsync(d, host.data(), sizeof(double) * 2 * Gl, hipMemcpyHostToDevice, s->stream);
   if (e == hipSuccess)
     e = launch_balance_sums(static_cast<const double *>(s->mom.p), d, d + Gl, dx, d + host.size(), d + 2 * Gl,
@@ -1764,7 +1914,7 @@ static rt_status balance_sums(rt_solver *s, std::vector<double> &ab, std::vector
     e = hipMemcpyAsync(host.data() + 2 * Gl, d + 2 * Gl, sizeof(double) * 2 * Gl, hipMemcpyDeviceToHost, s->stream);
   if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
   (void)hipStreamSynchronize(s->stream);
-  (void)hipFree(d);
+  dbuf.reset();
   if (e != hipSuccess) return fail(s, RT_ERR_DEVICE, std::string("balance sums: ") + hipGetErrorString(e));
   ab.assign(host.begin() + 2 * Gl, host.begin() + 3 * Gl);
   sr.assign(host.begin() + 3 * Gl, host.end());
@@ -1900,8 +2050,9 @@ extern "C" rt_status rt_set_profiling(rt_solver *s, int on) {
   s->sweep_ms = 0.0;
   s->profiled = 0;
   if (s->profiling && s->ev_pool.empty()) {
+    HIP_TRY(s, hipSetDevice(s->device));
     s->ev_pool.resize(256, nullptr);
-    for (hipEvent_t &e : s->ev_pool) HIP_TRY(s, hipEventCreate(&e));
+    for (hipEvent_t &e : s->ev_pool) HIP_TRY(s, ResourcePool::get().event(true, &e));
   }
   return RT_OK;
 }
