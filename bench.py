@@ -627,7 +627,52 @@ def material_params(p: dict) -> dict:
     return dict(p, ts_method=1, V=0.0, dt=1e-3)
 
 
-def run_material(p: dict, info, world: int, device, local: int, steps: int, dirs=None, rank: int = 0) -> dict:
+def open_comm(world: int, rank: int, local: int):
+    """The RCCL communicator behind the C ABI (rt_comm: ncclCommInitRank over every rank's
+    GPU), or (None, reason) where RCCL cannot form it -- the one-GPU multi-rank rehearsal
+    (two ranks on one device).  Collective over the ranks."""
+    import torch.distributed as dist
+    import rtsn
+    try:
+        uid = [rtsn.Comm.unique_id() if rank == 0 else None]
+        if world > 1:
+            dist.broadcast_object_list(uid, src=0)
+        return rtsn.Comm(world, rank, uid[0], local), None
+    except rtsn.RtError as e:
+        return None, str(e)
+
+
+def rccl_gather_check(comm, solver, gathered, dirs) -> dict:
+    """The end-of-run result arrays gathered a second way, by RCCL behind the C ABI
+    (rt_comm_gather_moments / _group_ends / _balance: the shard table all-gathered, one
+    all-gather of every rank's padded blocks, assembled by comm_layout.cpp's copy plans --
+    the code a C++ host uses without torch), against the torch.distributed gather above:
+    bitwise for group shards; direction shards' sums (an all-reduce) within rounding.
+    Outside the timed region; runs only where a communicator formed (every rank calls
+    the same collectives in the same order, sequenced after torch's)."""
+    import numpy as np
+    t0 = time.perf_counter()
+    phi, F, pp = comm.gather_moments(solver)     # (G, N) each, on the host
+    left, right = comm.gather_group_ends(solver)
+    bal = None if dirs else comm.gather_balance(solver)[0]
+    ms = 1e3 * (time.perf_counter() - t0)
+    ours = {"phi": phi.T, "F": F.T, "phi_plus": pp.T, "left": left, "right": right}
+    if bal is not None:
+        ours["balance"] = bal
+    rel = {}
+    for k, v in ours.items():
+        ref = gathered[k].cpu().numpy()
+        scale = max(float(np.abs(ref).max()), 1e-300)
+        rel[k] = float(np.abs(v - ref).max() / scale) if v.shape == ref.shape else float("inf")
+    bitwise = all(np.array_equal(v, gathered[k].cpu().numpy()) for k, v in ours.items())
+    ok = bitwise if not dirs else max(rel.values()) <= 1e-12
+    return {"what": "rt_comm gathers (RCCL in librtsn) vs the torch.distributed gather of the same arrays",
+            "ok": bool(ok), "bitwise": bool(bitwise), "max_rel_diff": rel, "ms": ms,
+            "fields": sorted(ours)}
+
+
+def run_material(p: dict, info, world: int, device, local: int, steps: int, dirs=None, rank: int = 0,
+                 comm=None, comm_error=None) -> dict:
     """The material-temperature coupling (rt_material_*, beyond the reference) on
     the same SL shard: BE steps (the reference's BDF2 diverges on SL within a few
     steps, DESIGN.md §4, which would leave T meaningless; the v/c correction off, as
@@ -646,14 +691,9 @@ def run_material(p: dict, info, world: int, device, local: int, steps: int, dirs
 
     G_total, g_lo, g_hi = info
     q = material_params(p)
-    comm, path = None, "rt_comm_material_step (RCCL in librtsn, stream-ordered)"
-    try:
-        uid = [rtsn.Comm.unique_id() if rank == 0 else None]
-        if world > 1:
-            dist.broadcast_object_list(uid, src=0)
-        comm = rtsn.Comm(world, rank, uid[0], local)
-    except rtsn.RtError as e:
-        path = f"torch.distributed all-reduce on the handle's stream (rt_comm unavailable: {e})"
+    path = "rt_comm_material_step (RCCL in librtsn, stream-ordered)"
+    if comm is None:
+        path = f"torch.distributed all-reduce on the handle's stream (rt_comm unavailable: {comm_error})"
     with make_solver(q, local, info, dirs) as s:  # q(x): each rank's groups or directions, summed
         number = s.material_enable(1.0)
         buf = torch.zeros(q["N"], dtype=torch.float64, device=device)
@@ -679,8 +719,6 @@ def run_material(p: dict, info, world: int, device, local: int, steps: int, dirs
         wall = time.perf_counter() - t0
         T = s.temperature()
         M_local = s.M  # the handle's directions (a direction shard holds 2 (d_hi - d_lo))
-    if comm is not None:
-        comm.close()
     t = torch.tensor([wall], dtype=torch.float64, device=device)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -767,8 +805,15 @@ def main():
     warmup = warmup_steps(args.warmup, fill, tb)
     shards = [shard(args.scaling, args.groups, world, r)[1:] for r in range(world)]
     solver_tb = solver.time_block
-    line, _, _ = run_rank(solver, p, steps, warmup, world, device, info, args.scaling, shards, dirs=dirs)
+    line, _, gathered = run_rank(solver, p, steps, warmup, world, device, info, args.scaling, shards, dirs=dirs)
     line["warmup_requested"] = args.warmup if args.warmup >= 0 else None
+    # one RCCL communicator behind the C ABI for the rest of the run (the gather cross-check
+    # on N > 1 GPUs, the material leg's per-step all-reduce)
+    comm, comm_error = open_comm(world, rank, local) if (world > 1 or args.material_steps > 0) else (None, None)
+    if world > 1:
+        line["rt_comm_gather"] = (rccl_gather_check(comm, solver, gathered, dirs) if comm is not None
+                                  else {"ok": None, "skipped": f"rt_comm unavailable: {comm_error}"})
+    del gathered
     line["roofline"]["traffic"] = load_traffic(args.variant, solver.time_block,
                                                line["roofline"]["algorithmic_bytes_per_launch"])
     solver.close()  # frees the sweep's state before the next run allocates its own
@@ -790,7 +835,10 @@ def main():
                                             f"{5.994 if other == 'corr' else 0.0}, v/c correction "
                                             f"{'on' if other == 'corr' else 'inactive'}), same timing", dirs)
     if args.material_steps > 0:
-        line["material"] = run_material(p, info, world, device, local, args.material_steps, dirs, rank)
+        line["material"] = run_material(p, info, world, device, local, args.material_steps, dirs, rank,
+                                        comm, comm_error)
+    if comm is not None:
+        comm.close()
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(args.variant, args.dt)
         line["reference_config"] = reference_config_timings()

@@ -820,3 +820,29 @@ def test_timed_kernels_multi_line_group(rtsn_mod, mlg_oracle, case, tb, steps):
                 gpu.advance(40)
                 out.append(gpu.ends())
         assert np.array_equal(out[0], out[1])
+
+
+def test_resource_cache_reuse(rtsn_mod):
+    """rt_destroy returns a handle's buffers, staging, stream and events to the process-wide
+    cache and rt_create* takes them back (RTSN_POOL_MB): handles created on recycled resources
+    give bitwise the same results, and recycling them while another handle lives leaves that
+    handle's state untouched."""
+    def run(name, steps=None):
+        ph = rtsn_mod.ParameterHandler(PRM_DIR / name, table_dir=str(PRM_DIR) + "/")
+        params = dict(ph.params) if steps is None else dict(ph.params, max_timesteps=steps)
+        with rtsn_mod.Solver(params) as s:
+            s.solve()
+            return s.ends(), s.moments()[0], s.compute_balance()
+
+    ref = run("llnl_slab_test.prm", 40)
+    ph = rtsn_mod.ParameterHandler(PRM_DIR / "llnl_slab_test.prm", table_dir=str(PRM_DIR) + "/")
+    with rtsn_mod.Solver(dict(ph.params, max_timesteps=40)) as live:
+        live.solve()
+        for name in ("multi_group_equilibrium.prm", "single_group.prm", "llnl_slab_test.prm", "template.prm"):
+            for _ in range(2):
+                run(name, 30)  # other handles come and go on recycled resources
+        again = run("llnl_slab_test.prm", 40)
+        for a, b in zip(ref, again):
+            assert np.array_equal(a, b)
+        assert np.array_equal(live.ends(), ref[0])
+        assert np.array_equal(live.moments()[0], ref[1])

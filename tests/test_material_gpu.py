@@ -427,7 +427,29 @@ def test_bench_material_leg(rtsn_mod, variant):
     sys.path.insert(0, str(REPO))
     import bench
     p = bench.slab_params(8, variant, N=20000, M=8)
-    out = bench.run_material(p, (8, 0, 8), 1, torch.device("cuda", 0), 0, 2)
+    comm, err = bench.open_comm(1, 0, 0)
+    assert comm is not None, err
+    out = bench.run_material(p, (8, 0, 8), 1, torch.device("cuda", 0), 0, 2, comm=comm, comm_error=err)
+    comm.close()
     assert out["allreduce"].startswith("rt_comm_material_step")
     assert out["state_finite"] and 0.0 < out["stability_number"] < 2.0
     assert out["T_range_keV"][0] > 0.0
+
+
+def test_bench_rccl_gather_check(rtsn_mod):
+    """bench.rccl_gather_check (the N > 1 bench line's `rt_comm_gather`) on a one-rank
+    communicator: the rt_comm gathers equal bench.gather_results' arrays bitwise."""
+    import torch
+    sys.path.insert(0, str(REPO))
+    import bench
+    p = dict(bench.slab_params(12, "v0", N=3000, M=8), dt=1e-9)
+    dev = torch.device("cuda", 0)
+    comm, err = bench.open_comm(1, 0, 0)
+    assert comm is not None, err
+    with rtsn_mod.Solver(p, device=0, g_lo=0, g_hi=12) as s:
+        s.advance(7)
+        s.finish()
+        gathered = bench.gather_results(s, p["N"], 1, (12, 0, 12), None, dev)
+        out = bench.rccl_gather_check(comm, s, gathered, None)
+    comm.close()
+    assert out["ok"] and out["bitwise"], out
