@@ -172,7 +172,7 @@ REFERENCE_CONFIGS = ("single_group.prm", "multi_group_equilibrium.prm", "llnl_sl
 
 def gpu_rate(params: dict, ts_method: int, rate_steps: int = 1000) -> dict:
     """rate_steps steps of a configuration on the GPU as rt_solve runs them -- the short-line
-    wavefront (one launch per advance) where the lines fit a wave, else the segment
+    wavefront (one launch per advance) where the lines fit a chain of waves, else the segment
     pipeline at the time block rt_solve would pick (rt_plan_time_block) -- the handle
     created and warmed outside the timer, advance + finish + device sync timed: BDF2
     steps/s and cell-angle-group updates/s, with the number of sweep launches (HIP event
@@ -192,7 +192,8 @@ def gpu_rate(params: dict, ts_method: int, rate_steps: int = 1000) -> dict:
         s.synchronize()
     with rtsn.Solver(params) as s:
         schedule(s)
-        path = "wavefront" if s.wavefront_state()["active"] else "segments"
+        wst = s.wavefront_state()
+        path = "wavefront" if wst["active"] else "segments"
         s.set_profiling(True)
         s.synchronize()
         t0 = time.perf_counter()
@@ -206,7 +207,8 @@ def gpu_rate(params: dict, ts_method: int, rate_steps: int = 1000) -> dict:
         tb = s.time_block
     return {"steps": rate_steps, "bdf2_steps_per_s": rate_steps / gpu_s, "updates_per_s": upd_step * rate_steps / gpu_s,
             "ms": 1e3 * gpu_s, "sweep_passes": passes, "path": path,
-            "time_block": None if path == "wavefront" else tb, "state_finite": finite}
+            "time_block": None if path == "wavefront" else tb, "state_finite": finite,
+            **({"cells_per_lane": wst["cells_per_lane"], "waves_per_chain": wst["waves"]} if path == "wavefront" else {})}
 
 
 def llnl_slab_test_rate(ref_configs=None, rate_steps: int = 1000) -> dict:

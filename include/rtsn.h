@@ -234,18 +234,28 @@ rt_status rt_get_pipeline(rt_solver *s, int *on);
  * steps queued but not launched, whether a correction is pending; any NULL skipped. */
 rt_status rt_pipeline_state(rt_solver *s, long long *lag_steps, int *queued_steps, int *pending);
 rt_status rt_get_time_block(rt_solver *s, int *steps_per_pass);
-/* Short lines: a wavefront over (cell, time level) with lanes over cells -- a line (with the
- * reflective left boundary: a mu < 0 line and its mirror) in one wave, C cells per lane in
- * registers, every step of an advance in one launch (up to 65536 steps per launch), the
- * upwind recurrence carried lane to lane by a DPP shift each tick: for lines of up to
- * 64 C cells (reflective: 32 C), C = 1, 2, 4 or 8.  Results are bitwise those of the
- * pipelined segment schedule.  mode 0: off; 1 (default): used when the line fits and the
- * caller set neither a time block (rt_set_time_block) nor a schedule (rt_set_pipeline);
- * 2: used whenever the line fits.  RTSN_WAVEFRONT=0|2 at creation sets 0 or 2. */
+/* Short and mid-length lines: a wavefront over (cell, time level) with lanes over cells -- a
+ * line (with the reflective left boundary: a mu < 0 line and its mirror) is a chain of lanes
+ * of one workgroup, C cells per lane in registers, every step of an advance in one launch (up
+ * to 65536 steps per launch), the upwind recurrence carried lane to lane by a DPP shift each
+ * tick: one wave with the fewest cells per lane (C = 1, 2, 4, 8) while the line fits 64 C
+ * cells (reflective: 32 C), else a chain of up to rt_set_wavefront_waves' waves (default 8,
+ * lines of up to 4096 cells, reflective 2048) handing the carried state from wave to wave
+ * through LDS.  Results are bitwise those of the pipelined segment schedule, whatever C and
+ * the waves per chain.  mode 0: off; 1 (default): used when the line fits, the caller set
+ * neither a time block (rt_set_time_block) nor a schedule (rt_set_pipeline), and -- for a
+ * chain of several waves -- the chains need at most two waves per SIMD; 2: used whenever the
+ * line fits.  RTSN_WAVEFRONT=0|2 at creation sets 0 or 2. */
 rt_status rt_set_wavefront(rt_solver *s, int mode);
 /* *mode as set; *active: the next rt_advance takes the wavefront; *cells_per_lane: C for
  * this handle's lines (0: too long for a wave).  Any NULL skipped. */
 rt_status rt_get_wavefront(rt_solver *s, int *mode, int *active, int *cells_per_lane);
+/* Waves a wavefront chain may span, 1..8 (default 8; 1 = one wave per chain, lines of up to
+ * 512 cells).  The chain's lanes per line are ceil(N / C); replaces nothing in the reference
+ * (its sweep is serial, solver.cpp:700-717).  RTSN_WAVE_WAVES=1..8 at creation sets it. */
+rt_status rt_set_wavefront_waves(rt_solver *s, int max_waves);
+/* *max_waves as set; *waves_per_chain: this handle's chain (0: too long).  NULLs skipped. */
+rt_status rt_get_wavefront_waves(rt_solver *s, int *max_waves, int *waves_per_chain);
 /* Waves per segment of a pipelined BDF2 pass of 8, 10, 12, 16 or 20 steps: 1 runs
  * all levels in one wave; 2 (or 4, T divisible by 4) shares them between the waves of
  * a workgroup through LDS; 0 (default) = 2 at T = 20 (its one-wave kernel leans on

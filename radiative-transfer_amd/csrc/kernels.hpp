@@ -105,9 +105,20 @@ hipError_t sweep_occupancy(int scheme, int T, int level_waves, int *waves_per_cu
 hipError_t coupled_occupancy(int scheme, int *waves_per_cu);  // the material-coupled pass (T = 1)
 hipError_t launch_fold(int KC, const FoldArgs &f, hipStream_t st);
 // short lines (kernels_wave.hip): nsteps full steps of every line in one launch, lanes over
-// cells (a.Gl, a.H set: lines ell < H Gl); cells per lane C for lines of N cells (0: too long)
-int wavefront_cells_per_lane(int N, bool reflective);
-hipError_t launch_wavefront(int scheme, const SegArgs &a, int nsteps, hipStream_t st);
+// cells (a.Gl, a.H set: lines ell < H Gl).  A line (reflective: a line pair) is a chain of
+// `lanes` lanes per line holding C cells each, on `waves` waves of one workgroup (C = 0: too
+// long for kWaveMaxWaves waves); waves > 1 hand the chain over through LDS once per tick
+// and meet at a barrier every kWaveBlockTicks ticks
+constexpr int kWaveMaxWaves = 8;
+#ifndef RT_WAVE_BLOCK
+#define RT_WAVE_BLOCK 8
+#endif
+constexpr int kWaveBlockTicks = RT_WAVE_BLOCK;
+struct WavePlan {
+  int C, waves, lanes;
+};
+WavePlan wavefront_plan(int N, bool reflective, int max_waves);
+hipError_t launch_wavefront(int scheme, const WavePlan &p, const SegArgs &a, int nsteps, hipStream_t st);
 hipError_t launch_init_state(double2 *E, const double *lineB, const Geometry &g, hipStream_t st);
 // reference-layout psi / ends of the cells [c0, c0 + nc) (ends: node 0 block, then node 1)
 hipError_t launch_export_psi(const double2 *E, double *psi, const Geometry &g, int c0, int nc, hipStream_t st);

@@ -6,17 +6,26 @@
 // segment and time block -- for the reference's own configurations (llnl_slab_test: 50
 // cells, single_group / multi_group_equilibrium: 100) that is microseconds of dependent
 // latency per step on a handful of workgroups.  Here a line (or, with the reflective left
-// boundary, a mu < 0 line followed by its mu > 0 mirror) lives in ONE wave: lane j holds
-// C consecutive cells of the chain in registers and, at tick tau, runs time level
-// t = tau - j of its cells -- the upwind recurrence x_{k+1} = A x_k + b_k of every level is
-// carried across lanes by one DPP lane shift of the carried state per tick (wave_shr:1), so
-// level t of lane j starts from lane j - 1's exit state of the same level, produced one tick
-// earlier.  n steps of an L-lane chain take n + L - 1 ticks of C cell maps each; the state
-// is read once and written once per launch.
+// boundary, a mu < 0 line followed by its mu > 0 mirror) is a CHAIN of lanes of one
+// workgroup: chain lane g holds C consecutive cells in registers and, at tick tau, runs
+// time level t = tau - g of its cells -- the upwind recurrence x_{k+1} = A x_k + b_k of
+// every level is carried across lanes by one DPP lane shift of the carried state per tick
+// (wave_shr:1), so level t of lane g starts from lane g - 1's exit state of the same level,
+// produced one tick earlier.  n steps of an L-lane chain take n + L - 1 ticks of C cell
+// maps each; the state is read once and written once per launch.
+//
+// A chain longer than one wave (up to kWaveMaxWaves waves) crosses wave boundaries through
+// LDS: wave w runs a block of ticks (plus the read-ahead) behind wave w - 1, lane 63 of wave
+// w - 1 appends its exit state to a ring in LDS every tick, and lane 0 of wave w takes it --
+// one tick after it was produced in chain time, a block of ticks later in wall time -- as the
+// `old` operand of its DPP shifts.  The waves meet at one barrier per block of ticks (not per
+// tick), so a 100-cell line runs one cell per lane on two waves instead of two cells per
+// lane on one: half the dependent instructions per tick.
 //
 // Same arithmetic per (cell, level) as the pipelined segment pass (the per-line affine map
 // of cell.hpp, exact carries; the reflective mu > 0 head cell by the reference's algebra
-// with the mirror's per-substep outflows, sweep_device.hpp head_cell): bitwise equal to it.
+// with the mirror's per-substep outflows, sweep_device.hpp head_cell): bitwise equal to it,
+// whatever the cells per lane and waves per chain.
 #include <hip/hip_runtime.h>
 
 #include <type_traits>
@@ -27,8 +36,8 @@
 namespace rtamd {
 
 // DPP wave_shr:1 (gfx9 family): lane l receives lane l - 1's value; lane 0 has no source and
-// keeps `old` -- the chain head's inflow state, loop-carried in the same registers, so the
-// head needs no per-tick select or copy.
+// keeps `old` -- the chain head's inflow state, loop-carried in the same registers (or the
+// previous wave's exit state from LDS), so the head needs no per-tick select or copy.
 __device__ __forceinline__ double lane_shift_up(double old, double v) {
   const unsigned long long b = __builtin_bit_cast(unsigned long long, v);
   const unsigned long long o = __builtin_bit_cast(unsigned long long, old);
@@ -40,30 +49,53 @@ __device__ __forceinline__ double lane_shift_up(double old, double v) {
                                         static_cast<unsigned int>(lo));
 }
 
-// grid: one wave per line (mu < 0 lines then mu > 0 lines, ell < H Gl) -- or, PAIR (the
-// reflective left boundary), one wave per line pair ell (lanes [0, Lw) the mu < 0 line,
-// [Lw, 2 Lw) its mirror).  Lw = lanes per line = ceil(N / C) <= 64 (PAIR: 32).  nsteps full
-// steps from the stored state.  Padding cells (the last lane of a line holds N mod C real
-// cells) feed nothing real -- except, with PAIR and N mod C != 0 (PAD), those of the mu < 0
-// line, whose exit state is the mirror head's inflow: there they pass X through by a select
-// (a per-lane branch would make every tick divergent).
-template <int S, int C, bool PAIR, bool PAD>
-__global__ __launch_bounds__(64) void wavefront_kernel(SegArgs a, int nsteps, int Lw) {
+// Chain hand-over between waves (MULTI).  Lane 63 of wave w - 1 stores its exit state of
+// chain tick s in ring slot s (during its tick s + 1, after that tick's shifts, so that no
+// wait for a ring read ever waits on a fresh store); lane 0 of wave w reads slot s
+// kWavePrefetch ticks before it needs it (at tick s + 1), so the LDS latency hides behind
+// whole ticks of FMAs.  The waves of a chain meet at a barrier every B = kWaveBlockTicks
+// ticks of wall time (one tick stream per wave, the barrier inside it), and wave w runs
+// kWaveSkew = B + kWavePrefetch chain ticks behind wave w - 1: every slot a wave reads in a
+// block was stored in an earlier block; 4 blocks of slots keep a block's stores clear of
+// the slots still to be read.
+#ifndef RT_WAVE_PREFETCH
+#define RT_WAVE_PREFETCH 2
+#endif
+constexpr int kWavePrefetch = RT_WAVE_PREFETCH;
+constexpr int kWaveSkew = kWaveBlockTicks + kWavePrefetch;
+constexpr int kWaveRing = 4 * kWaveBlockTicks;
+static_assert((kWaveBlockTicks & (kWaveBlockTicks - 1)) == 0 && (kWaveRing & (kWaveRing - 1)) == 0,
+              "block and ring indices are masks");
+static_assert(kWavePrefetch >= 1 && kWaveSkew + kWaveBlockTicks + 1 <= kWaveRing, "ring too short for the skew");
+
+// grid: one workgroup per line (mu < 0 lines then mu > 0 lines, ell < H Gl) -- or, PAIR (the
+// reflective left boundary), one per line pair ell (chain lanes [0, Lw) the mu < 0 line,
+// [Lw, 2 Lw) its mirror).  Lw = lanes per line = ceil(N / C); the chain's lanes fill
+// blockDim.x / 64 waves (MULTI; one wave otherwise).  nsteps full steps from the stored
+// state.  Padding cells (the last lane of a line holds N mod C real cells) feed nothing
+// real -- except, with PAIR and N mod C != 0 (PAD), those of the mu < 0 line, whose exit
+// state is the mirror head's inflow: there they pass X through by a select (a per-lane
+// branch would make every tick divergent).
+template <int S, int C, bool PAIR, bool PAD, bool MULTI>
+__global__ __launch_bounds__(MULTI ? 64 * kWaveMaxWaves : 64) void wavefront_kernel(SegArgs a, int nsteps, int Lw) {
   constexpr int K = SchemeDim<S>::K, WN = map_count<S>();
-  const int lane = threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  const int w = MULTI ? __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6)) : 0;
+  const int nw = MULTI ? static_cast<int>(blockDim.x >> 6) : 1;
+  const int g = w * 64 + lane;  // chain lane
   const int nl = a.H * a.Gl;
   int half, ell, j;
   if (PAIR) {
     ell = blockIdx.x;
-    half = lane < Lw ? 0 : 1;
-    j = lane - half * Lw;
+    half = g < Lw ? 0 : 1;
+    j = g - half * Lw;
   } else {
     half = static_cast<int>(blockIdx.x) / nl;
     ell = static_cast<int>(blockIdx.x) % nl;
-    j = lane;
+    j = g;
   }
-  const int used = PAIR ? 2 * Lw : Lw;  // lanes holding cells; the chain's lane index is `lane`
-  const bool real = lane < used;
+  const int used = PAIR ? 2 * Lw : Lw;  // chain lanes holding cells
+  const bool real = g < used;
   const size_t stride = static_cast<size_t>(a.Lpad);
   double2 *Eh = a.E + static_cast<size_t>(half) * a.Nrow * stride + ell;
 
@@ -86,7 +118,7 @@ __global__ __launch_bounds__(64) void wavefront_kernel(SegArgs a, int nsteps, in
   // are issued, so that they are in flight together)
 #pragma unroll
   for (int n = 0; n < WN; ++n) asm volatile("" : "+v"(W[n]));
-  const bool refl_head = PAIR && half == 1 && j == 0;  // one lane of a pair wave
+  const bool refl_head = PAIR && half == 1 && j == 0;  // one lane of a pair chain
   LineConst L{};
   if (refl_head) {
     const double *lcp = a.lc + static_cast<size_t>(half) * LC_COUNT * stride + ell;
@@ -95,7 +127,7 @@ __global__ __launch_bounds__(64) void wavefront_kernel(SegArgs a, int nsteps, in
   }
 
   // Xin: the state each lane receives at its tick -- lane - 1's exit state of the same level;
-  // lane 0's stays the chain head's inflow state (solver.cpp:695-697), the mu < 0 line's
+  // chain lane 0's is the chain head's inflow state (solver.cpp:695-697), the mu < 0 line's
   // with PAIR.  Every lane runs its cells every tick (no divergent branch, no register
   // shuffling at a join); only lanes at a level in [0, nsteps) commit their nodes, and
   // an idle lane's exit state only ever reaches idle lanes.
@@ -107,30 +139,66 @@ __global__ __launch_bounds__(64) void wavefront_kernel(SegArgs a, int nsteps, in
 #pragma unroll
     for (int r = 0; r < K; ++r) X[r] = Xin[r];
   }
-  // ticks [used, nsteps) have every lane of the chain at a level in [1, nsteps): that
-  // stretch (all but the chain's fill and drain) runs without the commit masks, and there
-  // component 0 of the received state (the upwind cell's node before level t, which the
-  // map copies from dout) is not shifted in: it is the upwind cell's output node of level
-  // t - 1, which this lane received one tick earlier as component K - 1 (CN, BDF2; the
-  // chain head's inflow state has equal components) -- one DPP lane shift fewer per tick
+  // MULTI: rd = where lane 0 of this wave takes its `old` operands -- wave 0 a fixed slot
+  // holding the head's inflow state (mask 0), wave w the ring of boundary w - 1
+  extern __shared__ double lds_ring[];
+  const double *rd = lds_ring;
+  double *wr = lds_ring;
+  int rd_mask = 0;
+  if constexpr (MULTI) {
+    if (threadIdx.x < K) lds_ring[threadIdx.x] = Xin[threadIdx.x];
+    for (int i = threadIdx.x; i < (nw - 1) * kWaveRing * K; i += blockDim.x) lds_ring[K + i] = 0.0;
+    rd = w == 0 ? lds_ring : lds_ring + K + static_cast<size_t>(w - 1) * kWaveRing * K;
+    rd_mask = w == 0 ? 0 : kWaveRing - 1;
+    wr = lds_ring + K + static_cast<size_t>(w) * kWaveRing * K;
+    __syncthreads();
+  }
+  const bool writer = MULTI && lane == 63 && w < nw - 1;
+  // the ticks between the chain's fill and drain (every lane of this wave at a level in
+  // [1, nsteps)) run without the commit masks, and there component 0 of the received state
+  // (the upwind cell's node before level t, which the map copies from dout) is not shifted
+  // in: it is the upwind cell's output node of level t - 1, which this lane received one
+  // tick earlier as component K - 1 (CN, BDF2; the chain head's inflow state has equal
+  // components) -- one DPP lane shift fewer per tick
+  const auto publish = [&](int tick) {  // MULTI: lane 63's exit state of chain tick `tick`
+#pragma unroll
+    for (int r = 0; r < K; ++r) wr[(tick & (kWaveRing - 1)) * K + r] = X[r];
+  };
+  // MULTI: lane 0's received states for the next kWavePrefetch ticks (nxt[0]: this tick's),
+  // carried along the wave's whole tick stream; wave w's chain tick `tick` runs at wall tick
+  // tick + w kWaveSkew, and a barrier follows every wall tick B - 1 mod B
+  double nxt[kWavePrefetch][K];
+  const int wskew = w * kWaveSkew;
   const auto run = [&](int tick0, int tick1, auto masked) {
     const auto body = [&](int tick) {
+      double o[K];
+#pragma unroll
+      for (int r = 0; r < K; ++r) o[r] = MULTI ? nxt[0][r] : Xin[r];
       if constexpr (K > 1 && !decltype(masked)::value) {
-        // the shift of component K - 1 keeps Xin[0] as its `old` (lane 0: the head's
-        // inflow state, all of whose components are equal), so the two registers trade
+        // the shift of component K - 1 keeps Xin[0] as its `old` (lane 0 of the chain: the
+        // head's inflow state, all of whose components are equal), so the two registers trade
         // roles each tick and two ticks per iteration need no copy
         const double x0 = Xin[K - 1];
-        Xin[K - 1] = lane_shift_up(Xin[0], X[K - 1]);
+        Xin[K - 1] = lane_shift_up(MULTI ? o[K - 1] : Xin[0], X[K - 1]);
 #pragma unroll
-        for (int r = 1; r < K - 1; ++r) Xin[r] = lane_shift_up(Xin[r], X[r]);
+        for (int r = 1; r < K - 1; ++r) Xin[r] = lane_shift_up(o[r], X[r]);
         Xin[0] = x0;
       } else {
 #pragma unroll
-        for (int r = 0; r < K; ++r) Xin[r] = lane_shift_up(Xin[r], X[r]);
+        for (int r = 0; r < K; ++r) Xin[r] = lane_shift_up(o[r], X[r]);
+      }
+      if constexpr (MULTI) {  // after the shifts, which wait for an earlier tick's read
+        if (writer && tick > 0) publish(tick - 1);  // X: the previous tick's exit state
+#pragma unroll
+        for (int q = 0; q + 1 < kWavePrefetch; ++q)
+#pragma unroll
+          for (int r = 0; r < K; ++r) nxt[q][r] = nxt[q + 1][r];
+#pragma unroll
+        for (int r = 0; r < K; ++r) nxt[kWavePrefetch - 1][r] = rd[((tick + kWavePrefetch - 1) & rd_mask) * K + r];
       }
       bool active = true;
       if constexpr (decltype(masked)::value) {
-        const int t = tick - lane;
+        const int t = tick - g;
         active = real && t >= 0 && t < nsteps;
       }
 #pragma unroll
@@ -162,6 +230,9 @@ __global__ __launch_bounds__(64) void wavefront_kernel(SegArgs a, int nsteps, in
         ein[c] = active ? oi : ein[c];
         eout[c] = active ? oo : eout[c];
       }
+      if constexpr (MULTI) {
+        if (((tick + wskew) & (kWaveBlockTicks - 1)) == kWaveBlockTicks - 1) __syncthreads();
+      }
     };
     // two ticks per iteration: the loop-carried renames of X, ein and eout then cancel
     int tick = tick0;
@@ -172,13 +243,28 @@ __global__ __launch_bounds__(64) void wavefront_kernel(SegArgs a, int nsteps, in
     if (tick < tick1) body(tick);
   };
   const int ticks = nsteps + used - 1;
-  if (nsteps > used) {
-    run(0, used, std::true_type{});
-    run(used, nsteps, std::false_type{});
-    run(nsteps, ticks, std::true_type{});
+  // this wave's unmasked chain ticks: its real lanes all at a level in [1, nsteps)
+  const int u_lo = min(64 * w + 63, used - 1) + 1, u_hi = max(u_lo, nsteps + 64 * w);
+  int barriers = 0;  // MULTI: the same count for every wave
+  if constexpr (MULTI) {
+    const int total = (ticks + (nw - 1) * kWaveSkew + kWaveBlockTicks - 1) / kWaveBlockTicks;
+    barriers = total - wskew / kWaveBlockTicks;
+    for (int i = 0; i < wskew / kWaveBlockTicks; ++i) __syncthreads();  // wall ticks before the chain's
+#pragma unroll
+    for (int q = 0; q < kWavePrefetch; ++q)
+#pragma unroll
+      for (int r = 0; r < K; ++r) nxt[q][r] = rd[((q - 1) & rd_mask) * K + r];
+    // barriers inside the stream: wall ticks wskew .. wskew + ticks - 1 that are B - 1 mod B
+    barriers -= (wskew + ticks) / kWaveBlockTicks - wskew / kWaveBlockTicks;
+  }
+  if (u_lo < u_hi && u_hi <= ticks) {
+    run(0, u_lo, std::true_type{});
+    run(u_lo, u_hi, std::false_type{});
+    run(u_hi, ticks, std::true_type{});
   } else {
     run(0, ticks, std::true_type{});
   }
+  for (int i = 0; i < barriers; ++i) __syncthreads();  // MULTI: wall ticks after the chain's
 #pragma unroll
   for (int c = 0; c < C; ++c) {
     const int k = j * C + c;
@@ -187,16 +273,36 @@ __global__ __launch_bounds__(64) void wavefront_kernel(SegArgs a, int nsteps, in
 }
 
 template <int S, bool PAIR>
-static hipError_t launch_wave_s(int C, const SegArgs &a, int nsteps, int Lw, int grid, hipStream_t st) {
-  const bool pad = PAIR && a.N % C != 0;
-  switch (C) {
-#define RT_WAVE_CASE(c)                                                                                      \
-  case c:                                                                                                    \
-    if (pad)                                                                                                 \
-      hipLaunchKernelGGL((wavefront_kernel<S, c, PAIR, PAIR && (c > 1)>), dim3(grid), dim3(64), 0, st, a, nsteps, \
-                         Lw);                                                                                \
-    else                                                                                                     \
-      hipLaunchKernelGGL((wavefront_kernel<S, c, PAIR, false>), dim3(grid), dim3(64), 0, st, a, nsteps, Lw); \
+static hipError_t launch_wave_s(const WavePlan &p, const SegArgs &a, int nsteps, int grid, hipStream_t st) {
+  const bool pad = PAIR && a.N % p.C != 0;
+  const int Lw = p.lanes;
+  if (p.waves > 1) {
+    const size_t lds = sizeof(double) * SchemeDim<S>::K * (1 + static_cast<size_t>(p.waves - 1) * kWaveRing);
+    switch (p.C) {
+#define RT_WAVE_CASE(c)                                                                                          \
+  case c:                                                                                                        \
+    if (pad)                                                                                                     \
+      hipLaunchKernelGGL((wavefront_kernel<S, c, PAIR, PAIR && (c > 1), true>), dim3(grid), dim3(64 * p.waves), \
+                         lds, st, a, nsteps, Lw);                                                                \
+    else                                                                                                         \
+      hipLaunchKernelGGL((wavefront_kernel<S, c, PAIR, false, true>), dim3(grid), dim3(64 * p.waves), lds, st, a, \
+                         nsteps, Lw);                                                                            \
+    break;
+      RT_WAVE_CASE(1) RT_WAVE_CASE(2) RT_WAVE_CASE(4) RT_WAVE_CASE(8)
+#undef RT_WAVE_CASE
+      default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+  }
+  switch (p.C) {
+#define RT_WAVE_CASE(c)                                                                                          \
+  case c:                                                                                                        \
+    if (pad)                                                                                                     \
+      hipLaunchKernelGGL((wavefront_kernel<S, c, PAIR, PAIR && (c > 1), false>), dim3(grid), dim3(64), 0, st, a, \
+                         nsteps, Lw);                                                                            \
+    else                                                                                                         \
+      hipLaunchKernelGGL((wavefront_kernel<S, c, PAIR, false, false>), dim3(grid), dim3(64), 0, st, a, nsteps,   \
+                         Lw);                                                                                    \
     break;
     RT_WAVE_CASE(1) RT_WAVE_CASE(2) RT_WAVE_CASE(4) RT_WAVE_CASE(8)
 #undef RT_WAVE_CASE
@@ -205,33 +311,43 @@ static hipError_t launch_wave_s(int C, const SegArgs &a, int nsteps, int Lw, int
   return hipGetLastError();
 }
 
-// lanes of a chain: 64, a reflective pair 2 x 32
-int wavefront_cells_per_lane(int N, bool reflective) {
-  const int lanes = reflective ? 32 : 64;
-  const int c = (N + lanes - 1) / lanes;
-  for (int C : {1, 2, 4, 8})
-    if (c <= C) return C;
-  return 0;  // too long: the segment pipeline
+// One wave per chain whenever the chain fits 64 lanes of up to 8 cells (the fewest cells per
+// lane); otherwise the fewest cells per lane whose chain fits max_waves waves.  A chain
+// over several waves ticks ~2.3x slower than one wave (multi_group_equilibrium, 1000 steps:
+// 2 waves x 1 cell per lane 250 us, 1 wave x 2 cells 157 us; profiles/r03ah_rates.jsonl),
+// so more cells per lane on one wave win while they fit.  max_waves = 1: one wave only.
+WavePlan wavefront_plan(int N, bool reflective, int max_waves) {
+  max_waves = max_waves < 1 ? 1 : (max_waves > kWaveMaxWaves ? kWaveMaxWaves : max_waves);
+  if (N < 1) return WavePlan{0, 0, 0};
+  for (int waves_cap : {1, max_waves})
+    for (int C : {1, 2, 4, 8}) {
+      const int Lw = (N + C - 1) / C;
+      const int used = reflective ? 2 * Lw : Lw;
+      const int waves = (used + 63) / 64;
+      if (waves <= waves_cap) return WavePlan{C, waves, Lw};
+    }
+  return WavePlan{0, 0, 0};  // too long: the segment pipeline
 }
 
-hipError_t launch_wavefront(int scheme, const SegArgs &a, int nsteps, hipStream_t st) {
+hipError_t launch_wavefront(int scheme, const WavePlan &p, const SegArgs &a, int nsteps, hipStream_t st) {
   const bool pair = a.reflective != 0;
-  const int C = wavefront_cells_per_lane(a.N, pair);
   const int nl = a.H * a.Gl;
-  if (C == 0 || nl <= 0 || nsteps < 0) return hipErrorInvalidValue;
+  if (p.C == 0 || p.waves < 1 || p.waves > kWaveMaxWaves || nl <= 0 || nsteps < 0) return hipErrorInvalidValue;
+  // the chain must fit the plan's waves: checked here, since the kernel indexes by it
+  const int used = pair ? 2 * p.lanes : p.lanes;
+  if (p.lanes * p.C < a.N || used > 64 * p.waves || used <= 64 * (p.waves - 1)) return hipErrorInvalidValue;
   if (nsteps == 0) return hipSuccess;
-  const int Lw = (a.N + C - 1) / C;
   const int grid = pair ? nl : 2 * nl;
   switch (scheme) {
     case SCHEME_BE:
-      return pair ? launch_wave_s<SCHEME_BE, true>(C, a, nsteps, Lw, grid, st)
-                  : launch_wave_s<SCHEME_BE, false>(C, a, nsteps, Lw, grid, st);
+      return pair ? launch_wave_s<SCHEME_BE, true>(p, a, nsteps, grid, st)
+                  : launch_wave_s<SCHEME_BE, false>(p, a, nsteps, grid, st);
     case SCHEME_CN:
-      return pair ? launch_wave_s<SCHEME_CN, true>(C, a, nsteps, Lw, grid, st)
-                  : launch_wave_s<SCHEME_CN, false>(C, a, nsteps, Lw, grid, st);
+      return pair ? launch_wave_s<SCHEME_CN, true>(p, a, nsteps, grid, st)
+                  : launch_wave_s<SCHEME_CN, false>(p, a, nsteps, grid, st);
     default:
-      return pair ? launch_wave_s<SCHEME_BDF2, true>(C, a, nsteps, Lw, grid, st)
-                  : launch_wave_s<SCHEME_BDF2, false>(C, a, nsteps, Lw, grid, st);
+      return pair ? launch_wave_s<SCHEME_BDF2, true>(p, a, nsteps, grid, st)
+                  : launch_wave_s<SCHEME_BDF2, false>(p, a, nsteps, grid, st);
   }
 }
 

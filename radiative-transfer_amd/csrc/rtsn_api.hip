@@ -225,6 +225,7 @@ struct rt_solver {
   int pipe = 1;                  // 0 off, 1 auto (runs long enough to fill), 2 always
   bool pipe_set = false;         // the caller chose the schedule (rt_set_pipeline)
   int wave = 1;                  // short lines, one launch per advance (rt_set_wavefront): 0 off, 1 auto, 2 on
+  int wave_max = kWaveMaxWaves;  // waves a wavefront chain may span (rt_set_wavefront_waves)
   std::vector<long long> tau;    // full steps completed per chain position
   long long target = 0;          // full steps every position must reach
   long long pipe_base = 0;       // tau of every position when the pipeline started
@@ -866,6 +867,8 @@ static rt_status create_impl(const rt_params *pin, int g_lo, int g_hi, int d_lo,
     }
   if (const char *wv = std::getenv("RTSN_WAVEFRONT"))  // experiments: "0" off, "2" on for every short line
     if (!std::strcmp(wv, "0") || !std::strcmp(wv, "2")) h->wave = wv[0] - '0';
+  if (const char *ww = std::getenv("RTSN_WAVE_WAVES"))  // experiments: waves per wavefront chain, 1..8
+    if (std::atoi(ww) >= 1 && std::atoi(ww) <= kWaveMaxWaves) h->wave_max = std::atoi(ww);
   if (const char *lw = std::getenv("RTSN_LEVEL_WAVES"))  // experiments: only "1", "2" or "4" are read
     if (!std::strcmp(lw, "1") || !std::strcmp(lw, "2") || !std::strcmp(lw, "4")) h->level_waves = lw[0] - '0';
   h->cus = prop.multiProcessorCount;
@@ -1194,12 +1197,27 @@ static rt_status finalize(rt_solver *s) {
 }
 
 // Short lines (kernels_wave.hip): every step of an advance in one launch per chunk of
-// steps, lanes over cells -- by default (rt_set_wavefront 1) when the line fits a wave and
-// the caller chose neither a time block nor a schedule, always with rt_set_wavefront 2.
+// steps, lanes over cells -- by default (rt_set_wavefront 1) when the line fits a
+// workgroup's chain and the caller chose neither a time block nor a schedule, always with
+// rt_set_wavefront 2.
+static WavePlan wave_plan(const rt_solver *s) {
+  return wavefront_plan(s->p.N, s->p.bc_left_indicator == 2, s->wave_max);
+}
+
+// Auto (mode 1) takes a chain of several waves while the chains need at most two waves per
+// SIMD: mid-length lines run 4-7x faster as chains than as segment passes there (1000 BDF2
+// steps, N = 600-4000 cells: 4 groups 0.46-1.5 ms vs 2.7-6.6 ms, 124 groups, i.e. 1984 waves,
+// 0.67-1.7 ms vs 4.0-8.1 ms; profiles/r03ai_mid.jsonl).  Beyond, the chains time-share the
+// SIMDs, and the segment pipeline's full-chip passes (28 FMAs per cell and level at ~90% of
+// the FP64 issue rate) carry the same work with less overhead per cell.
 static bool use_wavefront(const rt_solver *s) {
   if (s->material || s->wave == 0) return false;
-  if (wavefront_cells_per_lane(s->p.N, s->p.bc_left_indicator == 2) == 0) return false;
-  return s->wave == 2 || (!s->T_set && !s->pipe_set);
+  const WavePlan p = wave_plan(s);
+  if (p.C == 0) return false;
+  if (s->wave == 2) return true;
+  if (s->T_set || s->pipe_set) return false;
+  const long long chains = static_cast<long long>(s->H) * s->Gl * (s->p.bc_left_indicator == 2 ? 1 : 2);
+  return p.waves == 1 || chains * p.waves <= 8LL * s->cus;
 }
 
 constexpr int kWaveMaxSteps = 1 << 16;  // steps per wavefront launch (bounds one launch's length)
@@ -1214,7 +1232,7 @@ static rt_status wave_advance(rt_solver *s, int nsteps) {
     hipEvent_t e1;
     rt_status st = event_begin(s, &e1);
     if (st) return st;
-    HIP_TRY(s, launch_wavefront(s->scheme, a, m, s->stream));
+    HIP_TRY(s, launch_wavefront(s->scheme, wave_plan(s), a, m, s->stream));
     if ((st = event_end(s, e1))) return st;
     ++s->state_version;
     for (long long &t : s->tau) t += m;
@@ -2109,7 +2127,21 @@ extern "C" rt_status rt_get_wavefront(rt_solver *s, int *mode, int *active, int 
   if (!s) return fail(nullptr, RT_ERR_ARG, "rt_get_wavefront: NULL handle");
   if (mode) *mode = s->wave;
   if (active) *active = use_wavefront(s) ? 1 : 0;
-  if (cells_per_lane) *cells_per_lane = wavefront_cells_per_lane(s->p.N, s->p.bc_left_indicator == 2);
+  if (cells_per_lane) *cells_per_lane = wave_plan(s).C;
+  return RT_OK;
+}
+
+extern "C" rt_status rt_set_wavefront_waves(rt_solver *s, int max_waves) {
+  if (!s) return fail(nullptr, RT_ERR_ARG, "rt_set_wavefront_waves: NULL handle");
+  if (max_waves < 1 || max_waves > kWaveMaxWaves) return fail(s, RT_ERR_ARG, "rt_set_wavefront_waves: 1..8 waves");
+  s->wave_max = max_waves;
+  return RT_OK;
+}
+
+extern "C" rt_status rt_get_wavefront_waves(rt_solver *s, int *max_waves, int *waves_per_chain) {
+  if (!s) return fail(nullptr, RT_ERR_ARG, "rt_get_wavefront_waves: NULL handle");
+  if (max_waves) *max_waves = s->wave_max;
+  if (waves_per_chain) *waves_per_chain = wave_plan(s).waves;
   return RT_OK;
 }
 

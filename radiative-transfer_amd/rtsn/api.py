@@ -125,6 +125,8 @@ def lib():
         L.rt_get_level_waves.argtypes = [vp, C.POINTER(C.c_int)]
         L.rt_set_wavefront.argtypes = [vp, C.c_int]
         L.rt_get_wavefront.argtypes = [vp, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)]
+        L.rt_set_wavefront_waves.argtypes = [vp, C.c_int]
+        L.rt_get_wavefront_waves.argtypes = [vp, C.POINTER(C.c_int), C.POINTER(C.c_int)]
         L.rt_material_enable.argtypes = [vp, C.c_double, dp]
         L.rt_material_sweep.argtypes = [vp, vp]
         L.rt_material_update.argtypes = [vp, vp]
@@ -559,11 +561,24 @@ class Solver:
     def wavefront(self, mode):
         _check(lib().rt_set_wavefront(self._h, int(mode)), "rt_set_wavefront", self._h)
 
+    @property
+    def wavefront_waves(self) -> int:
+        """Waves a wavefront chain may span, 1..8 (rt_set_wavefront_waves; default 8)."""
+        v = C.c_int()
+        _check(lib().rt_get_wavefront_waves(self._h, C.byref(v), None), "rt_get_wavefront_waves", self._h)
+        return v.value
+
+    @wavefront_waves.setter
+    def wavefront_waves(self, n):
+        _check(lib().rt_set_wavefront_waves(self._h, int(n)), "rt_set_wavefront_waves", self._h)
+
     def wavefront_state(self) -> dict:
-        """{"mode", "active" (the next advance takes the wavefront), "cells_per_lane" (0: too long)}."""
-        m, a, c = C.c_int(), C.c_int(), C.c_int()
+        """{"mode", "active" (the next advance takes the wavefront), "cells_per_lane" (0: too
+        long), "waves" (per chain; 0: too long)}."""
+        m, a, c, w = C.c_int(), C.c_int(), C.c_int(), C.c_int()
         _check(lib().rt_get_wavefront(self._h, C.byref(m), C.byref(a), C.byref(c)), "rt_get_wavefront", self._h)
-        return {"mode": m.value, "active": bool(a.value), "cells_per_lane": c.value}
+        _check(lib().rt_get_wavefront_waves(self._h, None, C.byref(w)), "rt_get_wavefront_waves", self._h)
+        return {"mode": m.value, "active": bool(a.value), "cells_per_lane": c.value, "waves": w.value}
 
     def plan_schedule(self, nsteps: int) -> dict:
         """rt_plan_schedule: the pipelined BDF2 schedule rt_solve picks for nsteps on this

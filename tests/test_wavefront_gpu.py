@@ -5,9 +5,10 @@ Same arithmetic per (cell, level) as the pipelined segment pass -- the per-line 
 with exact carries, the reflective mu > 0 head by the reference's algebra -- so its node
 array must equal the pipelined schedule's BITWISE (the segment kernels are pinned to the
 oracle by test_gpu_parity.py), for every scheme, boundary pair and line length around the
-lane-count edges (C = 1, 2, 4, 8 cells per lane on 64 lanes, 32 per line when reflective); and
-through the reference's own configurations it runs by default (rt_solve with no block or
-schedule chosen), which test_gpu_parity.test_reference_configs checks against the oracle.
+lane-count edges (C = 1, 2, 4, 8 cells per lane; a chain of up to 8 waves handing over
+through LDS, or one wave with rt_set_wavefront_waves(1)); and through the reference's own
+configurations it runs by default (rt_solve with no block or schedule chosen), which
+test_gpu_parity.test_reference_configs checks against the oracle.
 """
 import numpy as np
 import pytest
@@ -17,7 +18,20 @@ from parity import per_group_rel
 
 pytestmark = pytest.mark.gpu
 
-LENGTHS = [1, 5, 31, 32, 33, 50, 63, 64, 65, 100, 127, 128, 129, 255, 256, 257, 511, 512, 513]
+LENGTHS = [1, 5, 31, 32, 33, 50, 63, 64, 65, 100, 127, 128, 129, 255, 256, 257, 511, 512, 513, 1000, 2049,
+           4096]
+
+
+def wave_plan(N, reflective, max_waves=8):
+    """kernels_wave.hip wavefront_plan: one wave with the fewest cells per lane (1, 2, 4, 8)
+    when the chain of ceil(N / C) lanes per line (a reflective pair: both lines) fits 64
+    lanes, else the fewest cells per lane whose chain fits max_waves waves."""
+    for cap in (1, max_waves):
+        for C in (1, 2, 4, 8):
+            lanes = -(-N // C) * (2 if reflective else 1)
+            if -(-lanes // 64) <= cap:
+                return C, -(-lanes // 64)
+    return 0, 0
 
 
 def _params(oracle_mod, N, ts, bc_left, bc_right, M=6, V=5.994, dt=1e-6):
@@ -45,31 +59,37 @@ def test_wavefront_bitwise_pipelined(rtsn_mod, oracle_mod, N, ts, bc_left, bc_ri
     B = oracle_mod.OracleSolver(p, g_lo=lo, g_hi=hi).groups()["B"][lo:hi]
     ends0 = _random_ends(q, lo, hi, B, SEED + N + 7 * ts + 3 * bc_left + bc_right)
     out = {}
-    for wave in (2, 0):
+    for wave, maxw in ((2, 8), (2, 1), (0, 8)):
         with rtsn_mod.Solver(q, g_lo=lo, g_hi=hi) as s:
             s.wavefront = wave
+            s.wavefront_waves = maxw
             if wave == 0:
                 s.pipeline = 2
                 s.time_block = 1
             st = s.wavefront_state()
             fits = st["cells_per_lane"] > 0
+            assert (st["cells_per_lane"], st["waves"]) == wave_plan(N, bc_left == 2, maxw)
             assert st["active"] == (wave == 2 and fits)
             s.set_ends(ends0)
             s.advance(steps)
-            out[wave] = s.ends()
-    assert fits == (N <= (256 if bc_left == 2 else 512))  # 32 / 64 lanes x 8 cells
-    if fits:  # (too long: both handles ran segment schedules of their own choosing)
-        assert np.array_equal(out[2], out[0])
+            out[(wave, maxw)] = (fits, s.ends())
+    # one wave: up to 64 lanes x 8 cells (32 per line when reflective); 8 waves: 8 x that
+    assert out[(2, 1)][0] == (N <= (256 if bc_left == 2 else 512))
+    assert out[(2, 8)][0] == (N <= (2048 if bc_left == 2 else 4096))
+    for key in ((2, 8), (2, 1)):  # (too long: the handle ran a segment schedule of its own choosing)
+        if out[key][0]:
+            assert np.array_equal(out[key][1], out[(0, 8)][1]), key
 
 
-@pytest.mark.parametrize("N", [1, 33, 64, 100, 129, 255, 256, 512])
+@pytest.mark.parametrize("N", [1, 33, 64, 100, 129, 255, 256, 512, 1000, 2000])
 @pytest.mark.parametrize("ts", [1, 2, 3])
 @pytest.mark.parametrize("bc_left,bc_right", [(0, 0), (2, 1), (1, 1)])
 def test_wavefront_bitwise_pipelined_long(rtsn_mod, oracle_mod, N, ts, bc_left, bc_right):
-    """As above for 150 steps, more than a chain has lanes: the ticks between the chain's fill
-    and drain (every lane at a level in [1, n)) run unmasked and take component 0 of the
-    carried state from the previous tick instead of a lane shift -- bitwise the pipelined
-    schedule still (dt = 1e-9 keeps the reference's BDF2 finite over the run)."""
+    """As above for 150 steps, more than a chain's wave has lanes: the ticks between a wave's
+    fill and drain (every lane at a level in [1, n)) run unmasked and take component 0 of
+    the carried state from the previous tick instead of a lane shift, and the waves of a
+    multi-wave chain run skewed by a block of ticks -- bitwise the pipelined schedule still
+    (dt = 1e-9 keeps the reference's BDF2 finite over the run)."""
     lo, hi, steps = 40, 44, 150
     p, q = _params(oracle_mod, N, ts, bc_left, bc_right, dt=1e-9)
     B = oracle_mod.OracleSolver(p, g_lo=lo, g_hi=hi).groups()["B"][lo:hi]
@@ -100,7 +120,7 @@ def test_wavefront_oracle_and_default(rtsn_mod, oracle_mod, ts):
     orc = oracle_mod.OracleSolver(p)
     orc.solve()
     with rtsn_mod.Solver(q) as s:
-        assert s.wavefront_state() == {"mode": 1, "active": True, "cells_per_lane": 2}
+        assert s.wavefront_state() == {"mode": 1, "active": True, "cells_per_lane": 2, "waves": 1}
         s.solve()
         assert per_group_rel(s.psi(), orc.psi(), 1) <= 1e-10
         assert per_group_rel(s.ends(), orc.ends(), 1) <= 1e-10
