@@ -62,6 +62,9 @@ __device__ __forceinline__ double lane_shift_up(double old, double v) {
 #define RT_WAVE_PREFETCH 2
 #endif
 constexpr int kWavePrefetch = RT_WAVE_PREFETCH;
+#ifndef RT_WAVE_ABLATE
+#define RT_WAVE_ABLATE 0  // timing experiments only (wrong results): 1 no barriers, 2 no ring reads, 4 no ring stores
+#endif
 constexpr int kWaveSkew = kWaveBlockTicks + kWavePrefetch;
 constexpr int kWaveRing = 4 * kWaveBlockTicks;
 static_assert((kWaveBlockTicks & (kWaveBlockTicks - 1)) == 0 && (kWaveRing & (kWaveRing - 1)) == 0,
@@ -188,13 +191,15 @@ __global__ __launch_bounds__(MULTI ? 64 * kWaveMaxWaves : 64) void wavefront_ker
         for (int r = 0; r < K; ++r) Xin[r] = lane_shift_up(o[r], X[r]);
       }
       if constexpr (MULTI) {  // after the shifts, which wait for an earlier tick's read
-        if (writer && tick > 0) publish(tick - 1);  // X: the previous tick's exit state
+        if (!(RT_WAVE_ABLATE & 4) && writer && tick > 0) publish(tick - 1);  // X: the previous tick's exit state
 #pragma unroll
         for (int q = 0; q + 1 < kWavePrefetch; ++q)
 #pragma unroll
           for (int r = 0; r < K; ++r) nxt[q][r] = nxt[q + 1][r];
 #pragma unroll
-        for (int r = 0; r < K; ++r) nxt[kWavePrefetch - 1][r] = rd[((tick + kWavePrefetch - 1) & rd_mask) * K + r];
+        for (int r = 0; r < K; ++r)
+          nxt[kWavePrefetch - 1][r] =
+              (RT_WAVE_ABLATE & 2) ? nxt[0][r] : rd[((tick + kWavePrefetch - 1) & rd_mask) * K + r];
       }
       bool active = true;
       if constexpr (decltype(masked)::value) {
@@ -231,7 +236,7 @@ __global__ __launch_bounds__(MULTI ? 64 * kWaveMaxWaves : 64) void wavefront_ker
         eout[c] = active ? oo : eout[c];
       }
       if constexpr (MULTI) {
-        if (((tick + wskew) & (kWaveBlockTicks - 1)) == kWaveBlockTicks - 1) __syncthreads();
+        if (!(RT_WAVE_ABLATE & 1) && ((tick + wskew) & (kWaveBlockTicks - 1)) == kWaveBlockTicks - 1) __syncthreads();
       }
     };
     // two ticks per iteration: the loop-carried renames of X, ein and eout then cancel
@@ -311,21 +316,31 @@ static hipError_t launch_wave_s(const WavePlan &p, const SegArgs &a, int nsteps,
   return hipGetLastError();
 }
 
-// One wave per chain whenever the chain fits 64 lanes of up to 8 cells (the fewest cells per
-// lane); otherwise the fewest cells per lane whose chain fits max_waves waves.  A chain
-// over several waves ticks ~2.3x slower than one wave (multi_group_equilibrium, 1000 steps:
-// 2 waves x 1 cell per lane 250 us, 1 wave x 2 cells 157 us; profiles/r03ah_rates.jsonl),
-// so more cells per lane on one wave win while they fit.  max_waves = 1: one wave only.
+// Which (cells per lane, waves) a chain takes: a tick costs ~148 C cycles of FP64 issue on
+// one wave (~200 at C = 1: latency), and a chain over several waves adds ~160-200 cycles of
+// cross-wave coupling per tick -- more beyond 4 waves, where two waves share a SIMD (1000
+// steps, 1000 cells: 4 waves x 4 cells 477 us, 8 x 2 595 us; profiles/r03ak_waves.jsonl).
+// Measured crossover (profiles/r03an_plan.jsonl, 1000 steps): one wave wins up to 4 cells
+// per lane (256 cells: one wave x 4 cells 244 us, 4 waves x 1 cell 298 us), a chain at 2
+// cells per lane beats one wave at 8 (512 cells: 361 vs 448 us; reflective 200 cells: 453
+// vs 563 us).  So: one wave while up to 4 cells per lane fit it; else the fewest cells per
+// lane on at most 4 waves; else on at most max_waves waves.  max_waves = 1: one wave only
+// (up to 8 cells per lane).
 WavePlan wavefront_plan(int N, bool reflective, int max_waves) {
   max_waves = max_waves < 1 ? 1 : (max_waves > kWaveMaxWaves ? kWaveMaxWaves : max_waves);
   if (N < 1) return WavePlan{0, 0, 0};
-  for (int waves_cap : {1, max_waves})
-    for (int C : {1, 2, 4, 8}) {
-      const int Lw = (N + C - 1) / C;
-      const int used = reflective ? 2 * Lw : Lw;
-      const int waves = (used + 63) / 64;
-      if (waves <= waves_cap) return WavePlan{C, waves, Lw};
-    }
+  const auto fit = [&](int C, int cap, WavePlan *p) {
+    const int Lw = (N + C - 1) / C;
+    const int waves = ((reflective ? 2 * Lw : Lw) + 63) / 64;
+    *p = WavePlan{C, waves, Lw};
+    return waves <= cap;
+  };
+  WavePlan p{};
+  for (int C : {1, 2, 4})
+    if (fit(C, 1, &p)) return p;
+  for (int cap : {max_waves < 4 ? max_waves : 4, max_waves})
+    for (int C : {1, 2, 4, 8})
+      if (fit(C, cap, &p)) return p;
   return WavePlan{0, 0, 0};  // too long: the segment pipeline
 }
 

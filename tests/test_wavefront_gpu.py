@@ -23,14 +23,18 @@ LENGTHS = [1, 5, 31, 32, 33, 50, 63, 64, 65, 100, 127, 128, 129, 255, 256, 257, 
 
 
 def wave_plan(N, reflective, max_waves=8):
-    """kernels_wave.hip wavefront_plan: one wave with the fewest cells per lane (1, 2, 4, 8)
-    when the chain of ceil(N / C) lanes per line (a reflective pair: both lines) fits 64
-    lanes, else the fewest cells per lane whose chain fits max_waves waves."""
-    for cap in (1, max_waves):
+    """kernels_wave.hip wavefront_plan: one wave while up to 4 cells per lane fit its 64 lanes
+    (a reflective pair: both lines' lanes), else the fewest cells per lane (1, 2, 4, 8) whose
+    chain of ceil(N / C) lanes per line fits min(4, max_waves) waves, else max_waves waves."""
+    def waves(C):
+        return -(-(-(-N // C) * (2 if reflective else 1)) // 64)
+    for C in (1, 2, 4):
+        if waves(C) == 1:
+            return C, 1
+    for cap in (min(4, max_waves), max_waves):
         for C in (1, 2, 4, 8):
-            lanes = -(-N // C) * (2 if reflective else 1)
-            if -(-lanes // 64) <= cap:
-                return C, -(-lanes // 64)
+            if waves(C) <= cap:
+                return C, waves(C)
     return 0, 0
 
 
