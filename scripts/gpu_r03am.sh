@@ -1,8 +1,11 @@
 # Round 3 full check at HEAD (after the wavefront chains): the driver's bench command, its
-# rocprofv3 kernel trace (+ stats) and the PMC passes of the headline pass (tests: r03an).
+# rocprofv3 kernel trace (+ stats) and the PMC passes of the headline pass (all tests: r03an;
+# the wavefront tests again after the plan's last change).
 set -o pipefail
 export TMPDIR=/tmp
 mkdir -p gpurun_out
+timeout -k 10 300 python -u -m pytest tests/test_wavefront_gpu.py -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/r03am_wave_tests.log 2>&1 || { tail -60 gpurun_out/r03am_wave_tests.log; exit 1; }
+tail -1 gpurun_out/r03am_wave_tests.log
 timeout -k 10 600 python -u bench.py --steps 20 --warmup 5 > gpurun_out/r03am_bench.log 2>&1 || { tail -30 gpurun_out/r03am_bench.log; exit 1; }
 grep "^{" gpurun_out/r03am_bench.log | tail -1 > gpurun_out/r03am_bench.json
 python3 -c "
