@@ -62,9 +62,6 @@ __device__ __forceinline__ double lane_shift_up(double old, double v) {
 #define RT_WAVE_PREFETCH 2
 #endif
 constexpr int kWavePrefetch = RT_WAVE_PREFETCH;
-#ifndef RT_WAVE_ABLATE
-#define RT_WAVE_ABLATE 0  // timing experiments only (wrong results): 1 no barriers, 2 no ring reads, 4 no ring stores
-#endif
 constexpr int kWaveSkew = kWaveBlockTicks + kWavePrefetch;
 constexpr int kWaveRing = 4 * kWaveBlockTicks;
 static_assert((kWaveBlockTicks & (kWaveBlockTicks - 1)) == 0 && (kWaveRing & (kWaveRing - 1)) == 0,
@@ -191,15 +188,13 @@ __global__ __launch_bounds__(MULTI ? 64 * kWaveMaxWaves : 64) void wavefront_ker
         for (int r = 0; r < K; ++r) Xin[r] = lane_shift_up(o[r], X[r]);
       }
       if constexpr (MULTI) {  // after the shifts, which wait for an earlier tick's read
-        if (!(RT_WAVE_ABLATE & 4) && writer && tick > 0) publish(tick - 1);  // X: the previous tick's exit state
+        if (writer && tick > 0) publish(tick - 1);  // X: the previous tick's exit state
 #pragma unroll
         for (int q = 0; q + 1 < kWavePrefetch; ++q)
 #pragma unroll
           for (int r = 0; r < K; ++r) nxt[q][r] = nxt[q + 1][r];
 #pragma unroll
-        for (int r = 0; r < K; ++r)
-          nxt[kWavePrefetch - 1][r] =
-              (RT_WAVE_ABLATE & 2) ? nxt[0][r] : rd[((tick + kWavePrefetch - 1) & rd_mask) * K + r];
+        for (int r = 0; r < K; ++r) nxt[kWavePrefetch - 1][r] = rd[((tick + kWavePrefetch - 1) & rd_mask) * K + r];
       }
       bool active = true;
       if constexpr (decltype(masked)::value) {
@@ -236,7 +231,7 @@ __global__ __launch_bounds__(MULTI ? 64 * kWaveMaxWaves : 64) void wavefront_ker
         eout[c] = active ? oo : eout[c];
       }
       if constexpr (MULTI) {
-        if (!(RT_WAVE_ABLATE & 1) && ((tick + wskew) & (kWaveBlockTicks - 1)) == kWaveBlockTicks - 1) __syncthreads();
+        if (((tick + wskew) & (kWaveBlockTicks - 1)) == kWaveBlockTicks - 1) __syncthreads();
       }
     };
     // two ticks per iteration: the loop-carried renames of X, ein and eout then cancel
