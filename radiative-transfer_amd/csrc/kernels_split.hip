@@ -261,12 +261,22 @@ __device__ __forceinline__ void split_role(const SegArgs &a, double2 (*hand)[2][
   for (int I = 0; I < 2 * (KW - 1 - w); ++I) __syncthreads();  // the later waves drain it
 }
 
+#ifndef RT_SPLIT_PRIO
+#define RT_SPLIT_PRIO 1  // 1 + the wave given issue priority 1; 0: none (timing experiments)
+#endif
 template <int S, int T, int KW>
 __global__ __launch_bounds__(64 * KW) __attribute__((amdgpu_waves_per_eu(2, 2))) void sweep_split_kernel(SegArgs a) {
   static_assert(T % KW == 0 && (KW == 2 || KW == 4), "levels split evenly over 2 or 4 waves");
   __shared__ double2 hand[KW - 1][2][split_chunk_cells() * 64];  // link w: wave w -> w + 1, chunk m in [m & 1]
   __shared__ double2 hhead[64];                                    // reflective head cell, wave to wave
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  // Static issue priority for wave 0 (it streams the rows in and runs the first levels; the
+  // SIMD it shares with another workgroup's wave gives it the issue slot first): the T = 20
+  // pass 8.42-8.46 vs 8.61-8.65 ms/step, priority for wave 1 instead 8.52-8.57
+  // (profiles/r03ap_prio.jsonl); on another box 8.17-8.18 vs 8.36-8.41, and the four-wave
+  // T = 40 pass 7.85-7.88 vs 7.90-7.91 (r03aq_prio.jsonl; MI355X_MICROARCH.md, two waves per
+  // SIMD, item 4).
+  if (RT_SPLIT_PRIO > 0 && w == RT_SPLIT_PRIO - 1) __builtin_amdgcn_s_setprio(1);
   if constexpr (KW == 2) {
     if (w == 0)
       split_role<S, T, 2, 0>(a, hand, hhead);
