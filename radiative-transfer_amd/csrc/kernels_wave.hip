@@ -19,8 +19,9 @@
 // w - 1 appends its exit state to a ring in LDS every tick, and lane 0 of wave w takes it --
 // one tick after it was produced in chain time, a block of ticks later in wall time -- as the
 // `old` operand of its DPP shifts.  The waves meet at one barrier per block of ticks (not per
-// tick), so a 100-cell line runs one cell per lane on two waves instead of two cells per
-// lane on one: half the dependent instructions per tick.
+// tick).  The coupling costs ~160-200 cycles per tick, so lines that fit one wave at up to 4
+// cells per lane stay on one wave (wavefront_plan); longer lines -- up to 4096 cells, which
+// used to fall to the segment pipeline's launch per segment position -- run as chains.
 //
 // Same arithmetic per (cell, level) as the pipelined segment pass (the per-line affine map
 // of cell.hpp, exact carries; the reflective mu > 0 head cell by the reference's algebra
