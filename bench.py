@@ -511,7 +511,15 @@ def run_rank(solver, p: dict, steps: int, warmup: int, world: int, device, shard
                 if gather else None)
     gather_ms = 1e3 * (time.perf_counter() - t2)
 
-    t = torch.tensor([wall, kern_ms / max(nlaunch, 1)], dtype=torch.float64, device=device)
+    mine = torch.tensor([wall, kern_ms / max(nlaunch, 1), upd_step * steps], dtype=torch.float64, device=device)
+    per_rank = None
+    if world > 1:  # every rank's own timing (the line reports the max; a slow rank shows here)
+        allr = torch.zeros(world * 3, dtype=torch.float64, device=device)
+        dist.all_gather_into_tensor(allr, mine)
+        allr = allr.view(world, 3).cpu().numpy()
+        per_rank = [{"rank": r, "wall_ms": 1e3 * float(a[0]), "kernel_ms": float(a[1]),
+                     "updates_per_s": float(a[2] / a[0]) if a[0] > 0 else None} for r, a in enumerate(allr)]
+    t = mine[:2].clone()
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     wall_max, kern_avg_ms = float(t[0]), float(t[1])
@@ -580,6 +588,8 @@ def run_rank(solver, p: dict, steps: int, warmup: int, world: int, device, shard
         },
         "state_finite": finite,
     }
+    if per_rank is not None:
+        line["per_rank"] = per_rank
     # BASELINE.md's roofline definition for the north_star target (>= 0.5): updates/s per GPU
     # x the unfused algorithm's minimal state bytes per update (48 B, 52 B with the
     # v/c correction active) / 8.0 TB/s.  Above 1 means the fused pass moves fewer bytes per
@@ -629,19 +639,42 @@ def material_params(p: dict) -> dict:
     return dict(p, ts_method=1, V=0.0, dt=1e-3)
 
 
-def open_comm(world: int, rank: int, local: int):
-    """The RCCL communicator behind the C ABI (rt_comm: ncclCommInitRank over every rank's
-    GPU), or (None, reason) where RCCL cannot form it -- the one-GPU multi-rank rehearsal
-    (two ranks on one device).  Collective over the ranks."""
+COMM_TIMEOUT_S = "120"  # the bench's bound on every rt_comm wait (RTSN_COMM_TIMEOUT_S unless set)
+
+
+def comm_agree(comm, err, world: int, device):
+    """Collective: keep the communicator only if every rank still has a live one (a rank
+    whose init or gather timed out would otherwise leave the others in a collective it
+    never joins).  Returns (comm or None, reason or None)."""
+    import torch
+    import torch.distributed as dist
+    if world > 1:
+        ok = torch.tensor([1.0 if comm is not None else 0.0], dtype=torch.float64, device=device)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        if float(ok.item()) < 1.0 and comm is not None:
+            comm.close()
+            return None, err or "another rank's rt_comm failed"
+    return comm, err
+
+
+def open_comm(world: int, rank: int, local: int, device=None):
+    """The RCCL communicator behind the C ABI (rt_comm: non-blocking ncclCommInitRankConfig
+    over every rank's GPU, bounded by RTSN_COMM_TIMEOUT_S), or (None, reason) where RCCL
+    cannot form it -- the one-GPU multi-rank rehearsal (two ranks on one device), or a rank
+    that does not join in time (RT_ERR_TIMEOUT: "skipped (timeout)").  Collective over the
+    ranks; every rank ends with a communicator or none does."""
     import torch.distributed as dist
     import rtsn
+    os.environ.setdefault("RTSN_COMM_TIMEOUT_S", COMM_TIMEOUT_S)
+    comm, err = None, None
     try:
         uid = [rtsn.Comm.unique_id() if rank == 0 else None]
         if world > 1:
             dist.broadcast_object_list(uid, src=0)
-        return rtsn.Comm(world, rank, uid[0], local), None
+        comm = rtsn.Comm(world, rank, uid[0], local)
     except rtsn.RtError as e:
-        return None, str(e)
+        err = ("skipped (timeout): " if e.status == 7 else "") + str(e)
+    return comm_agree(comm, err, world, device) if device is not None else (comm, err)
 
 
 def rccl_gather_check(comm, solver, gathered, dirs) -> dict:
@@ -709,7 +742,10 @@ def run_material(p: dict, info, world: int, device, local: int, steps: int, dirs
         step(1)
 
         def barrier():
-            s.synchronize()
+            if comm is not None:
+                comm.synchronize(s)  # bounded by RTSN_COMM_TIMEOUT_S (RCCL all-reduces in the stream)
+            else:
+                s.synchronize()
             if world > 1:
                 dist.barrier()
             torch.cuda.synchronize(device)
@@ -811,10 +847,19 @@ def main():
     line["warmup_requested"] = args.warmup if args.warmup >= 0 else None
     # one RCCL communicator behind the C ABI for the rest of the run (the gather cross-check
     # on N > 1 GPUs, the material leg's per-step all-reduce)
-    comm, comm_error = open_comm(world, rank, local) if (world > 1 or args.material_steps > 0) else (None, None)
+    comm, comm_error = (open_comm(world, rank, local, device) if (world > 1 or args.material_steps > 0)
+                        else (None, None))
     if world > 1:
-        line["rt_comm_gather"] = (rccl_gather_check(comm, solver, gathered, dirs) if comm is not None
-                                  else {"ok": None, "skipped": f"rt_comm unavailable: {comm_error}"})
+        if comm is not None:
+            try:
+                line["rt_comm_gather"] = rccl_gather_check(comm, solver, gathered, dirs)
+            except rtsn.RtError as e:  # a bounded wait expired: the communicator is aborted
+                comm.close()
+                comm, comm_error = None, ("skipped (timeout): " if e.status == 7 else "") + str(e)
+                line["rt_comm_gather"] = {"ok": None, "skipped": comm_error}
+            comm, comm_error = comm_agree(comm, comm_error, world, device)
+        else:
+            line["rt_comm_gather"] = {"ok": None, "skipped": f"rt_comm unavailable: {comm_error}"}
     del gathered
     line["roofline"]["traffic"] = load_traffic(args.variant, solver.time_block,
                                                line["roofline"]["algorithmic_bytes_per_launch"])

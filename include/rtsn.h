@@ -42,7 +42,7 @@ typedef enum {
   RT_ERR_VALIDATION = 4,  /* assert(validate_correction()) would fire (solver.cpp:609-612) */
   RT_ERR_NOMEM = 5,       /* host or device allocation failed */
   RT_ERR_DEVICE = 6,      /* HIP runtime error / no usable gfx950 device */
-  RT_ERR_TIMEOUT = 7,     /* reserved (no in-kernel waits in this version) */
+  RT_ERR_TIMEOUT = 7,     /* an rt_comm wait passed RTSN_COMM_TIMEOUT_S: the communicator was aborted */
   RT_ERR_ARG = 8,         /* NULL handle / bad argument */
   RT_ERR_STATE = 9,       /* call not valid in the handle's mode (e.g. rt_advance with material coupling on) */
   RT_WARN_UNSTABLE = 10   /* a warning, not a failure: rt_material_enable turned coupling on, but its explicit
@@ -325,12 +325,18 @@ rt_status rt_get_cell_planck(rt_solver *s, double *B);
  * between) the steps: every call below is collective (all ranks, same order), runs on
  * the handle's stream (RCCL over xGMI) and, where it returns host arrays, synchronises.
  * Shards must be all group shards that tile [0, G) in rank order, or all direction
- * shards of the same groups that tile [0, M/2) in rank order (else RT_ERR_PARAM). */
+ * shards of the same groups that tile [0, M/2) in rank order (else RT_ERR_PARAM).
+ * No call waits unboundedly: the communicator is non-blocking and every wait on it (the
+ * init, a collective call in progress, the host synchronisations of the gathers) has a
+ * deadline of RTSN_COMM_TIMEOUT_S seconds (default 300).  On expiry -- a rank missing or
+ * stalled -- the communicator is aborted, the call returns RT_ERR_TIMEOUT and later
+ * collectives on it RT_ERR_STATE. */
 typedef struct rt_comm rt_comm;
 #define RT_COMM_ID_BYTES 128
 /* ncclGetUniqueId: on one rank, then handed to every rank (file, pipe, MPI, ...). */
 rt_status rt_comm_unique_id(void *id);
-/* ncclCommInitRank on `device` (the device of the rank's handle). */
+/* ncclCommInitRankConfig (non-blocking) on `device` (the device of the rank's handle),
+ * waited for up to RTSN_COMM_TIMEOUT_S: RT_ERR_TIMEOUT if the other ranks do not join. */
 rt_status rt_comm_init(int nranks, int rank, const void *id, int device, rt_comm **out);
 void rt_comm_destroy(rt_comm *c);
 rt_status rt_comm_rank(rt_comm *c, int *nranks, int *rank);
@@ -359,6 +365,10 @@ rt_status rt_comm_allreduce_absorption(rt_comm *c, rt_solver *s, double *d_out);
  * q(x), one ncclAllReduce(sum) of q (N doubles) on the handle's stream, then the T
  * update -- stream-ordered, no host synchronisation; every rank ends with the same T(x). */
 rt_status rt_comm_material_step(rt_comm *c, rt_solver *s, int nsteps);
+/* Host wait for everything enqueued on the handle's stream (its sweeps and c's stream-
+ * ordered collectives), bounded by RTSN_COMM_TIMEOUT_S like the gathers: the replacement
+ * for rt_synchronize after rt_comm_material_step / rt_comm_allreduce_absorption. */
+rt_status rt_comm_synchronize(rt_comm *c, rt_solver *s);
 const char *rt_comm_last_error(rt_comm *c);
 /* The RCCL this library's collectives run on (host only, no device call): ncclGetVersion
  * (e.g. 22707 for 2.27.7) and the file the process resolved ncclGetVersion from.  librtsn

@@ -130,19 +130,37 @@ void apply(const std::vector<Copy2D> &plan, const double *src, double *dst) {
 // ---------------------------------------------------------------------------
 using namespace rtamd::layout;
 
+// rtsn_api.hip: the text rt_last_error(NULL) returns (weak: the plans also build alone, e.g.
+// under the host sanitizer, tools/layout_sanitize.cpp)
+namespace rtsn_detail {
+__attribute__((weak)) void set_last_error(const char *msg);
+}
+
+namespace {
+rt_status lfail(rt_status st, const char *msg) {
+  if (rtsn_detail::set_last_error) rtsn_detail::set_last_error(msg);
+  return st;
+}
+constexpr const char *kBadTiling =
+    "shards must be group shards tiling [0, G) in rank order (each d_lo = 0, d_hi = M/2) or direction-pair "
+    "shards tiling [0, M/2) (each g_lo = 0, g_hi = G), with equal G, M, N > 0 and M even";
+}  // namespace
+
 extern "C" rt_status rt_layout_mode(const rt_shard *shards, int nranks, int *mode, int *max_groups_out) {
-  if (!shards || nranks < 1) return RT_ERR_ARG;
+  if (!shards || nranks < 1) return lfail(RT_ERR_ARG, "rt_layout_mode: NULL shards or nranks < 1");
   const int m = shard_mode(shards, nranks);
   if (mode) *mode = m;
   if (max_groups_out) *max_groups_out = max_groups(shards, nranks);
-  return m < 0 ? RT_ERR_PARAM : RT_OK;
+  return m < 0 ? lfail(RT_ERR_PARAM, kBadTiling) : RT_OK;
 }
 
 extern "C" rt_status rt_layout_pack_moments(const rt_shard *shards, int nranks, int rank, const double *local,
                                             double *block) {
-  if (!shards || nranks < 1 || rank < 0 || rank >= nranks || !block) return RT_ERR_ARG;
-  if (shard_mode(shards, nranks) < 0) return RT_ERR_PARAM;
-  if (!local && groups_of(shards[rank]) > 0) return RT_ERR_ARG;  // an empty shard has no local arrays
+  if (!shards || nranks < 1 || rank < 0 || rank >= nranks || !block)
+    return lfail(RT_ERR_ARG, "rt_layout_pack_moments: NULL argument or rank outside [0, nranks)");
+  if (shard_mode(shards, nranks) < 0) return lfail(RT_ERR_PARAM, kBadTiling);
+  if (!local && groups_of(shards[rank]) > 0)
+    return lfail(RT_ERR_ARG, "rt_layout_pack_moments: NULL local moments for a non-empty shard");  // an empty shard has no local arrays
   std::fill(block, block + 3 * static_cast<size_t>(shards[0].N) * max_groups(shards, nranks), 0.0);
   apply(moments_pack(shards, nranks, rank), local, block);
   return RT_OK;
@@ -150,8 +168,8 @@ extern "C" rt_status rt_layout_pack_moments(const rt_shard *shards, int nranks, 
 
 extern "C" rt_status rt_layout_unpack_moments(const rt_shard *shards, int nranks, const double *gathered,
                                               double *phi, double *F, double *phi_plus) {
-  if (!shards || nranks < 1 || !gathered) return RT_ERR_ARG;
-  if (shard_mode(shards, nranks) < 0) return RT_ERR_PARAM;
+  if (!shards || nranks < 1 || !gathered) return lfail(RT_ERR_ARG, "rt_layout_unpack_moments: NULL argument");
+  if (shard_mode(shards, nranks) < 0) return lfail(RT_ERR_PARAM, kBadTiling);
   double *want[3] = {phi, F, phi_plus};
   for (int k = 0; k < 3; ++k)
     if (want[k]) apply(moments_unpack(shards, nranks, k), gathered, want[k]);
@@ -160,8 +178,9 @@ extern "C" rt_status rt_layout_unpack_moments(const rt_shard *shards, int nranks
 
 extern "C" rt_status rt_layout_pack_vectors(const rt_shard *shards, int nranks, int rank, int k,
                                             const double *const *in, double *block) {
-  if (!shards || nranks < 1 || rank < 0 || rank >= nranks || k < 1 || !in || !block) return RT_ERR_ARG;
-  if (shard_mode(shards, nranks) < 0) return RT_ERR_PARAM;
+  if (!shards || nranks < 1 || rank < 0 || rank >= nranks || k < 1 || !in || !block)
+    return lfail(RT_ERR_ARG, "rt_layout_pack_vectors: NULL argument, k < 1 or rank outside [0, nranks)");
+  if (shard_mode(shards, nranks) < 0) return lfail(RT_ERR_PARAM, kBadTiling);
   std::fill(block, block + static_cast<size_t>(k) * max_groups(shards, nranks), 0.0);
   for (int j = 0; j < k; ++j)
     if (in[j]) apply(vectors_pack(shards, nranks, rank, k, j), in[j], block);
@@ -170,27 +189,30 @@ extern "C" rt_status rt_layout_pack_vectors(const rt_shard *shards, int nranks, 
 
 extern "C" rt_status rt_layout_unpack_vectors(const rt_shard *shards, int nranks, int k, const double *gathered,
                                               double *const *out) {
-  if (!shards || nranks < 1 || k < 1 || !gathered || !out) return RT_ERR_ARG;
-  if (shard_mode(shards, nranks) < 0) return RT_ERR_PARAM;
+  if (!shards || nranks < 1 || k < 1 || !gathered || !out)
+    return lfail(RT_ERR_ARG, "rt_layout_unpack_vectors: NULL argument or k < 1");
+  if (shard_mode(shards, nranks) < 0) return lfail(RT_ERR_PARAM, kBadTiling);
   for (int j = 0; j < k; ++j)
     if (out[j]) apply(vectors_unpack(shards, nranks, k, j), gathered, out[j]);
   return RT_OK;
 }
 
 extern "C" rt_status rt_layout_place_psi(const rt_shard *shard, const double *block, double *psi) {
-  if (!shard || !block || !psi) return RT_ERR_ARG;
+  if (!shard || !block || !psi) return lfail(RT_ERR_ARG, "rt_layout_place_psi: NULL argument");
   const rt_shard &a = *shard;
   if (a.M <= 0 || a.M % 2 || a.g_lo < 0 || a.g_lo >= a.g_hi || a.g_hi > a.G || a.d_lo < 0 || a.d_lo >= a.d_hi ||
       a.d_hi > a.M / 2 || a.N <= 0)
-    return RT_ERR_PARAM;
+    return lfail(RT_ERR_PARAM, "rt_layout_place_psi: the shard needs M > 0 even, 0 <= g_lo < g_hi <= G, "
+                               "0 <= d_lo < d_hi <= M/2 and N > 0");
   apply(psi_place(a), block, psi);
   return RT_OK;
 }
 
 extern "C" rt_status rt_layout_place_psi_source(const rt_shard *shard, const double *rows, double *psi_source) {
-  if (!shard || !rows || !psi_source) return RT_ERR_ARG;
+  if (!shard || !rows || !psi_source) return lfail(RT_ERR_ARG, "rt_layout_place_psi_source: NULL argument");
   const rt_shard &a = *shard;
-  if (a.M <= 0 || a.M % 2 || a.G <= 0 || a.d_lo < 0 || a.d_lo >= a.d_hi || a.d_hi > a.M / 2) return RT_ERR_PARAM;
+  if (a.M <= 0 || a.M % 2 || a.G <= 0 || a.d_lo < 0 || a.d_lo >= a.d_hi || a.d_hi > a.M / 2)
+    return lfail(RT_ERR_PARAM, "rt_layout_place_psi_source: the shard needs M > 0 even, G > 0 and 0 <= d_lo < d_hi <= M/2");
   apply(psi_source_place(a), rows, psi_source);
   return RT_OK;
 }

@@ -69,6 +69,28 @@ static_assert((kWaveBlockTicks & (kWaveBlockTicks - 1)) == 0 && (kWaveRing & (kW
               "block and ring indices are masks");
 static_assert(kWavePrefetch >= 1 && kWaveSkew + kWaveBlockTicks + 1 <= kWaveRing, "ring too short for the skew");
 
+// Diagnostic builds only (make variant V=stamps RT_DEFS=-DRT_WAVE_STAMPS): lane 0 of every wave
+// records (s_memtime, s_memrealtime) at entry, before and after its tick stream; the product
+// never reads them.  rt_debug_wave_stamps copies them out (tools/wave_clock.py).
+#ifdef RT_WAVE_STAMPS
+constexpr int kStampWaves = 16384;
+__device__ unsigned long long g_wave_stamps[kStampWaves * 6];
+#define RT_STAMP(slot)                                                                              \
+  do {                                                                                              \
+    const unsigned long long t_ = __builtin_amdgcn_s_memtime();                                     \
+    const unsigned long long r_ = __builtin_amdgcn_s_memrealtime();                                 \
+    const int wv_ = static_cast<int>(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));          \
+    if ((threadIdx.x & 63) == 0 && wv_ < kStampWaves) {                                             \
+      g_wave_stamps[wv_ * 6 + 2 * (slot)] = t_;                                                     \
+      g_wave_stamps[wv_ * 6 + 2 * (slot) + 1] = r_;                                                 \
+    }                                                                                               \
+  } while (0)
+#else
+#define RT_STAMP(slot) \
+  do {                 \
+  } while (0)
+#endif
+
 // grid: one workgroup per line (mu < 0 lines then mu > 0 lines, ell < H Gl) -- or, PAIR (the
 // reflective left boundary), one per line pair ell (chain lanes [0, Lw) the mu < 0 line,
 // [Lw, 2 Lw) its mirror).  Lw = lanes per line = ceil(N / C); the chain's lanes fill
@@ -80,6 +102,7 @@ static_assert(kWavePrefetch >= 1 && kWaveSkew + kWaveBlockTicks + 1 <= kWaveRing
 template <int S, int C, bool PAIR, bool PAD, bool MULTI>
 __global__ __launch_bounds__(MULTI ? 64 * kWaveMaxWaves : 64) void wavefront_kernel(SegArgs a, int nsteps, int Lw) {
   constexpr int K = SchemeDim<S>::K, WN = map_count<S>();
+  RT_STAMP(0);
   const int lane = threadIdx.x & 63;
   const int w = MULTI ? __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6)) : 0;
   const int nw = MULTI ? static_cast<int>(blockDim.x >> 6) : 1;
@@ -258,6 +281,7 @@ __global__ __launch_bounds__(MULTI ? 64 * kWaveMaxWaves : 64) void wavefront_ker
     // barriers inside the stream: wall ticks wskew .. wskew + ticks - 1 that are B - 1 mod B
     barriers -= (wskew + ticks) / kWaveBlockTicks - wskew / kWaveBlockTicks;
   }
+  RT_STAMP(1);
   if (u_lo < u_hi && u_hi <= ticks) {
     run(0, u_lo, std::true_type{});
     run(u_lo, u_hi, std::false_type{});
@@ -265,6 +289,7 @@ __global__ __launch_bounds__(MULTI ? 64 * kWaveMaxWaves : 64) void wavefront_ker
   } else {
     run(0, ticks, std::true_type{});
   }
+  RT_STAMP(2);
   for (int i = 0; i < barriers; ++i) __syncthreads();  // MULTI: wall ticks after the chain's
 #pragma unroll
   for (int c = 0; c < C; ++c) {
@@ -363,3 +388,14 @@ hipError_t launch_wavefront(int scheme, const WavePlan &p, const SegArgs &a, int
 }
 
 }  // namespace rtamd
+
+#ifdef RT_WAVE_STAMPS
+// diagnostic builds only: the stamps of the last wavefront launch, 6 per wave
+extern "C" int rt_debug_wave_stamps(unsigned long long *out, int waves) {
+  if (waves > rtamd::kStampWaves) waves = rtamd::kStampWaves;
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(rtamd::g_wave_stamps), sizeof(unsigned long long) * 6 * waves) != hipSuccess)
+    return -1;
+  return waves;
+}
+#endif

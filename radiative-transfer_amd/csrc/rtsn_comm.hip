@@ -14,14 +14,24 @@
 // and the assembly into the (G, N) / (G) arrays is the copy plans of comm_layout.cpp --
 // host code shared with the rt_layout_* entry points, which the CPU tests check at world
 // sizes 2, 3 and 8 -- run here with hipMemcpy2DAsync (device blocks) or on the host.
+//
+// No call can hang a job: the communicator is created non-blocking (ncclCommInitRankConfig,
+// blocking = 0) and every wait on it -- the init, a collective call that reports
+// ncclInProgress, and each host synchronisation after collectives -- polls with a deadline
+// of RTSN_COMM_TIMEOUT_S seconds (default 300).  On expiry the communicator is aborted
+// (ncclCommAbort: RCCL stops the kernels still waiting on a peer) and the call returns
+// RT_ERR_TIMEOUT; the handle then refuses further collectives (RT_ERR_STATE).
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/rtsn.h"
@@ -32,12 +42,25 @@ namespace layout = rtamd::layout;
 struct rt_comm {
   ncclComm_t nc = nullptr;
   int nranks = 0, rank = 0, device = 0;
+  bool aborted = false;  // a wait expired: the communicator was aborted
+  double timeout_s = 300.0;
   double *q = nullptr;  // material coupling: q(x) of the running step (N doubles)
   size_t q_len = 0;
   std::string err;
   ~rt_comm() {
     if (q) (void)hipFree(q);
-    if (nc) (void)ncclCommDestroy(nc);
+    if (nc) {  // non-blocking: finalize, wait (bounded) for quiescence, then free
+      const auto end = std::chrono::steady_clock::now() + std::chrono::duration<double>(timeout_s);
+      ncclResult_t st = ncclCommFinalize(nc);
+      while (st == ncclInProgress && std::chrono::steady_clock::now() < end) {
+        std::this_thread::sleep_for(std::chrono::milliseconds(1));
+        if (ncclCommGetAsyncError(nc, &st) != ncclSuccess) break;
+      }
+      if (st == ncclSuccess)
+        (void)ncclCommDestroy(nc);
+      else
+        (void)ncclCommAbort(nc);
+    }
   }
 };
 
@@ -51,10 +74,79 @@ rt_status cfail(rt_comm *c, rt_status st, const std::string &msg) {
   return st;
 }
 
-#define NC_TRY(c, expr)                                                                                    \
-  do {                                                                                                     \
-    ncclResult_t r_ = (expr);                                                                              \
-    if (r_ != ncclSuccess) return cfail((c), RT_ERR_DEVICE, std::string(#expr ": ") + ncclGetErrorString(r_)); \
+double comm_timeout_s() {
+  const char *env = std::getenv("RTSN_COMM_TIMEOUT_S");
+  const double t = env ? std::atof(env) : 300.0;
+  return t > 0.0 ? t : 300.0;
+}
+
+// The deadline expired or RCCL reported an error: abort the communicator (RCCL stops the
+// kernels still waiting on a peer), after which the handle refuses collectives.
+rt_status abort_comm(rt_comm *c, rt_status st, const std::string &msg) {
+  if (c->nc) (void)ncclCommAbort(c->nc);
+  c->nc = nullptr;
+  c->aborted = true;
+  return cfail(c, st, msg);
+}
+
+// A non-blocking call's result: ncclInProgress is polled (ncclCommGetAsyncError) until it
+// settles or the deadline passes.
+rt_status nc_settle(rt_comm *c, ncclResult_t r, const char *what) {
+  if (r == ncclSuccess) return RT_OK;
+  if (r != ncclInProgress || !c || !c->nc)
+    return c && c->nc ? abort_comm(c, RT_ERR_DEVICE, std::string(what) + ": " + ncclGetErrorString(r))
+                      : cfail(c, RT_ERR_DEVICE, std::string(what) + ": " + ncclGetErrorString(r));
+  const auto t0 = std::chrono::steady_clock::now();
+  for (;;) {
+    ncclResult_t st = ncclInProgress;
+    const ncclResult_t q = ncclCommGetAsyncError(c->nc, &st);
+    if (q != ncclSuccess) st = q;
+    if (st == ncclSuccess) return RT_OK;
+    if (st != ncclInProgress) return abort_comm(c, RT_ERR_DEVICE, std::string(what) + ": " + ncclGetErrorString(st));
+    const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    if (el > c->timeout_s)
+      return abort_comm(c, RT_ERR_TIMEOUT, std::string(what) + ": no progress within RTSN_COMM_TIMEOUT_S = " +
+                                               std::to_string(c->timeout_s) + " s (a rank is missing or stalled); "
+                                               "communicator aborted");
+    std::this_thread::sleep_for(std::chrono::microseconds(200));
+  }
+}
+
+// Host wait for the collectives enqueued on st, bounded like nc_settle: a peer that never
+// joins leaves RCCL's kernel spinning, which the abort ends.
+rt_status comm_sync(rt_comm *c, hipStream_t st, const char *what) {
+  const auto t0 = std::chrono::steady_clock::now();
+  for (;;) {
+    const hipError_t e = hipStreamQuery(st);
+    if (e == hipSuccess) return RT_OK;
+    if (e != hipErrorNotReady) return cfail(c, RT_ERR_DEVICE, std::string(what) + ": " + hipGetErrorString(e));
+    ncclResult_t as = ncclSuccess;
+    if (c->nc && ncclCommGetAsyncError(c->nc, &as) == ncclSuccess && as != ncclSuccess && as != ncclInProgress)
+      return abort_comm(c, RT_ERR_DEVICE, std::string(what) + ": " + ncclGetErrorString(as));
+    const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    if (el > c->timeout_s) {
+      (void)abort_comm(c, RT_ERR_TIMEOUT, "");
+      (void)hipStreamSynchronize(st);  // the aborted kernels have returned
+      return cfail(c, RT_ERR_TIMEOUT, std::string(what) + ": collectives did not complete within RTSN_COMM_TIMEOUT_S = " +
+                                          std::to_string(c->timeout_s) + " s; communicator aborted");
+    }
+    std::this_thread::sleep_for(std::chrono::microseconds(50));
+  }
+}
+
+#define NC_TRY(c, expr)                                          \
+  do {                                                           \
+    if (rt_status st_ = nc_settle((c), (expr), #expr)) return st_; \
+  } while (0)
+#define CS_TRY(c, st)                                                         \
+  do {                                                                        \
+    if (rt_status e_ = comm_sync((c), (st), __func__)) return e_;             \
+  } while (0)
+// every collective entry point: the communicator must be live
+#define LIVE(c, what)                                                                                     \
+  do {                                                                                                    \
+    if ((c)->aborted) return cfail((c), RT_ERR_STATE, std::string(what) + ": the communicator was aborted " \
+                                                      "after a timeout or an RCCL error; create a new one"); \
   } while (0)
 #define HC_TRY(c, expr)                                                                                    \
   do {                                                                                                     \
@@ -100,7 +192,7 @@ rt_status all_shards(rt_comm *c, rt_solver *s, std::vector<rt_shard> &out, int &
   NC_TRY(c, ncclAllGather(d, d + kInts, kInts, ncclInt32, c->nc, st));
   out.resize(c->nranks);
   HC_TRY(c, hipMemcpyAsync(out.data(), d + kInts, sizeof(rt_shard) * c->nranks, hipMemcpyDeviceToHost, st));
-  HC_TRY(c, hipStreamSynchronize(st));
+  CS_TRY(c, st);
   mode = layout::shard_mode(out.data(), c->nranks);
   if (mode < 0)
     return cfail(c, RT_ERR_PARAM, "shards must be group shards tiling [0, G) or direction shards tiling [0, M/2), "
@@ -140,7 +232,7 @@ rt_status combine_vectors(rt_comm *c, rt_solver *s, const std::vector<rt_shard> 
     NC_TRY(c, ncclAllReduce(d, d, cnt, ncclFloat64, ncclSum, c->nc, st));
     HC_TRY(c, hipMemcpyAsync(all.data(), d, sizeof(double) * cnt, hipMemcpyDeviceToHost, st));
   }
-  HC_TRY(c, hipStreamSynchronize(st));
+  CS_TRY(c, st);
   for (int j = 0; j < k; ++j)
     if (out[j]) layout::apply(layout::vectors_unpack(sh.data(), n, k, j), all.data(), out[j]);
   return RT_OK;
@@ -166,13 +258,17 @@ extern "C" rt_status rt_comm_init(int nranks, int rank, const void *id, int devi
   c->nranks = nranks;
   c->rank = rank;
   c->device = device;
+  c->timeout_s = comm_timeout_s();
   ncclUniqueId u;
   std::memcpy(&u, id, sizeof(u));
-  ncclResult_t r = ncclCommInitRank(&c->nc, nranks, u, rank);
-  if (r != ncclSuccess) {
-    c->nc = nullptr;
-    delete c;
-    return cfail(nullptr, RT_ERR_DEVICE, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
+  ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+  cfg.blocking = 0;  // returns at once; the wait below is bounded
+  const ncclResult_t r = ncclCommInitRankConfig(&c->nc, nranks, u, rank, &cfg);
+  if (r != ncclSuccess && r != ncclInProgress) c->nc = nullptr;
+  if (rt_status st = nc_settle(c, r, "ncclCommInitRankConfig")) {
+    const std::string msg = c->err;
+    delete c;  // aborted (nc cleared) or never created
+    return cfail(nullptr, st, msg);
   }
   *out = c;
   return RT_OK;
@@ -191,6 +287,7 @@ extern "C" const char *rt_comm_last_error(rt_comm *c) { return c ? c->err.c_str(
 
 extern "C" rt_status rt_comm_gather_moments(rt_comm *c, rt_solver *s, double *phi, double *F, double *phi_plus) {
   if (!c || !s) return cfail(c, RT_ERR_ARG, "rt_comm_gather_moments: NULL argument");
+  LIVE(c, "rt_comm_gather_moments");
   HC_TRY(c, hipSetDevice(c->device));
   std::vector<rt_shard> sh;
   int mode = 0;
@@ -230,12 +327,13 @@ extern "C" rt_status rt_comm_gather_moments(rt_comm *c, rt_solver *s, double *ph
       if (rt_status e = run_plan(c, layout::moments_unpack(sh.data(), n, k), gathered, want[k],
                                  hipMemcpyDeviceToHost, st))
         return e;
-  HC_TRY(c, hipStreamSynchronize(st));
+  CS_TRY(c, st);
   return RT_OK;
 }
 
 extern "C" rt_status rt_comm_gather_group_ends(rt_comm *c, rt_solver *s, double *left, double *right) {
   if (!c || !s) return cfail(c, RT_ERR_ARG, "rt_comm_gather_group_ends: NULL argument");
+  LIVE(c, "rt_comm_gather_group_ends");
   HC_TRY(c, hipSetDevice(c->device));
   std::vector<rt_shard> sh;
   int mode = 0;
@@ -249,6 +347,7 @@ extern "C" rt_status rt_comm_gather_group_ends(rt_comm *c, rt_solver *s, double 
 extern "C" rt_status rt_comm_gather_balance(rt_comm *c, rt_solver *s, double *balance, double *sources,
                                             double *sinks) {
   if (!c || !s) return cfail(c, RT_ERR_ARG, "rt_comm_gather_balance: NULL argument");
+  LIVE(c, "rt_comm_gather_balance");
   HC_TRY(c, hipSetDevice(c->device));
   std::vector<rt_shard> sh;
   int mode = 0;
@@ -275,6 +374,7 @@ extern "C" rt_status rt_comm_gather_balance(rt_comm *c, rt_solver *s, double *ba
 extern "C" rt_status rt_comm_gather_psi(rt_comm *c, rt_solver *s, int root, double *psi) {
   if (!c || !s || root < 0 || root >= c->nranks || (c->rank == root && !psi))
     return cfail(c, RT_ERR_ARG, "rt_comm_gather_psi: bad argument");
+  LIVE(c, "rt_comm_gather_psi");
   HC_TRY(c, hipSetDevice(c->device));
   std::vector<rt_shard> sh;
   int mode = 0;
@@ -295,7 +395,7 @@ extern "C" rt_status rt_comm_gather_psi(rt_comm *c, rt_solver *s, int root, doub
   HC_TRY(c, hipMemcpyAsync(d, mine.data(), sizeof(double) * mine.size(), hipMemcpyHostToDevice, st));
   if (c->rank != root) {
     NC_TRY(c, ncclSend(d, block(me), ncclFloat64, root, c->nc, st));
-    HC_TRY(c, hipStreamSynchronize(st));
+    CS_TRY(c, st);
     return RT_OK;
   }
   double *rx = d + big;
@@ -306,13 +406,14 @@ extern "C" rt_status rt_comm_gather_psi(rt_comm *c, rt_solver *s, int root, doub
       src = rx;
     }
     if (rt_status e = run_plan(c, layout::psi_place(sh[r]), src, psi, hipMemcpyDeviceToHost, st)) return e;
-    HC_TRY(c, hipStreamSynchronize(st));  // rx is reused by the next rank
+    CS_TRY(c, st);  // rx is reused by the next rank
   }
   return RT_OK;
 }
 
 extern "C" rt_status rt_comm_gather_psi_source(rt_comm *c, rt_solver *s, double *out) {
   if (!c || !s || !out) return cfail(c, RT_ERR_ARG, "rt_comm_gather_psi_source: bad argument");
+  LIVE(c, "rt_comm_gather_psi_source");
   HC_TRY(c, hipSetDevice(c->device));
   std::vector<rt_shard> sh;
   int mode = 0;
@@ -337,13 +438,14 @@ extern "C" rt_status rt_comm_gather_psi_source(rt_comm *c, rt_solver *s, double 
   NC_TRY(c, ncclAllGather(d, d + cnt, cnt, ncclFloat64, c->nc, st));
   std::vector<double> all(cnt * c->nranks);
   HC_TRY(c, hipMemcpyAsync(all.data(), d + cnt, sizeof(double) * all.size(), hipMemcpyDeviceToHost, st));
-  HC_TRY(c, hipStreamSynchronize(st));
+  CS_TRY(c, st);
   for (int r = 0; r < c->nranks; ++r) layout::apply(layout::psi_source_place(sh[r]), all.data() + cnt * r, out);
   return RT_OK;
 }
 
 extern "C" rt_status rt_comm_allreduce_absorption(rt_comm *c, rt_solver *s, double *d_out) {
   if (!c || !s || !d_out) return cfail(c, RT_ERR_ARG, "rt_comm_allreduce_absorption: bad argument");
+  LIVE(c, "rt_comm_allreduce_absorption");
   HC_TRY(c, hipSetDevice(c->device));
   int N = 0;
   RT_TRY(c, s, rt_get_dims(s, nullptr, nullptr, &N, nullptr, nullptr));
@@ -354,13 +456,14 @@ extern "C" rt_status rt_comm_allreduce_absorption(rt_comm *c, rt_solver *s, doub
 
 extern "C" rt_status rt_comm_material_step(rt_comm *c, rt_solver *s, int nsteps) {
   if (!c || !s || nsteps < 0) return cfail(c, RT_ERR_ARG, "rt_comm_material_step: bad argument");
+  LIVE(c, "rt_comm_material_step");
   HC_TRY(c, hipSetDevice(c->device));
   int N = 0;
   RT_TRY(c, s, rt_get_dims(s, nullptr, nullptr, &N, nullptr, nullptr));
   hipStream_t st = static_cast<hipStream_t>(rt_stream(s));
   if (c->q_len < static_cast<size_t>(N)) {
     if (c->q) {
-      HC_TRY(c, hipStreamSynchronize(st));
+      CS_TRY(c, st);
       HC_TRY(c, hipFree(c->q));
       c->q = nullptr;
     }
@@ -372,6 +475,14 @@ extern "C" rt_status rt_comm_material_step(rt_comm *c, rt_solver *s, int nsteps)
     NC_TRY(c, ncclAllReduce(c->q, c->q, N, ncclFloat64, ncclSum, c->nc, st));
     RT_TRY(c, s, rt_material_update(s, c->q));
   }
+  return RT_OK;
+}
+
+extern "C" rt_status rt_comm_synchronize(rt_comm *c, rt_solver *s) {
+  if (!c || !s) return cfail(c, RT_ERR_ARG, "rt_comm_synchronize: NULL argument");
+  LIVE(c, "rt_comm_synchronize");
+  HC_TRY(c, hipSetDevice(c->device));
+  CS_TRY(c, static_cast<hipStream_t>(rt_stream(s)));
   return RT_OK;
 }
 

@@ -1,0 +1,354 @@
+// rtsn_lines.hip -- per-line setup of a handle: the line constants of the reference algebra,
+// the per-line affine cell map (cell.hpp) and the aligned schedule's segment propagators,
+// boundary inflows, and the segmentation of the lines (segment_lines / resegment).
+
+#include "rtsn_internal.hpp"
+
+using namespace rtamd;
+using namespace rtsn_detail;
+
+// ---------------------------------------------------------------------------
+// per-line setup
+// ---------------------------------------------------------------------------
+// Line l of half h: direction i = H-1-i' (h = 0, mu < 0) or H+i' (h = 1),
+// local group gl, with l = i' + H*gl; both halves share (i', gl) numbering so
+// a reflective mu > 0 line and its mirror have the same l.
+static int line_direction(int H, int half, int ip) { return half == 0 ? H - 1 - ip : H + ip; }
+
+// unit_B: the source for B_g = 1 (material coupling scales it per cell)
+static LineConst line_constants(const rt_solver &s, int i, int g, bool unit_B = false) {
+  const rt_params &p = s.p;
+  const double c = phys::kLight;
+  const double dx = p.X / p.N;
+  const double dt = p.dt;
+  const double tau = (p.ts_method == 3) ? dt / 2.0 : dt;
+  const double mu = s.mu[i], m = std::fabs(mu);
+  const double sigma = s.gt.rho[g] * s.gt.kappa[g];
+  LineConst L{};
+  const double half = 0.5 * c * tau * dx;
+  // S = 1/2 c tau dx (sigma B_g + total_correction), psi = (e_in + e_out)/2
+  L.c[LC_SC] = half * sigma * (unit_B ? 1.0 : s.gt.B[g]);
+  L.c[LC_SL] = 0.0;
+  if (p.use_correction) {
+    const double beta = p.V / c;
+    L.c[LC_SC] += half * ((s.gt.cor2[g] * mu) * beta - s.gt.cor3[g] * (mu * mu) * (beta * beta));
+    L.c[LC_SL] = half * s.gt.cor1[g] * mu * beta * 0.5;
+  }
+  auto inverse = [](double d, double o, double &i0, double &i1) {
+    const double det = d * d + o * o;
+    i0 = d / det;
+    i1 = o / det;
+  };
+  {  // BE(tau)
+    const double a = 1.0 + c * tau * sigma, b = c * tau * m;
+    L.c[LC_BE_B] = b;
+    inverse((a * dx + b) / 2.0, b / 2.0, L.c[LC_BE_I0], L.c[LC_BE_I1]);
+  }
+  {  // CN(tau)
+    const double t = 0.5 * c * tau * sigma, A = 0.5 * c * m * tau;
+    const double Bp = 1.0 + t, Cp = 1.0 - t;
+    L.c[LC_CN_A] = A;
+    L.c[LC_CN_K1] = 0.5 * (Cp * dx - A);
+    L.c[LC_CN_K2] = 0.5 * A;
+    inverse(0.5 * (A + Bp * dx), A / 2.0, L.c[LC_CN_I0], L.c[LC_CN_I1]);
+  }
+  {  // BDF(tau) with const_B from the full dt
+    const double t = c * sigma * tau / 6.0, Ab = 1.0 + t, Bc = c * m * dt / 6.0, Cb = 1.0 - 4.0 * t, D = t;
+    L.c[LC_BD_BC] = Bc;
+    L.c[LC_BD_Q1] = 0.5 * (Cb * dx - 4.0 * Bc);
+    L.c[LC_BD_Q2] = 2.0 * Bc;
+    L.c[LC_BD_Q3] = 0.5 * (Bc + D * dx);
+    L.c[LC_BD_Q4] = 0.5 * Bc;
+    inverse(0.5 * (Ab * dx + Bc), 0.5 * Bc, L.c[LC_BD_I0], L.c[LC_BD_I1]);
+  }
+  return L;
+}
+
+// The per-line affine cell map (cell.hpp, map_apply): coefficients from
+// cell_step<S> on unit inputs (constants and data zeroed), constants from
+// cell_step<S> on zero inputs.  Every coefficient outside the structural
+// pattern must come out exactly zero; false otherwise.
+template <int S>
+static bool cell_map(const LineConst &Lin, double hd, bool neg, double *W) {
+  constexpr int K = SchemeDim<S>::K;
+  double dense[K + 1][K + 3];  // [row][input 0..K+1, constant K+2]
+  for (int col = 0; col <= K + 2; ++col) {
+    LineConst L = Lin;
+    if (col != K + 2) L.c[LC_SC] = 0.0;
+    double X[K] = {};
+    double pin = 0.0, pout = 0.0;
+    if (col < K) X[col] = 1.0;
+    if (col == K) pin = 1.0;
+    if (col == K + 1) pout = 1.0;
+    double oi, oo;
+    cell_step<S>(L, hd, neg, pin, pout, X, oi, oo);
+    for (int r = 0; r < K; ++r) dense[r][col] = X[r];
+    dense[K][col] = oi;
+    if (X[K - 1] != oo) return false;  // oout is X'[K-1]
+  }
+  for (int r = 0; r <= K; ++r)
+    for (int col = 0; col <= K + 2; ++col) {
+      const bool copy = map_copy_row0<S>() && r == 0;
+      const bool used = !copy && (col == K + 2 || map_dep<S>(r, col));
+      if (used) {
+        W[map_slot<S>(r, col)] = dense[r][col];
+      } else if (dense[r][col] != (copy && col == K + 1 ? 1.0 : 0.0)) {
+        return false;
+      }
+    }
+  return true;
+}
+
+// Linear part of the T-level combined map on the carried state (X_0..X_{T-1}):
+// level t's outputs are level t+1's data (KC x KC row-major, lower triangular).
+template <int S>
+static void combined_linear(const double *W, int T, double *A) {
+  constexpr int K = SchemeDim<S>::K;
+  const int KC = T * K;
+  for (int col = 0; col < KC; ++col) {
+    double di = 0.0, dd = 0.0;
+    for (int t = 0; t < T; ++t) {
+      double X[K] = {}, Xn[K], a, e;
+      if (col / K == t) X[col % K] = 1.0;
+      map_apply<S, false>(W, X, di, dd, Xn, a, e);
+      for (int r = 0; r < K; ++r) A[(t * K + r) * KC + col] = Xn[r];
+      di = a;
+      dd = e;
+    }
+  }
+}
+
+static void matmul(int K, const double *A, const double *B, double *C) {
+  for (int r = 0; r < K; ++r)
+    for (int c = 0; c < K; ++c) {
+      double acc = 0.0;
+      for (int m = 0; m < K; ++m) acc += A[r * K + m] * B[m * K + c];
+      C[r * K + c] = acc;
+    }
+}
+
+// A^n by binary exponentiation
+static void matpow(int K, const double *A, long long n, double *out) {
+  std::vector<double> base(A, A + K * K), acc(K * K, 0.0), tmp(K * K);
+  for (int r = 0; r < K; ++r) acc[r * K + r] = 1.0;
+  while (n > 0) {
+    if (n & 1) {
+      matmul(K, acc.data(), base.data(), tmp.data());
+      acc.swap(tmp);
+    }
+    n >>= 1;
+    if (n) {
+      matmul(K, base.data(), base.data(), tmp.data());
+      base.swap(tmp);
+    }
+  }
+  std::copy(acc.begin(), acc.end(), out);
+}
+
+rt_status rtsn_detail::upload(rt_solver *s, DeviceBuf &b, const void *src, size_t bytes) {
+  HIP_TRY(s, hipMemcpyAsync(b.p, src, bytes, hipMemcpyHostToDevice, s->stream));
+  return RT_OK;
+}
+
+// boundary inflow per line (solver.cpp:635-692) from the solver's psi_source
+static void line_inflow(const rt_solver &s, std::vector<double> &bd) {
+  const int M = s.p.M, G = s.p.G;
+  bd.assign(static_cast<size_t>(2) * s.Lpad, 0.0);
+  for (int half = 0; half < 2; ++half) {
+    const int bc = half == 0 ? s.p.bc_right_indicator : s.p.bc_left_indicator;
+    for (int gl = 0; gl < s.Gl; ++gl)
+      for (int ip = 0; ip < s.H; ++ip) {
+        const int i = line_direction(s.H, half, ip), g = s.g_lo + gl;
+        double v = 0.0;
+        if (half == 0 && bc == 1) v = s.psi_source[static_cast<size_t>(i) * G + g];
+        if (half == 1 && (bc == 0 || bc == 1)) v = s.psi_source[static_cast<size_t>(i) * G + g];
+        bd[static_cast<size_t>(half) * s.Lpad + ip + s.H * gl] = v;
+      }
+  }
+  (void)M;
+}
+
+// Per-line maps and constants into (map, lc); unit_B: sources for B_g = 1
+// (material coupling), leaving map_host (the propagators' source) alone.
+template <int S>
+rt_status rtsn_detail::line_maps_s(rt_solver *s, bool unit_B, DeviceBuf &map_dev, DeviceBuf &lc_dev) {
+  constexpr int WN = map_count<S>();
+  const double hd = 0.5 * (s->p.X / s->p.N);
+  const size_t Lp = s->Lpad;
+  std::vector<double> lc(2 * LC_COUNT * Lp, 0.0), unit_map;
+  std::vector<double> &map = unit_B ? unit_map : s->map_host;
+  map.assign(2 * WN * Lp, 0.0);
+  double W[WN];
+  for (int half = 0; half < 2; ++half)
+    for (int gl = 0; gl < s->Gl; ++gl)
+      for (int ip = 0; ip < s->H; ++ip) {
+        const int i = line_direction(s->H, half, ip), g = s->g_lo + gl;
+        const size_t ell = ip + static_cast<size_t>(s->H) * gl;
+        const LineConst L = line_constants(*s, i, g, unit_B);
+        for (int n = 0; n < LC_COUNT; ++n) lc[(half * LC_COUNT + n) * Lp + ell] = L.c[n];
+        if (!cell_map<S>(L, hd, half == 0, W))
+          return fail(s, RT_ERR_PARAM, "cell map: a structurally zero coefficient is not zero");
+        for (int n = 0; n < WN; ++n) map[(half * WN + n) * Lp + ell] = W[n];
+      }
+  rt_status st;
+  if ((st = upload(s, lc_dev, lc.data(), lc.size() * sizeof(double)))) return st;
+  if ((st = upload(s, map_dev, map.data(), map.size() * sizeof(double)))) return st;
+  HIP_TRY(s, hipStreamSynchronize(s->stream));  // host vectors die at return
+  return RT_OK;
+}
+
+template <int S>
+static rt_status setup_lines_s(rt_solver *s) {
+  const size_t Lp = s->Lpad;
+  rt_status st;
+  if ((st = line_maps_s<S>(s, false, s->map, s->lc))) return st;
+  std::vector<double> lineB(2 * Lp, 0.0);
+  for (int half = 0; half < 2; ++half)
+    for (int gl = 0; gl < s->Gl; ++gl)
+      for (int ip = 0; ip < s->H; ++ip) lineB[half * Lp + ip + static_cast<size_t>(s->H) * gl] = s->gt.B[s->g_lo + gl];
+  if ((st = upload(s, s->lineB, lineB.data(), lineB.size() * sizeof(double)))) return st;
+  std::vector<double> sig(s->Gl);
+  for (int gl = 0; gl < s->Gl; ++gl) sig[gl] = s->gt.rho[s->g_lo + gl] * s->gt.kappa[s->g_lo + gl];
+  if ((st = upload(s, s->sigma, sig.data(), sig.size() * sizeof(double)))) return st;
+  std::vector<double> muwt(2 * s->p.M);
+  std::copy(s->mu.begin(), s->mu.end(), muwt.begin());
+  std::copy(s->wt.begin(), s->wt.end(), muwt.begin() + s->p.M);
+  if ((st = upload(s, s->muwt, muwt.data(), muwt.size() * sizeof(double)))) return st;
+  HIP_TRY(s, hipStreamSynchronize(s->stream));  // host vectors die at return
+  return RT_OK;
+}
+
+// Segment propagators A_T^Ls, A_T^Llast of every line for the aligned schedule
+// (fold_kernel), built on first use of a time block T: the pipelined schedule
+// never needs them.  Lines are independent: host threads split them.
+template <int S>
+static rt_status build_propagators_s(rt_solver *s, int T) {
+  constexpr int K = SchemeDim<S>::K, WN = map_count<S>();
+  const int KC = T * K, NTC = KC * (KC + 1) / 2;
+  const long long L_last = s->p.N - static_cast<long long>(s->Sg - 1) * s->Ls;
+  const size_t Lp = s->Lpad, lines = 2 * Lp;
+  std::vector<double> pr(2 * prop_count(K, T) * Lp, 0.0);
+  auto work = [&](size_t l0, size_t l1) {
+    std::vector<double> A(KC * KC), Aseg(KC * KC), Alast(KC * KC);
+    double W[WN];
+    for (size_t idx = l0; idx < l1; ++idx) {
+      const size_t half = idx / Lp, ell = idx % Lp;
+      for (int n = 0; n < WN; ++n) W[n] = s->map_host[(half * WN + n) * Lp + ell];
+      std::fill(A.begin(), A.end(), 0.0);
+      combined_linear<S>(W, T, A.data());
+      matpow(KC, A.data(), s->Ls, Aseg.data());
+      matpow(KC, A.data(), L_last, Alast.data());
+      double *dst = pr.data() + half * prop_count(K, T) * Lp + ell;
+      for (int r = 0; r < KC; ++r)
+        for (int c = 0; c <= r; ++c) {
+          dst[tri(r, c) * Lp] = Aseg[r * KC + c];
+          dst[(NTC + tri(r, c)) * Lp] = Alast[r * KC + c];
+        }
+    }
+  };
+  const size_t nt = std::max<size_t>(1, std::min<size_t>(16, std::thread::hardware_concurrency()));
+  std::vector<std::thread> pool;
+  for (size_t t = 0; t < nt; ++t) pool.emplace_back(work, lines * t / nt, lines * (t + 1) / nt);
+  for (std::thread &th : pool) th.join();
+  rt_status st = upload(s, s->prop[T], pr.data(), pr.size() * sizeof(double));
+  if (st) return st;
+  HIP_TRY(s, hipStreamSynchronize(s->stream));  // pr dies at return
+  s->prop_ready[T] = true;
+  return RT_OK;
+}
+
+rt_status rtsn_detail::ensure_propagators(rt_solver *s, int T) {
+  if (s->prop_ready[T]) return RT_OK;
+  switch (s->scheme) {
+    case SCHEME_BE: return build_propagators_s<SCHEME_BE>(s, T);
+    case SCHEME_CN: return build_propagators_s<SCHEME_CN>(s, T);
+    default: return build_propagators_s<SCHEME_BDF2>(s, T);
+  }
+}
+
+rt_status rtsn_detail::setup_lines(rt_solver *s) {
+  switch (s->scheme) {
+    case SCHEME_BE: return setup_lines_s<SCHEME_BE>(s);
+    case SCHEME_CN: return setup_lines_s<SCHEME_CN>(s);
+    default: return setup_lines_s<SCHEME_BDF2>(s);
+  }
+}
+
+rt_status rtsn_detail::upload_inflow(rt_solver *s) {
+  std::vector<double> bd;
+  line_inflow(*s, bd);
+  rt_status st = upload(s, s->bdry, bd.data(), bd.size() * sizeof(double));
+  if (st) return st;
+  HIP_TRY(s, hipStreamSynchronize(s->stream));
+  return RT_OK;
+}
+
+// Segments per line: enough waves (2 Q Sg) to fill the chip at the sweep
+// kernel's occupancy, Ls a multiple of the register chunk.
+void rtsn_detail::segment_lines(rt_solver *h, int waves_per_cu) {
+  waves_per_cu = std::max(1, std::min(waves_per_cu, 64));
+  const long long target = static_cast<long long>(h->cus) * waves_per_cu;
+  long long sg = std::max<long long>(1, target / (2LL * h->Q));
+  const long long max_sg = (h->p.N + kSweepCells - 1) / kSweepCells;
+  sg = std::min(sg, max_sg);
+  long long ls = (h->p.N + sg - 1) / sg;
+  ls = ((ls + kSweepCells - 1) / kSweepCells) * kSweepCells;
+  h->Ls = static_cast<int>(ls);
+  h->Sg = static_cast<int>((h->p.N + ls - 1) / ls);
+}
+
+// Per-segment buffers (aggregates, folded incoming states), zeroed; the
+// segment propagators are rebuilt on their next use.
+hipError_t rtsn_detail::alloc_segments(rt_solver *h) {
+  // the handle's device, whatever the caller's current one (dalloc records the device)
+  if (hipError_t e = hipSetDevice(h->device)) return e;
+  const size_t Lp = h->Lpad;
+  const int K = h->K;
+  if (h->agg[0].p || h->agg[1].p || h->yseg.p) (void)hipStreamSynchronize(h->stream);  // before the cache may hand them out
+  for (DeviceBuf *b : {&h->agg[0], &h->agg[1], &h->yseg}) b->reset();
+  hipError_t e = dalloc(h->agg[0], sizeof(double) * 2 * h->Sg * kMaxTimeBlock * K * Lp);
+  if (!e) e = dalloc(h->agg[1], sizeof(double) * 2 * h->Sg * kMaxTimeBlock * K * Lp);
+  if (!e) e = dalloc(h->yseg, sizeof(double) * 2 * (h->Sg + 1) * kMaxAlignedBlock * K * Lp);
+  if (!e) e = hipMemsetAsync(h->agg[0].p, 0, h->agg[0].bytes, h->stream);
+  if (!e) e = hipMemsetAsync(h->agg[1].p, 0, h->agg[1].bytes, h->stream);
+  for (bool &r : h->prop_ready) r = false;
+  return e;
+}
+
+// Segments sized for the pipelined pass of the current time block (its occupancy: one
+// wave per SIMD at T = 16 and 20, two at T = 10, ...), applied only while every chain
+// position is at the same time with no correction outstanding -- the state rows do not
+// depend on the segmentation, only the aggregates and propagators do.  Called by
+// rt_set_time_block and again before the next pipelined or aligned pass, so a handle
+// always runs its passes with segments for the time block it runs.
+
+rt_status rtsn_detail::resegment(rt_solver *h) {
+  if (h->material || h->pending || h->Tpipe) return RT_OK;
+  int w = 0;
+  if (rt_status st = segment_target(h, &w)) return st;
+  if (h->seg_T == h->T && h->seg_w == w) return RT_OK;
+  const int sg0 = h->Sg, ls0 = h->Ls;
+  segment_lines(h, w);
+  h->seg_T = h->T;
+  h->seg_w = w;
+  if (h->Sg == sg0 && h->Ls == ls0) return RT_OK;
+  if (2LL * h->Q * h->Sg >= (1LL << 31)) return fail(h, RT_ERR_PARAM, "too many lines for one handle: shard the groups");
+  HIP_TRY(h, alloc_segments(h));
+  h->tau.assign(chain_positions(h), h->target);  // every position at the same, requested time
+  return RT_OK;
+}
+
+// Workgroups per CU the segments of the current time block are sized for: the caller's
+// (rt_set_segmentation, or the schedule rt_solve planned), else the pipelined pass's
+// occupancy (RTSN_WAVES_PER_CU overrides, for experiments).
+rt_status rtsn_detail::segment_target(rt_solver *h, int *w_out) {
+  int w = h->seg_wgs;
+  if (!w) HIP_TRY(h, sweep_occupancy(h->scheme, h->T, level_waves_of(h, h->T), &w));
+  if (const char *env = std::getenv("RTSN_WAVES_PER_CU")) w = std::atoi(env);  // experiments
+  *w_out = std::max(1, std::min(w, 64));
+  return RT_OK;
+}
+
+template rt_status rtsn_detail::line_maps_s<SCHEME_BE>(rt_solver *, bool, DeviceBuf &, DeviceBuf &);
+template rt_status rtsn_detail::line_maps_s<SCHEME_CN>(rt_solver *, bool, DeviceBuf &, DeviceBuf &);
+template rt_status rtsn_detail::line_maps_s<SCHEME_BDF2>(rt_solver *, bool, DeviceBuf &, DeviceBuf &);

@@ -17,7 +17,7 @@ LIB_PATH = Path(os.environ.get("RTSN_LIB", PKG_ROOT / "lib" / "librtsn.so"))  # 
 HEADER = REPO_ROOT / "include" / "rtsn.h"
 
 STATUS = {0: "ok", 1: "io error", 2: "parse error", 3: "invalid parameter", 4: "correction validation failed",
-          5: "out of memory", 6: "device error", 7: "timeout (reserved)", 8: "bad argument",
+          5: "out of memory", 6: "device error", 7: "timeout (communicator aborted)", 8: "bad argument",
           9: "not valid in the handle's mode", 10: "warning: explicit emission above its stability limit"}
 
 
@@ -148,6 +148,7 @@ def lib():
         L.rt_comm_gather_psi_source.argtypes = [vp, vp, dp]
         L.rt_comm_allreduce_absorption.argtypes = [vp, vp, vp]
         L.rt_comm_material_step.argtypes = [vp, vp, C.c_int]
+        L.rt_comm_synchronize.argtypes = [vp, vp]
         L.rt_comm_version.argtypes = [C.POINTER(C.c_int), C.c_char_p, C.c_size_t]
         sp = C.POINTER(rt_shard)
         L.rt_layout_mode.argtypes = [sp, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int)]
@@ -629,7 +630,9 @@ class Comm:
     handles, one process per GPU.  Every method is collective over the ranks.
 
     uid = Comm.unique_id() on one rank, handed to the others (e.g. by torch.distributed's
-    broadcast_object_list or a file); Comm(nranks, rank, uid, device)."""
+    broadcast_object_list or a file); Comm(nranks, rank, uid, device).  Every wait on the
+    communicator is bounded by RTSN_COMM_TIMEOUT_S seconds (default 300): a missing or
+    stalled rank gives RtError status 7 (RT_ERR_TIMEOUT) instead of a hang."""
 
     def __init__(self, nranks: int, rank: int, uid: bytes, device: int = 0):
         assert len(uid) == 128
@@ -709,6 +712,11 @@ class Comm:
         """nsteps coupled steps with one all-reduce of q(x) per step on the handle's stream."""
         self._check(lib().rt_comm_material_step(self._h, solver._h, int(nsteps)), "rt_comm_material_step")
 
+    def synchronize(self, solver: "Solver"):
+        """Host wait for the handle's stream (its sweeps and this communicator's stream-ordered
+        collectives), bounded by RTSN_COMM_TIMEOUT_S (RtError status 7 after an abort)."""
+        self._check(lib().rt_comm_synchronize(self._h, solver._h), "rt_comm_synchronize")
+
 
 def comm_version() -> dict:
     """rt_comm_version: the RCCL the library's collectives run on -- ncclGetVersion's code
@@ -747,6 +755,25 @@ class Layout:
     def shard(self, r: int) -> rt_shard:
         return self._sh[r]
 
+    @staticmethod
+    def _need(arr, count: int, what: str, out: bool = False) -> np.ndarray:
+        """The C plans read and write through raw pointers: a float64 array of at least count
+        elements (an output also C-contiguous, since it is written in place)."""
+        if out:
+            if not (isinstance(arr, np.ndarray) and arr.dtype == np.float64 and arr.flags["C_CONTIGUOUS"]):
+                raise ValueError(f"{what}: the output must be a C-contiguous float64 numpy array")
+        else:
+            arr = np.ascontiguousarray(arr, dtype=np.float64)
+        if arr.size < count:
+            raise ValueError(f"{what}: {arr.size} elements, the layout needs at least {count}")
+        return arr
+
+    def _shard_dims(self, rank: int):
+        if not 0 <= rank < self.n:
+            raise ValueError(f"rank {rank} outside [0, {self.n})")
+        sh = self._sh[rank]
+        return 2 * (sh.d_hi - sh.d_lo), sh.g_hi - sh.g_lo
+
     def pack_moments(self, rank: int, phi, F, phi_plus) -> np.ndarray:
         """rank's (N, G_local) fields (g fastest) -> its wire block (3, N, Gmax)."""
         local = np.ascontiguousarray(np.stack([phi, F, phi_plus]), dtype=np.float64)
@@ -756,7 +783,8 @@ class Layout:
 
     def unpack_moments(self, gathered: np.ndarray):
         """gathered wire blocks -> phi, F, phi_plus as (N, G) arrays (g fastest)."""
-        g = np.ascontiguousarray(gathered, dtype=np.float64)
+        blocks = 1 if self.mode == 1 else self.n  # direction shards: one summed block
+        g = self._need(gathered, blocks * 3 * self.N * self.max_groups, "unpack_moments: gathered")
         out = [np.empty((self.N, self.G)) for _ in range(3)]
         _check(lib().rt_layout_unpack_moments(self._sh, self.n, _dp(g), *[_dp(a) for a in out]),
                "rt_layout_unpack_moments")
@@ -771,7 +799,8 @@ class Layout:
         return block
 
     def unpack_vectors(self, k: int, gathered: np.ndarray):
-        g = np.ascontiguousarray(gathered, dtype=np.float64)
+        blocks = 1 if self.mode == 1 else self.n
+        g = self._need(gathered, blocks * k * self.max_groups, "unpack_vectors: gathered")
         out = [np.empty(self.G) for _ in range(k)]
         ptrs = (C.POINTER(C.c_double) * k)(*[_dp(v) for v in out])
         _check(lib().rt_layout_unpack_vectors(self._sh, self.n, k, _dp(g), ptrs), "rt_layout_unpack_vectors")
@@ -780,10 +809,14 @@ class Layout:
     def place_psi(self, rank: int, block: np.ndarray, psi_flat: np.ndarray):
         """rank's psi (as rt_get_psi's flat ColMajor (M_l, G_l, N) buffer) into psi_flat
         (the (M, G, N) ColMajor buffer, i + M (g + G c))."""
-        b = np.ascontiguousarray(block, dtype=np.float64)
+        Ml, Gl = self._shard_dims(rank)
+        b = self._need(block, Ml * Gl * self.N, "place_psi: block")
+        self._need(psi_flat, self.M * self.G * self.N, "place_psi: psi_flat", out=True)
         _check(lib().rt_layout_place_psi(C.byref(self._sh[rank]), _dp(b), _dp(psi_flat)), "rt_layout_place_psi")
 
     def place_psi_source(self, rank: int, rows: np.ndarray, table: np.ndarray):
-        r = np.ascontiguousarray(rows, dtype=np.float64)
+        Ml, _ = self._shard_dims(rank)
+        r = self._need(rows, Ml * self.G, "place_psi_source: rows")
+        self._need(table, self.M * self.G, "place_psi_source: table", out=True)
         _check(lib().rt_layout_place_psi_source(C.byref(self._sh[rank]), _dp(r), _dp(table)),
                "rt_layout_place_psi_source")

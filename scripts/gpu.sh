@@ -1,0 +1,87 @@
+# One parameterised GPU runner (replaces the per-experiment scripts of rounds 1-3).
+#   gpurun -- bash scripts/gpu.sh TAG STEP [STEP ...]
+# Each STEP runs under its own time limit; the script stops at the first failure and
+# leaves its logs in gpurun_out/TAG_*.  Steps:
+#   tests[=PYTEST_ARGS]   pytest -m gpu (all, or e.g. tests=tests/test_wavefront_gpu.py)
+#   smoke                 __graft_entry__.smoke()
+#   bench[=ARGS]          python bench.py ARGS (default: the driver's --steps 20 --warmup 5) -> TAG_bench.json
+#   kt[=ARGS]             rocprofv3 kernel trace + stats of bench.py ARGS (no side legs) -> TAG_kernel_stats.csv,
+#                         TAG_trace_summary.json
+#   pmc[=ARGS]            the four PMC passes of the headline pass -> profiles/pmc_TAG_v0_t20.json
+#   py=SCRIPT[:ARGS]      python SCRIPT ARGS (':' separates arguments), stdout -> TAG_py_N.jsonl
+#   env=NAME:VALUE        export NAME=VALUE for the steps after it
+set -o pipefail
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+TAG=$1
+shift
+DEF_BENCH="--steps 20 --warmup 5"
+QUIET="--no-cpu-baseline --side-legs 0 --material-steps 0"
+n=0
+for step in "$@"; do
+  n=$((n + 1))
+  name=${step%%=*}
+  arg=""
+  [ "$name" != "$step" ] && arg=${step#*=}
+  log=gpurun_out/${TAG}_${n}_${name}.log
+  echo "== step $n: $step ($(date +%T))"
+  case $name in
+    env)
+      export "${arg%%:*}=${arg#*:}"
+      ;;
+    tests)
+      [ -z "$arg" ] && arg=tests
+      timeout -k 10 1100 python -u -m pytest $arg -m gpu -x -q --timeout 300 --timeout-method thread > $log 2>&1 \
+        || { tail -60 $log; exit 1; }
+      tail -2 $log
+      ;;
+    smoke)
+      timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $log 2>&1 || { tail -20 $log; exit 1; }
+      tail -2 $log
+      ;;
+    bench)
+      [ -z "$arg" ] && arg=$DEF_BENCH
+      timeout -k 10 600 python -u bench.py $arg > $log 2>&1 || { tail -30 $log; exit 1; }
+      grep "^{" $log | tail -1 > gpurun_out/${TAG}_bench.json
+      python3 -c "
+import json; d=json.load(open('gpurun_out/${TAG}_bench.json')); r=d['roofline']
+print('value', d['value'], 'ms/step', d['ms_per_step'], 'kern', r.get('kernel_ms'), 'frac', r['frac'], 'finite', d.get('state_finite'))
+print('llnl', {k: d['llnl_slab_test'].get(k) for k in ('bdf2_steps_per_s', 'ms', 'path')} if 'llnl_slab_test' in d else None)
+s = d.get('schedule', {}); print('schedule', {k: s.get(k) for k in ('end_to_end_updates_per_s', 'drain_ms', 'fill_ms')})"
+      ;;
+    kt)
+      [ -z "$arg" ] && arg=$DEF_BENCH
+      timeout -k 10 500 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_kt -o run --output-format csv \
+        -- python3 bench.py $arg $QUIET > $log 2>&1 || { tail -20 $log; exit 1; }
+      python3 scripts/trace_summary.py gpurun_out/${TAG}_kt/run_kernel_trace.csv gpurun_out/${TAG}_trace_summary.json
+      cp gpurun_out/${TAG}_kt/run_kernel_stats.csv gpurun_out/${TAG}_kernel_stats.csv
+      rm -f gpurun_out/${TAG}_kt/run_kernel_trace.csv
+      ;;
+    pmc)
+      [ -z "$arg" ] && arg=$DEF_BENCH
+      i=0
+      for pmc in "FETCH_SIZE" "WRITE_SIZE" \
+          "SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU" \
+          "GRBM_GUI_ACTIVE SQ_INSTS_SALU SQ_INSTS_VMEM SQ_INSTS_LDS"; do
+        i=$((i + 1))
+        timeout -k 10 -s KILL 300 rocprofv3 --pmc $pmc -d gpurun_out/${TAG}_pmc_$i -o run --output-format csv \
+          -- python3 bench.py $arg $QUIET > ${log%.log}_$i.log 2>&1 || { tail -5 ${log%.log}_$i.log; exit 1; }
+      done
+      python3 scripts/pmc_summary.py ${TAG}_v0_t20 gpurun_out/${TAG}_pmc_1 gpurun_out/${TAG}_pmc_2 \
+        gpurun_out/${TAG}_pmc_3 gpurun_out/${TAG}_pmc_4
+      cp profiles/pmc_${TAG}_v0_t20.json gpurun_out/ 2>/dev/null || true
+      ;;
+    py)
+      script=${arg%%:*}
+      rest=""
+      [ "$script" != "$arg" ] && rest=$(echo "${arg#*:}" | tr ':' ' ')
+      timeout -k 10 600 python -u $script $rest > gpurun_out/${TAG}_py_${n}.jsonl 2> $log \
+        || { tail -30 $log; tail -5 gpurun_out/${TAG}_py_${n}.jsonl; exit 1; }
+      tail -40 gpurun_out/${TAG}_py_${n}.jsonl
+      ;;
+    *)
+      echo "unknown step $step"; exit 2
+      ;;
+  esac
+done
+echo "== done ($(date +%T))"

@@ -94,3 +94,38 @@ def test_comm_version_is_the_loaded_rccl(rtsn_mod, comm):
     assert os.path.exists(v["path"]) and "rccl" in os.path.basename(v["path"])
     loaded = [l.split()[-1] for l in open("/proc/self/maps") if "librccl" in l]
     assert os.path.realpath(v["path"]) in {os.path.realpath(x) for x in loaded}
+
+
+_MISSING_PEER = r"""
+import sys, time
+sys.path[:0] = [sys.argv[1], sys.argv[1] + "/radiative-transfer_amd"]
+import rtsn
+uid = rtsn.Comm.unique_id()
+t0 = time.perf_counter()
+try:
+    rtsn.Comm(2, 0, uid, 0)      # rank 0 of two; rank 1 never starts
+except rtsn.RtError as e:
+    print("STATUS", e.status, round(time.perf_counter() - t0, 2), str(e)[:200], flush=True)
+else:
+    print("STATUS 0", flush=True)
+"""
+
+
+def test_comm_init_without_peer_times_out(tmp_path):
+    """rt_comm_init is non-blocking and bounded: rank 0 of a 2-rank communicator whose
+    peer never joins returns RT_ERR_TIMEOUT (7) once RTSN_COMM_TIMEOUT_S passes, instead of
+    waiting in ncclCommInitRank for ever (a child process, so a regression cannot hang the
+    test session: it is killed at the subprocess limit)."""
+    import os
+    import subprocess
+    import sys
+    from conftest import REPO
+    env = dict(os.environ, RTSN_COMM_TIMEOUT_S="5")
+    r = subprocess.run([sys.executable, "-c", _MISSING_PEER, str(REPO)], env=env, capture_output=True, text=True,
+                       timeout=150)
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith("STATUS")]
+    assert line, (r.stdout[-2000:], r.stderr[-2000:])
+    parts = line[0].split()
+    assert parts[1] == "7", line[0]
+    assert 4.5 <= float(parts[2]) <= 60.0, line[0]
+    assert "RTSN_COMM_TIMEOUT_S" in line[0]

@@ -190,6 +190,14 @@ def test_two_rank_group_shards(tmp_path, scaling, groups):
     assert line["config"]["groups_total"] == G_total
     assert line["state_finite"] is True
     assert line["roofline"]["kernel_ms"] >= max(l["wall_ms"] for l in lines) / steps * (1 - 1e-9)
+    # every rank's own timing beside the max: the same table on both ranks, the max its worst
+    pr = line["per_rank"]
+    assert pr == lines[1]["line"]["per_rank"] and [r["rank"] for r in pr] == [0, 1]
+    assert max(r["wall_ms"] for r in pr) == pytest.approx(line["ms_per_step"] * steps, rel=1e-12)
+    assert max(r["kernel_ms"] for r in pr) == line["roofline"]["kernel_ms"]
+    for r, l in zip(pr, lines):
+        upd = 4.0 * 8 * (l["info"][2] - l["info"][1]) * 48 * steps
+        assert r["updates_per_s"] == pytest.approx(upd / (r["wall_ms"] * 1e-3), rel=1e-12)
 
 
 def test_shard_table():

@@ -146,8 +146,35 @@ def test_direction_shard_assembly(rtsn_mod, full, M, n):
     [(0, 62, 0, 2), (62, 124, 2, 4)],           # neither tiling
 ])
 def test_layout_rejects_bad_tilings(rtsn_mod, shards):
-    with pytest.raises(rtsn_mod.RtError):
+    # the status comes with its own reason (rt_last_error(NULL)), not an earlier failure's text
+    with pytest.raises(rtsn_mod.RtError, match="tiling"):
         rtsn_mod.Layout([dict(G=124, M=8, g_lo=a, g_hi=b, d_lo=c, d_hi=d, N=5) for a, b, c, d in shards])
+
+
+def test_layout_checks_buffers(rtsn_mod):
+    """The plans write through raw pointers: undersized inputs, undersized or non-float64 /
+    non-contiguous outputs and bad ranks are refused before the C call (ValueError)."""
+    G, M, N = 6, 4, 5
+    lay = rtsn_mod.Layout([dict(G=G, M=M, g_lo=0, g_hi=G, d_lo=0, d_hi=1, N=N),
+                           dict(G=G, M=M, g_lo=0, g_hi=G, d_lo=1, d_hi=2, N=N)])
+    block = np.zeros(2 * G * N)
+    lay.place_psi(0, block, np.zeros(M * G * N))                        # the right sizes pass
+    with pytest.raises(ValueError, match="psi_flat"):
+        lay.place_psi(0, block, np.zeros(M * G * N - 1))
+    with pytest.raises(ValueError, match="float64"):
+        lay.place_psi(0, block, np.zeros(M * G * N, dtype=np.float32))
+    with pytest.raises(ValueError, match="float64"):
+        lay.place_psi(0, block, np.zeros(2 * M * G * N)[::2])
+    with pytest.raises(ValueError, match="block"):
+        lay.place_psi(0, block[:-1], np.zeros(M * G * N))
+    with pytest.raises(ValueError, match="rank"):
+        lay.place_psi(2, block, np.zeros(M * G * N))
+    with pytest.raises(ValueError, match="table"):
+        lay.place_psi_source(1, np.zeros(2 * G), np.zeros(M * G - 1))
+    with pytest.raises(ValueError, match="gathered"):
+        lay.unpack_moments(np.zeros(3 * N * lay.max_groups - 1))
+    with pytest.raises(ValueError, match="gathered"):
+        lay.unpack_vectors(2, np.zeros(2 * lay.max_groups - 1))
 
 
 def test_comm_version_host_only(rtsn_mod):
