@@ -292,7 +292,7 @@ def reference_config_timings(rate_steps: int = 1000) -> dict:
 
 
 def load_traffic(variant: str, tb: int, algorithmic_bytes: float):
-    """Measured HBM bytes per sweep launch (rocprofv3 PMC, scripts/gpu_profile.sh) for
+    """Measured HBM bytes per sweep launch (rocprofv3 PMC: scripts/gpu.sh TAG pmc) for
     this variant and time block, or None -- also None when the profile was taken on a
     different problem size (its bytes are not within 10% of this launch's)."""
     f = REPO / "profiles" / f"pmc_{variant}_t{tb}.json"
