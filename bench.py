@@ -171,44 +171,40 @@ REFERENCE_CONFIGS = ("single_group.prm", "multi_group_equilibrium.prm", "llnl_sl
 
 
 def gpu_rate(params: dict, ts_method: int, rate_steps: int = 1000) -> dict:
-    """rate_steps steps of a configuration on the GPU as rt_solve runs them -- the short-line
-    wavefront (one launch per advance) where the lines fit a chain of waves, else the segment
-    pipeline at the time block rt_solve would pick (rt_plan_time_block) -- the handle
-    created and warmed outside the timer, advance + finish + device sync timed: BDF2
-    steps/s and cell-angle-group updates/s, with the number of sweep launches (HIP event
-    pairs) that ran."""
+    """rate_steps steps of a configuration on the GPU exactly as rt_solve runs them (the
+    handle's max_timesteps = rate_steps): the short-line wavefront (one launch per advance)
+    where the lines fit a chain of waves, else the pipelined schedule rt_solve plans for the
+    run (rt_plan_schedule: time block, waves per segment, segmentation).  The handle is
+    created and warmed outside the timer; rt_solve + rt_finish (the pending correction of an
+    aligned remainder, if any) + device sync are timed: BDF2 steps/s and cell-angle-group
+    updates/s, with the number of sweep launches (HIP event pairs) that ran."""
     import rtsn
     params = dict(params, max_timesteps=rate_steps)
     upd_step = (4.0 if ts_method == 3 else 1.0) * params["M"] * params["G"] * params["N"]
 
-    def schedule(s):  # rt_solve's choice
-        if not s.wavefront_state()["active"]:
-            s.time_block = rtsn.plan_time_block(ts_method, rate_steps)
-
     with rtsn.Solver(params) as s:  # warm: kernels loaded, equilibrium sources built
-        schedule(s)
-        s.advance(2 * s.time_block)
+        s.solve()
         s.finish()
         s.synchronize()
     with rtsn.Solver(params) as s:
-        schedule(s)
         wst = s.wavefront_state()
         path = "wavefront" if wst["active"] else "segments"
+        plan = None if wst["active"] else s.plan_schedule(rate_steps)
         s.set_profiling(True)
         s.synchronize()
         t0 = time.perf_counter()
-        s.advance(rate_steps)
+        s.solve()
         s.finish()
         s.synchronize()
         gpu_s = time.perf_counter() - t0
         passes = s.sweep_time()[1]
         s.set_profiling(False)
         finite = s.state_finite()
-        tb = s.time_block
     return {"steps": rate_steps, "bdf2_steps_per_s": rate_steps / gpu_s, "updates_per_s": upd_step * rate_steps / gpu_s,
             "ms": 1e3 * gpu_s, "sweep_passes": passes, "path": path,
-            "time_block": None if path == "wavefront" else tb, "state_finite": finite,
-            **({"cells_per_lane": wst["cells_per_lane"], "waves_per_chain": wst["waves"]} if path == "wavefront" else {})}
+            "time_block": plan["time_block"] if plan else None, "state_finite": finite,
+            **({"cells_per_lane": wst["cells_per_lane"], "waves_per_chain": wst["waves"]} if path == "wavefront"
+               else {"plan": plan})}
 
 
 def llnl_slab_test_rate(ref_configs=None, rate_steps: int = 1000) -> dict:
@@ -241,9 +237,9 @@ def reference_config_timings(rate_steps: int = 1000) -> dict:
         against the oracle's (max per-group relative difference); for llnl_slab_test also
         the oracle with the reference's literal per-cell half_ends copy (solver.cpp:733,
         quadratic in the state size);
-      * as a rate: `rate_steps` BDF2 steps of the same configuration at the time block
-        rt_solve would pick (rt_plan_time_block; handle created and warmed outside the
-        timer; advance + finish + device sync timed), GPU BDF2 steps/s
+      * as a rate: `rate_steps` BDF2 steps of the same configuration as rt_solve runs them
+        (gpu_rate: handle created and warmed outside the timer; rt_solve + finish + device
+        sync timed), GPU BDF2 steps/s
         and updates/s beside the oracle's on one core over the same steps, with the
         number of sweep passes (HIP event pairs) the GPU ran -- the metric's named config,
         llnl_slab_test, among them."""

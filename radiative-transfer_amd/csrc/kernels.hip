@@ -42,42 +42,123 @@ namespace rtamd {
 // True incoming carried state of every segment from the aggregates of one
 // pass (each segment swept from X = 0):  Y_1 = agg_0,
 // Y_{s+1} = P_s Y_s + agg_s with P = A^Ls, or A^Llast for the last segment;
-// Y_Sg is the state after the whole line (the reflective outflow).  One
-// thread per (half, line); only_last: write Y_Sg alone, to y[KC][Lpad].
+// Y_Sg is the state after the whole line (the reflective outflow); only_last: write
+// Y_Sg alone, to y[KC][Lpad].  One wave per (half, 64-line group), lane = line.  The
+// chain is a dependent walk over the segments, so what bounds it is the latency of each
+// step: the line's propagator A^Ls (the same for every segment but the last) is staged in
+// LDS once -- [NTC/2][64 lanes] double pairs, a lane reading only its own column, so one
+// ds_read_b128 fetches its next two coefficients and no barrier is needed -- and the next
+// segment's aggregate is prefetched while the current step runs.  (The first version
+// re-read the propagator from memory at every segment: ~23 us per segment on few long
+// lines, 1.4-4.5 s for 1000 aligned steps of 4000-50000 cells, profiles/r03ao_solve_mid.jsonl.)
+constexpr int kFoldChunk = 8;  // LDS pairs per read chunk of fold_kernel's walk
+
+// fold_kernel's memory traffic: a buffer descriptor over a wave-uniform base, the row as a
+// scalar byte offset and the lane as the one VGPR offset -- a 64-bit VGPR address per row
+// would hold 2 NTC registers for the propagator alone (spills at KC = 20)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t fold_rsrc(const double *base, size_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(base), 0,
+                                           static_cast<int>(bytes < 0x7fffffffULL ? bytes : 0x7fffffffULL), 0x00020000);
+}
+__device__ __forceinline__ double fold_load(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
+  return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0));
+}
+__device__ __forceinline__ void fold_store(__amdgpu_buffer_rsrc_t r, int voff, int soff, double v) {
+  typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), r, voff, soff, 0);
+}
+
 template <int KC>
-__global__ void fold_kernel(FoldArgs f) {
-  constexpr int NTC = KC * (KC + 1) / 2;
-  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= f.nhalf * f.Lpad) return;
-  const int half = f.half0 + idx / f.Lpad, ell = idx % f.Lpad;
+__global__ __launch_bounds__(64) void fold_kernel(FoldArgs f) {
+  constexpr int NTC = KC * (KC + 1) / 2, NP = (NTC + 1) / 2;
+  __shared__ double2 lds_p[NP * 64];
+  const int lane = threadIdx.x;
+  const int groups = f.Lpad / 64;
+  const int half = f.half0 + static_cast<int>(blockIdx.x) / groups;
+  const int ell0 = (static_cast<int>(blockIdx.x) % groups) * 64;  // the wave's first line
   const size_t stride = f.Lpad, seg_stride = static_cast<size_t>(KC) * stride;
-  const double *ag = f.agg + static_cast<size_t>(half) * f.Sg * seg_stride + ell;
-  const double *pr = f.prop + static_cast<size_t>(half) * f.prop_half * stride + ell;
-  double *y = f.y + static_cast<size_t>(half) * (f.Sg + 1) * seg_stride + ell;
-  double X[KC];
+  const int rb = static_cast<int>(stride * sizeof(double));      // bytes per row (a coefficient, a component)
+  const int voff = lane * static_cast<int>(sizeof(double));
+  const double *ag = f.agg + static_cast<size_t>(half) * f.Sg * seg_stride + ell0;
+  const double *pr = f.prop + static_cast<size_t>(half) * f.prop_half * stride + ell0;
+  double *y = f.y + static_cast<size_t>(half) * (f.Sg + 1) * seg_stride + ell0;
+  const __amdgpu_buffer_rsrc_t Rp = fold_rsrc(pr, static_cast<size_t>(2 * NTC) * rb);
+  const auto seg = [&](const double *base, long long s) {  // segment s's KC rows
+    return fold_rsrc(base + static_cast<size_t>(s) * seg_stride, static_cast<size_t>(KC) * rb);
+  };
+  // a propagator (at coefficient offset o) into LDS, kFoldChunk pairs at a time
+  const auto stage = [&](int o) {
 #pragma unroll
-  for (int r = 0; r < KC; ++r) X[r] = ag[r * stride];
+    for (int q = 0; q < NP; ++q) {
+      if (q % kFoldChunk == 0) __builtin_amdgcn_sched_barrier(0);
+      lds_p[q * 64 + lane] = make_double2(fold_load(Rp, voff, (o + 2 * q) * rb),
+                                          2 * q + 1 < NTC ? fold_load(Rp, voff, (o + 2 * q + 1) * rb) : 0.0);
+    }
+  };
+  if (f.Sg > 1) stage(0);
+  double X[KC], nx[KC];
+  {
+    const __amdgpu_buffer_rsrc_t R0 = seg(ag, 0);
+#pragma unroll
+    for (int r = 0; r < KC; ++r) X[r] = fold_load(R0, voff, r * rb);
+  }
+  if (f.Sg > 1) {
+    const __amdgpu_buffer_rsrc_t R1 = seg(ag, 1);
+#pragma unroll
+    for (int r = 0; r < KC; ++r) nx[r] = fold_load(R1, voff, r * rb);
+  }
   for (int s = 1; s <= f.Sg; ++s) {
     if (!f.only_last) {
+      const __amdgpu_buffer_rsrc_t Ry = seg(y, s);
 #pragma unroll
-      for (int r = 0; r < KC; ++r) y[(s * KC + r) * stride] = X[r];
+      for (int r = 0; r < KC; ++r) fold_store(Ry, voff, r * rb, X[r]);
     }
     if (s == f.Sg) break;
-    const double *P = (f.last_short && s == f.Sg - 1) ? pr + NTC * stride : pr;
+    double cur[KC];
+#pragma unroll
+    for (int r = 0; r < KC; ++r) cur[r] = nx[r];
+    if (s + 1 < f.Sg) {  // the next segment's aggregate, in flight during this step
+      const __amdgpu_buffer_rsrc_t Rn = seg(ag, s + 1);
+#pragma unroll
+      for (int r = 0; r < KC; ++r) nx[r] = fold_load(Rn, voff, r * rb);
+    }
+    if (f.last_short && s == f.Sg - 1) stage(NTC);  // A^Llast for the last step: over P, no longer needed
+    // coefficients in tri order = LDS pair order, read in chunks of kFoldChunk pairs: the
+    // next chunk's reads are issued before the current chunk's FMAs (two buffers), with a
+    // scheduling barrier at each chunk so the compiler cannot hoist every read to the top.
+    // An opaque copy of the lane index keeps the loop-invariant reads inside the walk.
+    constexpr int CH = kFoldChunk;
+    int lo = lane;
+    asm volatile("" : "+v"(lo));
+    double2 buf[2][CH];
+#pragma unroll
+    for (int j = 0; j < CH; ++j)
+      if (j < NP) buf[0][j] = lds_p[j * 64 + lo];
     double t[KC];
 #pragma unroll
     for (int r = 0; r < KC; ++r) {
-      double acc = ag[(static_cast<size_t>(s) * KC + r) * stride];
+      double acc = cur[r];
 #pragma unroll
-      for (int c = 0; c <= r; ++c) acc += P[tri(r, c) * stride] * X[c];
+      for (int c = 0; c <= r; ++c) {
+        const int i = tri(r, c), k = i / (2 * CH), j = (i % (2 * CH)) / 2;
+        if (i % (2 * CH) == 0) {
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int jj = 0; jj < CH; ++jj)
+            if ((k + 1) * CH + jj < NP) buf[(k + 1) & 1][jj] = lds_p[((k + 1) * CH + jj) * 64 + lo];
+        }
+        const double2 pq = buf[k & 1][j];
+        acc += ((i & 1) ? pq.y : pq.x) * X[c];
+      }
       t[r] = acc;
     }
 #pragma unroll
     for (int r = 0; r < KC; ++r) X[r] = t[r];
   }
   if (f.only_last) {
+    const __amdgpu_buffer_rsrc_t Ry = fold_rsrc(f.y + ell0, static_cast<size_t>(KC) * rb);
 #pragma unroll
-    for (int r = 0; r < KC; ++r) f.y[r * stride + ell] = X[r];
+    for (int r = 0; r < KC; ++r) fold_store(Ry, voff, r * rb, X[r]);
   }
 }
 
@@ -1367,7 +1448,8 @@ hipError_t launch_sweep(int scheme, int T, int mode, const SegArgs &a, int grid,
 }
 
 hipError_t launch_fold(int KC, const FoldArgs &f, hipStream_t st) {
-  const dim3 grid((f.nhalf * f.Lpad + 255) / 256), block(256);
+  if (f.Lpad % 64) return hipErrorInvalidValue;  // one wave per 64-line group
+  const dim3 grid(f.nhalf * (f.Lpad / 64)), block(64);
   switch (KC) {
 #define RT_FOLD_CASE(n) \
   case n: hipLaunchKernelGGL(fold_kernel<n>, grid, block, 0, st, f); break;

@@ -271,7 +271,7 @@ extern "C" rt_status rt_set_pipeline(rt_solver *s, int on) {
   }
   s->pipe = on;
   s->pipe_set = true;
-  s->planned = false;
+  end_plan(s);  // a planned run's schedule gives way to the caller's
   return RT_OK;
 }
 
@@ -325,7 +325,7 @@ extern "C" rt_status rt_set_time_block(rt_solver *s, int steps_per_pass) {
   HIP_TRY(s, hipSetDevice(s->device));
   s->T = steps_per_pass;
   s->T_set = true;
-  s->planned = false;
+  end_plan(s);  // a planned run's schedule gives way to the caller's
   return resegment(s);  // now if the positions are aligned, else when they next are
 }
 
@@ -341,7 +341,7 @@ extern "C" rt_status rt_set_level_waves(rt_solver *s, int waves) {
   HIP_TRY(s, hipSetDevice(s->device));
   s->level_waves = waves;  // segments re-sized for its occupancy before the next pass (the schedule is exact
   s->lw_set = true;        // for any segmentation)
-  s->planned = false;
+  end_plan(s);  // a planned run's schedule gives way to the caller's
   if (rt_status st = resegment(s)) return st;
   return RT_OK;
 }
@@ -352,7 +352,7 @@ extern "C" rt_status rt_set_segmentation(rt_solver *s, int wgs_per_cu) {
   HIP_TRY(s, hipSetDevice(s->device));
   s->seg_wgs = wgs_per_cu;
   s->seg_set = true;
-  s->planned = false;
+  end_plan(s);  // a planned run's schedule gives way to the caller's
   return resegment(s);  // now if the positions are aligned, else before the next pass
 }
 

@@ -207,7 +207,8 @@ struct rt_solver {
   bool lw_set = false;           // the caller chose the waves per segment (rt_set_level_waves)
   int seg_wgs = 0;               // segments sized for this many workgroups per CU (0: the pass's occupancy)
   bool seg_set = false;          // the caller chose the segmentation (rt_set_segmentation)
-  bool planned = false;          // rt_solve planned the schedule (plan_schedule): pipelined from one pass
+  bool planned = false;          // the run's schedule was planned (plan_schedule): pipelined from one pass
+  int plan_T0 = 0, plan_lw0 = 0, plan_w0 = 0;  // ... over the handle's own T, level_waves, seg_wgs (end_plan)
   int d_lo = 0, d_hi = 0;        // direction-pair shard [d_lo, d_hi) of the M/2 pairs (d_hi = 0: all)
   int M_full = 0;                // the configuration's M (p.M is the handle's own direction count)
   int device = 0, cus = 0;
@@ -347,10 +348,11 @@ rt_status line_maps_s(rt_solver *s, bool unit_B, DeviceBuf &map_dev, DeviceBuf &
 rt_status ensure_propagators(rt_solver *s, int T);
 rt_status setup_lines(rt_solver *s);
 rt_status upload_inflow(rt_solver *s);
-void segment_lines(rt_solver *h, int waves_per_cu);
+void segment_lines(rt_solver *h, int waves_per_cu, long long max_sg = 1LL << 40);
+long long aligned_segments(const rt_solver *h);
 hipError_t alloc_segments(rt_solver *h);
 rt_status segment_target(rt_solver *h, int *w_out);
-rt_status resegment(rt_solver *h);
+rt_status resegment(rt_solver *h, bool aligned = false);
 
 // rtsn_schedule.hip
 rt_status check_validation(rt_solver *s);
@@ -363,6 +365,7 @@ rt_status enqueue_pass(rt_solver *s, int T, bool coupled = false);
 rt_status complete(rt_solver *s);
 rt_status finalize(rt_solver *s);
 WavePlan wave_plan(const rt_solver *s);
+void end_plan(rt_solver *s);  // the planned schedule gives way to the handle's own
 bool use_wavefront(const rt_solver *s);
 
 // rtsn_readout.hip

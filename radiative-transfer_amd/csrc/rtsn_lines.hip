@@ -284,17 +284,31 @@ rt_status rtsn_detail::upload_inflow(rt_solver *s) {
 }
 
 // Segments per line: enough waves (2 Q Sg) to fill the chip at the sweep
-// kernel's occupancy, Ls a multiple of the register chunk.
-void rtsn_detail::segment_lines(rt_solver *h, int waves_per_cu) {
+// kernel's occupancy, Ls a multiple of the register chunk; at most max_sg segments.
+void rtsn_detail::segment_lines(rt_solver *h, int waves_per_cu, long long max_sg) {
   waves_per_cu = std::max(1, std::min(waves_per_cu, 64));
   const long long target = static_cast<long long>(h->cus) * waves_per_cu;
   long long sg = std::max<long long>(1, target / (2LL * h->Q));
-  const long long max_sg = (h->p.N + kSweepCells - 1) / kSweepCells;
-  sg = std::min(sg, max_sg);
+  sg = std::min(sg, std::max<long long>(1, max_sg));
+  sg = std::min<long long>(sg, (h->p.N + kSweepCells - 1) / kSweepCells);
   long long ls = (h->p.N + sg - 1) / sg;
   ls = ((ls + kSweepCells - 1) / kSweepCells) * kSweepCells;
   h->Ls = static_cast<int>(ls);
   h->Sg = static_cast<int>((h->p.N + ls - 1) / ls);
+}
+
+// Segments of an aligned pass.  The pass sweeps every segment at once (Ls cells x Ta
+// levels per wave) and the fold walks the Sg segments one after another, so beyond the
+// chip's occupancy more segments only lengthen the walk: Sg balances Ls Ta t_cell against
+// Sg t_fold, with t_cell ~ 145 ns per cell-level and wave (the aligned T = 4 pass with its
+// correction, SL: 72.3 ms for 62500 x 4 cell-levels per wave at two waves per SIMD) and
+// t_fold ~ 200 ns + 4 ns per propagator coefficient (fold_kernel's step, LDS-resident
+// propagator).  On the SL slab the occupancy's 16 segments stay (the balance is ~900);
+// few long lines get ~100-200 segments instead of the pipeline's hundreds or thousands.
+long long rtsn_detail::aligned_segments(const rt_solver *h) {
+  const int Ta = std::min(h->T, kMaxAlignedBlock), KC = Ta * h->K;
+  const double t_cell = 145.0, t_fold = 200.0 + 4.0 * KC * (KC + 1) / 2;
+  return std::max(1LL, std::llround(std::sqrt(static_cast<double>(h->p.N) * Ta * t_cell / t_fold)));
 }
 
 // Per-segment buffers (aggregates, folded incoming states), zeroed; the
@@ -319,18 +333,20 @@ hipError_t rtsn_detail::alloc_segments(rt_solver *h) {
 // wave per SIMD at T = 16 and 20, two at T = 10, ...), applied only while every chain
 // position is at the same time with no correction outstanding -- the state rows do not
 // depend on the segmentation, only the aggregates and propagators do.  Called by
-// rt_set_time_block and again before the next pipelined or aligned pass, so a handle
-// always runs its passes with segments for the time block it runs.
+// rt_set_time_block and again before the next pipelined or aligned pass (aligned: at
+// most aligned_segments), so a handle always runs its passes with segments for the time
+// block and the kind of pass it runs.
 
-rt_status rtsn_detail::resegment(rt_solver *h) {
+rt_status rtsn_detail::resegment(rt_solver *h, bool aligned) {
   if (h->material || h->pending || h->Tpipe) return RT_OK;
   int w = 0;
   if (rt_status st = segment_target(h, &w)) return st;
-  if (h->seg_T == h->T && h->seg_w == w) return RT_OK;
+  const int key = aligned ? -w : w;  // which kind of pass the segments were sized for
+  if (h->seg_T == h->T && h->seg_w == key) return RT_OK;
   const int sg0 = h->Sg, ls0 = h->Ls;
-  segment_lines(h, w);
+  segment_lines(h, w, aligned ? aligned_segments(h) : (1LL << 40));
   h->seg_T = h->T;
-  h->seg_w = w;
+  h->seg_w = key;
   if (h->Sg == sg0 && h->Ls == ls0) return RT_OK;
   if (2LL * h->Q * h->Sg >= (1LL << 31)) return fail(h, RT_ERR_PARAM, "too many lines for one handle: shard the groups");
   HIP_TRY(h, alloc_segments(h));

@@ -159,7 +159,7 @@ rt_status rtsn_detail::enqueue_pass(rt_solver *s, int T, bool coupled) {
 
 // nsteps full steps in aligned passes of at most T (and kMaxAlignedBlock) steps.
 static rt_status enqueue_steps(rt_solver *s, int nsteps) {
-  if (rt_status st = resegment(s)) return st;
+  if (rt_status st = resegment(s, true)) return st;
   const int T = std::min(s->T, kMaxAlignedBlock);
   while (nsteps > 0) {
     const int n = std::min(T, nsteps);
@@ -227,31 +227,42 @@ static int auto_pipeline_passes(const rt_solver *s) {
   return P;
 }
 
-// Queue nsteps; launch whole passes while the chain head is behind.
+static bool plan_allowed(const rt_solver *s);
+static bool plan_for_advance(rt_solver *s);
+
+// Queue nsteps; launch whole passes while the chain head is behind.  A run not yet
+// pipelined starts its pipeline only once it has queued enough passes for one
+// (auto_pipeline_passes; for an unplanned BDF2 run, once rt_solve's plan for the .prm's run
+// length would pipeline them: plan_for_advance); until then the steps stay queued, and a
+// read-out (finalize) runs them as aligned passes.  So a run advanced in chunks pipelines
+// through its chunks -- the same launches as one rt_solve -- while a short advance followed
+// by a read-out costs aligned passes, not a pipeline fill and drain.
 static rt_status pipe_advance(rt_solver *s, int nsteps) {
   s->queued += nsteps;
-  const int T = s->T;
   rt_status st;
-  if (s->Tpipe && s->Tpipe != T) {  // a lagged pipeline of another block size: let it drain
+  if (s->Tpipe && s->Tpipe != s->T) {  // a lagged pipeline of another block size: let it drain
     while (s->tau.back() < s->target)
       if ((st = pipe_launch(s))) return st;
     s->Tpipe = 0;
   }
-  const long long passes = s->queued / T;
-  if (passes == 0) return RT_OK;
   if (!s->Tpipe) {
-    if (s->pipe == 1 && passes < auto_pipeline_passes(s)) {
-      // too few passes to fill the pipeline (it would run its segments nearly one
-      // at a time): aligned passes of at most kMaxAlignedBlock steps instead
-      s->queued -= static_cast<int>(passes * T);
-      return enqueue_steps(s, static_cast<int>(passes * T));
+    if (s->pipe == 1) {  // auto: deferred until enough passes are queued for a pipeline
+      if (plan_allowed(s)) {
+        if (!plan_for_advance(s)) return RT_OK;
+      } else if (s->queued / s->T < auto_pipeline_passes(s)) {
+        return RT_OK;
+      }
     }
+    if (s->queued / s->T == 0) return RT_OK;
     // start from aligned positions with an exact state, segments sized for this T
     if ((st = apply_correction(s))) return st;
     if ((st = resegment(s))) return st;
-    s->Tpipe = T;
+    s->Tpipe = s->T;
     s->pipe_base = s->tau[0];
   }
+  const int T = s->T;
+  const long long passes = s->queued / T;
+  if (passes == 0) return RT_OK;
   s->queued -= static_cast<int>(passes * T);
   s->target += passes * T;
   while (s->tau[0] < s->target)
@@ -259,7 +270,8 @@ static rt_status pipe_advance(rt_solver *s, int nsteps) {
   return RT_OK;
 }
 
-// Bring every position to the target (drain) and run the queued remainder.
+// Bring every position to the target (drain) and run the queued remainder.  A planned
+// schedule ends with its run's pipeline.
 rt_status rtsn_detail::complete(rt_solver *s) {
   rt_status st;
   if (s->Tpipe) {
@@ -267,6 +279,7 @@ rt_status rtsn_detail::complete(rt_solver *s) {
       if ((st = pipe_launch(s))) return st;
     s->Tpipe = 0;
   }
+  end_plan(s);
   if (s->queued) {
     const int r = s->queued;
     s->queued = 0;
@@ -463,34 +476,69 @@ extern "C" rt_status rt_plan_schedule(rt_solver *s, long long nsteps, int *steps
   return RT_OK;
 }
 
-static void solve_time_block(rt_solver *s) {
-  if (s->scheme != SCHEME_BDF2 || s->Tpipe || s->queued || use_wavefront(s)) return;
-  if (s->T_set || s->lw_set || s->seg_set) return;  // the caller chose (part of) the schedule
-  const Schedule sc = plan_schedule(run_geom(s), s->p.max_timesteps);
-  if (!sc.T) return;
+// The planned schedule for a run (time block, four waves per segment, segmentation),
+// over the handle's own choices, which end_plan restores: the plan holds for one run's
+// pipeline (rt_solve, or a run of advances) and a later run plans again.
+static void begin_plan(rt_solver *s, const Schedule &sc) {
+  s->plan_T0 = s->T;
+  s->plan_lw0 = s->level_waves;
+  s->plan_w0 = s->seg_wgs;
   s->T = sc.T;
   s->level_waves = 4;
   s->seg_wgs = sc.w;
   s->planned = true;
 }
 
-// The planned schedule holds for this run only: the handle's time block, waves per segment
-// and segmentation are the caller's (or the defaults) again afterwards, so a later
+void rtsn_detail::end_plan(rt_solver *s) {
+  if (!s->planned) return;
+  s->T = s->plan_T0;
+  s->level_waves = s->plan_lw0;
+  s->seg_wgs = s->plan_w0;
+  s->planned = false;
+}
+
+static bool plan_allowed(const rt_solver *s) {
+  if (s->scheme != SCHEME_BDF2 || s->planned || s->Tpipe || use_wavefront(s)) return false;
+  return !(s->T_set || s->lw_set || s->seg_set || s->pipe_set);  // the caller chose (part of) the schedule
+}
+
+static void solve_time_block(rt_solver *s) {
+  if (s->queued || !plan_allowed(s)) return;
+  const Schedule sc = plan_schedule(run_geom(s), s->p.max_timesteps);
+  if (sc.T) begin_plan(s, sc);
+}
+
+// An unplanned BDF2 run of advances: rt_solve's plan for the .prm's run length (at least the
+// steps queued), taken -- and its pipeline started -- once the queued steps hold 1/8 of the
+// planned chain's depth in passes (the rule of auto_pipeline_passes, on the planned
+// segments) or the whole run (max_timesteps, which rt_solve would pipeline with this plan).
+// True when the plan is in place.
+static bool plan_for_advance(rt_solver *s) {
+  if (s->planned) return true;
+  if (!plan_allowed(s)) return false;
+  const RunGeom g = run_geom(s);
+  const long long run = std::max<long long>(s->p.max_timesteps, s->queued);
+  const Schedule sc = plan_schedule(g, run);
+  if (!sc.T) return false;
+  long long Sg = 0, Ls = 0;
+  model_segments(g, sc.w, &Sg, &Ls);
+  const long long depth = g.reflective ? 2 * Sg : Sg;
+  const long long need = std::min(std::max<long long>(1, (depth + 7) / 8) * sc.T, std::max<long long>(sc.T, run / sc.T * sc.T));
+  if (s->queued < need) return false;
+  begin_plan(s, sc);
+  return true;
+}
+
+// The planned schedule holds for this run only: afterwards the handle's time block, waves
+// per segment and segmentation are the caller's (or the defaults) again, so a later
 // rt_advance is scheduled as if rt_solve had not run (the segments are re-sized at its
 // first pass).
 extern "C" rt_status rt_solve(rt_solver *s) {
   if (!s) return fail(nullptr, RT_ERR_ARG, "rt_solve: NULL handle");
-  const int T0 = s->T, lw0 = s->level_waves, w0 = s->seg_wgs;
   solve_time_block(s);
-  const bool planned = s->planned;
   rt_status st = rt_advance(s, s->p.max_timesteps);
   if (!st) st = complete(s);
-  if (planned) {
-    s->T = T0;
-    s->level_waves = lw0;
-    s->seg_wgs = w0;
-    s->planned = false;
-  }
+  end_plan(s);
   if (st) return st;
   return rt_synchronize(s);
 }

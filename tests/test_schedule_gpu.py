@@ -1,0 +1,105 @@
+"""GPU parity of the run schedules on few long lines (round 4): chunked rt_advance calls,
+the deferred start of the pipeline, the aligned schedule's own segmentation and the fold
+with its LDS-resident propagator, and the transient planned schedule.
+
+Geometry: llnl_slab_test's material and tabulated opacities resampled to 4 groups, M = 2
+(8 lines), N = 5000 or 50000 cells, dt = 1e-9 -- lines beyond the wavefront chain's 4096
+cells, with few lines, where round 3 measured 1000 aligned steps at 1.4-4.5 s against
+3.5-17 ms for rt_solve (profiles/r03ao_solve_mid.jsonl).  Every field against the oracle
+to 1e-10 per group (tests/test_gpu_parity.compare_all)."""
+import numpy as np
+import pytest
+
+from conftest import PRM_DIR
+from test_gpu_parity import compare_all, to_rt
+
+pytestmark = pytest.mark.gpu
+
+
+def _params(oracle_mod, N, steps, bc_left=0, bc_right=0, G=4):
+    p = oracle_mod.parse_prm(PRM_DIR / "llnl_slab_test.prm", table_dir=PRM_DIR)
+    p.update(N=N, G=G, group_bounds=None, group_kappa=None, dt=1e-9, max_timesteps=steps, bc_left=bc_left,
+             bc_right=bc_right)
+    p["dx"] = p["X"] / p["N"]
+    p["psi_source"] = np.full((p["M"], G), 0.5)
+    return p
+
+
+def _oracle(oracle_mod, p):
+    orc = oracle_mod.OracleSolver(p)
+    orc.solve()
+    return orc
+
+
+@pytest.mark.parametrize("bc_left", [0, 2])
+def test_chunked_advances_pipeline_through(rtsn_mod, oracle_mod, bc_left):
+    """A run advanced in 7-step chunks with no read-out in between: the first chunks stay
+    queued (no pipeline fill for a handful of steps), then the run takes rt_solve's plan for
+    the .prm's length and pipelines through the remaining chunks (lag > 0 while running);
+    the read-out drains it, and the handle's own schedule (time block 16) is back after."""
+    steps = 420
+    p = _params(oracle_mod, 5000, steps, bc_left=bc_left)
+    orc = _oracle(oracle_mod, p)
+    with rtsn_mod.Solver(to_rt(p)) as gpu:
+        assert not gpu.wavefront_state()["active"]
+        plan = gpu.plan_schedule(steps)
+        gpu.advance(7)
+        st = gpu.pipeline_state()
+        assert st["queued_steps"] == 7 and st["lag_steps"] == 0  # deferred
+        done = 7
+        lagged = False
+        while done < steps:
+            n = min(7, steps - done)
+            gpu.advance(n)
+            done += n
+            lagged = lagged or gpu.pipeline_state()["lag_steps"] > 0
+        assert lagged, "the chunked run never pipelined"
+        assert gpu.time_block == plan["time_block"]
+        compare_all(gpu, orc)
+        assert gpu.time_block == 16 and gpu.pipeline_state()["lag_steps"] == 0
+
+
+@pytest.mark.parametrize("N", [5000, 50000])
+def test_short_advances_with_readouts(rtsn_mod, oracle_mod, N):
+    """Short advances each followed by a read-out run as aligned passes (the deferred steps
+    at finalize) on the aligned schedule's own, coarser segmentation -- not the pipeline's
+    hundreds of segments -- and the fold walks them from LDS.  The state after every
+    read-out equals the oracle's at the same step."""
+    chunks = [5, 9, 3, 7]
+    p = _params(oracle_mod, N, sum(chunks))
+    with rtsn_mod.Solver(to_rt(p)) as gpu:
+        done = 0
+        for n in chunks:
+            gpu.advance(n)
+            done += n
+            orc = _oracle(oracle_mod, dict(p, max_timesteps=done))
+            compare_all(gpu, orc)
+        _, segs = gpu.sweep_geometry()
+        assert segs <= 400, segs  # aligned_segments: ~100-200 here (the pipeline's would be 312 / 1024+)
+
+
+def test_aligned_schedule_chunked_long_line(rtsn_mod, oracle_mod):
+    """The aligned schedule on request (rt_set_pipeline 0): 50000 cells in chunked advances
+    of 1-8 steps with the correction pending across calls, reflective left boundary (the
+    mid-pass fold of the mu < 0 outflow): against the oracle."""
+    chunks = [3, 8, 1, 4, 6, 2]
+    p = _params(oracle_mod, 50000, sum(chunks), bc_left=2, bc_right=1)
+    orc = _oracle(oracle_mod, p)
+    with rtsn_mod.Solver(to_rt(p)) as gpu:
+        gpu.pipeline = 0
+        for n in chunks:
+            gpu.advance(n)
+        compare_all(gpu, orc)
+
+
+def test_solve_plan_is_transient(rtsn_mod, oracle_mod):
+    """rt_solve plans its run (time block, four waves per segment, segmentation) and gives
+    the handle back its own schedule afterwards: the reported time block and waves per
+    segment are the defaults again, and a following advance + read-out is still exact."""
+    p = _params(oracle_mod, 5000, 64)
+    with rtsn_mod.Solver(to_rt(p)) as gpu:
+        tb0, lw0 = gpu.time_block, gpu.level_waves
+        gpu.solve()
+        assert (gpu.time_block, gpu.level_waves) == (tb0, lw0)
+        gpu.advance(10)
+        compare_all(gpu, _oracle(oracle_mod, dict(p, max_timesteps=74)))
