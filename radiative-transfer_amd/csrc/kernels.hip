@@ -545,11 +545,11 @@ __global__ void import_ends_kernel(double2 *E, const double *ends, LineMap m, in
 // transposed through LDS (lane g then reads its MOM_W values), and the next
 // chunk's loads are in flight while the current one is summed.  The weights
 // are wave-uniform (scalar loads).
-constexpr int MOM_W = 8;  // directions per chunk: 8 x 16 B = one 128 B line per group
-
+// MOM_W directions per chunk: 8 x 16 B = one 128 B line per group, 16 = two (16 KB of the
+// state in flight per wave instead of 8: round 4).
 // FAST: H % MOM_W == 0, so every chunk is 64 groups x MOM_W directions and lane
-// (gr, col) = (lane / 8, lane % 8) loads group gr + 8 r, direction col of it.
-template <bool FAST>
+// (gr, col) = (lane / MOM_W, lane % MOM_W) loads group gr + (64 / MOM_W) r, direction col.
+template <bool FAST, int MOM_W>
 __global__ void __launch_bounds__(64) moments_kernel(const double2 *__restrict__ E, const double *__restrict__ mu,
                                                      const double *__restrict__ wt, double *phi, double *F,
                                                      double *phi_plus, LineMap m) {
@@ -575,7 +575,7 @@ __global__ void __launch_bounds__(64) moments_kernel(const double2 *__restrict__
           __builtin_amdgcn_make_buffer_rsrc(const_cast<double2 *>(row), 0, ng * H * 16, 0x00020000);
       const int voff = (H * (lane / MOM_W) + lane % MOM_W) * 16;
 #pragma unroll
-      for (int r = 0; r < MOM_W; ++r) v[r] = row_load(R, voff, r * 8 * H * 16);
+      for (int r = 0; r < MOM_W; ++r) v[r] = row_load(R, voff, r * (64 / MOM_W) * H * 16);
     } else {
       const int w = min(MOM_W, H - i0);
 #pragma unroll
@@ -600,7 +600,7 @@ __global__ void __launch_bounds__(64) moments_kernel(const double2 *__restrict__
         const int gr = lane / MOM_W, col = lane % MOM_W;
 #pragma unroll
         for (int r = 0; r < MOM_W; ++r)
-          if (gr + 8 * r < ng) tile[(gr + 8 * r) * (MOM_W + 1) + col] = 0.5 * (v[r].x + v[r].y);
+          if (gr + (64 / MOM_W) * r < ng) tile[(gr + (64 / MOM_W) * r) * (MOM_W + 1) + col] = 0.5 * (v[r].x + v[r].y);
       } else {
 #pragma unroll
         for (int r = 0; r < MOM_W; ++r) {
@@ -1551,18 +1551,27 @@ hipError_t launch_import_ends(double2 *E, const double *ends, const Geometry &g,
   return hipGetLastError();
 }
 
+#ifndef RT_MOM_W
+#define RT_MOM_W 16
+#endif
 hipError_t launch_moments(const double2 *E, const double *mu, const double *wt, double *phi, double *F,
                           double *phi_plus, const Geometry &g, hipStream_t st) {
   const LineMap m = make_map(g);
   const size_t tasks = static_cast<size_t>(g.N) * ((g.Gl + 63) / 64);
-  // as many waves as the chip holds at once; each walks its tasks with a one-chunk prefetch
-  const bool fast = m.H % MOM_W == 0;
-  static const size_t resident[2] = {resident_blocks(moments_kernel<false>, 64), resident_blocks(moments_kernel<true>, 64)};
-  const dim3 grid(static_cast<unsigned>(tasks < resident[fast] ? tasks : resident[fast]));
-  if (fast)
-    hipLaunchKernelGGL(moments_kernel<true>, grid, dim3(64), 0, st, E, mu, wt, phi, F, phi_plus, m);
+  // as many waves as the chip holds at once; each walks its tasks with a one-chunk prefetch:
+  // 16-direction chunks where the half's directions come in whole ones, else 8
+  constexpr int W = RT_MOM_W;
+  static const size_t resident[3] = {resident_blocks(moments_kernel<false, 8>, 64),
+                                     resident_blocks(moments_kernel<true, 8>, 64),
+                                     resident_blocks(moments_kernel<true, W>, 64)};
+  const int kind = m.H % W == 0 ? 2 : (m.H % 8 == 0 ? 1 : 0);
+  const dim3 grid(static_cast<unsigned>(tasks < resident[kind] ? tasks : resident[kind]));
+  if (kind == 2)
+    hipLaunchKernelGGL((moments_kernel<true, W>), grid, dim3(64), 0, st, E, mu, wt, phi, F, phi_plus, m);
+  else if (kind == 1)
+    hipLaunchKernelGGL((moments_kernel<true, 8>), grid, dim3(64), 0, st, E, mu, wt, phi, F, phi_plus, m);
   else
-    hipLaunchKernelGGL(moments_kernel<false>, grid, dim3(64), 0, st, E, mu, wt, phi, F, phi_plus, m);
+    hipLaunchKernelGGL((moments_kernel<false, 8>), grid, dim3(64), 0, st, E, mu, wt, phi, F, phi_plus, m);
   return hipGetLastError();
 }
 
