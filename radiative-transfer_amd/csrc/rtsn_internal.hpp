@@ -291,16 +291,28 @@ inline int level_waves_of(const rt_solver *s, int T) {
 // Waves per segment of one pipelined launch of `grid` workgroups.  The segments are sized
 // so that a full launch (every chain position active) fills the chip; the pipeline's fill
 // and drain launches hold fewer positions, and with the default level_waves (0) their
-// segments are split over 2 or 4 waves (sweep_split_kernel) as long as the launch stays
-// within the full launch's wave count -- the lines are then traversed 2-4x faster while
-// the chip would otherwise idle (BDF2 time blocks the split kernel has: 8, 10, 12, 16, 20).
+// segments are split over 2 or 4 waves (sweep_split_kernel; BDF2 time blocks the split
+// kernel has) -- the lines are then traversed 2-4x faster while the chip would otherwise
+// idle.  The pick minimises the levels the busiest SIMD runs (a workgroup's k waves take
+// one SIMD each; T / k levels per wave): e.g. 5 of 8 positions of the driver's T = 20 window
+// as four waves run 3 x 5 levels per SIMD instead of 2 x 10 (round 3 had kept two waves
+// beyond the full launch's wave count: 133 of the full launch's 164 ms for 5/8 of its work,
+// profiles/r03ar_trace_summary.json).  Ties go to the most waves within that count.
 inline int fill_level_waves(const rt_solver *s, int grid) {
   const int base = level_waves_of(s, s->Tpipe);
   if (s->level_waves || s->scheme != SCHEME_BDF2 || !split_block(s->Tpipe)) return base;
+  const int T = s->Tpipe;
   const long long full = 2LL * s->Q * s->Sg * base;  // waves of a launch with every position active
-  int k = base;
-  while (k < 4 && s->Tpipe % (2 * k) == 0 && static_cast<long long>(grid) * 2 * k <= full) k *= 2;
-  return k;
+  int within = base;                                 // the most waves per segment within `full`
+  while (within < 4 && T % (2 * within) == 0 && static_cast<long long>(grid) * 2 * within <= full) within *= 2;
+  const long long per_cu = (static_cast<long long>(grid) + s->cus - 1) / s->cus;  // workgroups on the busiest CU
+  const auto cost = [&](int k) { return (per_cu * k + 3) / 4 * (T / k); };       // levels on its busiest SIMD
+  int best = base;
+  for (int k = 2 * base; k <= 4 && T % k == 0; k *= 2) {
+    const long long c = cost(k), cb = cost(best);
+    if (c < cb || (c == cb && k <= within)) best = k;
+  }
+  return best;
 }
 
 // Chain positions of the pipelined schedule: the Sg segments of a line (both
