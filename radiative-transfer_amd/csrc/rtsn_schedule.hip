@@ -375,7 +375,8 @@ extern "C" rt_status rt_synchronize(rt_solver *s) {
 // runs in rounds of the resident 2 per CU, and a round's time is one segment's Ls x T / 4
 // cell-levels per wave at the per-level cost of its block (t_T) times the workgroups the
 // busiest CU holds (ceil(W / CUs): a wave per SIMD each).  n mod T steps more run as aligned
-// passes with the cross-segment correction (~3 steps' cost each, ~30 ms of folds).
+// passes with the cross-segment correction (~3 steps' cost each, ~3 ms of folds and the
+// finalize on the aligned segmentation; ~30 ms before the fold kept its propagator in LDS).
 struct RunGeom {
   long long N;
   int M, Gl, cus;
@@ -428,7 +429,7 @@ static double run_ms_model(const RunGeom &g, long long n, int T, int w) {
   s += static_cast<double>(std::max(P, C) - m + 1) * launch(m);
   if (rem) {
     const double step = static_cast<double>(R) * g.N * tf / (4.0 * g.cus);  // one step, every line, full load
-    s += rem * 3.0 * step + 0.03;
+    s += rem * 3.0 * step + 0.003;  // + the folds and the finalize (aligned segmentation, LDS fold)
   }
   return 1e3 * s;
 }
