@@ -298,11 +298,242 @@ __global__ __launch_bounds__(MULTI ? 64 * kWaveMaxWaves : 64) void wavefront_ker
   }
 }
 
+// ---------------------------------------------------------------------------
+// Chains over several waves, round 4 (chain_kernel).  Round 3's MULTI path of
+// wavefront_kernel ran ~75 instructions per tick against the single wave's 37: the compiler
+// turned its runtime ring indices, the per-tick barrier test, the writer's branch and the
+// rotating prefetch registers into SALU address arithmetic, exec-mask branches, a copy of
+// every DPP `old` operand into the DPP's destination and ~6.5 register-rotation moves per
+// tick -- the "160-200 cycles of cross-wave coupling" (DESIGN.md §2).  Here every wave runs
+// its tick stream in blocks of kChainBlock wall ticks that end in the barrier, so inside a
+// block every ring slot is a compile-time offset from one per-block base: wave w runs
+// kChainSkew = 2 blocks of chain ticks behind wave w - 1, so the chain tick of a block's
+// first wall tick is a multiple of the block (mod the ring) for every wave.  Slot s of
+// boundary w holds what lane 0 of wave w receives at chain tick s (lane 63 of wave w - 1's
+// exit state of tick s - 1: written at wall tick s - 1 + 16 (w - 1), read one tick ahead,
+// at wall tick s - 1 + 16 w: two barriers later; overwritten 32 chain ticks on, after the
+// read and a barrier).  Components 1..K-1 sit first in a slot (two 16-byte pairs for BDF2,
+// the whole unmasked exchange), component 0 after them (needed only by masked ticks: in the
+// unmasked stretch it is the previous tick's component K-1, as in the single wave).  Region
+// 0 holds the chain head's inflow state in every slot, so wave 0 reads the same way.  Writer
+// stores go two ticks at a time (one exec-mask branch per pair).  Same arithmetic per (cell,
+// level) as wavefront_kernel: bitwise the pipelined schedule.
+constexpr int kChainBlock = 8;                 // wall ticks per barrier block
+constexpr int kChainSkew = 2 * kChainBlock;    // chain ticks wave w runs behind wave w - 1
+constexpr int kChainRing = 4 * kChainBlock;    // slots per boundary (and region 0)
+constexpr int kChainSlot = 6;                  // doubles per slot (48 B: 16-byte aligned)
+static_assert(kChainSkew >= kChainBlock + 2 && kChainSkew + kChainBlock <= kChainRing, "ring too short for the skew");
+static_assert(kChainSkew % kChainBlock == 0 && kChainRing % kChainBlock == 0, "blocks align with the ring");
+
+template <int K>
+__device__ __forceinline__ constexpr int slot_pos(int r) {  // component r's double in a slot
+  return r == 0 ? K - 1 : r - 1;
+}
+
+template <int S, int C, bool PAIR, bool PAD>
+__global__ __launch_bounds__(64 * kWaveMaxWaves) void chain_kernel(SegArgs a, int nsteps, int Lw) {
+  constexpr int K = SchemeDim<S>::K, WN = map_count<S>();
+  static_assert(K <= kChainSlot - 1, "a slot holds the carried state");
+  RT_STAMP(0);
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
+  const int nw = static_cast<int>(blockDim.x >> 6);
+  const int g = w * 64 + lane;  // chain lane
+  const int nl = a.H * a.Gl;
+  int half, ell, j;
+  if (PAIR) {
+    ell = blockIdx.x;
+    half = g < Lw ? 0 : 1;
+    j = g - half * Lw;
+  } else {
+    half = static_cast<int>(blockIdx.x) / nl;
+    ell = static_cast<int>(blockIdx.x) % nl;
+    j = g;
+  }
+  const int used = PAIR ? 2 * Lw : Lw;
+  const bool real = g < used;
+  const size_t stride = static_cast<size_t>(a.Lpad);
+  double2 *Eh = a.E + static_cast<size_t>(half) * a.Nrow * stride + ell;
+  double ein[C], eout[C];
+#pragma unroll
+  for (int c = 0; c < C; ++c) {
+    const int k = j * C + c;
+    ein[c] = eout[c] = 0.0;
+    if (real && k < a.N) {
+      const double2 v = Eh[static_cast<size_t>(k) * stride];
+      ein[c] = v.x;
+      eout[c] = v.y;
+    }
+  }
+  double W[WN];
+#pragma unroll
+  for (int n = 0; n < WN; ++n) W[n] = a.map[(static_cast<size_t>(half) * WN + n) * stride + ell];
+#pragma unroll
+  for (int n = 0; n < WN; ++n) asm volatile("" : "+v"(W[n]));  // VGPR-resident map (wavefront_kernel)
+  const bool refl_head = PAIR && half == 1 && j == 0;
+  LineConst L{};
+  if (refl_head) {
+    const double *lcp = a.lc + static_cast<size_t>(half) * LC_COUNT * stride + ell;
+#pragma unroll
+    for (int n = 0; n < LC_COUNT; ++n) L.c[n] = lcp[n * stride];
+  }
+  double Xin[K], X[K];
+  {
+    const double bv = a.bdry[static_cast<size_t>(PAIR ? 0 : half) * stride + ell];
+    const double b[4] = {bv, bv, bv, bv};
+    head_state<S>(b, Xin);
+#pragma unroll
+    for (int r = 0; r < K; ++r) X[r] = Xin[r];
+  }
+  // ring: [nw][kChainRing][kChainSlot] doubles, 16-byte aligned; region 0 the head's state
+  extern __shared__ double2 ring2[];
+  double *ring = reinterpret_cast<double *>(ring2);
+  {
+    const int n = nw * kChainRing * kChainSlot;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+      const int p = i % kChainSlot;
+      double v = 0.0;
+#pragma unroll
+      for (int r = 0; r < K; ++r)
+        if (p == slot_pos<K>(r)) v = Xin[r];
+      ring[i] = i < kChainRing * kChainSlot ? v : 0.0;
+    }
+  }
+  __syncthreads();
+  double *const rd_region = ring + static_cast<size_t>(w) * kChainRing * kChainSlot;
+  double *const wr_region = ring + static_cast<size_t>(w + 1) * kChainRing * kChainSlot;  // unused by the last wave
+  const bool writer = lane == 63 && w < nw - 1;
+  constexpr int RM = kChainRing - 1;
+
+  // one tick's cells: X (received state, the shifts done) through the lane's C cells
+  const auto cells = [&](bool active) {
+    if (PAIR && refl_head) {
+      if constexpr (S == SCHEME_BDF2) X[0] = X[2];
+      if constexpr (S == SCHEME_CN) X[0] = X[1];
+    }
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      double Xn[K], oi, oo;
+      if (PAIR && c == 0 && refl_head) {
+        cell_step_maybe_head<S>(L, a.hd, false, ein[0], eout[0], X, true, X[K - 1], oi, oo);
+#pragma unroll
+        for (int r = 0; r < K; ++r) Xn[r] = X[r];
+      } else {
+        map_apply<S, true>(W, X, ein[c], eout[c], Xn, oi, oo);
+      }
+      if constexpr (PAD) {
+        const bool pad = j * C + c >= a.N;
+#pragma unroll
+        for (int r = 0; r < K; ++r) X[r] = pad ? X[r] : Xn[r];
+      } else {
+#pragma unroll
+        for (int r = 0; r < K; ++r) X[r] = Xn[r];
+      }
+      ein[c] = active ? oi : ein[c];
+      eout[c] = active ? oo : eout[c];
+    }
+  };
+  const auto read_slot = [&](const double *sl, double (&o)[K], bool all) {
+    if constexpr (K == 5) {
+      const double2 p0 = *reinterpret_cast<const double2 *>(sl), p1 = *reinterpret_cast<const double2 *>(sl + 2);
+      o[1] = p0.x;
+      o[2] = p0.y;
+      o[3] = p1.x;
+      o[4] = p1.y;
+      if (all) o[0] = sl[4];
+    } else {
+#pragma unroll
+      for (int r = 0; r < K; ++r)
+        if (all || r > 0) o[r] = sl[slot_pos<K>(r)];
+    }
+  };
+  const auto write_slot = [&](double *sl, const double (&x)[K], bool all) {
+    if constexpr (K == 5) {
+      *reinterpret_cast<double2 *>(sl) = make_double2(x[1], x[2]);
+      *reinterpret_cast<double2 *>(sl + 2) = make_double2(x[3], x[4]);
+      if (all) sl[4] = x[0];
+    } else {
+#pragma unroll
+      for (int r = 0; r < K; ++r)
+        if (all || r > 0) sl[slot_pos<K>(r)] = x[r];
+    }
+  };
+
+  const int wsk = w * kChainSkew;
+  const int ticks = nsteps + used - 1;
+  const int nblocks = (ticks + (nw - 1) * kChainSkew + kChainBlock - 1) / kChainBlock;  // every wave: same barriers
+  // this wave's unmasked chain ticks: its real lanes all at a level in [1, nsteps)
+  const int u_lo = min(64 * w + 63, used - 1) + 1, u_hi = max(u_lo, nsteps + 64 * w);
+  double nx[K];  // the ring values lane 0 receives at the next tick
+#pragma unroll
+  for (int r = 0; r < K; ++r) nx[r] = 0.0;
+  read_slot(rd_region, nx, true);  // chain tick 0 (slot 0)
+  RT_STAMP(1);
+  for (int b = 0; b < nblocks; ++b) {
+    const int t0 = b * kChainBlock - wsk;  // chain tick of the block's first wall tick (= 0 mod the block)
+    if (K > 1 && t0 >= u_lo && t0 + kChainBlock <= u_hi) {
+      // unmasked block: ring offsets fixed relative to the block's slot base
+      const int base = t0 & RM, nbase = (t0 + kChainBlock) & RM;
+      const double *rb = rd_region + base * kChainSlot, *rn = rd_region + nbase * kChainSlot;
+      double *wb = wr_region + base * kChainSlot, *wn = wr_region + nbase * kChainSlot;
+      double prev[K];
+#pragma unroll
+      for (int i = 0; i < kChainBlock; ++i) {
+        // ticks are not interleaved: at 8 cells per lane an 8-tick block would not fit
+        // the registers
+        if (C >= 4) __builtin_amdgcn_sched_barrier(0);
+        const double x0 = Xin[K - 1];
+        Xin[K - 1] = lane_shift_up(nx[K - 1], X[K - 1]);
+#pragma unroll
+        for (int r = 1; r < K - 1; ++r) Xin[r] = lane_shift_up(nx[r], X[r]);
+        Xin[0] = x0;
+        // the next tick's ring values (slot t + 1), after this tick's shifts
+        read_slot(i + 1 < kChainBlock ? rb + (i + 1) * kChainSlot : rn, nx, false);
+#pragma unroll
+        for (int r = 0; r < K; ++r) X[r] = Xin[r];
+        cells(true);
+        if constexpr (C >= 4) {  // a tick of 4-8 cells per lane: the store's branch is cheap beside it
+          if (writer) write_slot(i + 1 < kChainBlock ? wb + (i + 1) * kChainSlot : wn, X, false);
+        } else if (i & 1) {  // exit states of ticks t - 1 and t into slots t and t + 1, one branch per pair
+          if (writer) {
+            write_slot(wb + i * kChainSlot, prev, false);
+            write_slot(i + 1 < kChainBlock ? wb + (i + 1) * kChainSlot : wn, X, false);
+          }
+        } else {
+#pragma unroll
+          for (int r = 0; r < K; ++r) prev[r] = X[r];
+        }
+      }
+    } else {
+      for (int i = 0; i < kChainBlock; ++i) {
+        const int t = t0 + i;
+        if (t < 0 || t >= ticks) continue;  // wall ticks before or after this wave's chain
+#pragma unroll
+        for (int r = 0; r < K; ++r) Xin[r] = lane_shift_up(nx[r], X[r]);
+        read_slot(rd_region + ((t + 1) & RM) * kChainSlot, nx, true);
+        const int lv = t - g;
+#pragma unroll
+        for (int r = 0; r < K; ++r) X[r] = Xin[r];
+        cells(real && lv >= 0 && lv < nsteps);
+        if (writer) write_slot(wr_region + ((t + 1) & RM) * kChainSlot, X, true);
+      }
+    }
+    __syncthreads();
+  }
+  RT_STAMP(2);
+#pragma unroll
+  for (int c = 0; c < C; ++c) {
+    const int k = j * C + c;
+    if (real && k < a.N) Eh[static_cast<size_t>(k) * stride] = make_double2(ein[c], eout[c]);
+  }
+}
+
 template <int S, bool PAIR>
 static hipError_t launch_wave_s(const WavePlan &p, const SegArgs &a, int nsteps, int grid, hipStream_t st) {
   const bool pad = PAIR && a.N % p.C != 0;
   const int Lw = p.lanes;
   if (p.waves > 1) {
+#ifdef RT_CHAIN_V1  // round 3's chain (timing comparisons)
     const size_t lds = sizeof(double) * SchemeDim<S>::K * (1 + static_cast<size_t>(p.waves - 1) * kWaveRing);
     switch (p.C) {
 #define RT_WAVE_CASE(c)                                                                                          \
@@ -318,6 +549,23 @@ static hipError_t launch_wave_s(const WavePlan &p, const SegArgs &a, int nsteps,
 #undef RT_WAVE_CASE
       default: return hipErrorInvalidValue;
     }
+#else
+    const size_t lds = sizeof(double) * kChainSlot * kChainRing * static_cast<size_t>(p.waves);
+    switch (p.C) {
+#define RT_CHAIN_CASE(c)                                                                                         \
+  case c:                                                                                                        \
+    if (pad)                                                                                                     \
+      hipLaunchKernelGGL((chain_kernel<S, c, PAIR, PAIR && (c > 1)>), dim3(grid), dim3(64 * p.waves), lds, st, a, \
+                         nsteps, Lw);                                                                            \
+    else                                                                                                         \
+      hipLaunchKernelGGL((chain_kernel<S, c, PAIR, false>), dim3(grid), dim3(64 * p.waves), lds, st, a, nsteps,   \
+                         Lw);                                                                                    \
+    break;
+      RT_CHAIN_CASE(1) RT_CHAIN_CASE(2) RT_CHAIN_CASE(4) RT_CHAIN_CASE(8)
+#undef RT_CHAIN_CASE
+      default: return hipErrorInvalidValue;
+    }
+#endif
     return hipGetLastError();
   }
   switch (p.C) {
