@@ -313,8 +313,9 @@ __global__ __launch_bounds__(MULTI ? 64 * kWaveMaxWaves : 64) void wavefront_ker
 // exit state of tick s - 1: written at wall tick s - 1 + 16 (w - 1), read one tick ahead,
 // at wall tick s - 1 + 16 w: two barriers later; overwritten 32 chain ticks on, after the
 // read and a barrier).  Components 1..K-1 sit first in a slot (two 16-byte pairs for BDF2,
-// the whole unmasked exchange), component 0 after them (needed only by masked ticks: in the
-// unmasked stretch it is the previous tick's component K-1, as in the single wave).  Region
+// the whole unmasked exchange), component 0 after them: lane 0 needs it from the ring only
+// while it is at level 0 (at levels >= 1 it is the component K-1 lane 0 received one tick
+// earlier, as in the single wave), so the writer's unmasked ticks store components 1..K-1.  Region
 // 0 holds the chain head's inflow state in every slot, so wave 0 reads the same way.  Writer
 // stores go two ticks at a time (one exec-mask branch per pair).  Same arithmetic per (cell,
 // level) as wavefront_kernel: bitwise the pipelined schedule.
@@ -508,8 +509,13 @@ __global__ __launch_bounds__(64 * kWaveMaxWaves) void chain_kernel(SegArgs a, in
       for (int i = 0; i < kChainBlock; ++i) {
         const int t = t0 + i;
         if (t < 0 || t >= ticks) continue;  // wall ticks before or after this wave's chain
+        // lane 0's component 0: the ring's only where lane 0 is at level 0 or idle -- at a
+        // level >= 1 it is the component K - 1 lane 0 received one tick earlier (the unmasked
+        // stretch's rule), since the writer's unmasked ticks store components 1..K-1 only
+        const double old0 = (K > 1 && t - 64 * w >= 1) ? Xin[K - 1] : nx[0];
+        Xin[0] = lane_shift_up(old0, X[0]);
 #pragma unroll
-        for (int r = 0; r < K; ++r) Xin[r] = lane_shift_up(nx[r], X[r]);
+        for (int r = 1; r < K; ++r) Xin[r] = lane_shift_up(nx[r], X[r]);
         read_slot(rd_region + ((t + 1) & RM) * kChainSlot, nx, true);
         const int lv = t - g;
 #pragma unroll
