@@ -69,6 +69,13 @@ static_assert((kWaveBlockTicks & (kWaveBlockTicks - 1)) == 0 && (kWaveRing & (kW
               "block and ring indices are masks");
 static_assert(kWavePrefetch >= 1 && kWaveSkew + kWaveBlockTicks + 1 <= kWaveRing, "ring too short for the skew");
 
+// Ticks per loop iteration of the single-wave kernel (even; timing experiments: RT_WAVE_UNROLL)
+#ifndef RT_WAVE_UNROLL
+#define RT_WAVE_UNROLL 2
+#endif
+constexpr int kWaveUnroll = RT_WAVE_UNROLL;
+static_assert(kWaveUnroll >= 2 && kWaveUnroll % 2 == 0, "renames cancel over an even number of ticks");
+
 // Diagnostic builds only (make variant V=stamps RT_DEFS=-DRT_WAVE_STAMPS): lane 0 of every wave
 // records (s_memtime, s_memrealtime) at entry, before and after its tick stream; the product
 // never reads them.  rt_debug_wave_stamps copies them out (tools/wave_clock.py).
@@ -258,13 +265,14 @@ __global__ __launch_bounds__(MULTI ? 64 * kWaveMaxWaves : 64) void wavefront_ker
         if (((tick + wskew) & (kWaveBlockTicks - 1)) == kWaveBlockTicks - 1) __syncthreads();
       }
     };
-    // two ticks per iteration: the loop-carried renames of X, ein and eout then cancel
+    // kWaveUnroll (even) ticks per iteration: the loop-carried renames of X, ein and eout
+    // then cancel
     int tick = tick0;
-    for (; tick + 1 < tick1; tick += 2) {
-      body(tick);
-      body(tick + 1);
+    for (; tick + kWaveUnroll - 1 < tick1; tick += kWaveUnroll) {
+#pragma unroll
+      for (int u = 0; u < kWaveUnroll; ++u) body(tick + u);
     }
-    if (tick < tick1) body(tick);
+    for (; tick < tick1; ++tick) body(tick);
   };
   const int ticks = nsteps + used - 1;
   // this wave's unmasked chain ticks: its real lanes all at a level in [1, nsteps)
