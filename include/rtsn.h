@@ -136,9 +136,12 @@ rt_status rt_plan_schedule(rt_solver *s, long long nsteps, int *steps_per_pass, 
  * groups, 256 CUs) for a BDF2 run of nsteps (host only, no handle), e.g. 20 for 300 steps,
  * 40 for 1000; the default block for BE / CN. */
 rt_status rt_plan_time_block(int ts_method, long long nsteps, int *steps_per_pass);
-/* Asynchronous: enqueue nsteps full steps on the handle's stream (with the
- * pipelined schedule, whole passes are launched now and a remainder of fewer
- * than T steps when the state is next read). */
+/* Asynchronous: request nsteps full steps on the handle's stream.  Steps may stay queued
+ * on the host until enough accumulate for an efficient launch -- a pipelined schedule
+ * starts once its run would pipeline (a remainder of fewer than T steps waits for the
+ * next read-out), the wavefront kernel launches once 8 times its chain's fill is queued --
+ * and rt_finish or any read-out launches whatever is queued.  Results do not depend on how
+ * a run is cut into rt_advance calls. */
 rt_status rt_advance(rt_solver *s, int nsteps);
 /* Enqueue what brings the stored state exactly to the requested time --
  * pipeline drain, queued remainder steps, pending correction.  Every

@@ -71,7 +71,7 @@ static_assert(kWavePrefetch >= 1 && kWaveSkew + kWaveBlockTicks + 1 <= kWaveRing
 
 // Ticks per loop iteration of the single-wave kernel (even; timing experiments: RT_WAVE_UNROLL)
 #ifndef RT_WAVE_UNROLL
-#define RT_WAVE_UNROLL 2
+#define RT_WAVE_UNROLL 4
 #endif
 constexpr int kWaveUnroll = RT_WAVE_UNROLL;
 static_assert(kWaveUnroll >= 2 && kWaveUnroll % 2 == 0, "renames cancel over an even number of ticks");
@@ -92,9 +92,21 @@ __device__ unsigned long long g_wave_stamps[kStampWaves * 6];
       g_wave_stamps[wv_ * 6 + 2 * (slot) + 1] = r_;                                                 \
     }                                                                                               \
   } while (0)
+// chain_kernel, workgroup 0 only: every wave's s_memtime before and after each block's barrier
+constexpr int kBlockStamps = 2048;
+__device__ unsigned long long g_block_stamps[kWaveMaxWaves * kBlockStamps * 2];
+#define RT_BLOCK_STAMP(b, k)                                                                        \
+  do {                                                                                              \
+    const unsigned long long t_ = __builtin_amdgcn_s_memtime();                                     \
+    if (blockIdx.x == 0 && (threadIdx.x & 63) == 0 && (b) < kBlockStamps)                           \
+      g_block_stamps[((threadIdx.x >> 6) * kBlockStamps + (b)) * 2 + (k)] = t_;                     \
+  } while (0)
 #else
 #define RT_STAMP(slot) \
   do {                 \
+  } while (0)
+#define RT_BLOCK_STAMP(b, k) \
+  do {                       \
   } while (0)
 #endif
 
@@ -331,6 +343,9 @@ constexpr int kChainBlock = 8;                 // wall ticks per barrier block
 constexpr int kChainSkew = 2 * kChainBlock;    // chain ticks wave w runs behind wave w - 1
 constexpr int kChainRing = 4 * kChainBlock;    // slots per boundary (and region 0)
 constexpr int kChainSlot = 6;                  // doubles per slot (48 B: 16-byte aligned)
+#ifndef RT_CHAIN_EARLY
+#define RT_CHAIN_EARLY 1  // ring stores and reads issued before the tick's FMAs (0: round 4's first order)
+#endif
 static_assert(kChainSkew >= kChainBlock + 2 && kChainSkew + kChainBlock <= kChainRing, "ring too short for the skew");
 static_assert(kChainSkew % kChainBlock == 0 && kChainRing % kChainBlock == 0, "blocks align with the ring");
 
@@ -339,8 +354,11 @@ __device__ __forceinline__ constexpr int slot_pos(int r) {  // component r's dou
   return r == 0 ? K - 1 : r - 1;
 }
 
-template <int S, int C, bool PAIR, bool PAD>
-__global__ __launch_bounds__(64 * kWaveMaxWaves) void chain_kernel(SegArgs a, int nsteps, int Lw) {
+// WIDE: more than 4 waves (two share a SIMD: 256 registers per lane); up to 4 waves a lane
+// has the SIMD's 512 (VGPRs + AGPRs), which the reflective pair at 8 cells per lane needs
+// (256 VGPRs + 376 B of scratch under the 8-wave bound).
+template <int S, int C, bool PAIR, bool PAD, bool WIDE>
+__global__ __launch_bounds__(64 * (WIDE ? kWaveMaxWaves : 4)) void chain_kernel(SegArgs a, int nsteps, int Lw) {
   constexpr int K = SchemeDim<S>::K, WN = map_count<S>();
   static_assert(K <= kChainSlot - 1, "a slot holds the carried state");
   RT_STAMP(0);
@@ -496,6 +514,33 @@ __global__ __launch_bounds__(64 * kWaveMaxWaves) void chain_kernel(SegArgs a, in
 #pragma unroll
         for (int r = 1; r < K - 1; ++r) Xin[r] = lane_shift_up(nx[r], X[r]);
         Xin[0] = x0;
+#if RT_CHAIN_EARLY
+        // the ring traffic of this tick goes out before its FMAs: the stores of the exit
+        // states computed so far in the block (the previous tick's, or the previous two in
+        // one branch below 4 cells per lane), then the read of slot t + 1.  The next tick's
+        // lgkmcnt wait then finds them complete; issued at the end of the tick (the
+        // compiler's placement otherwise) every tick began by waiting out their latency.
+        if constexpr (C >= 4) {
+          if (i > 0 && writer) write_slot(wb + i * kChainSlot, X, false);
+        } else if (i > 0 && !(i & 1)) {
+          if (writer) {
+            write_slot(wb + (i - 1) * kChainSlot, prev, false);
+            write_slot(wb + i * kChainSlot, X, false);
+          }
+        } else if (i & 1) {
+#pragma unroll
+          for (int r = 0; r < K; ++r) prev[r] = X[r];
+        }
+        read_slot(i + 1 < kChainBlock ? rb + (i + 1) * kChainSlot : rn, nx, false);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int r = 0; r < K; ++r) X[r] = Xin[r];
+        cells(true);
+        if (i == kChainBlock - 1 && writer) {  // the block's last exit state(s), before the barrier
+          if constexpr (C < 4) write_slot(wb + i * kChainSlot, prev, false);
+          write_slot(wn, X, false);
+        }
+#else
         // the next tick's ring values (slot t + 1), after this tick's shifts
         read_slot(i + 1 < kChainBlock ? rb + (i + 1) * kChainSlot : rn, nx, false);
 #pragma unroll
@@ -512,6 +557,7 @@ __global__ __launch_bounds__(64 * kWaveMaxWaves) void chain_kernel(SegArgs a, in
 #pragma unroll
           for (int r = 0; r < K; ++r) prev[r] = X[r];
         }
+#endif
       }
     } else {
       for (int i = 0; i < kChainBlock; ++i) {
@@ -532,7 +578,9 @@ __global__ __launch_bounds__(64 * kWaveMaxWaves) void chain_kernel(SegArgs a, in
         if (writer) write_slot(wr_region + ((t + 1) & RM) * kChainSlot, X, true);
       }
     }
+    RT_BLOCK_STAMP(b, 0);
     __syncthreads();
+    RT_BLOCK_STAMP(b, 1);
   }
   RT_STAMP(2);
 #pragma unroll
@@ -566,17 +614,22 @@ static hipError_t launch_wave_s(const WavePlan &p, const SegArgs &a, int nsteps,
 #else
     const size_t lds = sizeof(double) * kChainSlot * kChainRing * static_cast<size_t>(p.waves);
     switch (p.C) {
+#define RT_CHAIN_LAUNCH(c, pd, wide)                                                                             \
+  hipLaunchKernelGGL((chain_kernel<S, c, PAIR, pd, wide>), dim3(grid), dim3(64 * p.waves), lds, st, a, nsteps, Lw)
 #define RT_CHAIN_CASE(c)                                                                                         \
   case c:                                                                                                        \
-    if (pad)                                                                                                     \
-      hipLaunchKernelGGL((chain_kernel<S, c, PAIR, PAIR && (c > 1)>), dim3(grid), dim3(64 * p.waves), lds, st, a, \
-                         nsteps, Lw);                                                                            \
+    if (pad && p.waves > 4)                                                                                      \
+      RT_CHAIN_LAUNCH(c, PAIR && (c > 1), true);                                                                 \
+    else if (pad)                                                                                                \
+      RT_CHAIN_LAUNCH(c, PAIR && (c > 1), false);                                                                \
+    else if (p.waves > 4)                                                                                        \
+      RT_CHAIN_LAUNCH(c, false, true);                                                                           \
     else                                                                                                         \
-      hipLaunchKernelGGL((chain_kernel<S, c, PAIR, false>), dim3(grid), dim3(64 * p.waves), lds, st, a, nsteps,   \
-                         Lw);                                                                                    \
+      RT_CHAIN_LAUNCH(c, false, false);                                                                          \
     break;
       RT_CHAIN_CASE(1) RT_CHAIN_CASE(2) RT_CHAIN_CASE(4) RT_CHAIN_CASE(8)
 #undef RT_CHAIN_CASE
+#undef RT_CHAIN_LAUNCH
       default: return hipErrorInvalidValue;
     }
 #endif
@@ -659,5 +712,13 @@ extern "C" int rt_debug_wave_stamps(unsigned long long *out, int waves) {
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(rtamd::g_wave_stamps), sizeof(unsigned long long) * 6 * waves) != hipSuccess)
     return -1;
   return waves;
+}
+// per-block stamps of chain_kernel's workgroup 0: [wave][block][before, after the barrier]
+extern "C" int rt_debug_block_stamps(unsigned long long *out) {
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(rtamd::g_block_stamps),
+                          sizeof(unsigned long long) * 2 * rtamd::kWaveMaxWaves * rtamd::kBlockStamps) != hipSuccess)
+    return -1;
+  return rtamd::kBlockStamps;
 }
 #endif

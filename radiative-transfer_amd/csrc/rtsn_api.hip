@@ -278,6 +278,10 @@ extern "C" rt_status rt_set_pipeline(rt_solver *s, int on) {
 extern "C" rt_status rt_set_wavefront(rt_solver *s, int mode) {
   if (!s) return fail(nullptr, RT_ERR_ARG, "rt_set_wavefront: NULL handle");
   if (mode < 0 || mode > 2) return fail(s, RT_ERR_ARG, "rt_set_wavefront: 0 (off), 1 (auto) or 2 (on)");
+  if (s->wqueued) {  // steps queued for the current chain plan run on it first
+    HIP_TRY(s, hipSetDevice(s->device));
+    if (rt_status st = wave_flush(s)) return st;
+  }
   s->wave = mode;
   return RT_OK;
 }
@@ -293,6 +297,10 @@ extern "C" rt_status rt_get_wavefront(rt_solver *s, int *mode, int *active, int 
 extern "C" rt_status rt_set_wavefront_waves(rt_solver *s, int max_waves) {
   if (!s) return fail(nullptr, RT_ERR_ARG, "rt_set_wavefront_waves: NULL handle");
   if (max_waves < 1 || max_waves > kWaveMaxWaves) return fail(s, RT_ERR_ARG, "rt_set_wavefront_waves: 1..8 waves");
+  if (s->wqueued) {  // steps queued for the current chain plan run on it first
+    HIP_TRY(s, hipSetDevice(s->device));
+    if (rt_status st = wave_flush(s)) return st;
+  }
   s->wave_max = max_waves;
   return RT_OK;
 }
@@ -307,7 +315,7 @@ extern "C" rt_status rt_get_wavefront_waves(rt_solver *s, int *max_waves, int *w
 extern "C" rt_status rt_pipeline_state(rt_solver *s, long long *lag_steps, int *queued_steps, int *pending) {
   if (!s) return fail(nullptr, RT_ERR_ARG, "rt_pipeline_state: NULL handle");
   if (lag_steps) *lag_steps = s->tau.front() - s->tau.back();
-  if (queued_steps) *queued_steps = s->queued;
+  if (queued_steps) *queued_steps = static_cast<int>(std::min<long long>(s->queued + s->wqueued, INT32_MAX));
   if (pending) *pending = s->pending ? 1 : 0;
   return RT_OK;
 }

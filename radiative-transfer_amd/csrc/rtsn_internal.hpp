@@ -232,6 +232,7 @@ struct rt_solver {
   long long target = 0;          // full steps every position must reach
   long long pipe_base = 0;       // tau of every position when the pipeline started
   int queued = 0;                // requested steps not yet enqueued (< T)
+  long long wqueued = 0;         // requested steps queued for the wavefront kernel (wave_advance)
   int Tpipe = 0;                 // time block of the running pipeline (0: positions aligned)
   // material-temperature coupling (rt_material_enable)
   bool material = false;
@@ -376,6 +377,7 @@ rt_status apply_correction(rt_solver *s);
 rt_status enqueue_pass(rt_solver *s, int T, bool coupled = false);
 rt_status complete(rt_solver *s);
 rt_status finalize(rt_solver *s);
+rt_status wave_flush(rt_solver *s);
 WavePlan wave_plan(const rt_solver *s);
 void end_plan(rt_solver *s);  // the planned schedule gives way to the handle's own
 bool use_wavefront(const rt_solver *s);

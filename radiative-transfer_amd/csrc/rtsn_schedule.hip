@@ -274,6 +274,7 @@ static rt_status pipe_advance(rt_solver *s, int nsteps) {
 // schedule ends with its run's pipeline.
 rt_status rtsn_detail::complete(rt_solver *s) {
   rt_status st;
+  if (s->wqueued && (st = wave_flush(s))) return st;
   if (s->Tpipe) {
     while (s->tau.back() < s->target)
       if ((st = pipe_launch(s))) return st;
@@ -321,13 +322,25 @@ bool rtsn_detail::use_wavefront(const rt_solver *s) {
 
 constexpr int kWaveMaxSteps = 1 << 16;  // steps per wavefront launch (bounds one launch's length)
 
-static rt_status wave_advance(rt_solver *s, int nsteps) {
-  if (rt_status st = finalize(s)) return st;  // the stored state exact at the requested time
+// A wavefront launch of m steps runs m + L - 1 ticks (L lanes in the chain), so an advance
+// of a few steps is mostly the chain's fill and drain: 7-step advances of a 4000-cell line
+// (500 lanes) would cost 506 ticks for 7 steps' work.  The steps are queued instead and
+// launched together once they hold 8 (L - 1) -- the fill and drain then at most 1/8 of the
+// launch -- or when anything needs the state (complete: every read-out, rt_finish, the
+// setters that align the schedule, a switch to the segment schedules).  The arithmetic per
+// (cell, level) does not depend on how the steps are cut into launches: bitwise the same.
+static long long wave_defer_steps(const rt_solver *s) {
+  const WavePlan p = wave_plan(s);
+  const long long used = s->p.bc_left_indicator == 2 ? 2LL * p.lanes : p.lanes;
+  return std::max<long long>(1, 8 * (used - 1));
+}
+
+rt_status rtsn_detail::wave_flush(rt_solver *s) {
   SegArgs a = seg_args(s);
   a.Gl = s->Gl;
   a.H = s->H;
-  while (nsteps > 0) {
-    const int m = std::min(nsteps, kWaveMaxSteps);
+  while (s->wqueued > 0) {
+    const int m = static_cast<int>(std::min<long long>(s->wqueued, kWaveMaxSteps));
     hipEvent_t e1;
     rt_status st = event_begin(s, &e1);
     if (st) return st;
@@ -336,9 +349,16 @@ static rt_status wave_advance(rt_solver *s, int nsteps) {
     ++s->state_version;
     for (long long &t : s->tau) t += m;
     s->target += m;
-    nsteps -= m;
+    s->wqueued -= m;
   }
   return RT_OK;
+}
+
+static rt_status wave_advance(rt_solver *s, int nsteps) {
+  if (!s->wqueued)
+    if (rt_status st = finalize(s)) return st;  // the stored state exact at the requested time
+  s->wqueued += nsteps;
+  return s->wqueued >= wave_defer_steps(s) ? wave_flush(s) : RT_OK;
 }
 
 extern "C" rt_status rt_advance(rt_solver *s, int nsteps) {
@@ -349,6 +369,7 @@ extern "C" rt_status rt_advance(rt_solver *s, int nsteps) {
   if (st) return st;
   if ((st = ensure_equilibrium(s))) return st;
   if (use_wavefront(s)) return wave_advance(s, nsteps);
+  if (s->wqueued && (st = wave_flush(s))) return st;  // the path changed: queued wavefront steps first
   return s->pipe ? pipe_advance(s, nsteps) : enqueue_steps(s, nsteps);
 }
 

@@ -9,6 +9,8 @@
 #                         TAG_trace_summary.json
 #   pmc[=ARGS]            the four PMC passes of the headline pass -> profiles/pmc_TAG_v0_t20.json
 #   py=SCRIPT[:ARGS]      python SCRIPT ARGS (':' separates arguments), stdout -> TAG_py_N.jsonl
+#   pyk=SCRIPT[:ARGS]     rocprofv3 kernel trace + stats of a python script -> TAG_pyk_N/
+#   pyp=CTRS@SCRIPT[:ARGS] one rocprofv3 PMC pass (CTRS comma-separated) of a python script -> TAG_pyp_N/
 #   env=NAME:VALUE        export NAME=VALUE for the steps after it
 set -o pipefail
 export TMPDIR=/tmp
@@ -78,6 +80,22 @@ s = d.get('schedule', {}); print('schedule', {k: s.get(k) for k in ('end_to_end_
       timeout -k 10 600 python -u $script $rest > gpurun_out/${TAG}_py_${n}.jsonl 2> $log \
         || { tail -30 $log; tail -5 gpurun_out/${TAG}_py_${n}.jsonl; exit 1; }
       tail -40 gpurun_out/${TAG}_py_${n}.jsonl
+      ;;
+    pyk|pyp)
+      # pyk=SCRIPT[:ARGS]: kernel trace + stats of a python script -> TAG_pyk_N/;
+      # pyp=CTR,CTR,...@SCRIPT[:ARGS]: one PMC pass (counters of one pass only) -> TAG_pyp_N/
+      prof="--kernel-trace --stats"
+      if [ "$name" = pyp ]; then
+        prof="--pmc $(echo "${arg%%@*}" | tr ',' ' ')"
+        arg=${arg#*@}
+      fi
+      script=${arg%%:*}
+      rest=""
+      [ "$script" != "$arg" ] && rest=$(echo "${arg#*:}" | tr ':' ' ')
+      timeout -k 10 -s KILL 400 rocprofv3 $prof -d gpurun_out/${TAG}_${name}_${n} -o run --output-format csv \
+        -- python3 $script $rest > $log 2>&1 || { tail -20 $log; exit 1; }
+      rm -f gpurun_out/${TAG}_${name}_${n}/run_kernel_trace.csv
+      ls gpurun_out/${TAG}_${name}_${n}
       ;;
     *)
       echo "unknown step $step"; exit 2

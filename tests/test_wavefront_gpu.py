@@ -161,3 +161,43 @@ def test_wavefront_long_advance_chunks(rtsn_mod, oracle_mod):
             res.append(s.ends())
     assert np.array_equal(res[0], res[1])
     assert np.array_equal(res[0], res[2])
+
+
+@pytest.mark.parametrize("N,bc_left", [(50, 0), (300, 2), (1000, 0)])
+def test_wavefront_deferred_small_advances(rtsn_mod, oracle_mod, N, bc_left):
+    """Advances shorter than 8 x the chain's fill stay queued (pipeline_state's queued steps)
+    and run as one launch when they reach it or at a read-out: 2-9-step advances with
+    read-outs in between, and a switch to the segment schedule with steps still queued,
+    equal one advance of all the steps bitwise (BDF2, 150 steps, random state)."""
+    lo, hi, steps = 40, 44, 150
+    p, q = _params(oracle_mod, N, 3, bc_left, 1, dt=1e-9)
+    B = oracle_mod.OracleSolver(p, g_lo=lo, g_hi=hi).groups()["B"][lo:hi]
+    ends0 = _random_ends(q, lo, hi, B, SEED + 17 * N)
+    with rtsn_mod.Solver(q, g_lo=lo, g_hi=hi) as s:
+        assert s.wavefront_state()["active"]
+        s.set_ends(ends0)
+        s.advance(steps)
+        ref = s.ends()
+    chunks = [2, 9, 5, 3, 8, 4, 7, 6] * 4
+    with rtsn_mod.Solver(q, g_lo=lo, g_hi=hi) as s:
+        s.set_ends(ends0)
+        done, mids = 0, 0
+        for i, n in enumerate(chunks):
+            n = min(n, steps - done)
+            if n <= 0:
+                break
+            s.advance(n)
+            done += n
+            if i == 0:
+                assert s.pipeline_state()["queued_steps"] == n  # deferred
+            if i in (5, 13):
+                s.ends()  # a read-out runs what is queued
+                assert s.pipeline_state()["queued_steps"] == 0
+                mids += 1
+            if i == 20:  # switch schedules with steps queued: they run first, on the wavefront
+                s.wavefront = 0
+                s.pipeline = 2
+                s.time_block = 1
+        if done < steps:
+            s.advance(steps - done)
+        assert np.array_equal(s.ends(), ref)
