@@ -32,6 +32,7 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <cstdlib>
 
 #include "cell.hpp"
 #include "kernels.hpp"
@@ -651,6 +652,101 @@ __global__ void __launch_bounds__(64) moments_kernel(const double2 *__restrict__
       phi[o] = sphi;
       F[o] = sF;
       phi_plus[o] = splus;
+    }
+  }
+}
+
+// The same sums (same order, same expressions: bitwise moments_kernel) with the state
+// streamed HBM -> LDS by LDS-DMA (global_load_lds_dwordx4), round 4.  moments_kernel reads
+// through VGPRs at ~5.3 TB/s on SL whatever its chunking (8, 16 or 32 directions per chunk:
+// profiles/r04b_moments_rate.jsonl); its PMC (r04c) shows the texture units busy the whole
+// kernel and the L1 stalled on pending misses -- the VGPR return path, not HBM, bounds it.
+// Here one wave per CU (persistent) owns a ring of R units in LDS; a unit is one half-row of
+// a task (cell c, 64 groups): 64 H double2 = H KiB, contiguous in HBM, copied by H
+// wave-instructions of 1 KiB.  The copy is swizzled on the source address (the DMA's LDS
+// destination is lane-linear): LDS element (g, s) holds direction (s - g) mod H of group
+// g, so lane g reading its directions in order hits 16 distinct bank quads per 16 lanes.
+// The unit u + R - 1 is issued before unit u is summed; the wait for unit u is a counted
+// vmcnt (R - 1 units, i.e. (R - 1) H wave-instructions, capped at the counter's 63: loads
+// complete in order, so 63 still guarantees unit u).
+template <int H, int R>
+__global__ void __launch_bounds__(64) moments_dma_kernel(const double2 *__restrict__ E, const double *__restrict__ mu,
+                                                         const double *__restrict__ wt, double *phi, double *F,
+                                                         double *phi_plus, LineMap m) {
+#pragma clang fp contract(off)
+  static_assert((H & (H - 1)) == 0 && H >= 4 && H <= 64, "H a power of two");
+  constexpr int kUnit = 64 * H;  // double2 per unit
+  constexpr int kWait = (R - 1) * H < 63 ? (R - 1) * H : 63;
+  constexpr int kWaitImm = (kWait & 15) | ((kWait >> 4) << 14) | (7 << 4) | (15 << 8);  // vmcnt only
+  __shared__ double2 ring[R * kUnit];
+  const int lane = threadIdx.x;
+  const int nchunks = m.Gl / 64;  // the launcher checks Gl % 64 == 0 and H
+  const long long tasks = static_cast<long long>(m.N) * nchunks;
+  if (static_cast<long long>(blockIdx.x) >= tasks) return;
+  const long long units = 2 * ((tasks - blockIdx.x + gridDim.x - 1) / gridDim.x);
+  // The copy is inline asm: a DMA the compiler sees (__builtin_amdgcn_global_load_lds) makes
+  // it wait vmcnt(0) before every LDS read, which would drain the ring.  M0 holds the
+  // wave-uniform LDS destination (saved and restored).
+  const auto dma = [](const double2 *src, unsigned lds) {
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(src), "s"(lds)
+                 : "memory");
+  };
+  typedef __attribute__((address_space(3))) double2 lds_d2;
+  const unsigned ring_lds = static_cast<unsigned>((size_t)((lds_d2 *)ring));  // the LDS byte address
+  const auto issue = [&](long long u) {
+    const long long task = blockIdx.x + (u >> 1) * gridDim.x;
+    const int c = static_cast<int>(task / nchunks), g0 = static_cast<int>(task % nchunks) * 64;
+    const int half = static_cast<int>(u & 1);
+    const double2 *row = E + m.at(half, half == 0 ? m.N - 1 - c : c, H * g0);
+    const unsigned slot = ring_lds + static_cast<unsigned>(u % R) * kUnit * 16;
+#pragma unroll
+    for (int k = 0; k < H; ++k) {
+      const int pos = k * 64 + lane, g = pos / H, d = (pos - g) & (H - 1);
+      dma(row + g * H + d, slot + k * 1024);
+    }
+  };
+  for (int u = 0; u < R - 1; ++u)
+    if (u < units) issue(u);
+  double sphi = 0.0, sF = 0.0, splus = 0.0;
+  for (long long u = 0; u < units; ++u) {
+    if (u + R - 1 < units) {
+      issue(u + R - 1);  // into the slot unit u - 1 was summed from (its reads are complete)
+      __builtin_amdgcn_s_waitcnt(kWaitImm);
+    } else {
+      __builtin_amdgcn_s_waitcnt((7 << 4) | (15 << 8));  // vmcnt(0): the last units
+    }
+    asm volatile("" ::: "memory");  // the LDS reads below stay after the wait
+    const double2 *t = ring + static_cast<int>(u % R) * kUnit + lane * H;
+    const int half = static_cast<int>(u & 1);
+    if (half == 0) {  // i = 0 .. H-1 is direction H-1-i of the half
+#pragma unroll 8
+      for (int i = 0; i < H; ++i) {
+        const double2 v = t[(H - 1 - i + lane) & (H - 1)];
+        const double q = 0.5 * (v.x + v.y);
+        const double w = wt[i], x = mu[i];
+        sphi += w * q;
+        sF += x * w * q;
+      }
+    } else {  // i = H + d
+#pragma unroll 8
+      for (int d = 0; d < H; ++d) {
+        const double2 v = t[(d + lane) & (H - 1)];
+        const double q = 0.5 * (v.x + v.y);
+        const double w = wt[H + d], x = mu[H + d];
+        sphi += w * q;
+        sF += x * w * q;
+        splus += w * q;
+      }
+      const long long task = blockIdx.x + (u >> 1) * gridDim.x;
+      const int c = static_cast<int>(task / nchunks), g0 = static_cast<int>(task % nchunks) * 64;
+      const size_t o = static_cast<size_t>(c) * m.Gl + g0 + lane;
+      phi[o] = sphi;
+      F[o] = sF;
+      phi_plus[o] = splus;
+      sphi = sF = splus = 0.0;
     }
   }
 }
@@ -1554,6 +1650,9 @@ hipError_t launch_import_ends(double2 *E, const double *ends, const Geometry &g,
 #ifndef RT_MOM_W
 #define RT_MOM_W 16
 #endif
+#ifndef RT_MOM_DMA
+#define RT_MOM_DMA 3  // units in moments_dma_kernel's LDS ring (0: moments_kernel only)
+#endif
 hipError_t launch_moments(const double2 *E, const double *mu, const double *wt, double *phi, double *F,
                           double *phi_plus, const Geometry &g, hipStream_t st) {
   const LineMap m = make_map(g);
@@ -1561,6 +1660,21 @@ hipError_t launch_moments(const double2 *E, const double *mu, const double *wt, 
   // as many waves as the chip holds at once; each walks its tasks with a one-chunk prefetch:
   // 16-direction chunks where the half's directions come in whole ones, else 8
   constexpr int W = RT_MOM_W;
+#if RT_MOM_DMA
+  // RTSN_MOMENTS_DMA=0: moments_kernel instead (read per call: the parity test compares both)
+  const char *dma_env = getenv("RTSN_MOMENTS_DMA");
+  if ((!dma_env || atoi(dma_env) != 0) && g.Gl % 64 == 0 && (m.H == 32 || m.H == 16)) {  // S64, S32
+    static const size_t res32 = resident_blocks(moments_dma_kernel<32, RT_MOM_DMA>, 64);
+    static const size_t res16 = resident_blocks(moments_dma_kernel<16, RT_MOM_DMA>, 64);
+    const size_t res = m.H == 32 ? res32 : res16;
+    const dim3 grid(static_cast<unsigned>(tasks < res ? tasks : res));
+    if (m.H == 32)
+      hipLaunchKernelGGL((moments_dma_kernel<32, RT_MOM_DMA>), grid, dim3(64), 0, st, E, mu, wt, phi, F, phi_plus, m);
+    else
+      hipLaunchKernelGGL((moments_dma_kernel<16, RT_MOM_DMA>), grid, dim3(64), 0, st, E, mu, wt, phi, F, phi_plus, m);
+    return hipGetLastError();
+  }
+#endif
   static const size_t resident[3] = {resident_blocks(moments_kernel<false, 8>, 64),
                                      resident_blocks(moments_kernel<true, 8>, 64),
                                      resident_blocks(moments_kernel<true, W>, 64)};

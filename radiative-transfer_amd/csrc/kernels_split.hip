@@ -1,6 +1,6 @@
 // kernels_split.hip -- the level-split pipelined pass (sweep_split_kernel): a BDF2
 // segment's T levels shared by 2 or 4 waves of a workgroup.  Its own translation unit
-// (the kernel is instantiated for 12 (T, waves) pairs) so it compiles beside kernels.hip.
+// (the kernel is instantiated for 14 (T, waves) pairs) so it compiles beside kernels.hip.
 #include <hip/hip_runtime.h>
 
 #include "cell.hpp"
@@ -306,9 +306,10 @@ static hipError_t occupancy_split_t(int *w) {
 }
 
 // (T, waves) pairs with a split kernel: 2 waves up to 20 levels (beyond, 12 or more
-// levels per wave spill), 4 waves for T divisible by 4 up to 40.
-#define RT_SPLIT_PAIRS(X) X(8, 2) X(10, 2) X(12, 2) X(16, 2) X(20, 2) \
-  X(8, 4) X(12, 4) X(16, 4) X(20, 4) X(24, 4) X(32, 4) X(40, 4)
+// levels per wave spill), 4 waves for T divisible by 4 up to 40.  T = 4 over 4 waves (one
+// level per wave): short planned runs, whose time is the line's traversal (rt_plan_schedule).
+#define RT_SPLIT_PAIRS(X) X(4, 2) X(8, 2) X(10, 2) X(12, 2) X(16, 2) X(20, 2) \
+  X(4, 4) X(8, 4) X(12, 4) X(16, 4) X(20, 4) X(24, 4) X(32, 4) X(40, 4)
 
 hipError_t launch_split(int T, int waves, const SegArgs &a, int grid, hipStream_t st) {
 #define RT_SPLIT_LAUNCH(t, k) \

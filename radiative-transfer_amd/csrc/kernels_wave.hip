@@ -346,6 +346,9 @@ constexpr int kChainSlot = 6;                  // doubles per slot (48 B: 16-byt
 #ifndef RT_CHAIN_EARLY
 #define RT_CHAIN_EARLY 1  // ring stores and reads issued before the tick's FMAs (0: round 4's first order)
 #endif
+#ifndef RT_CHAIN_FENCE
+#define RT_CHAIN_FENCE 1  // scheduling fences at each tick's start (4-8 cells per lane) and after its ring read
+#endif
 static_assert(kChainSkew >= kChainBlock + 2 && kChainSkew + kChainBlock <= kChainRing, "ring too short for the skew");
 static_assert(kChainSkew % kChainBlock == 0 && kChainRing % kChainBlock == 0, "blocks align with the ring");
 
@@ -508,7 +511,7 @@ __global__ __launch_bounds__(64 * (WIDE ? kWaveMaxWaves : 4)) void chain_kernel(
       for (int i = 0; i < kChainBlock; ++i) {
         // ticks are not interleaved: at 8 cells per lane an 8-tick block would not fit
         // the registers
-        if (C >= 4) __builtin_amdgcn_sched_barrier(0);
+        if (RT_CHAIN_FENCE && C >= 4) __builtin_amdgcn_sched_barrier(0);
         const double x0 = Xin[K - 1];
         Xin[K - 1] = lane_shift_up(nx[K - 1], X[K - 1]);
 #pragma unroll
@@ -532,7 +535,7 @@ __global__ __launch_bounds__(64 * (WIDE ? kWaveMaxWaves : 4)) void chain_kernel(
           for (int r = 0; r < K; ++r) prev[r] = X[r];
         }
         read_slot(i + 1 < kChainBlock ? rb + (i + 1) * kChainSlot : rn, nx, false);
-        __builtin_amdgcn_sched_barrier(0);
+        if (RT_CHAIN_FENCE) __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int r = 0; r < K; ++r) X[r] = Xin[r];
         cells(true);

@@ -411,6 +411,30 @@ def test_moments_device(rtsn_mod, oracle_mod):
             np.testing.assert_array_equal(t[k].cpu().numpy().reshape(s.N, s.G).T, host[k])
 
 
+@pytest.mark.parametrize("M,G,bc_left", [(64, 64, 0), (64, 128, 2), (32, 128, 0), (32, 64, 2), (64, 70, 0)])
+def test_moments_dma_bitwise(rtsn_mod, oracle_mod, monkeypatch, M, G, bc_left):
+    """moments_dma_kernel (S64 / S32 with whole 64-group chunks: the LDS-DMA ring) gives
+    bitwise moments_kernel's phi, F, phi_plus (RTSN_MOMENTS_DMA=0) -- the same sums in the
+    reference's order -- and both match the oracle; G = 70 (a partial chunk) takes
+    moments_kernel either way."""
+    p = load(oracle_mod, "llnl_slab_test.prm", N=1537, M=M, G=G, group_bounds=None, group_kappa=None, dt=1e-9,
+             max_timesteps=5, bc_left=bc_left, bc_right=1)
+    p["dx"] = p["X"] / p["N"]
+    p["psi_source"] = np.linspace(0.5, 2.0, M * G).reshape(M, G)
+    orc = oracle_mod.OracleSolver(p)
+    orc.solve()
+    out = {}
+    for env in ("0", "1"):
+        monkeypatch.setenv("RTSN_MOMENTS_DMA", env)
+        with rtsn_mod.Solver(to_rt(p)) as gpu:
+            gpu.solve()
+            out[env] = gpu.moments()
+            if env == "1":
+                compare_all(gpu, orc)
+    for k in range(3):
+        assert np.array_equal(out["0"][k], out["1"][k]), k
+
+
 @pytest.fixture(scope="module")
 def sl_line_oracle(oracle_mod):
     """One group of the SL slab at its full line length, N = 1e6,
@@ -543,7 +567,7 @@ def test_level_waves_auto(rtsn_mod):
         assert s.level_waves == 1
 
 
-@pytest.mark.parametrize("tb", [8, 12, 16, 20])
+@pytest.mark.parametrize("tb", [4, 8, 12, 16, 20])
 @pytest.mark.parametrize("bc_left", [0, 2])
 def test_level_split_pass(rtsn_mod, oracle_mod, monkeypatch, tb, bc_left):
     """The level-split pipelined pass (sweep_split_kernel: the T levels of a BDF2 pass
