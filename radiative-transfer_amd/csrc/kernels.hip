@@ -656,97 +656,107 @@ __global__ void __launch_bounds__(64) moments_kernel(const double2 *__restrict__
   }
 }
 
-// The same sums (same order, same expressions: bitwise moments_kernel) with the state
-// streamed HBM -> LDS by LDS-DMA (global_load_lds_dwordx4), round 4.  moments_kernel reads
-// through VGPRs at ~5.3 TB/s on SL whatever its chunking (8, 16 or 32 directions per chunk:
-// profiles/r04b_moments_rate.jsonl); its PMC (r04c) shows the texture units busy the whole
-// kernel and the L1 stalled on pending misses -- the VGPR return path, not HBM, bounds it.
-// Here one wave per CU (persistent) owns a ring of R units in LDS; a unit is one half-row of
-// a task (cell c, 64 groups): 64 H double2 = H KiB, contiguous in HBM, copied by H
-// wave-instructions of 1 KiB.  The copy is swizzled on the source address (the DMA's LDS
-// destination is lane-linear): LDS element (g, s) holds direction (s - g) mod H of group
-// g, so lane g reading its directions in order hits 16 distinct bank quads per 16 lanes.
-// The unit u + R - 1 is issued before unit u is summed; the wait for unit u is a counted
-// vmcnt (R - 1 units, i.e. (R - 1) H wave-instructions, capped at the counter's 63: loads
-// complete in order, so 63 still guarantees unit u).
-template <int H, int R>
-__global__ void __launch_bounds__(64) moments_dma_kernel(const double2 *__restrict__ E, const double *__restrict__ mu,
-                                                         const double *__restrict__ wt, double *phi, double *F,
-                                                         double *phi_plus, LineMap m) {
+// The same sums (same order, same expressions: bitwise moments_kernel's FAST path) as two
+// passes, one per half of the directions, each reading its half of the state in address
+// order -- round 4.  moments_kernel reads the SL state at 5.3-5.7 TB/s whatever its chunk
+// width (8, 16, 32 directions) or the chunks it keeps in flight (1-4 per wave), while a plain
+// scan of the same 131 GB in address order (finite_scan_kernel) reads at 6.9 TB/s
+// (profiles/r04h_*): a task of moments_kernel reads row N-1-c of half 0 and row c of half 1,
+// two streams 65 GB apart.  Here pass 0 walks half 0's rows in order (cell N-1-k at row k),
+// summing i = 0 .. H-1 and storing the partial phi and F in the outputs; pass 1 walks half
+// 1's rows (cell k), reloads them, continues the same sums over i = H .. M-1 and stores phi,
+// F and phi_plus: the partials go through memory as doubles, so the sums are bitwise those
+// of one pass (4 GB more traffic on SL, 3%).  D chunks per wave in flight (a register ring,
+// the loop unrolled D chunks at a time so its registers are compile-time).
+template <int W, int D, int HALF>
+__global__ void __launch_bounds__(64) moments_half_kernel(const double2 *__restrict__ E, const double *__restrict__ mu,
+                                                          const double *__restrict__ wt, double *phi, double *F,
+                                                          double *phi_plus, LineMap m) {
 #pragma clang fp contract(off)
-  static_assert((H & (H - 1)) == 0 && H >= 4 && H <= 64, "H a power of two");
-  constexpr int kUnit = 64 * H;  // double2 per unit
-  constexpr int kWait = (R - 1) * H < 63 ? (R - 1) * H : 63;
-  constexpr int kWaitImm = (kWait & 15) | ((kWait >> 4) << 14) | (7 << 4) | (15 << 8);  // vmcnt only
-  __shared__ double2 ring[R * kUnit];
+  __shared__ double tile[64 * (W + 1)];
   const int lane = threadIdx.x;
-  const int nchunks = m.Gl / 64;  // the launcher checks Gl % 64 == 0 and H
-  const long long tasks = static_cast<long long>(m.N) * nchunks;
+  const int H = m.H;
+  const int nchunks = (m.Gl + 63) / 64;
+  const int nj = H / W;  // chunks per task (the launcher checks H % W == 0)
+  const long long tasks = static_cast<long long>(m.N) * nchunks;  // (row, 64 groups), rows in order
   if (static_cast<long long>(blockIdx.x) >= tasks) return;
-  const long long units = 2 * ((tasks - blockIdx.x + gridDim.x - 1) / gridDim.x);
-  // The copy is inline asm: a DMA the compiler sees (__builtin_amdgcn_global_load_lds) makes
-  // it wait vmcnt(0) before every LDS read, which would drain the ring.  M0 holds the
-  // wave-uniform LDS destination (saved and restored).
-  const auto dma = [](const double2 *src, unsigned lds) {
-    unsigned keep;
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
-                 : "=&s"(keep)
-                 : "v"(src), "s"(lds)
-                 : "memory");
-  };
-  typedef __attribute__((address_space(3))) double2 lds_d2;
-  const unsigned ring_lds = static_cast<unsigned>((size_t)((lds_d2 *)ring));  // the LDS byte address
-  const auto issue = [&](long long u) {
-    const long long task = blockIdx.x + (u >> 1) * gridDim.x;
-    const int c = static_cast<int>(task / nchunks), g0 = static_cast<int>(task % nchunks) * 64;
-    const int half = static_cast<int>(u & 1);
-    const double2 *row = E + m.at(half, half == 0 ? m.N - 1 - c : c, H * g0);
-    const unsigned slot = ring_lds + static_cast<unsigned>(u % R) * kUnit * 16;
+  const long long nq = (tasks - blockIdx.x + gridDim.x - 1) / gridDim.x * nj;  // this wave's chunks
+  const int gr = lane / W, col = lane % W;
+  double2 v[D][W];
+  const auto load = [&](double2 (&b)[W], long long q) {
+    if (q >= nq) return;
+    const long long task = blockIdx.x + q / nj * gridDim.x;
+    const int step = static_cast<int>(q % nj);
+    const int k = static_cast<int>(task / nchunks), g0 = static_cast<int>(task % nchunks) * 64;
+    const int ng = min(64, m.Gl - g0);
+    const int i0 = (HALF == 0 ? nj - 1 - step : step) * W;  // half 0: i' descending
+    const double2 *row = E + m.at(HALF, k, H * g0 + i0);
+    const __amdgpu_buffer_rsrc_t R =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<double2 *>(row), 0, ng * H * 16, 0x00020000);
+    const int voff = (H * gr + col) * 16;
 #pragma unroll
-    for (int k = 0; k < H; ++k) {
-      const int pos = k * 64 + lane, g = pos / H, d = (pos - g) & (H - 1);
-      dma(row + g * H + d, slot + k * 1024);
-    }
+    for (int r = 0; r < W; ++r) b[r] = row_load(R, voff, r * (64 / W) * H * 16);
   };
-  for (int u = 0; u < R - 1; ++u)
-    if (u < units) issue(u);
+#pragma unroll
+  for (int d = 0; d < D; ++d) load(v[d], d);
   double sphi = 0.0, sF = 0.0, splus = 0.0;
-  for (long long u = 0; u < units; ++u) {
-    if (u + R - 1 < units) {
-      issue(u + R - 1);  // into the slot unit u - 1 was summed from (its reads are complete)
-      __builtin_amdgcn_s_waitcnt(kWaitImm);
-    } else {
-      __builtin_amdgcn_s_waitcnt((7 << 4) | (15 << 8));  // vmcnt(0): the last units
-    }
-    asm volatile("" ::: "memory");  // the LDS reads below stay after the wait
-    const double2 *t = ring + static_cast<int>(u % R) * kUnit + lane * H;
-    const int half = static_cast<int>(u & 1);
-    if (half == 0) {  // i = 0 .. H-1 is direction H-1-i of the half
-#pragma unroll 8
-      for (int i = 0; i < H; ++i) {
-        const double2 v = t[(H - 1 - i + lane) & (H - 1)];
-        const double q = 0.5 * (v.x + v.y);
-        const double w = wt[i], x = mu[i];
-        sphi += w * q;
-        sF += x * w * q;
-      }
-    } else {  // i = H + d
-#pragma unroll 8
-      for (int d = 0; d < H; ++d) {
-        const double2 v = t[(d + lane) & (H - 1)];
-        const double q = 0.5 * (v.x + v.y);
-        const double w = wt[H + d], x = mu[H + d];
-        sphi += w * q;
-        sF += x * w * q;
-        splus += w * q;
-      }
-      const long long task = blockIdx.x + (u >> 1) * gridDim.x;
-      const int c = static_cast<int>(task / nchunks), g0 = static_cast<int>(task % nchunks) * 64;
+  for (long long q0 = 0; q0 < nq; q0 += D) {
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      const long long q = q0 + d;
+      if (q >= nq) break;
+      const long long task = blockIdx.x + q / nj * gridDim.x;
+      const int step = static_cast<int>(q % nj);
+      const int k = static_cast<int>(task / nchunks), g0 = static_cast<int>(task % nchunks) * 64;
+      const int c = HALF == 0 ? m.N - 1 - k : k;
+      const int ng = min(64, m.Gl - g0);
       const size_t o = static_cast<size_t>(c) * m.Gl + g0 + lane;
-      phi[o] = sphi;
-      F[o] = sF;
-      phi_plus[o] = splus;
-      sphi = sF = splus = 0.0;
+      if (HALF == 1 && step == 0 && lane < ng) {  // half 0's partial sums
+        sphi = phi[o];
+        sF = F[o];
+      }
+      const int i0 = (HALF == 0 ? nj - 1 - step : step) * W;
+#pragma unroll
+      for (int r = 0; r < W; ++r)
+        if (gr + (64 / W) * r < ng) tile[(gr + (64 / W) * r) * (W + 1) + col] = 0.5 * (v[d][r].x + v[d][r].y);
+      __syncthreads();
+      load(v[d], q + D);
+      const int ib = HALF == 0 ? H - i0 - W : H + i0;  // lowest i of the chunk
+      double wv[W], xv[W];
+#pragma unroll
+      for (int kk = 0; kk < W; ++kk) {
+        wv[kk] = wt[ib + kk];
+        xv[kk] = mu[ib + kk];
+      }
+      if (lane < ng) {
+        const double *t = tile + lane * (W + 1);
+        if (HALF == 0) {  // i = H-1-(i0+ii) = ib + (W-1-ii)
+#pragma unroll
+          for (int ii = W - 1; ii >= 0; --ii) {
+            const int kk = W - 1 - ii;
+            const double qv = t[ii];
+            sphi += wv[kk] * qv;
+            sF += xv[kk] * wv[kk] * qv;
+          }
+        } else {  // i = H + i0 + ii = ib + ii
+#pragma unroll
+          for (int ii = 0; ii < W; ++ii) {
+            const double qv = t[ii];
+            sphi += wv[ii] * qv;
+            sF += xv[ii] * wv[ii] * qv;
+            splus += wv[ii] * qv;
+          }
+        }
+      }
+      __syncthreads();
+      if (step == nj - 1) {
+        if (lane < ng) {
+          phi[o] = sphi;
+          F[o] = sF;
+          if (HALF == 1) phi_plus[o] = splus;
+        }
+        sphi = sF = splus = 0.0;
+      }
     }
   }
 }
@@ -1650,8 +1660,8 @@ hipError_t launch_import_ends(double2 *E, const double *ends, const Geometry &g,
 #ifndef RT_MOM_W
 #define RT_MOM_W 16
 #endif
-#ifndef RT_MOM_DMA
-#define RT_MOM_DMA 3  // units in moments_dma_kernel's LDS ring (0: moments_kernel only)
+#ifndef RT_MOM_D
+#define RT_MOM_D 2  // chunks in flight per wave in moments_half_kernel (0: moments_kernel only)
 #endif
 hipError_t launch_moments(const double2 *E, const double *mu, const double *wt, double *phi, double *F,
                           double *phi_plus, const Geometry &g, hipStream_t st) {
@@ -1660,18 +1670,16 @@ hipError_t launch_moments(const double2 *E, const double *mu, const double *wt, 
   // as many waves as the chip holds at once; each walks its tasks with a one-chunk prefetch:
   // 16-direction chunks where the half's directions come in whole ones, else 8
   constexpr int W = RT_MOM_W;
-#if RT_MOM_DMA
-  // RTSN_MOMENTS_DMA=0: moments_kernel instead (read per call: the parity test compares both)
-  const char *dma_env = getenv("RTSN_MOMENTS_DMA");
-  if ((!dma_env || atoi(dma_env) != 0) && g.Gl % 64 == 0 && (m.H == 32 || m.H == 16)) {  // S64, S32
-    static const size_t res32 = resident_blocks(moments_dma_kernel<32, RT_MOM_DMA>, 64);
-    static const size_t res16 = resident_blocks(moments_dma_kernel<16, RT_MOM_DMA>, 64);
-    const size_t res = m.H == 32 ? res32 : res16;
-    const dim3 grid(static_cast<unsigned>(tasks < res ? tasks : res));
-    if (m.H == 32)
-      hipLaunchKernelGGL((moments_dma_kernel<32, RT_MOM_DMA>), grid, dim3(64), 0, st, E, mu, wt, phi, F, phi_plus, m);
-    else
-      hipLaunchKernelGGL((moments_dma_kernel<16, RT_MOM_DMA>), grid, dim3(64), 0, st, E, mu, wt, phi, F, phi_plus, m);
+#if RT_MOM_D
+  // RTSN_MOMENTS_RING=0: moments_kernel instead (read per call: the parity test compares both)
+  const char *ring_env = getenv("RTSN_MOMENTS_RING");
+  if ((!ring_env || atoi(ring_env) != 0) && m.H % W == 0) {
+    static const size_t res0 = resident_blocks(moments_half_kernel<W, RT_MOM_D, 0>, 64);
+    static const size_t res1 = resident_blocks(moments_half_kernel<W, RT_MOM_D, 1>, 64);
+    hipLaunchKernelGGL((moments_half_kernel<W, RT_MOM_D, 0>), dim3(static_cast<unsigned>(tasks < res0 ? tasks : res0)),
+                       dim3(64), 0, st, E, mu, wt, phi, F, phi_plus, m);
+    hipLaunchKernelGGL((moments_half_kernel<W, RT_MOM_D, 1>), dim3(static_cast<unsigned>(tasks < res1 ? tasks : res1)),
+                       dim3(64), 0, st, E, mu, wt, phi, F, phi_plus, m);
     return hipGetLastError();
   }
 #endif

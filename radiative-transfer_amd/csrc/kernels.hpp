@@ -31,7 +31,7 @@ constexpr int chunk_cells(int S, int T) {
 // pipelined passes whose T levels two waves can share (sweep_split_kernel):
 // BDF2, where the carried states (5 per level) are what overflows 256 registers
 constexpr bool level_split_supported(int S, int T) {
-  return S == 3 && (T == 8 || T == 10 || T == 12 || T == 16 || T == 20 || T == 24 || T == 32 || T == 40);
+  return S == 3 && (T == 4 || T == 8 || T == 10 || T == 12 || T == 16 || T == 20 || T == 24 || T == 32 || T == 40);
 }
 // pipelined passes with a one-wave kernel: all but BDF2 beyond 20 levels (its carried
 // states would spill; those run split over four waves)

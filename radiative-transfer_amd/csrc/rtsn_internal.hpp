@@ -272,9 +272,7 @@ namespace rtsn_detail {
 rt_status fail(rt_solver *s, rt_status st, const std::string &msg);
 void set_last_error(const char *msg);  // the thread's error text alone (host-only units)
 
-inline bool split_block(int T) {
-  return T == 4 || T == 8 || T == 10 || T == 12 || T == 16 || T == 20 || T == 24 || T == 32 || T == 40;
-}
+inline bool split_block(int T) { return level_split_supported(SCHEME_BDF2, T); }
 
 // Waves per segment of the pipelined pass: the caller's choice, or by default two waves
 // (sweep_split_kernel) where measured faster -- BDF2 at T = 20, whose one-wave kernel

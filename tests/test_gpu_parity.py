@@ -411,12 +411,14 @@ def test_moments_device(rtsn_mod, oracle_mod):
             np.testing.assert_array_equal(t[k].cpu().numpy().reshape(s.N, s.G).T, host[k])
 
 
-@pytest.mark.parametrize("M,G,bc_left", [(64, 64, 0), (64, 128, 2), (32, 128, 0), (32, 64, 2), (64, 70, 0)])
-def test_moments_dma_bitwise(rtsn_mod, oracle_mod, monkeypatch, M, G, bc_left):
-    """moments_dma_kernel (S64 / S32 with whole 64-group chunks: the LDS-DMA ring) gives
-    bitwise moments_kernel's phi, F, phi_plus (RTSN_MOMENTS_DMA=0) -- the same sums in the
-    reference's order -- and both match the oracle; G = 70 (a partial chunk) takes
-    moments_kernel either way."""
+@pytest.mark.parametrize("M,G,bc_left", [(64, 64, 0), (64, 128, 2), (32, 128, 0), (32, 70, 2), (64, 70, 0),
+                                         (16, 64, 0)])
+def test_moments_two_pass_bitwise(rtsn_mod, oracle_mod, monkeypatch, M, G, bc_left):
+    """moments_half_kernel (two passes in row order, half 0's partial sums through the
+    outputs; the default where the half's directions come in whole chunks) gives bitwise
+    moments_kernel's phi, F, phi_plus (RTSN_MOMENTS_RING=0) -- the same sums in the
+    reference's order -- and both match the oracle; G = 70 leaves a partial 64-group chunk,
+    S16 (8 directions per half) takes moments_kernel's 8-wide path either way."""
     p = load(oracle_mod, "llnl_slab_test.prm", N=1537, M=M, G=G, group_bounds=None, group_kappa=None, dt=1e-9,
              max_timesteps=5, bc_left=bc_left, bc_right=1)
     p["dx"] = p["X"] / p["N"]
@@ -425,7 +427,7 @@ def test_moments_dma_bitwise(rtsn_mod, oracle_mod, monkeypatch, M, G, bc_left):
     orc.solve()
     out = {}
     for env in ("0", "1"):
-        monkeypatch.setenv("RTSN_MOMENTS_DMA", env)
+        monkeypatch.setenv("RTSN_MOMENTS_RING", env)
         with rtsn_mod.Solver(to_rt(p)) as gpu:
             gpu.solve()
             out[env] = gpu.moments()

@@ -33,8 +33,17 @@ with rtsn.Solver(p) as s:
         s.moments_device(phi, F, pp)
         s.synchronize()
         out.append(1e3 * (time.perf_counter() - t0))
+    # the same bytes read by the finite scan (a plain streaming read of the state, no sums)
+    scan = []
+    for rep in range(6):
+        s.synchronize()
+        t0 = time.perf_counter()
+        s.state_finite()
+        scan.append(1e3 * (time.perf_counter() - t0))
 state_bytes = 2 * 16.0 * p["M"] / 2 * G * p["N"]  # both halves' (e_in, e_out) rows
 best = min(out[1:])
 print(json.dumps({"what": "moments_kernel on SL (rt_get_moments_device, host-timed)", "groups": G,
                   "lib": os.environ.get("RTSN_LIB", "default"), "ms": out, "best_ms": best,
-                  "state_gb": state_bytes / 1e9, "tb_per_s": state_bytes / (best * 1e-3) / 1e12}), flush=True)
+                  "state_gb": state_bytes / 1e9, "tb_per_s": state_bytes / (best * 1e-3) / 1e12,
+                  "finite_scan_best_ms": min(scan[1:]),
+                  "finite_scan_tb_per_s": state_bytes / (min(scan[1:]) * 1e-3) / 1e12}), flush=True)
