@@ -668,16 +668,20 @@ __global__ void __launch_bounds__(64) moments_kernel(const double2 *__restrict__
 // F and phi_plus: the partials go through memory as doubles, so the sums are bitwise those
 // of one pass (4 GB more traffic on SL, 3%).  D chunks per wave in flight (a register ring,
 // the loop unrolled D chunks at a time so its registers are compile-time).
+constexpr int kMomMaxM = 256;
 template <int W, int D, int HALF>
 __global__ void __launch_bounds__(64) moments_half_kernel(const double2 *__restrict__ E, const double *__restrict__ mu,
                                                           const double *__restrict__ wt, double *phi, double *F,
                                                           double *phi_plus, LineMap m) {
 #pragma clang fp contract(off)
   __shared__ double tile[64 * (W + 1)];
+  __shared__ double2 wxl[kMomMaxM];  // (weight, mu) per direction: read in order with the tile
   const int lane = threadIdx.x;
   const int H = m.H;
+  for (int i = lane; i < 2 * H; i += 64) wxl[i] = make_double2(wt[i], mu[i]);
+  __syncthreads();
   const int nchunks = (m.Gl + 63) / 64;
-  const int nj = H / W;  // chunks per task (the launcher checks H % W == 0)
+  const int nj = H / W;  // chunks per task (the launcher checks H % W == 0, M <= kMomMaxM)
   const long long tasks = static_cast<long long>(m.N) * nchunks;  // (row, 64 groups), rows in order
   if (static_cast<long long>(blockIdx.x) >= tasks) return;
   const long long nq = (tasks - blockIdx.x + gridDim.x - 1) / gridDim.x * nj;  // this wave's chunks
@@ -725,8 +729,9 @@ __global__ void __launch_bounds__(64) moments_half_kernel(const double2 *__restr
       double wv[W], xv[W];
 #pragma unroll
       for (int kk = 0; kk < W; ++kk) {
-        wv[kk] = wt[ib + kk];
-        xv[kk] = mu[ib + kk];
+        const double2 wx = wxl[ib + kk];  // broadcast LDS reads: no scalar loads (their wait is lgkmcnt(0))
+        wv[kk] = wx.x;
+        xv[kk] = wx.y;
       }
       if (lane < ng) {
         const double *t = tile + lane * (W + 1);
@@ -756,6 +761,75 @@ __global__ void __launch_bounds__(64) moments_half_kernel(const double2 *__restr
           if (HALF == 1) phi_plus[o] = splus;
         }
         sphi = sF = splus = 0.0;
+      }
+    }
+  }
+}
+
+// Moments by whole rows: a 256-thread workgroup reads one row of one half (every line of
+// the shard at one cell: H Gl double2, 64 KiB on SL) the way the finite scan does -- lane-
+// contiguous 16-byte loads, 4 KiB per workgroup instruction, all of a thread's loads issued
+// before the first is used -- then transposes psi = (e_in + e_out) / 2 through LDS and one
+// thread per group runs the sequential sums over the half's directions.  Two passes as
+// moments_half_kernel (half 0 by rows, the partial phi and F through the outputs; then half
+// 1): the same sums in the same order, bitwise moments_kernel.  Round 4: every
+// chunked form (moments_kernel, moments_half_kernel at 8-32 directions per chunk, 1-4 chunks
+// in flight, LDS-DMA rings) read the SL state at 5.2-5.7 TB/s against the scan's 6.9
+// (profiles/r04*_moments_rate.jsonl).
+constexpr int kRowThreads = 256;
+template <int HALF, int NL>
+__global__ void __launch_bounds__(kRowThreads) moments_row_kernel(const double2 *__restrict__ E,
+                                                                  const double *__restrict__ mu,
+                                                                  const double *__restrict__ wt, double *phi,
+                                                                  double *F, double *phi_plus, LineMap m) {
+#pragma clang fp contract(off)
+  extern __shared__ double2 row_lds[];  // wxl[2H], then the tile [Gl][H + 1] doubles
+  double2 *wxl = row_lds;
+  double *tile = reinterpret_cast<double *>(row_lds + 2 * m.H);
+  const int t = threadIdx.x, H = m.H, L = H * m.Gl, HP = H + 1;
+  for (int i = t; i < 2 * H; i += kRowThreads) wxl[i] = make_double2(wt[i], mu[i]);
+  typedef double d2v __attribute__((ext_vector_type(2)));
+  for (int k = blockIdx.x; k < m.N; k += gridDim.x) {
+    const d2v *row = reinterpret_cast<const d2v *>(E) + m.at(HALF, k, 0);
+    d2v v[NL];
+#pragma unroll
+    for (int j = 0; j < NL; ++j) {
+      const int e = t + j * kRowThreads;
+      if (e < L) v[j] = __builtin_nontemporal_load(row + e);
+    }
+    __syncthreads();  // the previous row's sums are done with the tile
+#pragma unroll
+    for (int j = 0; j < NL; ++j) {
+      const int e = t + j * kRowThreads;
+      if (e < L) tile[(e / H) * HP + e % H] = 0.5 * (v[j].x + v[j].y);
+    }
+    __syncthreads();
+    const int c = HALF == 0 ? m.N - 1 - k : k;
+    for (int g = t; g < m.Gl; g += kRowThreads) {
+      const double *q = tile + g * HP;
+      const size_t o = static_cast<size_t>(c) * m.Gl + g;
+      if (HALF == 0) {  // i = 0 .. H-1 is direction H-1-i
+        double sphi = 0.0, sF = 0.0;
+        for (int i = 0; i < H; ++i) {
+          const double2 wx = wxl[i];
+          const double qv = q[H - 1 - i];
+          sphi += wx.x * qv;
+          sF += wx.y * wx.x * qv;
+        }
+        phi[o] = sphi;
+        F[o] = sF;
+      } else {  // i = H + d
+        double sphi = phi[o], sF = F[o], splus = 0.0;
+        for (int d = 0; d < H; ++d) {
+          const double2 wx = wxl[H + d];
+          const double qv = q[d];
+          sphi += wx.x * qv;
+          sF += wx.y * wx.x * qv;
+          splus += wx.x * qv;
+        }
+        phi[o] = sphi;
+        F[o] = sF;
+        phi_plus[o] = splus;
       }
     }
   }
@@ -1671,9 +1745,33 @@ hipError_t launch_moments(const double2 *E, const double *mu, const double *wt, 
   // 16-direction chunks where the half's directions come in whole ones, else 8
   constexpr int W = RT_MOM_W;
 #if RT_MOM_D
-  // RTSN_MOMENTS_RING=0: moments_kernel instead (read per call: the parity test compares both)
+  // RTSN_MOMENTS_RING=0: moments_kernel; =2: moments_half_kernel (read per call: the parity
+  // test compares them)
   const char *ring_env = getenv("RTSN_MOMENTS_RING");
-  if ((!ring_env || atoi(ring_env) != 0) && m.H % W == 0) {
+  const int mode = ring_env ? atoi(ring_env) : 1;
+  const size_t row_lds = sizeof(double2) * 2 * m.H + sizeof(double) * static_cast<size_t>(g.Gl) * (m.H + 1);
+  const int nl = (m.H * g.Gl + kRowThreads - 1) / kRowThreads;
+  if (mode == 1 && row_lds <= 40 * 1024 && nl <= 16) {  // whole rows (SL: 4096 lines per row, 34 KB of LDS)
+    static int cus = 0;
+    if (!cus) {
+      int dev = 0;
+      if (hipGetDevice(&dev) != hipSuccess ||
+          hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        cus = 256;
+    }
+    const unsigned grid = static_cast<unsigned>(std::min<long long>(g.N, 4LL * cus));
+#define RT_ROW_LAUNCH(n)                                                                                       \
+  if (nl <= n) {                                                                                               \
+    hipLaunchKernelGGL((moments_row_kernel<0, n>), dim3(grid), dim3(kRowThreads), row_lds, st, E, mu, wt, phi, F, \
+                       phi_plus, m);                                                                           \
+    hipLaunchKernelGGL((moments_row_kernel<1, n>), dim3(grid), dim3(kRowThreads), row_lds, st, E, mu, wt, phi, F, \
+                       phi_plus, m);                                                                           \
+    return hipGetLastError();                                                                                  \
+  }
+    RT_ROW_LAUNCH(4) RT_ROW_LAUNCH(8) RT_ROW_LAUNCH(16)
+#undef RT_ROW_LAUNCH
+  }
+  if (mode != 0 && m.H % W == 0 && m.M <= kMomMaxM) {
     static const size_t res0 = resident_blocks(moments_half_kernel<W, RT_MOM_D, 0>, 64);
     static const size_t res1 = resident_blocks(moments_half_kernel<W, RT_MOM_D, 1>, 64);
     hipLaunchKernelGGL((moments_half_kernel<W, RT_MOM_D, 0>), dim3(static_cast<unsigned>(tasks < res0 ? tasks : res0)),

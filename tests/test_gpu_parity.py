@@ -414,11 +414,12 @@ def test_moments_device(rtsn_mod, oracle_mod):
 @pytest.mark.parametrize("M,G,bc_left", [(64, 64, 0), (64, 128, 2), (32, 128, 0), (32, 70, 2), (64, 70, 0),
                                          (16, 64, 0)])
 def test_moments_two_pass_bitwise(rtsn_mod, oracle_mod, monkeypatch, M, G, bc_left):
-    """moments_half_kernel (two passes in row order, half 0's partial sums through the
-    outputs; the default where the half's directions come in whole chunks) gives bitwise
+    """The two-pass moments (half 0's partial sums through the outputs): moments_row_kernel
+    (whole rows, the default) and moments_half_kernel (RTSN_MOMENTS_RING=2) give bitwise
     moments_kernel's phi, F, phi_plus (RTSN_MOMENTS_RING=0) -- the same sums in the
-    reference's order -- and both match the oracle; G = 70 leaves a partial 64-group chunk,
-    S16 (8 directions per half) takes moments_kernel's 8-wide path either way."""
+    reference's order -- and match the oracle; G = 70 leaves a partial 64-group chunk and
+    rows of 1120-2240 lines, S16 (8 directions per half) takes moments_kernel's 8-wide path
+    in mode 2."""
     p = load(oracle_mod, "llnl_slab_test.prm", N=1537, M=M, G=G, group_bounds=None, group_kappa=None, dt=1e-9,
              max_timesteps=5, bc_left=bc_left, bc_right=1)
     p["dx"] = p["X"] / p["N"]
@@ -426,7 +427,7 @@ def test_moments_two_pass_bitwise(rtsn_mod, oracle_mod, monkeypatch, M, G, bc_le
     orc = oracle_mod.OracleSolver(p)
     orc.solve()
     out = {}
-    for env in ("0", "1"):
+    for env in ("0", "1", "2"):
         monkeypatch.setenv("RTSN_MOMENTS_RING", env)
         with rtsn_mod.Solver(to_rt(p)) as gpu:
             gpu.solve()
@@ -435,6 +436,7 @@ def test_moments_two_pass_bitwise(rtsn_mod, oracle_mod, monkeypatch, M, G, bc_le
                 compare_all(gpu, orc)
     for k in range(3):
         assert np.array_equal(out["0"][k], out["1"][k]), k
+        assert np.array_equal(out["0"][k], out["2"][k]), k
 
 
 @pytest.fixture(scope="module")
