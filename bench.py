@@ -12,13 +12,13 @@ with kappa_g resampled from the LLNL capped table, rho = 1, T = 1 keV, BDF2
 v/c correction (variant corr).  dt = 1e-9 (--dt): at SURVEY's dt = 1e-3 the
 reference's BDF2 (const_B from the full dt, solver.cpp:501) overflows the state
 to inf within the pipeline fill, and inf arithmetic runs ~4% faster than the
-finite state (interleaved A/B, profiles/r03c_ab_finite.jsonl), so the headline
+finite state (interleaved A/B, profiles/archive/r03c_ab_finite.jsonl), so the headline
 is timed on a finite one and dt = 1e-3 is a side leg (overflow_control).  The
 state stays finite for 200-400 steps at dt = 1e-7, 1200-1400 at 1e-8 and more
-than 4000 at 1e-9 (profiles/r03j_finite_horizon.jsonl); the fill grows as the
+than 4000 at 1e-9 (profiles/archive/r03j_finite_horizon.jsonl); the fill grows as the
 groups per GPU shrink (160 steps at 128 groups, 1280 at the 16 of an 8-GPU
 run), so every N runs the same dt = 1e-9, whose timing equals dt = 1e-7's
-(profiles/r03k_window_ab.jsonl).  A "step" is one full BDF2
+(profiles/archive/r03k_window_ab.jsonl).  A "step" is one full BDF2
 step (4 substeps) of every cell x angle x group of the GPU's groups, i.e.
 4 M G N cell-angle-group updates, computed in fp64 by the fused HIP sweep.
 State is resident in HBM before timing.
@@ -76,7 +76,7 @@ HBM_PEAK = 8.0e12
 SUPPORTED_TIME_BLOCKS = (1, 2, 3, 4, 5, 6, 7, 8, 10, 12, 16, 20, 24, 32, 40)  # rt_set_time_block
 # the bench's choice for K timed steps: the first of these dividing K, fastest per step first
 # (SL pipelined, same box, ms/step: T = 40 7.49-7.53, 32 7.69-7.75, 16 8.13-8.19, 20 8.22,
-# 24 8.26-8.29, 12 ~9.0, 10 8.9-9.0, 8 9.5, 4 12.3, 2 21; profiles/r02g_big_time_blocks.jsonl,
+# 24 8.26-8.29, 12 ~9.0, 10 8.9-9.0, 8 9.5, 4 12.3, 2 21; profiles/archive/r02g_big_time_blocks.jsonl,
 # r02a_windows.jsonl)
 TIME_BLOCK_PREFERENCE = (40, 32, 16, 20, 24, 12, 10, 8, 7, 6, 5, 4, 3, 2, 1)
 DEFAULT_TIME_BLOCK = 40  # the default window: two passes of the fastest block
@@ -787,7 +787,7 @@ def main():
     # SURVEY §8(d)'s SL names dt = 1e-3, at which the reference's BDF2 (const_B from the full dt,
     # solver.cpp:501) overflows the slab's state to inf within the pipeline fill; the headline is
     # timed on a finite state, which runs ~4% slower than the overflowed one on the same box
-    # (profiles/r03c_ab_finite.jsonl); dt = 1e-3 is the side leg "overflow_control".  1e-9 keeps
+    # (profiles/archive/r03c_ab_finite.jsonl); dt = 1e-3 is the side leg "overflow_control".  1e-9 keeps
     # the state finite through the longest fill (1280 steps for the 16 groups of an 8-GPU run)
     ap.add_argument("--dt", type=float, default=1e-9,
                     help="time step of the SL slab (default 1e-9: finite state at every GPU count)")
@@ -873,7 +873,7 @@ def main():
                                                        "headline (inf arithmetic runs ~4% faster)", dirs)
         other = "corr" if args.variant == "v0" else "v0"
         # at most 1e-9: with the v/c correction on, the reference's BDF2 overflows the SL state
-        # within the fill already at dt = 1e-7 (profiles/r03o_bench.json)
+        # within the fill already at dt = 1e-7 (profiles/archive/r03o_bench.json)
         line[f"variant_{other}"] = side_leg(dict(slab_params(info[0], other, N=args.cells), variant=other,
                                                  dt=min(args.dt, 1e-9)), info,
                                             world, device, local, args.scaling, solver_tb,

@@ -273,7 +273,7 @@ rt_status rt_set_level_waves(rt_solver *s, int waves);
  * wgs_per_cu workgroups per CU (1..64), or 0 (default) for the pass kernel's occupancy.
  * More segments than resident workgroups shorten the pipeline's fill and drain (the line
  * traversal per launch) at a small cost per segment: a 1000-step run of a 16-group SL
- * shard 1270 -> 1017 ms at 16 per CU (profiles/r03g_grid16.jsonl).  Applied now if the
+ * shard 1270 -> 1017 ms at 16 per CU (profiles/archive/r03g_grid16.jsonl).  Applied now if the
  * positions are aligned, else before the next pass; results bitwise independent of it in
  * the pipelined schedule. */
 rt_status rt_set_segmentation(rt_solver *s, int wgs_per_cu);

@@ -51,7 +51,7 @@ namespace rtamd {
 // ds_read_b128 fetches its next two coefficients and no barrier is needed -- and the next
 // segment's aggregate is prefetched while the current step runs.  (The first version
 // re-read the propagator from memory at every segment: ~23 us per segment on few long
-// lines, 1.4-4.5 s for 1000 aligned steps of 4000-50000 cells, profiles/r03ao_solve_mid.jsonl.)
+// lines, 1.4-4.5 s for 1000 aligned steps of 4000-50000 cells, profiles/archive/r03ao_solve_mid.jsonl.)
 constexpr int kFoldChunk = 8;  // LDS pairs per read chunk of fold_kernel's walk
 
 // fold_kernel's memory traffic: a buffer descriptor over a wave-uniform base, the row as a
@@ -777,6 +777,7 @@ __global__ void __launch_bounds__(64) moments_half_kernel(const double2 *__restr
 // in flight, LDS-DMA rings) read the SL state at 5.2-5.7 TB/s against the scan's 6.9
 // (profiles/r04*_moments_rate.jsonl).
 constexpr int kRowThreads = 256;
+constexpr int kMomMaxGroups = 256;  // groups per shard the row kernel takes (the launcher checks)
 template <int HALF, int NL>
 __global__ void __launch_bounds__(kRowThreads) moments_row_kernel(const double2 *__restrict__ E,
                                                                   const double *__restrict__ mu,
@@ -797,6 +798,18 @@ __global__ void __launch_bounds__(kRowThreads) moments_row_kernel(const double2 
       const int e = t + j * kRowThreads;
       if (e < L) v[j] = __builtin_nontemporal_load(row + e);
     }
+    const int c = HALF == 0 ? m.N - 1 - k : k;
+    double p0[(kMomMaxGroups + kRowThreads - 1) / kRowThreads], p1[(kMomMaxGroups + kRowThreads - 1) / kRowThreads];
+    if (HALF == 1) {  // half 0's partial sums, loaded with the row (their latency behind the row's)
+#pragma unroll
+      for (int n = 0; n < (kMomMaxGroups + kRowThreads - 1) / kRowThreads; ++n) {
+        const int g = t + n * kRowThreads;
+        if (g < m.Gl) {
+          p0[n] = phi[static_cast<size_t>(c) * m.Gl + g];
+          p1[n] = F[static_cast<size_t>(c) * m.Gl + g];
+        }
+      }
+    }
     __syncthreads();  // the previous row's sums are done with the tile
 #pragma unroll
     for (int j = 0; j < NL; ++j) {
@@ -804,8 +817,10 @@ __global__ void __launch_bounds__(kRowThreads) moments_row_kernel(const double2 
       if (e < L) tile[(e / H) * HP + e % H] = 0.5 * (v[j].x + v[j].y);
     }
     __syncthreads();
-    const int c = HALF == 0 ? m.N - 1 - k : k;
-    for (int g = t; g < m.Gl; g += kRowThreads) {
+#pragma unroll
+    for (int n = 0; n < (kMomMaxGroups + kRowThreads - 1) / kRowThreads; ++n) {
+      const int g = t + n * kRowThreads;
+      if (g >= m.Gl) break;
       const double *q = tile + g * HP;
       const size_t o = static_cast<size_t>(c) * m.Gl + g;
       if (HALF == 0) {  // i = 0 .. H-1 is direction H-1-i
@@ -819,7 +834,7 @@ __global__ void __launch_bounds__(kRowThreads) moments_row_kernel(const double2 
         phi[o] = sphi;
         F[o] = sF;
       } else {  // i = H + d
-        double sphi = phi[o], sF = F[o], splus = 0.0;
+        double sphi = p0[n], sF = p1[n], splus = 0.0;
         for (int d = 0; d < H; ++d) {
           const double2 wx = wxl[H + d];
           const double qv = q[d];
@@ -829,6 +844,84 @@ __global__ void __launch_bounds__(kRowThreads) moments_row_kernel(const double2 
         }
         phi[o] = sphi;
         F[o] = sF;
+        phi_plus[o] = splus;
+      }
+    }
+  }
+}
+
+// One pass over both halves of a cell (round 4): a workgroup takes cell c -- row N-1-c of
+// half 0, then row c of half 1 -- loading the half-1 row while it sums half 0, so the
+// partial sums stay in registers (no second pass, no partials through memory).
+template <int NL>
+__global__ void __launch_bounds__(kRowThreads) moments_cell_kernel(const double2 *__restrict__ E,
+                                                                   const double *__restrict__ mu,
+                                                                   const double *__restrict__ wt, double *phi,
+                                                                   double *F, double *phi_plus, LineMap m) {
+#pragma clang fp contract(off)
+  extern __shared__ double2 row_lds[];  // wxl[2H], then the tile [Gl][H + 1] doubles
+  double2 *wxl = row_lds;
+  double *tile = reinterpret_cast<double *>(row_lds + 2 * m.H);
+  const int t = threadIdx.x, H = m.H, L = H * m.Gl, HP = H + 1;
+  for (int i = t; i < 2 * H; i += kRowThreads) wxl[i] = make_double2(wt[i], mu[i]);
+  typedef double d2v __attribute__((ext_vector_type(2)));
+  const auto load = [&](d2v (&v)[NL], int half, int k) {
+    const d2v *row = reinterpret_cast<const d2v *>(E) + m.at(half, k, 0);
+#pragma unroll
+    for (int j = 0; j < NL; ++j) {
+      const int e = t + j * kRowThreads;
+      if (e < L) v[j] = __builtin_nontemporal_load(row + e);
+    }
+  };
+  const auto stage = [&](const d2v (&v)[NL]) {
+#pragma unroll
+    for (int j = 0; j < NL; ++j) {
+      const int e = t + j * kRowThreads;
+      if (e < L) tile[(e / H) * HP + e % H] = 0.5 * (v[j].x + v[j].y);
+    }
+  };
+  constexpr int GN = (kMomMaxGroups + kRowThreads - 1) / kRowThreads;
+  for (int c = blockIdx.x; c < m.N; c += gridDim.x) {
+    d2v v0[NL], v1[NL];
+    load(v0, 0, m.N - 1 - c);
+    __syncthreads();  // the previous cell's sums are done with the tile
+    stage(v0);
+    load(v1, 1, c);  // in flight during half 0's sums
+    __syncthreads();
+    double sphi[GN], sF[GN];
+#pragma unroll
+    for (int n = 0; n < GN; ++n) {
+      const int g = t + n * kRowThreads;
+      sphi[n] = sF[n] = 0.0;
+      if (g < m.Gl) {
+        const double *q = tile + g * HP;
+        for (int i = 0; i < H; ++i) {  // i = 0 .. H-1 is direction H-1-i
+          const double2 wx = wxl[i];
+          const double qv = q[H - 1 - i];
+          sphi[n] += wx.x * qv;
+          sF[n] += wx.y * wx.x * qv;
+        }
+      }
+    }
+    __syncthreads();
+    stage(v1);
+    __syncthreads();
+#pragma unroll
+    for (int n = 0; n < GN; ++n) {
+      const int g = t + n * kRowThreads;
+      if (g < m.Gl) {
+        const double *q = tile + g * HP;
+        double splus = 0.0;
+        for (int d = 0; d < H; ++d) {  // i = H + d
+          const double2 wx = wxl[H + d];
+          const double qv = q[d];
+          sphi[n] += wx.x * qv;
+          sF[n] += wx.y * wx.x * qv;
+          splus += wx.x * qv;
+        }
+        const size_t o = static_cast<size_t>(c) * m.Gl + g;
+        phi[o] = sphi[n];
+        F[o] = sF[n];
         phi_plus[o] = splus;
       }
     }
@@ -1751,7 +1844,28 @@ hipError_t launch_moments(const double2 *E, const double *mu, const double *wt, 
   const int mode = ring_env ? atoi(ring_env) : 1;
   const size_t row_lds = sizeof(double2) * 2 * m.H + sizeof(double) * static_cast<size_t>(g.Gl) * (m.H + 1);
   const int nl = (m.H * g.Gl + kRowThreads - 1) / kRowThreads;
-  if (mode == 1 && row_lds <= 40 * 1024 && nl <= 16) {  // whole rows (SL: 4096 lines per row, 34 KB of LDS)
+#ifndef RT_MOM_ROWS_PER_CU
+#define RT_MOM_ROWS_PER_CU 64  // workgroups per CU in the grid (more than resident: measured faster than persistent)
+#endif
+  if (mode == 3 && row_lds <= 40 * 1024 && nl <= 16 && g.Gl <= kMomMaxGroups) {  // one pass, a cell per workgroup
+    static int cus3 = 0;
+    if (!cus3) {
+      int dev = 0;
+      if (hipGetDevice(&dev) != hipSuccess ||
+          hipDeviceGetAttribute(&cus3, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        cus3 = 256;
+    }
+    const unsigned grid3 = static_cast<unsigned>(std::min<long long>(g.N, 1LL * RT_MOM_ROWS_PER_CU * cus3));
+#define RT_CELL_LAUNCH(n)                                                                                     \
+  if (nl <= n) {                                                                                              \
+    hipLaunchKernelGGL((moments_cell_kernel<n>), dim3(grid3), dim3(kRowThreads), row_lds, st, E, mu, wt, phi, F,  \
+                       phi_plus, m);                                                                          \
+    return hipGetLastError();                                                                                 \
+  }
+    RT_CELL_LAUNCH(4) RT_CELL_LAUNCH(8) RT_CELL_LAUNCH(16)
+#undef RT_CELL_LAUNCH
+  }
+  if (mode == 1 && row_lds <= 40 * 1024 && nl <= 16 && g.Gl <= kMomMaxGroups) {  // whole rows (SL: 4096 lines per row, 34 KB of LDS)
     static int cus = 0;
     if (!cus) {
       int dev = 0;
@@ -1759,14 +1873,20 @@ hipError_t launch_moments(const double2 *E, const double *mu, const double *wt, 
           hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
         cus = 256;
     }
-    const unsigned grid = static_cast<unsigned>(std::min<long long>(g.N, 4LL * cus));
-#define RT_ROW_LAUNCH(n)                                                                                       \
-  if (nl <= n) {                                                                                               \
-    hipLaunchKernelGGL((moments_row_kernel<0, n>), dim3(grid), dim3(kRowThreads), row_lds, st, E, mu, wt, phi, F, \
-                       phi_plus, m);                                                                           \
-    hipLaunchKernelGGL((moments_row_kernel<1, n>), dim3(grid), dim3(kRowThreads), row_lds, st, E, mu, wt, phi, F, \
-                       phi_plus, m);                                                                           \
-    return hipGetLastError();                                                                                  \
+    // persistent: as many workgroups as the CUs hold at once with this row's LDS
+    const auto grid_of = [&](auto kernel) {
+      int per_cu = 0;
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kRowThreads, row_lds) != hipSuccess || per_cu < 1)
+        per_cu = 1;
+      return static_cast<unsigned>(std::min<long long>(g.N, 1LL * std::max(per_cu, RT_MOM_ROWS_PER_CU) * cus));
+    };
+#define RT_ROW_LAUNCH(n)                                                                                      \
+  if (nl <= n) {                                                                                              \
+    hipLaunchKernelGGL((moments_row_kernel<0, n>), dim3(grid_of(moments_row_kernel<0, n>)), dim3(kRowThreads), \
+                       row_lds, st, E, mu, wt, phi, F, phi_plus, m);                                           \
+    hipLaunchKernelGGL((moments_row_kernel<1, n>), dim3(grid_of(moments_row_kernel<1, n>)), dim3(kRowThreads), \
+                       row_lds, st, E, mu, wt, phi, F, phi_plus, m);                                           \
+    return hipGetLastError();                                                                                 \
   }
     RT_ROW_LAUNCH(4) RT_ROW_LAUNCH(8) RT_ROW_LAUNCH(16)
 #undef RT_ROW_LAUNCH

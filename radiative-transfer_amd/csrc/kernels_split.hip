@@ -273,7 +273,7 @@ __global__ __launch_bounds__(64 * KW) __attribute__((amdgpu_waves_per_eu(2, 2)))
   // Static issue priority for wave 0 (it streams the rows in and runs the first levels; the
   // SIMD it shares with another workgroup's wave gives it the issue slot first): the T = 20
   // pass 8.42-8.46 vs 8.61-8.65 ms/step, priority for wave 1 instead 8.52-8.57
-  // (profiles/r03ap_prio.jsonl); on another box 8.17-8.18 vs 8.36-8.41, and the four-wave
+  // (profiles/archive/r03ap_prio.jsonl); on another box 8.17-8.18 vs 8.36-8.41, and the four-wave
   // T = 40 pass 7.85-7.88 vs 7.90-7.91 (r03aq_prio.jsonl; MI355X_MICROARCH.md, two waves per
   // SIMD, item 4).
   if (RT_SPLIT_PRIO > 0 && w == RT_SPLIT_PRIO - 1) __builtin_amdgcn_s_setprio(1);

@@ -658,8 +658,8 @@ static hipError_t launch_wave_s(const WavePlan &p, const SegArgs &a, int nsteps,
 // Which (cells per lane, waves) a chain takes: a tick costs ~148 C cycles of FP64 issue on
 // one wave (~200 at C = 1: latency), and a chain over several waves adds ~160-200 cycles of
 // cross-wave coupling per tick -- more beyond 4 waves, where two waves share a SIMD (1000
-// steps, 1000 cells: 4 waves x 4 cells 477 us, 8 x 2 595 us; profiles/r03ak_waves.jsonl).
-// Measured crossover (profiles/r03an_plan.jsonl, 1000 steps): one wave wins up to 4 cells
+// steps, 1000 cells: 4 waves x 4 cells 477 us, 8 x 2 595 us; profiles/archive/r03ak_waves.jsonl).
+// Measured crossover (profiles/archive/r03an_plan.jsonl, 1000 steps): one wave wins up to 4 cells
 // per lane (256 cells: one wave x 4 cells 244 us, 4 waves x 1 cell 298 us), a chain at 2
 // cells per lane beats one wave at 8 (512 cells: 361 vs 448 us; reflective 200 cells: 453
 // vs 563 us).  So: one wave while up to 4 cells per lane fit it; else the fewest cells per

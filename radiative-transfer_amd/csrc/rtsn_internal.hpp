@@ -277,7 +277,7 @@ inline bool split_block(int T) { return level_split_supported(SCHEME_BDF2, T); }
 // Waves per segment of the pipelined pass: the caller's choice, or by default two waves
 // (sweep_split_kernel) where measured faster -- BDF2 at T = 20, whose one-wave kernel
 // needs 126 AGPRs beside 256 VGPRs (9% extra moves; split 8.29-8.31 vs 8.52-8.53 ms/step
-// on SL, profiles/r02b_split20.jsonl) -- and one wave otherwise (T = 16: 4% faster).
+// on SL, profiles/archive/r02b_split20.jsonl) -- and one wave otherwise (T = 16: 4% faster).
 inline int level_waves_of(const rt_solver *s, int T) {
   if (s->scheme != SCHEME_BDF2 || !split_block(T)) return 1;  // the split kernel is BDF2's
   if (T > 20) return 4;                                         // one or two waves would spill
@@ -296,7 +296,7 @@ inline int level_waves_of(const rt_solver *s, int T) {
 // one SIMD each; T / k levels per wave): e.g. 5 of 8 positions of the driver's T = 20 window
 // as four waves run 3 x 5 levels per SIMD instead of 2 x 10 (round 3 had kept two waves
 // beyond the full launch's wave count: 133 of the full launch's 164 ms for 5/8 of its work,
-// profiles/r03ar_trace_summary.json).  Ties go to the most waves within that count.
+// profiles/archive/r03ar_trace_summary.json).  Ties go to the most waves within that count.
 inline int fill_level_waves(const rt_solver *s, int grid) {
   const int base = level_waves_of(s, s->Tpipe);
   if (s->level_waves || s->scheme != SCHEME_BDF2 || !split_block(s->Tpipe)) return base;

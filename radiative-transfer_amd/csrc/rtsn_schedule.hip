@@ -307,7 +307,7 @@ WavePlan rtsn_detail::wave_plan(const rt_solver *s) {
 // Auto (mode 1) takes a chain of several waves while the chains need at most two waves per
 // SIMD: mid-length lines run 4-7x faster as chains than as segment passes there (1000 BDF2
 // steps, N = 600-4000 cells: 4 groups 0.46-1.5 ms vs 2.7-6.6 ms, 124 groups, i.e. 1984 waves,
-// 0.67-1.7 ms vs 4.0-8.1 ms; profiles/r03ai_mid.jsonl).  Beyond, the chains time-share the
+// 0.67-1.7 ms vs 4.0-8.1 ms; profiles/archive/r03ai_mid.jsonl).  Beyond, the chains time-share the
 // SIMDs, and the segment pipeline's full-chip passes (28 FMAs per cell and level at ~90% of
 // the FP64 issue rate) carry the same work with less overhead per cell.
 bool rtsn_detail::use_wavefront(const rt_solver *s) {
@@ -390,7 +390,7 @@ extern "C" rt_status rt_synchronize(rt_solver *s) {
 // estimated whole-run time (plan_schedule): time block T of 8-40 steps, four waves per
 // segment (sweep_split_kernel<3, T, 4>, every launch of the run) and segments sized for w of
 // 4-32 workgroups per CU.  The model (fitted to the finite-state whole-run
-// grids profiles/r03l_grid{16,128}.jsonl: mean error 3%): a run of n steps is P = n / T
+// grids profiles/archive/r03l_grid{16,128}.jsonl: mean error 3%): a run of n steps is P = n / T
 // passes over a chain of C segment positions, launched as P + C - 1 launches whose active
 // positions form a band (ramp up, plateau of min(P, C), ramp down); a launch of W workgroups
 // runs in rounds of the resident 2 per CU, and a round's time is one segment's Ls x T / 4

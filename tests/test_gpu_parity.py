@@ -427,7 +427,7 @@ def test_moments_two_pass_bitwise(rtsn_mod, oracle_mod, monkeypatch, M, G, bc_le
     orc = oracle_mod.OracleSolver(p)
     orc.solve()
     out = {}
-    for env in ("0", "1", "2"):
+    for env in ("0", "1", "2", "3"):
         monkeypatch.setenv("RTSN_MOMENTS_RING", env)
         with rtsn_mod.Solver(to_rt(p)) as gpu:
             gpu.solve()
@@ -437,6 +437,7 @@ def test_moments_two_pass_bitwise(rtsn_mod, oracle_mod, monkeypatch, M, G, bc_le
     for k in range(3):
         assert np.array_equal(out["0"][k], out["1"][k]), k
         assert np.array_equal(out["0"][k], out["2"][k]), k
+        assert np.array_equal(out["0"][k], out["3"][k]), k
 
 
 @pytest.fixture(scope="module")

@@ -188,7 +188,7 @@ def test_direction_shard_argument_checks(rtsn_mod):
 def test_plan_time_block(rtsn_mod):
     """rt_solve's run-length-aware block on the SL slab's geometry (rt_plan_time_block: the
     schedule model of rt_plan_schedule at N = 1e6, S64, 128 groups, 256 CUs) picks the
-    measured fastest whole runs of the finite-state grid (profiles/r03l_grid128.jsonl): 300
+    measured fastest whole runs of the finite-state grid (profiles/archive/r03l_grid128.jsonl): 300
     steps T = 20 (2659 ms; T = 40 with its 20 aligned remainder steps 2838-2899), 1000 steps
     T = 40 (8139-8188 ms; T = 20 8524-8573); every choice has at least one whole pass."""
     plan = rtsn_mod.plan_time_block

@@ -5,7 +5,7 @@ with its LDS-resident propagator, and the transient planned schedule.
 Geometry: llnl_slab_test's material and tabulated opacities resampled to 4 groups, M = 2
 (8 lines), N = 5000 or 50000 cells, dt = 1e-9 -- lines beyond the wavefront chain's 4096
 cells, with few lines, where round 3 measured 1000 aligned steps at 1.4-4.5 s against
-3.5-17 ms for rt_solve (profiles/r03ao_solve_mid.jsonl).  Every field against the oracle
+3.5-17 ms for rt_solve (profiles/archive/r03ao_solve_mid.jsonl).  Every field against the oracle
 to 1e-10 per group (tests/test_gpu_parity.compare_all)."""
 import numpy as np
 import pytest

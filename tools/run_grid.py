@@ -3,7 +3,7 @@ pipelined) over a grid of time block T, waves per segment KW (rt_set_level_waves
 every launch of the run) and segments per line (RTSN_WAVES_PER_CU = w: Sg = CUs w / (2 Q)):
 the data behind the small-shard schedule.  A fresh handle per configuration
 at dt = 1e-9 (RTSN_GRID_DT), where the reference's BDF2 keeps the SL state finite for more
-than 4000 steps (profiles/r03j_finite_horizon.jsonl; at 1e-7 it overflows within 400 and
+than 4000 steps (profiles/archive/r03j_finite_horizon.jsonl; at 1e-7 it overflows within 400 and
 inf arithmetic runs faster).
 usage: python -u tools/run_grid.py G n1,n2 T1,T2 KW1,KW2 w1,w2"""
 import json
