@@ -406,7 +406,6 @@ struct RunGeom {
 
 static double level_ns(int T) {  // per cell-level and wave, a SIMD's issue shared by its waves
   switch (T) {
-    case 4: return 90.0;
     case 8: return 76.7;
     case 16: return 71.0;
     case 20: return 67.6;
@@ -462,7 +461,9 @@ struct Schedule {
 };
 
 static Schedule plan_schedule(const RunGeom &g, long long nsteps) {
-  static const int kBlocks[] = {40, 32, 24, 20, 16, 8, 4}, kWgs[] = {4, 8, 16, 32};
+  // T = 4 over four waves (no remainder for n % 4 == 0) measured slower than T = 8 with its
+  // aligned remainder (16-group shard, 100 steps: 181 vs 167 ms, profiles/r04d_solve_plan.jsonl)
+  static const int kBlocks[] = {40, 32, 24, 20, 16, 8}, kWgs[] = {4, 8, 16, 32};
   Schedule best;
   for (int T : kBlocks)
     for (int w : kWgs) {

@@ -33,6 +33,9 @@ for step in "$@"; do
       ;;
     tests)
       [ -z "$arg" ] && arg=tests
+      # collection first (no GPU): a test file that does not import or parse fails here in seconds
+      timeout -k 10 120 python -m pytest $arg -m gpu --collect-only -q > ${log%.log}_collect.log 2>&1 \
+        || { tail -30 ${log%.log}_collect.log; exit 1; }
       timeout -k 10 1100 python -u -m pytest $arg -m gpu -x -q --timeout 300 --timeout-method thread > $log 2>&1 \
         || { tail -60 $log; exit 1; }
       tail -2 $log
