@@ -118,15 +118,8 @@ __device__ unsigned long long g_block_stamps[kWaveMaxWaves * kBlockStamps * 2];
 // real -- except, with PAIR and N mod C != 0 (PAD), those of the mu < 0 line, whose exit
 // state is the mirror head's inflow: there they pass X through by a select (a per-lane
 // branch would make every tick divergent).
-// BPERM (one wave, no pair, BDF2, lane 63 idle: the line holds at most 63 lanes): in the
-// unmasked ticks components 1..K-2 of the carried state move by ds_bpermute (the LDS
-// crossbar, issued beside the VALU) instead of two DPP moves each, lane 0 reading lane 63.
-// Lane 63's map keeps only the rows' constants, set to the head's inflow state, and it
-// reads its own components back: its exit components 1..K-2 are the head's every tick
-// (0 * x + c = c exactly for finite x), which is what lane 0's DPP `old` held.
-template <int S, int C, bool PAIR, bool PAD, bool MULTI, bool BPERM = false>
+template <int S, int C, bool PAIR, bool PAD, bool MULTI>
 __global__ __launch_bounds__(MULTI ? 64 * kWaveMaxWaves : 64) void wavefront_kernel(SegArgs a, int nsteps, int Lw) {
-  static_assert(!BPERM || (!PAIR && !MULTI && S == SCHEME_BDF2), "ds_bpermute shifts: one wave, no pair, BDF2");
   constexpr int K = SchemeDim<S>::K, WN = map_count<S>();
   RT_STAMP(0);
   const int lane = threadIdx.x & 63;
@@ -189,23 +182,6 @@ __global__ __launch_bounds__(MULTI ? 64 * kWaveMaxWaves : 64) void wavefront_ker
 #pragma unroll
     for (int r = 0; r < K; ++r) X[r] = Xin[r];
   }
-  int bperm_addr = 0;
-  if constexpr (BPERM) {
-    bperm_addr = 4 * (lane == 0 || lane == 63 ? 63 : lane - 1);
-    if (lane == 63) {
-#pragma unroll
-      for (int n = 0; n < WN; ++n) W[n] = 0.0;
-#pragma unroll
-      for (int r = 1; r < K - 1; ++r) W[map_slot<S>(r, K + 2)] = Xin[r];
-    }
-  }
-  const auto bperm_shift = [&](double v) {
-    const unsigned long long bits = __builtin_bit_cast(unsigned long long, v);
-    const int lo = __builtin_amdgcn_ds_bpermute(bperm_addr, static_cast<int>(bits & 0xffffffffu));
-    const int hi = __builtin_amdgcn_ds_bpermute(bperm_addr, static_cast<int>(bits >> 32));
-    return __builtin_bit_cast(double, (static_cast<unsigned long long>(static_cast<unsigned int>(hi)) << 32) |
-                                          static_cast<unsigned int>(lo));
-  };
   // MULTI: rd = where lane 0 of this wave takes its `old` operands -- wave 0 a fixed slot
   // holding the head's inflow state (mask 0), wave w the ring of boundary w - 1
   extern __shared__ double lds_ring[];
@@ -248,7 +224,7 @@ __global__ __launch_bounds__(MULTI ? 64 * kWaveMaxWaves : 64) void wavefront_ker
         const double x0 = Xin[K - 1];
         Xin[K - 1] = lane_shift_up(MULTI ? o[K - 1] : Xin[0], X[K - 1]);
 #pragma unroll
-        for (int r = 1; r < K - 1; ++r) Xin[r] = BPERM ? bperm_shift(X[r]) : lane_shift_up(o[r], X[r]);
+        for (int r = 1; r < K - 1; ++r) Xin[r] = lane_shift_up(o[r], X[r]);
         Xin[0] = x0;
       } else {
 #pragma unroll
@@ -661,23 +637,6 @@ static hipError_t launch_wave_s(const WavePlan &p, const SegArgs &a, int nsteps,
     }
 #endif
     return hipGetLastError();
-  }
-#ifndef RT_WAVE_BPERM
-#define RT_WAVE_BPERM 1
-#endif
-  if constexpr (!PAIR && S == SCHEME_BDF2) {
-    if (RT_WAVE_BPERM && Lw <= 63) {  // lane 63 idle: ds_bpermute shifts (wavefront_kernel BPERM)
-      switch (p.C) {
-#define RT_WAVE_BPERM_CASE(c)                                                                                    \
-  case c:                                                                                                        \
-    hipLaunchKernelGGL((wavefront_kernel<S, c, false, false, false, true>), dim3(grid), dim3(64), 0, st, a, nsteps, \
-                       Lw);                                                                                      \
-    return hipGetLastError();
-        RT_WAVE_BPERM_CASE(1) RT_WAVE_BPERM_CASE(2) RT_WAVE_BPERM_CASE(4) RT_WAVE_BPERM_CASE(8)
-#undef RT_WAVE_BPERM_CASE
-        default: return hipErrorInvalidValue;
-      }
-    }
   }
   switch (p.C) {
 #define RT_WAVE_CASE(c)                                                                                          \
