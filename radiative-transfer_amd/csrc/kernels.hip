@@ -32,7 +32,6 @@
 
 #include <algorithm>
 #include <cstdint>
-#include <cstdlib>
 
 #include "cell.hpp"
 #include "kernels.hpp"
@@ -547,7 +546,12 @@ __global__ void import_ends_kernel(double2 *E, const double *ends, LineMap m, in
 // chunk's loads are in flight while the current one is summed.  The weights
 // are wave-uniform (scalar loads).
 // MOM_W directions per chunk: 8 x 16 B = one 128 B line per group, 16 = two (16 KB of the
-// state in flight per wave instead of 8: round 4).
+// state in flight per wave instead of 8: round 4).  23.0 ms on SL (5.7 TB/s of the 131 GB
+// state, profiles/r04q_*).  Round 4 measured and removed, all within +-5% of this kernel on
+// one box while a plain scan of the same state runs at 6.9 TB/s: 32-direction chunks; a
+// register ring of 2-4 chunks in flight per wave; LDS-DMA rings (global_load_lds) of 2-3
+// 32 KB units; two passes in row order (half 0's partial sums through the outputs); whole
+// rows per 256-thread workgroup loaded like the scan, in two passes and in one.
 // FAST: H % MOM_W == 0, so every chunk is 64 groups x MOM_W directions and lane
 // (gr, col) = (lane / MOM_W, lane % MOM_W) loads group gr + (64 / MOM_W) r, direction col.
 template <bool FAST, int MOM_W>
@@ -652,278 +656,6 @@ __global__ void __launch_bounds__(64) moments_kernel(const double2 *__restrict__
       phi[o] = sphi;
       F[o] = sF;
       phi_plus[o] = splus;
-    }
-  }
-}
-
-// The same sums (same order, same expressions: bitwise moments_kernel's FAST path) as two
-// passes, one per half of the directions, each reading its half of the state in address
-// order -- round 4.  moments_kernel reads the SL state at 5.3-5.7 TB/s whatever its chunk
-// width (8, 16, 32 directions) or the chunks it keeps in flight (1-4 per wave), while a plain
-// scan of the same 131 GB in address order (finite_scan_kernel) reads at 6.9 TB/s
-// (profiles/r04h_*): a task of moments_kernel reads row N-1-c of half 0 and row c of half 1,
-// two streams 65 GB apart.  Here pass 0 walks half 0's rows in order (cell N-1-k at row k),
-// summing i = 0 .. H-1 and storing the partial phi and F in the outputs; pass 1 walks half
-// 1's rows (cell k), reloads them, continues the same sums over i = H .. M-1 and stores phi,
-// F and phi_plus: the partials go through memory as doubles, so the sums are bitwise those
-// of one pass (4 GB more traffic on SL, 3%).  D chunks per wave in flight (a register ring,
-// the loop unrolled D chunks at a time so its registers are compile-time).
-constexpr int kMomMaxM = 256;
-template <int W, int D, int HALF>
-__global__ void __launch_bounds__(64) moments_half_kernel(const double2 *__restrict__ E, const double *__restrict__ mu,
-                                                          const double *__restrict__ wt, double *phi, double *F,
-                                                          double *phi_plus, LineMap m) {
-#pragma clang fp contract(off)
-  __shared__ double tile[64 * (W + 1)];
-  __shared__ double2 wxl[kMomMaxM];  // (weight, mu) per direction: read in order with the tile
-  const int lane = threadIdx.x;
-  const int H = m.H;
-  for (int i = lane; i < 2 * H; i += 64) wxl[i] = make_double2(wt[i], mu[i]);
-  __syncthreads();
-  const int nchunks = (m.Gl + 63) / 64;
-  const int nj = H / W;  // chunks per task (the launcher checks H % W == 0, M <= kMomMaxM)
-  const long long tasks = static_cast<long long>(m.N) * nchunks;  // (row, 64 groups), rows in order
-  if (static_cast<long long>(blockIdx.x) >= tasks) return;
-  const long long nq = (tasks - blockIdx.x + gridDim.x - 1) / gridDim.x * nj;  // this wave's chunks
-  const int gr = lane / W, col = lane % W;
-  double2 v[D][W];
-  const auto load = [&](double2 (&b)[W], long long q) {
-    if (q >= nq) return;
-    const long long task = blockIdx.x + q / nj * gridDim.x;
-    const int step = static_cast<int>(q % nj);
-    const int k = static_cast<int>(task / nchunks), g0 = static_cast<int>(task % nchunks) * 64;
-    const int ng = min(64, m.Gl - g0);
-    const int i0 = (HALF == 0 ? nj - 1 - step : step) * W;  // half 0: i' descending
-    const double2 *row = E + m.at(HALF, k, H * g0 + i0);
-    const __amdgpu_buffer_rsrc_t R =
-        __builtin_amdgcn_make_buffer_rsrc(const_cast<double2 *>(row), 0, ng * H * 16, 0x00020000);
-    const int voff = (H * gr + col) * 16;
-#pragma unroll
-    for (int r = 0; r < W; ++r) b[r] = row_load(R, voff, r * (64 / W) * H * 16);
-  };
-#pragma unroll
-  for (int d = 0; d < D; ++d) load(v[d], d);
-  double sphi = 0.0, sF = 0.0, splus = 0.0;
-  for (long long q0 = 0; q0 < nq; q0 += D) {
-#pragma unroll
-    for (int d = 0; d < D; ++d) {
-      const long long q = q0 + d;
-      if (q >= nq) break;
-      const long long task = blockIdx.x + q / nj * gridDim.x;
-      const int step = static_cast<int>(q % nj);
-      const int k = static_cast<int>(task / nchunks), g0 = static_cast<int>(task % nchunks) * 64;
-      const int c = HALF == 0 ? m.N - 1 - k : k;
-      const int ng = min(64, m.Gl - g0);
-      const size_t o = static_cast<size_t>(c) * m.Gl + g0 + lane;
-      if (HALF == 1 && step == 0 && lane < ng) {  // half 0's partial sums
-        sphi = phi[o];
-        sF = F[o];
-      }
-      const int i0 = (HALF == 0 ? nj - 1 - step : step) * W;
-#pragma unroll
-      for (int r = 0; r < W; ++r)
-        if (gr + (64 / W) * r < ng) tile[(gr + (64 / W) * r) * (W + 1) + col] = 0.5 * (v[d][r].x + v[d][r].y);
-      __syncthreads();
-      load(v[d], q + D);
-      const int ib = HALF == 0 ? H - i0 - W : H + i0;  // lowest i of the chunk
-      double wv[W], xv[W];
-#pragma unroll
-      for (int kk = 0; kk < W; ++kk) {
-        const double2 wx = wxl[ib + kk];  // broadcast LDS reads: no scalar loads (their wait is lgkmcnt(0))
-        wv[kk] = wx.x;
-        xv[kk] = wx.y;
-      }
-      if (lane < ng) {
-        const double *t = tile + lane * (W + 1);
-        if (HALF == 0) {  // i = H-1-(i0+ii) = ib + (W-1-ii)
-#pragma unroll
-          for (int ii = W - 1; ii >= 0; --ii) {
-            const int kk = W - 1 - ii;
-            const double qv = t[ii];
-            sphi += wv[kk] * qv;
-            sF += xv[kk] * wv[kk] * qv;
-          }
-        } else {  // i = H + i0 + ii = ib + ii
-#pragma unroll
-          for (int ii = 0; ii < W; ++ii) {
-            const double qv = t[ii];
-            sphi += wv[ii] * qv;
-            sF += xv[ii] * wv[ii] * qv;
-            splus += wv[ii] * qv;
-          }
-        }
-      }
-      __syncthreads();
-      if (step == nj - 1) {
-        if (lane < ng) {
-          phi[o] = sphi;
-          F[o] = sF;
-          if (HALF == 1) phi_plus[o] = splus;
-        }
-        sphi = sF = splus = 0.0;
-      }
-    }
-  }
-}
-
-// Moments by whole rows: a 256-thread workgroup reads one row of one half (every line of
-// the shard at one cell: H Gl double2, 64 KiB on SL) the way the finite scan does -- lane-
-// contiguous 16-byte loads, 4 KiB per workgroup instruction, all of a thread's loads issued
-// before the first is used -- then transposes psi = (e_in + e_out) / 2 through LDS and one
-// thread per group runs the sequential sums over the half's directions.  Two passes as
-// moments_half_kernel (half 0 by rows, the partial phi and F through the outputs; then half
-// 1): the same sums in the same order, bitwise moments_kernel.  Round 4: every
-// chunked form (moments_kernel, moments_half_kernel at 8-32 directions per chunk, 1-4 chunks
-// in flight, LDS-DMA rings) read the SL state at 5.2-5.7 TB/s against the scan's 6.9
-// (profiles/r04*_moments_rate.jsonl).
-constexpr int kRowThreads = 256;
-constexpr int kMomMaxGroups = 256;  // groups per shard the row kernel takes (the launcher checks)
-template <int HALF, int NL>
-__global__ void __launch_bounds__(kRowThreads) moments_row_kernel(const double2 *__restrict__ E,
-                                                                  const double *__restrict__ mu,
-                                                                  const double *__restrict__ wt, double *phi,
-                                                                  double *F, double *phi_plus, LineMap m) {
-#pragma clang fp contract(off)
-  extern __shared__ double2 row_lds[];  // wxl[2H], then the tile [Gl][H + 1] doubles
-  double2 *wxl = row_lds;
-  double *tile = reinterpret_cast<double *>(row_lds + 2 * m.H);
-  const int t = threadIdx.x, H = m.H, L = H * m.Gl, HP = H + 1;
-  for (int i = t; i < 2 * H; i += kRowThreads) wxl[i] = make_double2(wt[i], mu[i]);
-  typedef double d2v __attribute__((ext_vector_type(2)));
-  for (int k = blockIdx.x; k < m.N; k += gridDim.x) {
-    const d2v *row = reinterpret_cast<const d2v *>(E) + m.at(HALF, k, 0);
-    d2v v[NL];
-#pragma unroll
-    for (int j = 0; j < NL; ++j) {
-      const int e = t + j * kRowThreads;
-      if (e < L) v[j] = __builtin_nontemporal_load(row + e);
-    }
-    const int c = HALF == 0 ? m.N - 1 - k : k;
-    double p0[(kMomMaxGroups + kRowThreads - 1) / kRowThreads], p1[(kMomMaxGroups + kRowThreads - 1) / kRowThreads];
-    if (HALF == 1) {  // half 0's partial sums, loaded with the row (their latency behind the row's)
-#pragma unroll
-      for (int n = 0; n < (kMomMaxGroups + kRowThreads - 1) / kRowThreads; ++n) {
-        const int g = t + n * kRowThreads;
-        if (g < m.Gl) {
-          p0[n] = phi[static_cast<size_t>(c) * m.Gl + g];
-          p1[n] = F[static_cast<size_t>(c) * m.Gl + g];
-        }
-      }
-    }
-    __syncthreads();  // the previous row's sums are done with the tile
-#pragma unroll
-    for (int j = 0; j < NL; ++j) {
-      const int e = t + j * kRowThreads;
-      if (e < L) tile[(e / H) * HP + e % H] = 0.5 * (v[j].x + v[j].y);
-    }
-    __syncthreads();
-#pragma unroll
-    for (int n = 0; n < (kMomMaxGroups + kRowThreads - 1) / kRowThreads; ++n) {
-      const int g = t + n * kRowThreads;
-      if (g >= m.Gl) break;
-      const double *q = tile + g * HP;
-      const size_t o = static_cast<size_t>(c) * m.Gl + g;
-      if (HALF == 0) {  // i = 0 .. H-1 is direction H-1-i
-        double sphi = 0.0, sF = 0.0;
-        for (int i = 0; i < H; ++i) {
-          const double2 wx = wxl[i];
-          const double qv = q[H - 1 - i];
-          sphi += wx.x * qv;
-          sF += wx.y * wx.x * qv;
-        }
-        phi[o] = sphi;
-        F[o] = sF;
-      } else {  // i = H + d
-        double sphi = p0[n], sF = p1[n], splus = 0.0;
-        for (int d = 0; d < H; ++d) {
-          const double2 wx = wxl[H + d];
-          const double qv = q[d];
-          sphi += wx.x * qv;
-          sF += wx.y * wx.x * qv;
-          splus += wx.x * qv;
-        }
-        phi[o] = sphi;
-        F[o] = sF;
-        phi_plus[o] = splus;
-      }
-    }
-  }
-}
-
-// One pass over both halves of a cell (round 4): a workgroup takes cell c -- row N-1-c of
-// half 0, then row c of half 1 -- loading the half-1 row while it sums half 0, so the
-// partial sums stay in registers (no second pass, no partials through memory).
-template <int NL>
-__global__ void __launch_bounds__(kRowThreads) moments_cell_kernel(const double2 *__restrict__ E,
-                                                                   const double *__restrict__ mu,
-                                                                   const double *__restrict__ wt, double *phi,
-                                                                   double *F, double *phi_plus, LineMap m) {
-#pragma clang fp contract(off)
-  extern __shared__ double2 row_lds[];  // wxl[2H], then the tile [Gl][H + 1] doubles
-  double2 *wxl = row_lds;
-  double *tile = reinterpret_cast<double *>(row_lds + 2 * m.H);
-  const int t = threadIdx.x, H = m.H, L = H * m.Gl, HP = H + 1;
-  for (int i = t; i < 2 * H; i += kRowThreads) wxl[i] = make_double2(wt[i], mu[i]);
-  typedef double d2v __attribute__((ext_vector_type(2)));
-  const auto load = [&](d2v (&v)[NL], int half, int k) {
-    const d2v *row = reinterpret_cast<const d2v *>(E) + m.at(half, k, 0);
-#pragma unroll
-    for (int j = 0; j < NL; ++j) {
-      const int e = t + j * kRowThreads;
-      if (e < L) v[j] = __builtin_nontemporal_load(row + e);
-    }
-  };
-  const auto stage = [&](const d2v (&v)[NL]) {
-#pragma unroll
-    for (int j = 0; j < NL; ++j) {
-      const int e = t + j * kRowThreads;
-      if (e < L) tile[(e / H) * HP + e % H] = 0.5 * (v[j].x + v[j].y);
-    }
-  };
-  constexpr int GN = (kMomMaxGroups + kRowThreads - 1) / kRowThreads;
-  for (int c = blockIdx.x; c < m.N; c += gridDim.x) {
-    d2v v0[NL], v1[NL];
-    load(v0, 0, m.N - 1 - c);
-    __syncthreads();  // the previous cell's sums are done with the tile
-    stage(v0);
-    load(v1, 1, c);  // in flight during half 0's sums
-    __syncthreads();
-    double sphi[GN], sF[GN];
-#pragma unroll
-    for (int n = 0; n < GN; ++n) {
-      const int g = t + n * kRowThreads;
-      sphi[n] = sF[n] = 0.0;
-      if (g < m.Gl) {
-        const double *q = tile + g * HP;
-        for (int i = 0; i < H; ++i) {  // i = 0 .. H-1 is direction H-1-i
-          const double2 wx = wxl[i];
-          const double qv = q[H - 1 - i];
-          sphi[n] += wx.x * qv;
-          sF[n] += wx.y * wx.x * qv;
-        }
-      }
-    }
-    __syncthreads();
-    stage(v1);
-    __syncthreads();
-#pragma unroll
-    for (int n = 0; n < GN; ++n) {
-      const int g = t + n * kRowThreads;
-      if (g < m.Gl) {
-        const double *q = tile + g * HP;
-        double splus = 0.0;
-        for (int d = 0; d < H; ++d) {  // i = H + d
-          const double2 wx = wxl[H + d];
-          const double qv = q[d];
-          sphi[n] += wx.x * qv;
-          sF[n] += wx.y * wx.x * qv;
-          splus += wx.x * qv;
-        }
-        const size_t o = static_cast<size_t>(c) * m.Gl + g;
-        phi[o] = sphi[n];
-        F[o] = sF[n];
-        phi_plus[o] = splus;
-      }
     }
   }
 }
@@ -1827,9 +1559,6 @@ hipError_t launch_import_ends(double2 *E, const double *ends, const Geometry &g,
 #ifndef RT_MOM_W
 #define RT_MOM_W 16
 #endif
-#ifndef RT_MOM_D
-#define RT_MOM_D 2  // chunks in flight per wave in moments_half_kernel (0: moments_kernel only)
-#endif
 hipError_t launch_moments(const double2 *E, const double *mu, const double *wt, double *phi, double *F,
                           double *phi_plus, const Geometry &g, hipStream_t st) {
   const LineMap m = make_map(g);
@@ -1837,70 +1566,6 @@ hipError_t launch_moments(const double2 *E, const double *mu, const double *wt, 
   // as many waves as the chip holds at once; each walks its tasks with a one-chunk prefetch:
   // 16-direction chunks where the half's directions come in whole ones, else 8
   constexpr int W = RT_MOM_W;
-#if RT_MOM_D
-  // RTSN_MOMENTS_RING=0: moments_kernel; =2: moments_half_kernel (read per call: the parity
-  // test compares them)
-  const char *ring_env = getenv("RTSN_MOMENTS_RING");
-  const int mode = ring_env ? atoi(ring_env) : 1;
-  const size_t row_lds = sizeof(double2) * 2 * m.H + sizeof(double) * static_cast<size_t>(g.Gl) * (m.H + 1);
-  const int nl = (m.H * g.Gl + kRowThreads - 1) / kRowThreads;
-#ifndef RT_MOM_ROWS_PER_CU
-#define RT_MOM_ROWS_PER_CU 64  // workgroups per CU in the grid (more than resident: measured faster than persistent)
-#endif
-  if (mode == 3 && row_lds <= 40 * 1024 && nl <= 16 && g.Gl <= kMomMaxGroups) {  // one pass, a cell per workgroup
-    static int cus3 = 0;
-    if (!cus3) {
-      int dev = 0;
-      if (hipGetDevice(&dev) != hipSuccess ||
-          hipDeviceGetAttribute(&cus3, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-        cus3 = 256;
-    }
-    const unsigned grid3 = static_cast<unsigned>(std::min<long long>(g.N, 1LL * RT_MOM_ROWS_PER_CU * cus3));
-#define RT_CELL_LAUNCH(n)                                                                                     \
-  if (nl <= n) {                                                                                              \
-    hipLaunchKernelGGL((moments_cell_kernel<n>), dim3(grid3), dim3(kRowThreads), row_lds, st, E, mu, wt, phi, F,  \
-                       phi_plus, m);                                                                          \
-    return hipGetLastError();                                                                                 \
-  }
-    RT_CELL_LAUNCH(4) RT_CELL_LAUNCH(8) RT_CELL_LAUNCH(16)
-#undef RT_CELL_LAUNCH
-  }
-  if (mode == 1 && row_lds <= 40 * 1024 && nl <= 16 && g.Gl <= kMomMaxGroups) {  // whole rows (SL: 4096 lines per row, 34 KB of LDS)
-    static int cus = 0;
-    if (!cus) {
-      int dev = 0;
-      if (hipGetDevice(&dev) != hipSuccess ||
-          hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-        cus = 256;
-    }
-    // persistent: as many workgroups as the CUs hold at once with this row's LDS
-    const auto grid_of = [&](auto kernel) {
-      int per_cu = 0;
-      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kRowThreads, row_lds) != hipSuccess || per_cu < 1)
-        per_cu = 1;
-      return static_cast<unsigned>(std::min<long long>(g.N, 1LL * std::max(per_cu, RT_MOM_ROWS_PER_CU) * cus));
-    };
-#define RT_ROW_LAUNCH(n)                                                                                      \
-  if (nl <= n) {                                                                                              \
-    hipLaunchKernelGGL((moments_row_kernel<0, n>), dim3(grid_of(moments_row_kernel<0, n>)), dim3(kRowThreads), \
-                       row_lds, st, E, mu, wt, phi, F, phi_plus, m);                                           \
-    hipLaunchKernelGGL((moments_row_kernel<1, n>), dim3(grid_of(moments_row_kernel<1, n>)), dim3(kRowThreads), \
-                       row_lds, st, E, mu, wt, phi, F, phi_plus, m);                                           \
-    return hipGetLastError();                                                                                 \
-  }
-    RT_ROW_LAUNCH(4) RT_ROW_LAUNCH(8) RT_ROW_LAUNCH(16)
-#undef RT_ROW_LAUNCH
-  }
-  if (mode != 0 && m.H % W == 0 && m.M <= kMomMaxM) {
-    static const size_t res0 = resident_blocks(moments_half_kernel<W, RT_MOM_D, 0>, 64);
-    static const size_t res1 = resident_blocks(moments_half_kernel<W, RT_MOM_D, 1>, 64);
-    hipLaunchKernelGGL((moments_half_kernel<W, RT_MOM_D, 0>), dim3(static_cast<unsigned>(tasks < res0 ? tasks : res0)),
-                       dim3(64), 0, st, E, mu, wt, phi, F, phi_plus, m);
-    hipLaunchKernelGGL((moments_half_kernel<W, RT_MOM_D, 1>), dim3(static_cast<unsigned>(tasks < res1 ? tasks : res1)),
-                       dim3(64), 0, st, E, mu, wt, phi, F, phi_plus, m);
-    return hipGetLastError();
-  }
-#endif
   static const size_t resident[3] = {resident_blocks(moments_kernel<false, 8>, 64),
                                      resident_blocks(moments_kernel<true, 8>, 64),
                                      resident_blocks(moments_kernel<true, W>, 64)};

@@ -411,35 +411,6 @@ def test_moments_device(rtsn_mod, oracle_mod):
             np.testing.assert_array_equal(t[k].cpu().numpy().reshape(s.N, s.G).T, host[k])
 
 
-@pytest.mark.parametrize("M,G,bc_left", [(64, 64, 0), (64, 128, 2), (32, 128, 0), (32, 70, 2), (64, 70, 0),
-                                         (16, 64, 0)])
-def test_moments_two_pass_bitwise(rtsn_mod, oracle_mod, monkeypatch, M, G, bc_left):
-    """The two-pass moments (half 0's partial sums through the outputs): moments_row_kernel
-    (whole rows, the default) and moments_half_kernel (RTSN_MOMENTS_RING=2) give bitwise
-    moments_kernel's phi, F, phi_plus (RTSN_MOMENTS_RING=0) -- the same sums in the
-    reference's order -- and match the oracle; G = 70 leaves a partial 64-group chunk and
-    rows of 1120-2240 lines, S16 (8 directions per half) takes moments_kernel's 8-wide path
-    in mode 2."""
-    p = load(oracle_mod, "llnl_slab_test.prm", N=1537, M=M, G=G, group_bounds=None, group_kappa=None, dt=1e-9,
-             max_timesteps=5, bc_left=bc_left, bc_right=1)
-    p["dx"] = p["X"] / p["N"]
-    p["psi_source"] = np.linspace(0.5, 2.0, M * G).reshape(M, G)
-    orc = oracle_mod.OracleSolver(p)
-    orc.solve()
-    out = {}
-    for env in ("0", "1", "2", "3"):
-        monkeypatch.setenv("RTSN_MOMENTS_RING", env)
-        with rtsn_mod.Solver(to_rt(p)) as gpu:
-            gpu.solve()
-            out[env] = gpu.moments()
-            if env == "1":
-                compare_all(gpu, orc)
-    for k in range(3):
-        assert np.array_equal(out["0"][k], out["1"][k]), k
-        assert np.array_equal(out["0"][k], out["2"][k]), k
-        assert np.array_equal(out["0"][k], out["3"][k]), k
-
-
 @pytest.fixture(scope="module")
 def sl_line_oracle(oracle_mod):
     """One group of the SL slab at its full line length, N = 1e6,
