@@ -346,6 +346,9 @@ constexpr int kChainSlot = 6;                  // doubles per slot (48 B: 16-byt
 #ifndef RT_CHAIN_EARLY
 #define RT_CHAIN_EARLY 1  // ring stores and reads issued before the tick's FMAs (0: round 4's first order)
 #endif
+#ifndef RT_CHAIN_MASKED_UNROLL
+#define RT_CHAIN_MASKED_UNROLL 0  // masked blocks (a wave's fill and drain ramps) unrolled too
+#endif
 #ifndef RT_CHAIN_FENCE
 #define RT_CHAIN_FENCE 1  // scheduling fences at each tick's start (4-8 cells per lane) and after its ring read
 #endif
@@ -563,6 +566,9 @@ __global__ __launch_bounds__(64 * (WIDE ? kWaveMaxWaves : 4)) void chain_kernel(
 #endif
       }
     } else {
+#if RT_CHAIN_MASKED_UNROLL
+#pragma unroll
+#endif
       for (int i = 0; i < kChainBlock; ++i) {
         const int t = t0 + i;
         if (t < 0 || t >= ticks) continue;  // wall ticks before or after this wave's chain
