@@ -347,7 +347,7 @@ constexpr int kChainSlot = 6;                  // doubles per slot (48 B: 16-byt
 #define RT_CHAIN_EARLY 1  // ring stores and reads issued before the tick's FMAs (0: round 4's first order)
 #endif
 #ifndef RT_CHAIN_MASKED_UNROLL
-#define RT_CHAIN_MASKED_UNROLL 0  // masked blocks (a wave's fill and drain ramps) unrolled too
+#define RT_CHAIN_MASKED_UNROLL 1  // masked blocks (a wave's fill and drain ramps) unrolled too (2-6%: r04r)
 #endif
 #ifndef RT_CHAIN_FENCE
 #define RT_CHAIN_FENCE 1  // scheduling fences at each tick's start (4-8 cells per lane) and after its ring read

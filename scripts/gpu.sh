@@ -60,7 +60,7 @@ s = d.get('schedule', {}); print('schedule', {k: s.get(k) for k in ('end_to_end_
         -- python3 bench.py $arg $QUIET > $log 2>&1 || { tail -20 $log; exit 1; }
       python3 scripts/trace_summary.py gpurun_out/${TAG}_kt/run_kernel_trace.csv gpurun_out/${TAG}_trace_summary.json
       cp gpurun_out/${TAG}_kt/run_kernel_stats.csv gpurun_out/${TAG}_kernel_stats.csv
-      rm -f gpurun_out/${TAG}_kt/run_kernel_trace.csv
+      gzip -f gpurun_out/${TAG}_kt/run_kernel_trace.csv
       ;;
     pmc)
       [ -z "$arg" ] && arg=$DEF_BENCH
