@@ -71,7 +71,7 @@ static_assert(kWavePrefetch >= 1 && kWaveSkew + kWaveBlockTicks + 1 <= kWaveRing
 
 // Ticks per loop iteration of the single-wave kernel (even; timing experiments: RT_WAVE_UNROLL)
 #ifndef RT_WAVE_UNROLL
-#define RT_WAVE_UNROLL 4
+#define RT_WAVE_UNROLL 8
 #endif
 constexpr int kWaveUnroll = RT_WAVE_UNROLL;
 static_assert(kWaveUnroll >= 2 && kWaveUnroll % 2 == 0, "renames cancel over an even number of ticks");
