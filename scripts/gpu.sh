@@ -5,6 +5,7 @@
 #   tests[=PYTEST_ARGS]   pytest -m gpu (all, or e.g. tests=tests/test_wavefront_gpu.py)
 #   smoke                 __graft_entry__.smoke()
 #   bench[=ARGS]          python bench.py ARGS (default: the driver's --steps 20 --warmup 5) -> TAG_bench.json
+#   rehearsal             the 2-rank bench on the one GPU over gloo -> TAG_rehearsal2.json
 #   kt[=ARGS]             rocprofv3 kernel trace + stats of bench.py ARGS (no side legs) -> TAG_kernel_stats.csv,
 #                         TAG_trace_summary.json
 #   pmc[=ARGS]            the four PMC passes of the headline pass -> profiles/pmc_TAG_v0_t20.json
@@ -53,6 +54,17 @@ import json; d=json.load(open('gpurun_out/${TAG}_bench.json')); r=d['roofline']
 print('value', d['value'], 'ms/step', d['ms_per_step'], 'kern', r.get('kernel_ms'), 'frac', r['frac'], 'finite', d.get('state_finite'))
 print('llnl', {k: d['llnl_slab_test'].get(k) for k in ('bdf2_steps_per_s', 'ms', 'path')} if 'llnl_slab_test' in d else None)
 s = d.get('schedule', {}); print('schedule', {k: s.get(k) for k in ('end_to_end_updates_per_s', 'drain_ms', 'fill_ms')})"
+      ;;
+    rehearsal)
+      # the multi-rank bench path on the box's one GPU: 2 ranks sharing cuda:0 over gloo
+      # (RCCL refuses two ranks on one device) -> TAG_rehearsal2.json
+      timeout -k 10 600 python -m torch.distributed.run --nnodes 1 --nproc-per-node 2 --master-addr 127.0.0.1 \
+        --master-port 29517 bench.py --gpus 2 $DEF_BENCH --backend gloo --share-device --no-cpu-baseline > $log 2>&1 \
+        || { tail -30 $log; exit 1; }
+      grep "^{" $log | tail -1 > gpurun_out/${TAG}_rehearsal2.json
+      python3 -c "
+import json; d=json.load(open('gpurun_out/${TAG}_rehearsal2.json'))
+print('value', d['value'], 'n_gpus', d['n_gpus'], 'comm', d.get('rt_comm_gather'), 'per_rank', d.get('per_rank'))"
       ;;
     kt)
       [ -z "$arg" ] && arg=$DEF_BENCH
