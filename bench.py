@@ -170,14 +170,18 @@ REFERENCE_CONFIGS = ("single_group.prm", "multi_group_equilibrium.prm", "llnl_sl
                      "llnl_slab_test_uncapped.prm")
 
 
+RATE_REPS = 5
+
+
 def gpu_rate(params: dict, ts_method: int, rate_steps: int = 1000) -> dict:
     """rate_steps steps of a configuration on the GPU exactly as rt_solve runs them (the
     handle's max_timesteps = rate_steps): the short-line wavefront (one launch per advance)
     where the lines fit a chain of waves, else the pipelined schedule rt_solve plans for the
     run (rt_plan_schedule: time block, waves per segment, segmentation).  The handle is
     created and warmed outside the timer; rt_solve + rt_finish (the pending correction of an
-    aligned remainder, if any) + device sync are timed: BDF2 steps/s and cell-angle-group
-    updates/s, with the number of sweep launches (HIP event pairs) that ran."""
+    aligned remainder, if any) + device sync are timed, RATE_REPS times (a fresh handle from
+    the initial state each time): BDF2 steps/s and cell-angle-group updates/s from the median
+    run (all runs in ms_runs), with the number of sweep launches (HIP event pairs) of one run."""
     import rtsn
     params = dict(params, max_timesteps=rate_steps)
     upd_step = (4.0 if ts_method == 3 else 1.0) * params["M"] * params["G"] * params["N"]
@@ -186,17 +190,20 @@ def gpu_rate(params: dict, ts_method: int, rate_steps: int = 1000) -> dict:
         s.solve()
         s.finish()
         s.synchronize()
-    with rtsn.Solver(params) as s:
-        wst = s.wavefront_state()
-        path = "wavefront" if wst["active"] else "segments"
-        plan = None if wst["active"] else s.plan_schedule(rate_steps)
-        s.synchronize()
-        t0 = time.perf_counter()
-        s.solve()
-        s.finish()
-        s.synchronize()
-        gpu_s = time.perf_counter() - t0
-        finite = s.state_finite()
+    reps = []  # RATE_REPS runs, each on a fresh handle from the initial state: the median is reported
+    for _ in range(RATE_REPS):
+        with rtsn.Solver(params) as s:
+            wst = s.wavefront_state()
+            path = "wavefront" if wst["active"] else "segments"
+            plan = None if wst["active"] else s.plan_schedule(rate_steps)
+            s.synchronize()
+            t0 = time.perf_counter()
+            s.solve()
+            s.finish()
+            s.synchronize()
+            reps.append(time.perf_counter() - t0)
+            finite = s.state_finite()
+    gpu_s = sorted(reps)[len(reps) // 2]
     with rtsn.Solver(params) as s:  # the launches, counted by HIP event pairs outside the timed run
         s.set_profiling(True)
         s.solve()
@@ -204,7 +211,8 @@ def gpu_rate(params: dict, ts_method: int, rate_steps: int = 1000) -> dict:
         passes = s.sweep_time()[1]
         s.set_profiling(False)
     return {"steps": rate_steps, "bdf2_steps_per_s": rate_steps / gpu_s, "updates_per_s": upd_step * rate_steps / gpu_s,
-            "ms": 1e3 * gpu_s, "sweep_passes": passes, "path": path,
+            "ms": 1e3 * gpu_s, "ms_runs": [round(1e3 * r, 4) for r in reps], "timing": f"median of {RATE_REPS} runs",
+            "sweep_passes": passes, "path": path,
             "time_block": plan["time_block"] if plan else None, "state_finite": finite,
             **({"cells_per_lane": wst["cells_per_lane"], "waves_per_chain": wst["waves"]} if path == "wavefront"
                else {"plan": plan})}
