@@ -346,9 +346,6 @@ constexpr int kChainSlot = 6;                  // doubles per slot (48 B: 16-byt
 #ifndef RT_CHAIN_EARLY
 #define RT_CHAIN_EARLY 1  // ring stores and reads issued before the tick's FMAs (0: round 4's first order)
 #endif
-#ifndef RT_CHAIN_NOBRANCH
-#define RT_CHAIN_NOBRANCH 0  // ring stores by every lane (the others into a lane-private dummy) instead of a branch
-#endif
 #ifndef RT_CHAIN_MASKED_UNROLL
 #define RT_CHAIN_MASKED_UNROLL 1  // masked blocks (a wave's fill and drain ramps) unrolled too (2-6%: r04r)
 #endif
@@ -440,10 +437,6 @@ __global__ __launch_bounds__(64 * (WIDE ? kWaveMaxWaves : 4)) void chain_kernel(
   double *const wr_region = ring + static_cast<size_t>(w + 1) * kChainRing * kChainSlot;  // unused by the last wave
   const bool writer = lane == 63 && w < nw - 1;
   constexpr int RM = kChainRing - 1;
-  // RT_CHAIN_NOBRANCH: a lane that is not the writer stores into its own dummy slot after the
-  // rings, so the store needs no exec-mask branch
-  double *const dummy = ring + static_cast<size_t>(nw) * kChainRing * kChainSlot + lane * kChainSlot;
-  const auto wdst = [&](double *p) { return writer ? p : dummy; };
 
   // one tick's cells: X (received state, the shifts done) through the lane's C cells
   const auto cells = [&](bool active) {
@@ -534,13 +527,9 @@ __global__ __launch_bounds__(64 * (WIDE ? kWaveMaxWaves : 4)) void chain_kernel(
         // lgkmcnt wait then finds them complete; issued at the end of the tick (the
         // compiler's placement otherwise) every tick began by waiting out their latency.
         if constexpr (C >= 4) {
-          if (RT_CHAIN_NOBRANCH && i > 0) write_slot(wdst(wb + i * kChainSlot), X, false);
-          else if (i > 0 && writer) write_slot(wb + i * kChainSlot, X, false);
+          if (i > 0 && writer) write_slot(wb + i * kChainSlot, X, false);
         } else if (i > 0 && !(i & 1)) {
-          if (RT_CHAIN_NOBRANCH) {
-            write_slot(wdst(wb + (i - 1) * kChainSlot), prev, false);
-            write_slot(wdst(wb + i * kChainSlot), X, false);
-          } else if (writer) {
+          if (writer) {
             write_slot(wb + (i - 1) * kChainSlot, prev, false);
             write_slot(wb + i * kChainSlot, X, false);
           }
@@ -553,9 +542,9 @@ __global__ __launch_bounds__(64 * (WIDE ? kWaveMaxWaves : 4)) void chain_kernel(
 #pragma unroll
         for (int r = 0; r < K; ++r) X[r] = Xin[r];
         cells(true);
-        if (i == kChainBlock - 1 && (RT_CHAIN_NOBRANCH || writer)) {  // the block's last exit state(s)
-          if constexpr (C < 4) write_slot(wdst(wb + i * kChainSlot), prev, false);
-          write_slot(wdst(wn), X, false);
+        if (i == kChainBlock - 1 && writer) {  // the block's last exit state(s), before the barrier
+          if constexpr (C < 4) write_slot(wb + i * kChainSlot, prev, false);
+          write_slot(wn, X, false);
         }
 #else
         // the next tick's ring values (slot t + 1), after this tick's shifts
@@ -595,8 +584,7 @@ __global__ __launch_bounds__(64 * (WIDE ? kWaveMaxWaves : 4)) void chain_kernel(
 #pragma unroll
         for (int r = 0; r < K; ++r) X[r] = Xin[r];
         cells(real && lv >= 0 && lv < nsteps);
-        if (RT_CHAIN_NOBRANCH) write_slot(wdst(wr_region + ((t + 1) & RM) * kChainSlot), X, true);
-        else if (writer) write_slot(wr_region + ((t + 1) & RM) * kChainSlot, X, true);
+        if (writer) write_slot(wr_region + ((t + 1) & RM) * kChainSlot, X, true);
       }
     }
     RT_BLOCK_STAMP(b, 0);
@@ -633,7 +621,7 @@ static hipError_t launch_wave_s(const WavePlan &p, const SegArgs &a, int nsteps,
       default: return hipErrorInvalidValue;
     }
 #else
-    const size_t lds = sizeof(double) * kChainSlot * (kChainRing * static_cast<size_t>(p.waves) + 64);  // + dummies
+    const size_t lds = sizeof(double) * kChainSlot * kChainRing * static_cast<size_t>(p.waves);
     switch (p.C) {
 #define RT_CHAIN_LAUNCH(c, pd, wide)                                                                             \
   hipLaunchKernelGGL((chain_kernel<S, c, PAIR, pd, wide>), dim3(grid), dim3(64 * p.waves), lds, st, a, nsteps, Lw)
