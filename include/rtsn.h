@@ -228,13 +228,15 @@ rt_status rt_set_time_block(rt_solver *s, int steps_per_pass);
  * drains when a result is read (or rt_solve returns); those launches split
  * their segments over 2-4 waves (BDF2).  0: off -- every pass moves all
  * segments together (at most 4 steps) and corrects them in the next pass;
- * 1 (default): pipelined when an advance brings enough whole passes (BDF2 with
- * the split fill: at least 1/8 of the pipeline's depth; otherwise its depth),
- * else aligned; 2: always pipelined. */
+ * 1 (default): pipelined once the queued steps bring enough whole passes (BDF2 with
+ * the split fill: at least 1/8 of the pipeline's depth, or rt_solve's plan for the run;
+ * otherwise its depth) -- until then an advance's steps stay queued, and a read-out runs
+ * them as aligned passes; 2: always pipelined. */
 rt_status rt_set_pipeline(rt_solver *s, int on);
 rt_status rt_get_pipeline(rt_solver *s, int *on);
 /* Schedule state: steps the chain head is ahead of the tail (0 = aligned),
- * steps queued but not launched, whether a correction is pending; any NULL skipped. */
+ * steps queued but not launched (segment schedules and the wavefront kernel's queue),
+ * whether a correction is pending; any NULL skipped. */
 rt_status rt_pipeline_state(rt_solver *s, long long *lag_steps, int *queued_steps, int *pending);
 rt_status rt_get_time_block(rt_solver *s, int *steps_per_pass);
 /* Short and mid-length lines: a wavefront over (cell, time level) with lanes over cells -- a
