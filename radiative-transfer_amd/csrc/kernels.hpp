@@ -67,6 +67,7 @@ struct SegArgs {
   int pending;                // the stored state is provisional: apply the correction
   int pos_lo, npos, pass_lo;  // pipelined: active chain positions and the pass of the first
   int level_waves;            // pipelined: waves per segment, 1 (sweep_block_kernel) or 2, 4 (sweep_split_kernel)
+  int tail_levels;            // pipelined (launch_split_tail): position pos_lo runs this many (< T) levels
   double hd;                  // dx / 2
   // material coupling (SWEEP_PASS, T = 1 only): per-cell emission B_g(T(x)),
   // [N][Gl] (g fastest), scaling the map constants stored for B = 1
@@ -100,6 +101,10 @@ hipError_t launch_sweep(int scheme, int T, int mode, const SegArgs &a, int grid,
 // the level-split pipelined BDF2 pass (kernels_split.hip): T levels over `waves` waves
 hipError_t launch_split(int T, int waves, const SegArgs &a, int grid, hipStream_t st);
 hipError_t split_occupancy(int T, int waves, int *workgroups_per_cu);
+// a pipelined launch whose position pos_lo runs a.tail_levels < T levels (the run's n mod T
+// remainder; vacuum lines), the rest T: (T, waves) pairs split_tail_supported
+bool split_tail_supported(int T, int waves);
+hipError_t launch_split_tail(int T, int waves, const SegArgs &a, int grid, hipStream_t st);
 // segments resident per CU (workgroups of the pass: one wave, or two with level_waves 2)
 hipError_t sweep_occupancy(int scheme, int T, int level_waves, int *waves_per_cu);
 hipError_t coupled_occupancy(int scheme, int *waves_per_cu);  // the material-coupled pass (T = 1)

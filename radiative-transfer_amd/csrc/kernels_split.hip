@@ -1,6 +1,6 @@
 // kernels_split.hip -- the level-split pipelined pass (sweep_split_kernel): a BDF2
 // segment's T levels shared by 2 or 4 waves of a workgroup.  Its own translation unit
-// (the kernel is instantiated for 14 (T, waves) pairs) so it compiles beside kernels.hip.
+// (the kernel is instantiated for 14 (T, waves) pairs, the tail variant for 9) so it compiles beside kernels.hip.
 #include <hip/hip_runtime.h>
 
 #include "cell.hpp"
@@ -36,11 +36,14 @@ namespace rtamd {
 //     1/KW of the time while the chip would otherwise idle (rtsn_api.hip
 //     pipe_launch).
 // ------------------------------------------------------------------------
-template <int S, int TW, int C, bool IN_HBM, bool OUT_HBM, bool LASTCH>
+// TAIL: the wave runs only its first nl of the TW levels (wave-uniform), the rest pass the
+// nodes through unchanged -- the run's last n mod T steps as a pipelined block (tail_levels).
+template <int S, int TW, int C, bool IN_HBM, bool OUT_HBM, bool LASTCH, bool TAIL>
 __device__ __forceinline__ void split_chunk(const double *W, double (&ein)[C], double (&eout)[C],
                                             double (&X)[TW][SchemeDim<S>::K], bool head, double h_oi, double h_oo,
                                             const double2 *lin, double2 *lout, __amdgpu_buffer_rsrc_t Rw,
-                                            __amdgpu_buffer_rsrc_t Rn, int voff, int row_bytes, int nv, int lane) {
+                                            __amdgpu_buffer_rsrc_t Rn, int voff, int row_bytes, int nv, int lane,
+                                            int nl) {
   constexpr int K = SchemeDim<S>::K;
 #pragma unroll
   for (int c = 0; c < C; ++c) {
@@ -52,6 +55,8 @@ __device__ __forceinline__ void split_chunk(const double *W, double (&ein)[C], d
     } else {
 #pragma unroll
       for (int t = 0; t < TW; ++t) {
+        if constexpr (TAIL)
+          if (t >= nl) break;
         double Xn[K], a, e;
         map_apply<S, true>(W, X[t], oi, oo, Xn, a, e);
 #pragma unroll
@@ -98,7 +103,7 @@ __device__ __forceinline__ void split_chunk(const double *W, double (&ein)[C], d
 
 // Wave w's role (compile time: with the role a runtime branch inside one body the
 // allocation measured ~340 registers, each role alone ~215).
-template <int S, int T, int KW, int w>
+template <int S, int T, int KW, int w, bool TAIL>
 __device__ __forceinline__ void split_role(const SegArgs &a, double2 (*hand)[2][split_chunk_cells() * 64],
                                            double2 *hhead) {
   constexpr int K = SchemeDim<S>::K;
@@ -127,6 +132,9 @@ __device__ __forceinline__ void split_role(const SegArgs &a, double2 (*hand)[2][
     s = pos;
   }
   const int slot = (a.pass_lo - (pos - a.pos_lo)) & 1;
+  // TAIL: position pos_lo's block is a.tail_levels < T levels (layout and carried states
+  // still T's); every other position runs all T
+  const int nl = TAIL && pos == a.pos_lo ? min(max(a.tail_levels - t0, 0), TW) : TW;
   const int ell = q * 64 + lane;
   const bool neg = half == 0;
   const int k_begin = s * a.Ls;
@@ -245,13 +253,14 @@ __device__ __forceinline__ void split_role(const SegArgs &a, double2 (*hand)[2][
   }
   int k0 = k_begin;
   for (int m = 0; m + 1 < nch; ++m, k0 += C) {
-    split_chunk<S, TW, C, IN, OUT, false>(W, ein, eout, X, refl_head && m == 0, h_oi, h_oo, lin + ((m + 1) & 1) * LB,
-                                          lout + (m & 1) * LB, rows(k0), rows(k0 + C), voff, row_bytes, C, lane);
+    split_chunk<S, TW, C, IN, OUT, false, TAIL>(W, ein, eout, X, refl_head && m == 0, h_oi, h_oo,
+                                                lin + ((m + 1) & 1) * LB, lout + (m & 1) * LB, rows(k0), rows(k0 + C),
+                                                voff, row_bytes, C, lane, nl);
     __syncthreads();
   }
-  split_chunk<S, TW, C, IN, OUT, true>(W, ein, eout, X, refl_head && nch == 1, h_oi, h_oo, lin,
-                                       lout + ((nch - 1) & 1) * LB, rows(k0), rows(k0), voff, row_bytes, k_end - k0,
-                                       lane);
+  split_chunk<S, TW, C, IN, OUT, true, TAIL>(W, ein, eout, X, refl_head && nch == 1, h_oi, h_oo, lin,
+                                             lout + ((nch - 1) & 1) * LB, rows(k0), rows(k0), voff, row_bytes,
+                                             k_end - k0, lane, nl);
   __syncthreads();
   double *ag = a.aggs[slot] + half * half_stride + static_cast<size_t>(s) * seg_stride + ell;
 #pragma unroll
@@ -264,6 +273,39 @@ __device__ __forceinline__ void split_role(const SegArgs &a, double2 (*hand)[2][
 #ifndef RT_SPLIT_PRIO
 #define RT_SPLIT_PRIO 1  // 1 + the wave given issue priority 1; 0: none (timing experiments)
 #endif
+// Wave w's role; with `tail`, the waves whose levels reach past the tail's (levels >= t0 +
+// nl) take the TAIL body, the others the plain one.
+template <int S, int T, int KW, int w>
+__device__ __forceinline__ void split_role_of(const SegArgs &a, double2 (*hand)[2][split_chunk_cells() * 64],
+                                              double2 *hhead, bool tail) {
+  if (tail && a.tail_levels < (w + 1) * (T / KW))
+    split_role<S, T, KW, w, true>(a, hand, hhead);
+  else
+    split_role<S, T, KW, w, false>(a, hand, hhead);
+}
+
+template <int S, int T, int KW, bool TAIL>
+__device__ __forceinline__ void split_roles(const SegArgs &a, double2 (*hand)[2][split_chunk_cells() * 64],
+                                            double2 *hhead, int w) {
+  bool tail = false;  // workgroup-uniform: this workgroup is position pos_lo's, which runs the tail
+  if constexpr (TAIL) tail = (static_cast<int>(blockIdx.x) % (a.Q * a.npos)) / a.Q == 0;
+  if constexpr (KW == 2) {
+    if (w == 0)
+      split_role_of<S, T, 2, 0>(a, hand, hhead, tail);
+    else
+      split_role_of<S, T, 2, 1>(a, hand, hhead, tail);
+  } else {
+    if (w == 0)
+      split_role_of<S, T, 4, 0>(a, hand, hhead, tail);
+    else if (w == 1)
+      split_role_of<S, T, 4, 1>(a, hand, hhead, tail);
+    else if (w == 2)
+      split_role_of<S, T, 4, 2>(a, hand, hhead, tail);
+    else
+      split_role_of<S, T, 4, 3>(a, hand, hhead, tail);
+  }
+}
+
 template <int S, int T, int KW>
 __global__ __launch_bounds__(64 * KW) __attribute__((amdgpu_waves_per_eu(2, 2))) void sweep_split_kernel(SegArgs a) {
   static_assert(T % KW == 0 && (KW == 2 || KW == 4), "levels split evenly over 2 or 4 waves");
@@ -277,26 +319,38 @@ __global__ __launch_bounds__(64 * KW) __attribute__((amdgpu_waves_per_eu(2, 2)))
   // T = 40 pass 7.85-7.88 vs 7.90-7.91 (r03aq_prio.jsonl; MI355X_MICROARCH.md, two waves per
   // SIMD, item 4).
   if (RT_SPLIT_PRIO > 0 && w == RT_SPLIT_PRIO - 1) __builtin_amdgcn_s_setprio(1);
-  if constexpr (KW == 2) {
-    if (w == 0)
-      split_role<S, T, 2, 0>(a, hand, hhead);
-    else
-      split_role<S, T, 2, 1>(a, hand, hhead);
-  } else {
-    if (w == 0)
-      split_role<S, T, 4, 0>(a, hand, hhead);
-    else if (w == 1)
-      split_role<S, T, 4, 1>(a, hand, hhead);
-    else if (w == 2)
-      split_role<S, T, 4, 2>(a, hand, hhead);
-    else
-      split_role<S, T, 4, 3>(a, hand, hhead);
-  }
+  split_roles<S, T, KW, false>(a, hand, hhead, w);
+}
+
+// A pipelined launch whose first active position (pos_lo, vacuum lines only) runs the
+// run's last a.tail_levels < T steps while the positions behind it run whole T blocks: the
+// n mod T remainder rides the drain (one extra launch, for the last position) instead of
+// aligned passes with the cross-segment correction after it.  The tail positions keep T's
+// aggregate layout, so the two kinds share the aggs ring.  Same arithmetic per (cell,
+// level) as every other schedule.
+template <int S, int T, int KW>
+__global__ __launch_bounds__(64 * KW) __attribute__((amdgpu_waves_per_eu(2, 2))) void sweep_split_tail_kernel(
+    SegArgs a) {
+  __shared__ double2 hand[KW - 1][2][split_chunk_cells() * 64];
+  __shared__ double2 hhead[64];
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (RT_SPLIT_PRIO > 0 && w == RT_SPLIT_PRIO - 1) __builtin_amdgcn_s_setprio(1);
+  // The waves that run all their levels take the plain body: with the tail's level count a
+  // runtime bound in the level loop the workgroup ran ~55% slower (the loop's pinned loads
+  // lose their place), which set every drain launch's time (16-group shard, 100 steps: 237
+  // vs 150 ms for 96 steps, gpurun r04ac)
+  split_roles<S, T, KW, true>(a, hand, hhead, w);
 }
 
 template <int T, int KW>
 static hipError_t launch_split_t(const SegArgs &a, int grid, hipStream_t st) {
   hipLaunchKernelGGL((sweep_split_kernel<SCHEME_BDF2, T, KW>), dim3(grid), dim3(64 * KW), 0, st, a);
+  return hipGetLastError();
+}
+
+template <int T, int KW>
+static hipError_t launch_split_tail_t(const SegArgs &a, int grid, hipStream_t st) {
+  hipLaunchKernelGGL((sweep_split_tail_kernel<SCHEME_BDF2, T, KW>), dim3(grid), dim3(64 * KW), 0, st, a);
   return hipGetLastError();
 }
 
@@ -316,6 +370,28 @@ hipError_t launch_split(int T, int waves, const SegArgs &a, int grid, hipStream_
   if (T == t && waves == k) return launch_split_t<t, k>(a, grid, st);
   RT_SPLIT_PAIRS(RT_SPLIT_LAUNCH)
 #undef RT_SPLIT_LAUNCH
+  return hipErrorInvalidValue;
+}
+
+// the planned schedules' blocks (four waves) and two waves up to 16 levels; not (20, 2) and
+// (40, 4): 10 levels per wave with the tail's exit spill (416 B of scratch per lane)
+#define RT_SPLIT_TAIL_PAIRS(X) X(8, 2) X(12, 2) X(16, 2) \
+  X(8, 4) X(12, 4) X(16, 4) X(20, 4) X(24, 4) X(32, 4)
+
+bool split_tail_supported(int T, int waves) {
+#define RT_SPLIT_HAS(t, k) \
+  if (T == t && waves == k) return true;
+  RT_SPLIT_TAIL_PAIRS(RT_SPLIT_HAS)
+#undef RT_SPLIT_HAS
+  return false;
+}
+
+hipError_t launch_split_tail(int T, int waves, const SegArgs &a, int grid, hipStream_t st) {
+  if (a.reflective || a.tail_levels <= 0 || a.tail_levels >= T) return hipErrorInvalidValue;
+#define RT_SPLIT_TAIL_LAUNCH(t, k) \
+  if (T == t && waves == k) return launch_split_tail_t<t, k>(a, grid, st);
+  RT_SPLIT_TAIL_PAIRS(RT_SPLIT_TAIL_LAUNCH)
+#undef RT_SPLIT_TAIL_LAUNCH
   return hipErrorInvalidValue;
 }
 

@@ -234,6 +234,7 @@ struct rt_solver {
   int queued = 0;                // requested steps not yet enqueued (< T)
   long long wqueued = 0;         // requested steps queued for the wavefront kernel (wave_advance)
   int Tpipe = 0;                 // time block of the running pipeline (0: positions aligned)
+  int tail = 0;                  // draining: the run's last steps (< Tpipe), each position's final block
   // material-temperature coupling (rt_material_enable)
   bool material = false;
   double rho_cv = 0.0, wsum = 0.0;
@@ -312,6 +313,18 @@ inline int fill_level_waves(const rt_solver *s, int grid) {
     if (c < cb || (c == cb && k <= within)) best = k;
   }
   return best;
+}
+
+// Waves per segment for a drain launch carrying the run's remainder as a tail block
+// (launch_split_tail; any split is bitwise the same), or 0 when the pipeline cannot:
+// reflective chains (the mu > 0 heads take the mu < 0 outflow), other schemes, blocks
+// without a tail kernel.  complete() takes a tail of at least T / waves steps, so that wave
+// 0 (which streams the rows in) runs the plain body.
+inline int tail_waves(const rt_solver *s, int T) {
+  if (s->scheme != SCHEME_BDF2 || s->p.bc_left_indicator == 2) return 0;
+  for (int k : {4, 2})
+    if (split_tail_supported(T, k)) return k;
+  return 0;
 }
 
 // Chain positions of the pipelined schedule: the Sg segments of a line (both

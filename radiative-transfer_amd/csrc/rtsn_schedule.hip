@@ -181,11 +181,19 @@ static rt_status enqueue_steps(rt_solver *s, int nsteps) {
 // drain it; both happen once per run of advances, and the drain only when a
 // read-out needs the state (finalize).
 // ---------------------------------------------------------------------------
+//
+// The run's n mod T last steps (complete: the queued remainder) can ride the drain as a
+// final block of `tail` < T steps per position (launch_split_tail: vacuum lines, BDF2 split
+// blocks): position c runs it once position c - 1 has, in the launch where position c + 1
+// runs its last whole block -- one launch more than the drain, instead of aligned passes
+// with the cross-segment correction after it.
 static rt_status pipe_launch(rt_solver *s) {
   const int P = chain_positions(s), T = s->Tpipe;
+  const long long end = s->target + s->tail;
+  auto block = [&](int c) { return s->tau[c] < s->target ? T : s->tail; };
   int lo = -1, hi = -1;
   for (int c = 0; c < P; ++c) {
-    const bool ready = s->tau[c] < s->target && (c == 0 || s->tau[c - 1] >= s->tau[c] + T);
+    const bool ready = s->tau[c] < end && (c == 0 || s->tau[c - 1] >= s->tau[c] + block(c));
     if (!ready) continue;
     if (lo < 0) lo = c;
     if (hi >= 0 && hi != c - 1) return fail(s, RT_ERR_PARAM, "pipeline: active positions not contiguous");
@@ -193,7 +201,7 @@ static rt_status pipe_launch(rt_solver *s) {
   }
   if (lo < 0) return fail(s, RT_ERR_PARAM, "pipeline: no position can advance");  // loops below rely on progress
   for (int c = lo; c <= hi; ++c)
-    if (s->tau[c] != s->tau[lo] - static_cast<long long>(c - lo) * T)
+    if (s->tau[c] != s->tau[lo] - static_cast<long long>(c - lo) * T || (c > lo && block(c) != T))
       return fail(s, RT_ERR_PARAM, "pipeline: positions out of step");
   SegArgs a = seg_args(s);
   a.aggs[0] = static_cast<double *>(s->agg[0].p);
@@ -204,13 +212,19 @@ static rt_status pipe_launch(rt_solver *s) {
   a.pass_lo = static_cast<int>(((s->tau[lo] - s->pipe_base) / T) & 1);
   const int grid = (a.reflective ? 1 : 2) * a.npos * s->Q;
   a.level_waves = fill_level_waves(s, grid);
+  a.tail_levels = block(lo) == T ? 0 : s->tail;
   hipEvent_t e1;
   rt_status st = event_begin(s, &e1);
   if (st) return st;
-  HIP_TRY(s, launch_sweep(s->scheme, T, SWEEP_PIPELINED, a, grid, s->stream));
+  if (a.tail_levels) {
+    a.level_waves = tail_waves(s, T);  // (complete: wave 0 runs whole levels)
+    HIP_TRY(s, launch_split_tail(T, a.level_waves, a, grid, s->stream));
+  } else {
+    HIP_TRY(s, launch_sweep(s->scheme, T, SWEEP_PIPELINED, a, grid, s->stream));
+  }
   ++s->state_version;
   if ((st = event_end(s, e1))) return st;
-  for (int c = lo; c <= hi; ++c) s->tau[c] += T;
+  for (int c = lo; c <= hi; ++c) s->tau[c] += block(c);
   return RT_OK;
 }
 
@@ -276,8 +290,15 @@ rt_status rtsn_detail::complete(rt_solver *s) {
   rt_status st;
   if (s->wqueued && (st = wave_flush(s))) return st;
   if (s->Tpipe) {
-    while (s->tau.back() < s->target)
+    const int kw = tail_waves(s, s->Tpipe);
+    if (s->queued && kw && s->queued >= s->Tpipe / kw) {  // the remainder as every position's last block
+      s->tail = s->queued;
+      s->queued = 0;
+    }
+    while (s->tau.back() < s->target + s->tail)
       if ((st = pipe_launch(s))) return st;
+    s->target += s->tail;
+    s->tail = 0;
     s->Tpipe = 0;
   }
   end_plan(s);
@@ -395,9 +416,11 @@ extern "C" rt_status rt_synchronize(rt_solver *s) {
 // positions form a band (ramp up, plateau of min(P, C), ramp down); a launch of W workgroups
 // runs in rounds of the resident 2 per CU, and a round's time is one segment's Ls x T / 4
 // cell-levels per wave at the per-level cost of its block (t_T) times the workgroups the
-// busiest CU holds (ceil(W / CUs): a wave per SIMD each).  n mod T steps more run as aligned
-// passes with the cross-segment correction (~3 steps' cost each, ~3 ms of folds and the
-// finalize on the aligned segmentation; ~30 ms before the fold kept its propagator in LDS).
+// busiest CU holds (ceil(W / CUs): a wave per SIMD each).  n mod T steps more ride the drain as
+// every position's last block (one launch more, pipe_launch) when they are at least T / 4;
+// else, on reflective chains and at T = 40 (whose tail kernel would spill) they run
+// as aligned passes with the cross-segment correction (~3 steps' cost each, ~3 ms of folds
+// and the finalize on the aligned segmentation).
 struct RunGeom {
   long long N;
   int M, Gl, cus;
@@ -444,11 +467,16 @@ static double run_ms_model(const RunGeom &g, long long n, int T, int w) {
     }
     return t + 5e-6;  // + launch
   };
-  const long long m = std::min(P, C);
+  // launch l holds the positions c with 0 <= l - c < P (whole blocks) and, with a remainder
+  // riding the drain, the one at l - c == P (its tail block, counted as a whole position)
+  const bool tail = rem >= T / kw && !g.reflective && split_tail_supported(T, kw);
   double s = 0.0;
-  for (long long a = 1; a < m; ++a) s += 2.0 * launch(a);  // fill and drain ramps
-  s += static_cast<double>(std::max(P, C) - m + 1) * launch(m);
-  if (rem) {
+  for (long long l = 0; l < P + C - 1 + (tail ? 1 : 0); ++l) {
+    long long a = std::min(l + 1, C) - std::max<long long>(0, l - P + 1);
+    if (tail && l >= P && l - P < C) ++a;
+    s += launch(a);
+  }
+  if (rem && !tail) {
     const double step = static_cast<double>(R) * g.N * tf / (4.0 * g.cus);  // one step, every line, full load
     s += rem * 3.0 * step + 0.003;  // + the folds and the finalize (aligned segmentation, LDS fold)
   }

@@ -1,6 +1,7 @@
 """GPU parity of the run schedules on few long lines (round 4): chunked rt_advance calls,
 the deferred start of the pipeline, the aligned schedule's own segmentation and the fold
-with its LDS-resident propagator, and the transient planned schedule.
+with its LDS-resident propagator, the transient planned schedule, and the run's n mod T
+remainder riding the pipeline's drain as a tail block.
 
 Geometry: llnl_slab_test's material and tabulated opacities resampled to 4 groups, M = 2
 (8 lines), N = 5000 or 50000 cells, dt = 1e-9 -- lines beyond the wavefront chain's 4096
@@ -103,3 +104,49 @@ def test_solve_plan_is_transient(rtsn_mod, oracle_mod):
         assert (gpu.time_block, gpu.level_waves) == (tb0, lw0)
         gpu.advance(10)
         compare_all(gpu, _oracle(oracle_mod, dict(p, max_timesteps=74)))
+
+
+@pytest.mark.parametrize("T,waves,steps,bc_right", [(8, 4, 100, 0), (8, 1, 99, 0), (16, 2, 37, 1), (20, 4, 47, 0),
+                                                    (12, 4, 30, 1), (32, 4, 119, 0)])
+def test_pipelined_tail_bitwise(rtsn_mod, oracle_mod, T, waves, steps, bc_right):
+    """The pipelined run's last steps mod T as every position's final block in the drain
+    (launch_split_tail: the first active position runs `tail` < T levels while the ones
+    behind it run whole blocks): the node array equals the wavefront's -- the exact
+    sequential order, bitwise -- from a random state (3000 cells, 4 groups, M = 6).  Tails
+    of at least T / 4 steps ride the drain (the launch takes four waves, whatever the run's
+    split: T = 8 on one wave here); shorter ones run as aligned passes after it."""
+    from test_wavefront_gpu import _params as wparams, _random_ends
+    p, q = wparams(oracle_mod, 3000, 3, 0, bc_right, dt=1e-9)
+    lo, hi = 40, 44
+    B = oracle_mod.OracleSolver(p, g_lo=lo, g_hi=hi).groups()["B"][lo:hi]
+    ends0 = _random_ends(q, lo, hi, B, 1234 + T + steps)
+    out = {}
+    for wave in (2, 0):
+        with rtsn_mod.Solver(q, g_lo=lo, g_hi=hi) as s:
+            s.wavefront = wave
+            if wave == 0:
+                s.pipeline = 2
+                s.time_block = T
+                s.level_waves = waves
+            s.set_ends(ends0)
+            s.advance(steps)
+            if wave == 0:
+                st = s.pipeline_state()
+                assert st["queued_steps"] == steps % T and st["lag_steps"] > 0  # pipelined, remainder queued
+            out[wave] = s.ends()
+            if wave == 0:
+                assert s.pipeline_state()["queued_steps"] == 0
+    assert np.isfinite(out[0]).all()
+    assert np.array_equal(out[2], out[0])
+
+
+def test_solve_remainder_tail(rtsn_mod, oracle_mod):
+    """rt_solve of 100 steps on 50000 cells x 4 groups (the plan's block does not divide
+    100): the remainder rides the drain; every field against the oracle."""
+    p = _params(oracle_mod, 50000, 100)
+    orc = _oracle(oracle_mod, p)
+    with rtsn_mod.Solver(to_rt(p)) as gpu:
+        plan = gpu.plan_schedule(100)
+        assert 100 % plan["time_block"], plan
+        gpu.solve()
+        compare_all(gpu, orc)
