@@ -128,8 +128,9 @@ rt_status rt_solve(rt_solver *s);
  * the time block (8..40 steps), waves per segment (4) and segments sized for wgs_per_cu
  * workgroups per CU (4..32) with the least estimated whole-run time -- a model of the run
  * as P = n / T passes over the chain of segments (fill ramp, plateau, drain ramp; each
- * launch in rounds of the resident workgroups) plus the n mod T remainder as aligned
- * passes -- and that estimate.  Host arithmetic only; any NULL skipped. */
+ * launch in rounds of the resident workgroups) plus the n mod T remainder (on vacuum
+ * lines, at least T / 4 steps: a tail block riding the drain, one launch more; else aligned
+ * passes) -- and that estimate.  Host arithmetic only; any NULL skipped. */
 rt_status rt_plan_schedule(rt_solver *s, long long nsteps, int *steps_per_pass, int *level_waves, int *wgs_per_cu,
                            double *estimated_ms);
 /* The time block rt_plan_schedule picks on the SL slab's geometry (N = 1e6 cells, S64, 128
@@ -144,7 +145,9 @@ rt_status rt_plan_time_block(int ts_method, long long nsteps, int *steps_per_pas
  * a run is cut into rt_advance calls. */
 rt_status rt_advance(rt_solver *s, int nsteps);
 /* Enqueue what brings the stored state exactly to the requested time --
- * pipeline drain, queued remainder steps, pending correction.  Every
+ * pipeline drain (with the queued remainder as each position's last block where the
+ * pipeline can: vacuum lines, at least T / 4 steps), queued remainder steps as aligned
+ * passes otherwise, pending correction.  Every
  * read-out does this implicitly; asynchronous. */
 rt_status rt_finish(rt_solver *s);
 rt_status rt_synchronize(rt_solver *s);
