@@ -23,9 +23,13 @@ step (4 substeps) of every cell x angle x group of the GPU's groups, i.e.
 4 M G N cell-angle-group updates, computed in fp64 by the fused HIP sweep.
 State is resident in HBM before timing.
 
-Multi-GPU: one process per GPU (torch.distributed.run), groups sharded across
+Multi-GPU: one process per GPU, groups sharded across
 ranks with no collective in the data path (groups are independent for the
-whole run: T is constant).  strong scaling (default, the north_star's "same
+whole run: T is constant).  Launch: under torch.distributed.run (WORLD_SIZE set; it must
+equal --gpus), or plain `python bench.py --gpus N`, where this process -- which never
+touches the GPU -- starts the N rank processes itself (spawn_ranks: fresh interpreters with
+RANK / LOCAL_RANK / WORLD_SIZE / MASTER_*), relays rank 0's JSON line and fails if any rank
+fails.  strong scaling (default, the north_star's "same
 slab"): the 128 groups are split N ways (16 per GPU at N = 8); weak: every
 rank owns 128 groups of a 128*N-group grid.  Timing:
 barrier + device synchronise on both sides of the K timed steps, max over
@@ -781,6 +785,100 @@ def run_material(p: dict, info, world: int, device, local: int, steps: int, dirs
             "state_finite": bool(np.isfinite(T).all())}
 
 
+def launch_mode(gpus: int, env) -> str:
+    """How this process runs the job: "rank" (it is one of the ranks: WORLD_SIZE is set by a
+    launcher, or a one-GPU run without one) or "spawn" (no launcher and --gpus > 1: start the
+    ranks).  A launcher's WORLD_SIZE that differs from --gpus is an error: the line would
+    report a GPU count other than the one asked for."""
+    if gpus < 1:
+        raise ValueError(f"--gpus {gpus}: at least one GPU")
+    ws = env.get("WORLD_SIZE")
+    if ws is None:
+        return "spawn" if gpus > 1 else "rank"
+    if int(ws) != gpus:
+        raise ValueError(f"WORLD_SIZE={ws} from the launcher but --gpus {gpus}")
+    return "rank"
+
+
+def _free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def spawn_ranks(n: int, argv, script=None, env=None, grace_s: float = 20.0) -> int:
+    """Start n rank processes of `script` (default: this file) with `argv`, one per GPU
+    (LOCAL_RANK r -> cuda:r), rendezvous on 127.0.0.1 at a free port.  Each child is a fresh
+    interpreter started by fork+exec from this process, which has not initialised the GPU (it
+    imports neither torch nor librtsn).  Rank 0's stdout is relayed line by line; the other
+    ranks' output and every stderr pass through.  When a rank exits non-zero the others are
+    terminated (their own PIDs: SIGTERM, then SIGKILL after grace_s) and that status is
+    returned; 0 when all ranks succeed and rank 0 printed a JSON line whose n_gpus is n."""
+    import signal
+    import subprocess
+    import threading
+    script = str(script or Path(__file__).resolve())
+    base = dict(os.environ if env is None else env)
+    base.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), WORLD_SIZE=str(n),
+                LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0", RTSN_BENCH_LAUNCHER=f"bench.py --gpus {n} (child processes)")
+    procs = []
+    lines = []
+
+    def relay(stream):
+        for ln in stream:
+            sys.stdout.write(ln)
+            sys.stdout.flush()
+            if ln.startswith("{"):
+                lines.append(ln)
+
+    def stop_all(*_):
+        for q in procs:
+            if q.poll() is None:
+                q.terminate()
+        t_end = time.time() + grace_s
+        for q in procs:
+            try:
+                q.wait(timeout=max(0.1, t_end - time.time()))
+            except subprocess.TimeoutExpired:
+                q.kill()
+                q.wait()
+
+    old_term = signal.signal(signal.SIGTERM, lambda *a: (stop_all(), sys.exit(143)))
+    try:
+        for r in range(n):
+            e = dict(base, RANK=str(r), LOCAL_RANK=str(r))
+            procs.append(subprocess.Popen([sys.executable, "-u", script, *argv], env=e,
+                                          stdout=subprocess.PIPE if r == 0 else None, text=True))
+        reader = threading.Thread(target=relay, args=(procs[0].stdout,), daemon=True)
+        reader.start()
+        status = 0
+        while [q.poll() for q in procs].count(None):
+            bad = [q.returncode for q in procs if q.returncode not in (None, 0)]
+            if bad:
+                status = bad[0]
+                print(f"bench.py: a rank exited with status {status}; stopping the others", file=sys.stderr)
+                stop_all()
+                break
+            time.sleep(0.2)
+        reader.join(timeout=30)
+        if status == 0:
+            bad = [q.returncode for q in procs if q.returncode != 0]
+            status = bad[0] if bad else 0
+        if status == 0:
+            try:
+                got = json.loads(lines[-1]).get("n_gpus") if lines else None
+            except ValueError:
+                got = None
+            if got != n:
+                print(f"bench.py: rank 0 reported n_gpus={got}, expected {n}", file=sys.stderr)
+                status = 1
+        return status if status > 0 else (128 - status if status < 0 else 0)
+    finally:
+        stop_all()
+        signal.signal(signal.SIGTERM, old_term)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -812,6 +910,13 @@ def main():
     ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl", help=argparse.SUPPRESS)
     ap.add_argument("--share-device", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
+    try:
+        mode = launch_mode(args.gpus, os.environ)
+    except ValueError as e:
+        print(f"bench.py: {e}", file=sys.stderr)
+        sys.exit(2)
+    if mode == "spawn":  # no launcher: this process starts the ranks and touches no GPU
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
 
     import torch
     import torch.distributed as dist
@@ -856,6 +961,15 @@ def main():
     # on N > 1 GPUs, the material leg's per-step all-reduce)
     comm, comm_error = (open_comm(world, rank, local, device) if (world > 1 or args.material_steps > 0)
                         else (None, None))
+    # environment variables the library or this script reads (test and diagnostic hooks):
+    # reported so that a run under any of them is visible in its line
+    line["rtsn_env"] = {k: v for k, v in sorted(os.environ.items()) if k.startswith("RTSN_")}
+    line["launcher"] = os.environ.get("RTSN_BENCH_LAUNCHER", "torch.distributed.run" if world > 1 else "none")
+    if comm is not None:
+        try:
+            line["rccl_nranks"] = comm.count  # ncclCommCount behind the C ABI
+        except rtsn.RtError as e:
+            line["rccl_nranks"] = f"rt_comm_count failed: {e}"
     if world > 1:
         if comm is not None:
             try:

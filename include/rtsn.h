@@ -260,7 +260,7 @@ rt_status rt_set_wavefront(rt_solver *s, int mode);
 rt_status rt_get_wavefront(rt_solver *s, int *mode, int *active, int *cells_per_lane);
 /* Waves a wavefront chain may span, 1..8 (default 8; 1 = one wave per chain, lines of up to
  * 512 cells).  The chain's lanes per line are ceil(N / C); replaces nothing in the reference
- * (its sweep is serial, solver.cpp:700-717).  RTSN_WAVE_WAVES=1..8 at creation sets it. */
+ * (its sweep is serial, solver.cpp:700-717). */
 rt_status rt_set_wavefront_waves(rt_solver *s, int max_waves);
 /* *max_waves as set; *waves_per_chain: this handle's chain (0: too long).  NULLs skipped. */
 rt_status rt_get_wavefront_waves(rt_solver *s, int *max_waves, int *waves_per_chain);
@@ -270,9 +270,10 @@ rt_status rt_get_wavefront_waves(rt_solver *s, int *max_waves, int *waves_per_ch
  * AGPRs; the split one measured 2.7% faster on SL), 1 otherwise (at T = 16 one wave is
  * 4% faster), and with 0 the pipeline's fill and drain launches split
  * further (up to 4 waves) while the chip would idle.  T = 24, 32, 40 always run 4
- * waves.  rt_get_level_waves reports the effective choice for the current time block;
- * RTSN_LEVEL_WAVES=1|2|4 at creation forces one.  Bitwise-identical results.  Other
- * schemes always use one wave. */
+ * waves.  rt_get_level_waves reports the effective choice for the current time block.
+ * The choice covers whole blocks: a run's remainder block riding the drain (rt_plan_schedule)
+ * always takes the tail kernel with the most waves for T (4, else 2), whatever is set here.
+ * Bitwise-identical results.  Other schemes always use one wave. */
 rt_status rt_set_level_waves(rt_solver *s, int waves);
 /* Segments per line: sized so a pipelined launch with every segment active holds
  * wgs_per_cu workgroups per CU (1..64), or 0 (default) for the pass kernel's occupancy.
@@ -334,11 +335,13 @@ rt_status rt_get_cell_planck(rt_solver *s, double *B);
  * the handle's stream (RCCL over xGMI) and, where it returns host arrays, synchronises.
  * Shards must be all group shards that tile [0, G) in rank order, or all direction
  * shards of the same groups that tile [0, M/2) in rank order (else RT_ERR_PARAM).
- * No call waits unboundedly: the communicator is non-blocking and every wait on it (the
- * init, a collective call in progress, the host synchronisations of the gathers) has a
- * deadline of RTSN_COMM_TIMEOUT_S seconds (default 300).  On expiry -- a rank missing or
- * stalled -- the communicator is aborted, the call returns RT_ERR_TIMEOUT and later
- * collectives on it RT_ERR_STATE. */
+ * No wait on a peer is unbounded: the communicator is non-blocking and every wait on it
+ * (the init, a collective call in progress, the host synchronisations of the gathers) has
+ * a deadline of RTSN_COMM_TIMEOUT_S seconds (default 300) per collective, clocked from the
+ * moment the stream reaches that collective: the handle's own work queued before it (a long
+ * rt_advance, the sweeps of rt_comm_material_step) is waited for without the deadline.  On
+ * expiry -- a rank missing or stalled -- the communicator is aborted, the call returns
+ * RT_ERR_TIMEOUT and later collectives on it RT_ERR_STATE. */
 typedef struct rt_comm rt_comm;
 #define RT_COMM_ID_BYTES 128
 /* ncclGetUniqueId: on one rank, then handed to every rank (file, pipe, MPI, ...). */
@@ -348,6 +351,9 @@ rt_status rt_comm_unique_id(void *id);
 rt_status rt_comm_init(int nranks, int rank, const void *id, int device, rt_comm **out);
 void rt_comm_destroy(rt_comm *c);
 rt_status rt_comm_rank(rt_comm *c, int *nranks, int *rank);
+/* ncclCommCount: the number of ranks RCCL itself reports for the communicator (equal to
+ * rt_comm_init's nranks once it formed). */
+rt_status rt_comm_count(rt_comm *c, int *count);
 /* phi, F, phi_plus of ALL groups (G x N each, g + G c; NULL skipped; host, every rank):
  * group shards are gathered, direction shards summed (the reference's sequential sum
  * over i regrouped by shard: rounding only). */

@@ -82,17 +82,18 @@ __global__ __launch_bounds__(64) void fold_kernel(FoldArgs f) {
   const double *ag = f.agg + static_cast<size_t>(half) * f.Sg * seg_stride + ell0;
   const double *pr = f.prop + static_cast<size_t>(half) * f.prop_half * stride + ell0;
   double *y = f.y + static_cast<size_t>(half) * (f.Sg + 1) * seg_stride + ell0;
-  const __amdgpu_buffer_rsrc_t Rp = fold_rsrc(pr, static_cast<size_t>(2 * NTC) * rb);
   const auto seg = [&](const double *base, long long s) {  // segment s's KC rows
     return fold_rsrc(base + static_cast<size_t>(s) * seg_stride, static_cast<size_t>(KC) * rb);
   };
-  // a propagator (at coefficient offset o) into LDS, kFoldChunk pairs at a time
+  // a propagator (at coefficient offset o) into LDS, kFoldChunk pairs at a time; each pair of
+  // coefficient rows through its own descriptor (64-bit base), so no offset exceeds 2 rows --
+  // 2 NTC rows of a whole propagator overflow a 32-bit offset from ~640k lines on (KC = 20)
   const auto stage = [&](int o) {
 #pragma unroll
     for (int q = 0; q < NP; ++q) {
       if (q % kFoldChunk == 0) __builtin_amdgcn_sched_barrier(0);
-      lds_p[q * 64 + lane] = make_double2(fold_load(Rp, voff, (o + 2 * q) * rb),
-                                          2 * q + 1 < NTC ? fold_load(Rp, voff, (o + 2 * q + 1) * rb) : 0.0);
+      const __amdgpu_buffer_rsrc_t Rq = fold_rsrc(pr + static_cast<size_t>(o + 2 * q) * stride, 2 * static_cast<size_t>(rb));
+      lds_p[q * 64 + lane] = make_double2(fold_load(Rq, voff, 0), 2 * q + 1 < NTC ? fold_load(Rq, voff, rb) : 0.0);
     }
   };
   if (f.Sg > 1) stage(0);

@@ -7,9 +7,6 @@
 #include "kernels.hpp"
 #include "sweep_device.hpp"
 
-#ifndef RT_SPLIT_BIAS
-#define RT_SPLIT_BIAS 0
-#endif
 #ifndef RT_SPLIT_PIN_LOADS
 #define RT_SPLIT_PIN_LOADS 1
 #endif
@@ -101,21 +98,29 @@ __device__ __forceinline__ void split_chunk(const double *W, double (&ein)[C], d
   }
 }
 
+// Wave w of KW runs levels [split_t0, split_t0 + split_tw) of the T: split_role and the choice
+// of its TAIL body (split_role_of) take both from here.
+template <int T, int KW, int w>
+__device__ __forceinline__ constexpr int split_t0() {
+  return w * (T / KW);
+}
+template <int T, int KW, int w>
+__device__ __forceinline__ constexpr int split_tw() {
+  return T / KW;
+}
+
 // Wave w's role (compile time: with the role a runtime branch inside one body the
 // allocation measured ~340 registers, each role alone ~215).
 template <int S, int T, int KW, int w, bool TAIL>
 __device__ __forceinline__ void split_role(const SegArgs &a, double2 (*hand)[2][split_chunk_cells() * 64],
                                            double2 *hhead) {
   constexpr int K = SchemeDim<S>::K;
-  // levels [t0, t0 + TW); two waves: RT_SPLIT_BIAS levels moved from wave 0 (which also
-  // streams the rows in) to wave 1 (timing experiments; 0 = even)
-  constexpr int bias = KW == 2 ? RT_SPLIT_BIAS : 0;
-  constexpr int TW = T / KW + (w == 0 ? -bias : (w == 1 ? bias : 0));
+  constexpr int TW = split_tw<T, KW, w>();  // levels [t0, t0 + TW)
   constexpr int WN = map_count<S>();
   constexpr int C = split_chunk_cells();
   constexpr bool IN = w == 0, OUT = w == KW - 1;
   const int lane = threadIdx.x & 63;
-  constexpr int t0 = w * (T / KW) - (w == 1 ? bias : 0);  // this wave's first level
+  constexpr int t0 = split_t0<T, KW, w>();  // this wave's first level
   const size_t stride = static_cast<size_t>(a.Lpad);
   int half, s, q, pos;
   if (a.reflective) {
@@ -273,12 +278,13 @@ __device__ __forceinline__ void split_role(const SegArgs &a, double2 (*hand)[2][
 #ifndef RT_SPLIT_PRIO
 #define RT_SPLIT_PRIO 1  // 1 + the wave given issue priority 1; 0: none (timing experiments)
 #endif
-// Wave w's role; with `tail`, the waves whose levels reach past the tail's (levels >= t0 +
-// nl) take the TAIL body, the others the plain one.
+// Wave w's role; with `tail`, the waves whose levels reach past the tail's take the TAIL body,
+// the others the plain one -- correct only when wave 0's levels all lie inside the tail
+// (tail_levels >= split_tw of wave 0), which launch_split_tail enforces.
 template <int S, int T, int KW, int w>
 __device__ __forceinline__ void split_role_of(const SegArgs &a, double2 (*hand)[2][split_chunk_cells() * 64],
                                               double2 *hhead, bool tail) {
-  if (tail && a.tail_levels < (w + 1) * (T / KW))
+  if (tail && a.tail_levels < split_t0<T, KW, w>() + split_tw<T, KW, w>())
     split_role<S, T, KW, w, true>(a, hand, hhead);
   else
     split_role<S, T, KW, w, false>(a, hand, hhead);
@@ -387,7 +393,8 @@ bool split_tail_supported(int T, int waves) {
 }
 
 hipError_t launch_split_tail(int T, int waves, const SegArgs &a, int grid, hipStream_t st) {
-  if (a.reflective || a.tail_levels <= 0 || a.tail_levels >= T) return hipErrorInvalidValue;
+  // the tail must cover wave 0's levels: its plain body runs them all (split_role_of)
+  if (a.reflective || waves < 1 || a.tail_levels < T / waves || a.tail_levels >= T) return hipErrorInvalidValue;
 #define RT_SPLIT_TAIL_LAUNCH(t, k) \
   if (T == t && waves == k) return launch_split_tail_t<t, k>(a, grid, st);
   RT_SPLIT_TAIL_PAIRS(RT_SPLIT_TAIL_LAUNCH)

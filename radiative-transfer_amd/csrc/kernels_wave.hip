@@ -14,14 +14,10 @@
 // produced one tick earlier.  n steps of an L-lane chain take n + L - 1 ticks of C cell
 // maps each; the state is read once and written once per launch.
 //
-// A chain longer than one wave (up to kWaveMaxWaves waves) crosses wave boundaries through
-// LDS: wave w runs a block of ticks (plus the read-ahead) behind wave w - 1, lane 63 of wave
-// w - 1 appends its exit state to a ring in LDS every tick, and lane 0 of wave w takes it --
-// one tick after it was produced in chain time, a block of ticks later in wall time -- as the
-// `old` operand of its DPP shifts.  The waves meet at one barrier per block of ticks (not per
-// tick).  The coupling costs ~160-200 cycles per tick, so lines that fit one wave at up to 4
-// cells per lane stay on one wave (wavefront_plan); longer lines -- up to 4096 cells, which
-// used to fall to the segment pipeline's launch per segment position -- run as chains.
+// A chain longer than one wave (up to kWaveMaxWaves waves, 4096 cells) runs on chain_kernel
+// below: the waves of one workgroup hand the carried state over through an LDS ring and meet
+// at a barrier every kChainBlock ticks.  Which lines take one wave and which a chain is
+// wavefront_plan's choice, from measured tick costs (profiles/r05*_plan.jsonl).
 //
 // Same arithmetic per (cell, level) as the pipelined segment pass (the per-line affine map
 // of cell.hpp, exact carries; the reflective mu > 0 head cell by the reference's algebra
@@ -49,25 +45,6 @@ __device__ __forceinline__ double lane_shift_up(double old, double v) {
   return __builtin_bit_cast(double, (static_cast<unsigned long long>(static_cast<unsigned int>(hi)) << 32) |
                                         static_cast<unsigned int>(lo));
 }
-
-// Chain hand-over between waves (MULTI).  Lane 63 of wave w - 1 stores its exit state of
-// chain tick s in ring slot s (during its tick s + 1, after that tick's shifts, so that no
-// wait for a ring read ever waits on a fresh store); lane 0 of wave w reads slot s
-// kWavePrefetch ticks before it needs it (at tick s + 1), so the LDS latency hides behind
-// whole ticks of FMAs.  The waves of a chain meet at a barrier every B = kWaveBlockTicks
-// ticks of wall time (one tick stream per wave, the barrier inside it), and wave w runs
-// kWaveSkew = B + kWavePrefetch chain ticks behind wave w - 1: every slot a wave reads in a
-// block was stored in an earlier block; 4 blocks of slots keep a block's stores clear of
-// the slots still to be read.
-#ifndef RT_WAVE_PREFETCH
-#define RT_WAVE_PREFETCH 2
-#endif
-constexpr int kWavePrefetch = RT_WAVE_PREFETCH;
-constexpr int kWaveSkew = kWaveBlockTicks + kWavePrefetch;
-constexpr int kWaveRing = 4 * kWaveBlockTicks;
-static_assert((kWaveBlockTicks & (kWaveBlockTicks - 1)) == 0 && (kWaveRing & (kWaveRing - 1)) == 0,
-              "block and ring indices are masks");
-static_assert(kWavePrefetch >= 1 && kWaveSkew + kWaveBlockTicks + 1 <= kWaveRing, "ring too short for the skew");
 
 // Ticks per loop iteration of the single-wave kernel (even; timing experiments: RT_WAVE_UNROLL)
 #ifndef RT_WAVE_UNROLL
@@ -112,20 +89,16 @@ __device__ unsigned long long g_block_stamps[kWaveMaxWaves * kBlockStamps * 2];
 
 // grid: one workgroup per line (mu < 0 lines then mu > 0 lines, ell < H Gl) -- or, PAIR (the
 // reflective left boundary), one per line pair ell (chain lanes [0, Lw) the mu < 0 line,
-// [Lw, 2 Lw) its mirror).  Lw = lanes per line = ceil(N / C); the chain's lanes fill
-// blockDim.x / 64 waves (MULTI; one wave otherwise).  nsteps full steps from the stored
-// state.  Padding cells (the last lane of a line holds N mod C real cells) feed nothing
-// real -- except, with PAIR and N mod C != 0 (PAD), those of the mu < 0 line, whose exit
+// [Lw, 2 Lw) its mirror).  Lw = lanes per line = ceil(N / C); the chain fills one wave.
+// nsteps full steps from the stored state.  Padding cells (the last lane of a line holds
+// N mod C real cells) feed nothing real -- except, with PAIR and N mod C != 0 (PAD), those of the mu < 0 line, whose exit
 // state is the mirror head's inflow: there they pass X through by a select (a per-lane
 // branch would make every tick divergent).
-template <int S, int C, bool PAIR, bool PAD, bool MULTI>
-__global__ __launch_bounds__(MULTI ? 64 * kWaveMaxWaves : 64) void wavefront_kernel(SegArgs a, int nsteps, int Lw) {
+template <int S, int C, bool PAIR, bool PAD>
+__global__ __launch_bounds__(64) void wavefront_kernel(SegArgs a, int nsteps, int Lw) {
   constexpr int K = SchemeDim<S>::K, WN = map_count<S>();
   RT_STAMP(0);
-  const int lane = threadIdx.x & 63;
-  const int w = MULTI ? __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6)) : 0;
-  const int nw = MULTI ? static_cast<int>(blockDim.x >> 6) : 1;
-  const int g = w * 64 + lane;  // chain lane
+  const int g = threadIdx.x & 63;  // chain lane
   const int nl = a.H * a.Gl;
   int half, ell, j;
   if (PAIR) {
@@ -182,62 +155,29 @@ __global__ __launch_bounds__(MULTI ? 64 * kWaveMaxWaves : 64) void wavefront_ker
 #pragma unroll
     for (int r = 0; r < K; ++r) X[r] = Xin[r];
   }
-  // MULTI: rd = where lane 0 of this wave takes its `old` operands -- wave 0 a fixed slot
-  // holding the head's inflow state (mask 0), wave w the ring of boundary w - 1
-  extern __shared__ double lds_ring[];
-  const double *rd = lds_ring;
-  double *wr = lds_ring;
-  int rd_mask = 0;
-  if constexpr (MULTI) {
-    if (threadIdx.x < K) lds_ring[threadIdx.x] = Xin[threadIdx.x];
-    for (int i = threadIdx.x; i < (nw - 1) * kWaveRing * K; i += blockDim.x) lds_ring[K + i] = 0.0;
-    rd = w == 0 ? lds_ring : lds_ring + K + static_cast<size_t>(w - 1) * kWaveRing * K;
-    rd_mask = w == 0 ? 0 : kWaveRing - 1;
-    wr = lds_ring + K + static_cast<size_t>(w) * kWaveRing * K;
-    __syncthreads();
-  }
-  const bool writer = MULTI && lane == 63 && w < nw - 1;
   // the ticks between the chain's fill and drain (every lane of this wave at a level in
   // [1, nsteps)) run without the commit masks, and there component 0 of the received state
   // (the upwind cell's node before level t, which the map copies from dout) is not shifted
   // in: it is the upwind cell's output node of level t - 1, which this lane received one
   // tick earlier as component K - 1 (CN, BDF2; the chain head's inflow state has equal
   // components) -- one DPP lane shift fewer per tick
-  const auto publish = [&](int tick) {  // MULTI: lane 63's exit state of chain tick `tick`
-#pragma unroll
-    for (int r = 0; r < K; ++r) wr[(tick & (kWaveRing - 1)) * K + r] = X[r];
-  };
-  // MULTI: lane 0's received states for the next kWavePrefetch ticks (nxt[0]: this tick's),
-  // carried along the wave's whole tick stream; wave w's chain tick `tick` runs at wall tick
-  // tick + w kWaveSkew, and a barrier follows every wall tick B - 1 mod B
-  double nxt[kWavePrefetch][K];
-  const int wskew = w * kWaveSkew;
   const auto run = [&](int tick0, int tick1, auto masked) {
     const auto body = [&](int tick) {
       double o[K];
 #pragma unroll
-      for (int r = 0; r < K; ++r) o[r] = MULTI ? nxt[0][r] : Xin[r];
+      for (int r = 0; r < K; ++r) o[r] = Xin[r];
       if constexpr (K > 1 && !decltype(masked)::value) {
         // the shift of component K - 1 keeps Xin[0] as its `old` (lane 0 of the chain: the
         // head's inflow state, all of whose components are equal), so the two registers trade
         // roles each tick and two ticks per iteration need no copy
         const double x0 = Xin[K - 1];
-        Xin[K - 1] = lane_shift_up(MULTI ? o[K - 1] : Xin[0], X[K - 1]);
+        Xin[K - 1] = lane_shift_up(Xin[0], X[K - 1]);
 #pragma unroll
         for (int r = 1; r < K - 1; ++r) Xin[r] = lane_shift_up(o[r], X[r]);
         Xin[0] = x0;
       } else {
 #pragma unroll
         for (int r = 0; r < K; ++r) Xin[r] = lane_shift_up(o[r], X[r]);
-      }
-      if constexpr (MULTI) {  // after the shifts, which wait for an earlier tick's read
-        if (writer && tick > 0) publish(tick - 1);  // X: the previous tick's exit state
-#pragma unroll
-        for (int q = 0; q + 1 < kWavePrefetch; ++q)
-#pragma unroll
-          for (int r = 0; r < K; ++r) nxt[q][r] = nxt[q + 1][r];
-#pragma unroll
-        for (int r = 0; r < K; ++r) nxt[kWavePrefetch - 1][r] = rd[((tick + kWavePrefetch - 1) & rd_mask) * K + r];
       }
       bool active = true;
       if constexpr (decltype(masked)::value) {
@@ -273,9 +213,6 @@ __global__ __launch_bounds__(MULTI ? 64 * kWaveMaxWaves : 64) void wavefront_ker
         ein[c] = active ? oi : ein[c];
         eout[c] = active ? oo : eout[c];
       }
-      if constexpr (MULTI) {
-        if (((tick + wskew) & (kWaveBlockTicks - 1)) == kWaveBlockTicks - 1) __syncthreads();
-      }
     };
     // kWaveUnroll (even) ticks per iteration: the loop-carried renames of X, ein and eout
     // then cancel
@@ -287,20 +224,8 @@ __global__ __launch_bounds__(MULTI ? 64 * kWaveMaxWaves : 64) void wavefront_ker
     for (; tick < tick1; ++tick) body(tick);
   };
   const int ticks = nsteps + used - 1;
-  // this wave's unmasked chain ticks: its real lanes all at a level in [1, nsteps)
-  const int u_lo = min(64 * w + 63, used - 1) + 1, u_hi = max(u_lo, nsteps + 64 * w);
-  int barriers = 0;  // MULTI: the same count for every wave
-  if constexpr (MULTI) {
-    const int total = (ticks + (nw - 1) * kWaveSkew + kWaveBlockTicks - 1) / kWaveBlockTicks;
-    barriers = total - wskew / kWaveBlockTicks;
-    for (int i = 0; i < wskew / kWaveBlockTicks; ++i) __syncthreads();  // wall ticks before the chain's
-#pragma unroll
-    for (int q = 0; q < kWavePrefetch; ++q)
-#pragma unroll
-      for (int r = 0; r < K; ++r) nxt[q][r] = rd[((q - 1) & rd_mask) * K + r];
-    // barriers inside the stream: wall ticks wskew .. wskew + ticks - 1 that are B - 1 mod B
-    barriers -= (wskew + ticks) / kWaveBlockTicks - wskew / kWaveBlockTicks;
-  }
+  // the unmasked ticks: every real lane at a level in [1, nsteps)
+  const int u_lo = min(63, used - 1) + 1, u_hi = max(u_lo, nsteps);
   RT_STAMP(1);
   if (u_lo < u_hi && u_hi <= ticks) {
     run(0, u_lo, std::true_type{});
@@ -310,7 +235,6 @@ __global__ __launch_bounds__(MULTI ? 64 * kWaveMaxWaves : 64) void wavefront_ker
     run(0, ticks, std::true_type{});
   }
   RT_STAMP(2);
-  for (int i = 0; i < barriers; ++i) __syncthreads();  // MULTI: wall ticks after the chain's
 #pragma unroll
   for (int c = 0; c < C; ++c) {
     const int k = j * C + c;
@@ -319,12 +243,11 @@ __global__ __launch_bounds__(MULTI ? 64 * kWaveMaxWaves : 64) void wavefront_ker
 }
 
 // ---------------------------------------------------------------------------
-// Chains over several waves, round 4 (chain_kernel).  Round 3's MULTI path of
-// wavefront_kernel ran ~75 instructions per tick against the single wave's 37: the compiler
-// turned its runtime ring indices, the per-tick barrier test, the writer's branch and the
-// rotating prefetch registers into SALU address arithmetic, exec-mask branches, a copy of
-// every DPP `old` operand into the DPP's destination and ~6.5 register-rotation moves per
-// tick -- the "160-200 cycles of cross-wave coupling" (DESIGN.md §2).  Here every wave runs
+// Chains over several waves (chain_kernel, round 4).  Round 3's chain (a multi-wave path of
+// wavefront_kernel, removed in round 5) ran ~75 instructions per tick against the single
+// wave's 37: runtime ring indices, a per-tick barrier test, the writer's branch and rotating
+// prefetch registers became SALU address arithmetic, exec-mask branches and register moves
+// (DESIGN.md §2.7).  Here every wave runs
 // its tick stream in blocks of kChainBlock wall ticks that end in the barrier, so inside a
 // block every ring slot is a compile-time offset from one per-block base: wave w runs
 // kChainSkew = 2 blocks of chain ticks behind wave w - 1, so the chain tick of a block's
@@ -343,9 +266,6 @@ constexpr int kChainBlock = 8;                 // wall ticks per barrier block
 constexpr int kChainSkew = 2 * kChainBlock;    // chain ticks wave w runs behind wave w - 1
 constexpr int kChainRing = 4 * kChainBlock;    // slots per boundary (and region 0)
 constexpr int kChainSlot = 6;                  // doubles per slot (48 B: 16-byte aligned)
-#ifndef RT_CHAIN_EARLY
-#define RT_CHAIN_EARLY 1  // ring stores and reads issued before the tick's FMAs (0: round 4's first order)
-#endif
 #ifndef RT_CHAIN_MASKED_UNROLL
 #define RT_CHAIN_MASKED_UNROLL 1  // masked blocks (a wave's fill and drain ramps) unrolled too (2-6%: r04r)
 #endif
@@ -520,7 +440,6 @@ __global__ __launch_bounds__(64 * (WIDE ? kWaveMaxWaves : 4)) void chain_kernel(
 #pragma unroll
         for (int r = 1; r < K - 1; ++r) Xin[r] = lane_shift_up(nx[r], X[r]);
         Xin[0] = x0;
-#if RT_CHAIN_EARLY
         // the ring traffic of this tick goes out before its FMAs: the stores of the exit
         // states computed so far in the block (the previous tick's, or the previous two in
         // one branch below 4 cells per lane), then the read of slot t + 1.  The next tick's
@@ -546,24 +465,6 @@ __global__ __launch_bounds__(64 * (WIDE ? kWaveMaxWaves : 4)) void chain_kernel(
           if constexpr (C < 4) write_slot(wb + i * kChainSlot, prev, false);
           write_slot(wn, X, false);
         }
-#else
-        // the next tick's ring values (slot t + 1), after this tick's shifts
-        read_slot(i + 1 < kChainBlock ? rb + (i + 1) * kChainSlot : rn, nx, false);
-#pragma unroll
-        for (int r = 0; r < K; ++r) X[r] = Xin[r];
-        cells(true);
-        if constexpr (C >= 4) {  // a tick of 4-8 cells per lane: the store's branch is cheap beside it
-          if (writer) write_slot(i + 1 < kChainBlock ? wb + (i + 1) * kChainSlot : wn, X, false);
-        } else if (i & 1) {  // exit states of ticks t - 1 and t into slots t and t + 1, one branch per pair
-          if (writer) {
-            write_slot(wb + i * kChainSlot, prev, false);
-            write_slot(i + 1 < kChainBlock ? wb + (i + 1) * kChainSlot : wn, X, false);
-          }
-        } else {
-#pragma unroll
-          for (int r = 0; r < K; ++r) prev[r] = X[r];
-        }
-#endif
       }
     } else {
 #if RT_CHAIN_MASKED_UNROLL
@@ -604,23 +505,6 @@ static hipError_t launch_wave_s(const WavePlan &p, const SegArgs &a, int nsteps,
   const bool pad = PAIR && a.N % p.C != 0;
   const int Lw = p.lanes;
   if (p.waves > 1) {
-#ifdef RT_CHAIN_V1  // round 3's chain (timing comparisons)
-    const size_t lds = sizeof(double) * SchemeDim<S>::K * (1 + static_cast<size_t>(p.waves - 1) * kWaveRing);
-    switch (p.C) {
-#define RT_WAVE_CASE(c)                                                                                          \
-  case c:                                                                                                        \
-    if (pad)                                                                                                     \
-      hipLaunchKernelGGL((wavefront_kernel<S, c, PAIR, PAIR && (c > 1), true>), dim3(grid), dim3(64 * p.waves), \
-                         lds, st, a, nsteps, Lw);                                                                \
-    else                                                                                                         \
-      hipLaunchKernelGGL((wavefront_kernel<S, c, PAIR, false, true>), dim3(grid), dim3(64 * p.waves), lds, st, a, \
-                         nsteps, Lw);                                                                            \
-    break;
-      RT_WAVE_CASE(1) RT_WAVE_CASE(2) RT_WAVE_CASE(4) RT_WAVE_CASE(8)
-#undef RT_WAVE_CASE
-      default: return hipErrorInvalidValue;
-    }
-#else
     const size_t lds = sizeof(double) * kChainSlot * kChainRing * static_cast<size_t>(p.waves);
     switch (p.C) {
 #define RT_CHAIN_LAUNCH(c, pd, wide)                                                                             \
@@ -641,18 +525,16 @@ static hipError_t launch_wave_s(const WavePlan &p, const SegArgs &a, int nsteps,
 #undef RT_CHAIN_LAUNCH
       default: return hipErrorInvalidValue;
     }
-#endif
     return hipGetLastError();
   }
   switch (p.C) {
 #define RT_WAVE_CASE(c)                                                                                          \
   case c:                                                                                                        \
     if (pad)                                                                                                     \
-      hipLaunchKernelGGL((wavefront_kernel<S, c, PAIR, PAIR && (c > 1), false>), dim3(grid), dim3(64), 0, st, a, \
-                         nsteps, Lw);                                                                            \
-    else                                                                                                         \
-      hipLaunchKernelGGL((wavefront_kernel<S, c, PAIR, false, false>), dim3(grid), dim3(64), 0, st, a, nsteps,   \
+      hipLaunchKernelGGL((wavefront_kernel<S, c, PAIR, PAIR && (c > 1)>), dim3(grid), dim3(64), 0, st, a, nsteps, \
                          Lw);                                                                                    \
+    else                                                                                                         \
+      hipLaunchKernelGGL((wavefront_kernel<S, c, PAIR, false>), dim3(grid), dim3(64), 0, st, a, nsteps, Lw);      \
     break;
     RT_WAVE_CASE(1) RT_WAVE_CASE(2) RT_WAVE_CASE(4) RT_WAVE_CASE(8)
 #undef RT_WAVE_CASE

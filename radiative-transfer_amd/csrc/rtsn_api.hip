@@ -201,17 +201,8 @@ static rt_status create_impl(const rt_params *pin, int g_lo, int g_hi, int d_lo,
   // segments: enough waves to fill the chip (occupancy x CUs), Ls a multiple of the chunk
   int waves_per_cu = 0;
   h->T = default_time_block(h->scheme);
-  if (const char *t = std::getenv("RTSN_TIME_BLOCK"))  // experiments: the segment count follows
-    if (supported_time_block(std::atoi(t))) {
-      h->T = std::atoi(t);
-      h->T_set = true;
-    }
-  if (const char *wv = std::getenv("RTSN_WAVEFRONT"))  // experiments: "0" off, "2" on for every short line
-    if (!std::strcmp(wv, "0") || !std::strcmp(wv, "2")) h->wave = wv[0] - '0';
-  if (const char *ww = std::getenv("RTSN_WAVE_WAVES"))  // experiments: waves per wavefront chain, 1..8
-    if (std::atoi(ww) >= 1 && std::atoi(ww) <= kWaveMaxWaves) h->wave_max = std::atoi(ww);
-  if (const char *lw = std::getenv("RTSN_LEVEL_WAVES"))  // experiments: only "1", "2" or "4" are read
-    if (!std::strcmp(lw, "1") || !std::strcmp(lw, "2") || !std::strcmp(lw, "4")) h->level_waves = lw[0] - '0';
+  // the time block, wavefront use, waves per chain and level split are the caller's (rt_set_*);
+  // no environment variable changes them (round 5: the experiment overrides were removed)
   h->cus = prop.multiProcessorCount;
   if ((st = segment_target(h, &waves_per_cu))) return st;
   segment_lines(h, waves_per_cu);
@@ -315,7 +306,8 @@ extern "C" rt_status rt_get_wavefront_waves(rt_solver *s, int *max_waves, int *w
 extern "C" rt_status rt_pipeline_state(rt_solver *s, long long *lag_steps, int *queued_steps, int *pending) {
   if (!s) return fail(nullptr, RT_ERR_ARG, "rt_pipeline_state: NULL handle");
   if (lag_steps) *lag_steps = s->tau.front() - s->tau.back();
-  if (queued_steps) *queued_steps = static_cast<int>(std::min<long long>(s->queued + s->wqueued, INT32_MAX));
+  if (queued_steps)  // s->tail: a remainder block still owed by an interrupted drain (complete)
+    *queued_steps = static_cast<int>(std::min<long long>(s->queued + s->wqueued + s->tail, INT32_MAX));
   if (pending) *pending = s->pending ? 1 : 0;
   return RT_OK;
 }

@@ -15,12 +15,18 @@
 // host code shared with the rt_layout_* entry points, which the CPU tests check at world
 // sizes 2, 3 and 8 -- run here with hipMemcpy2DAsync (device blocks) or on the host.
 //
-// No call can hang a job: the communicator is created non-blocking (ncclCommInitRankConfig,
-// blocking = 0) and every wait on it -- the init, a collective call that reports
-// ncclInProgress, and each host synchronisation after collectives -- polls with a deadline
-// of RTSN_COMM_TIMEOUT_S seconds (default 300).  On expiry the communicator is aborted
-// (ncclCommAbort: RCCL stops the kernels still waiting on a peer) and the call returns
-// RT_ERR_TIMEOUT; the handle then refuses further collectives (RT_ERR_STATE).
+// No wait on a peer can hang a job: the communicator is created non-blocking
+// (ncclCommInitRankConfig, blocking = 0) and every wait on it -- the init, a collective call
+// that reports ncclInProgress, and each host synchronisation after collectives -- polls with a
+// deadline of RTSN_COMM_TIMEOUT_S seconds (default 300).  The deadline runs only while a
+// collective is executing: every collective is bracketed by two events on the stream
+// (Mark), and a host wait clocks the collective whose opening event has completed and whose
+// closing one has not.  The local work queued before it (a long rt_advance, the sweeps of
+// rt_comm_material_step) is the handle's own and is waited for without that deadline.  On
+// expiry the communicator is aborted (ncclCommAbort: RCCL stops the kernels still waiting on
+// a peer) and the call returns RT_ERR_TIMEOUT; the handle then refuses further collectives
+// (RT_ERR_STATE).  Scratch buffers are stream-ordered (hipMallocAsync / hipFreeAsync), so an
+// error path never blocks the host on the stream to free them.
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
@@ -39,6 +45,16 @@
 
 namespace layout = rtamd::layout;
 
+// One enqueued collective: `pre` completes when the stream reaches it (the local work before
+// it is done), `post` when the collective has finished.  `since` is when a host wait first
+// saw `pre` complete and `post` not: the collective's deadline runs from there.
+struct Mark {
+  hipStream_t st = nullptr;
+  hipEvent_t pre = nullptr, post = nullptr;
+  std::chrono::steady_clock::time_point since{};
+  bool started = false;
+};
+
 struct rt_comm {
   ncclComm_t nc = nullptr;
   int nranks = 0, rank = 0, device = 0;
@@ -46,9 +62,16 @@ struct rt_comm {
   double timeout_s = 300.0;
   double *q = nullptr;  // material coupling: q(x) of the running step (N doubles)
   size_t q_len = 0;
+  std::vector<Mark> marks;         // collectives enqueued since the last completed host wait
+  std::vector<hipEvent_t> events;  // recycled event pool
   std::string err;
   ~rt_comm() {
     if (q) (void)hipFree(q);
+    for (Mark &m : marks) {
+      events.push_back(m.pre);
+      events.push_back(m.post);
+    }
+    for (hipEvent_t e : events) (void)hipEventDestroy(e);
     if (nc) {  // non-blocking: finalize, wait (bounded) for quiescence, then free
       const auto end = std::chrono::steady_clock::now() + std::chrono::duration<double>(timeout_s);
       ncclResult_t st = ncclCommFinalize(nc);
@@ -112,23 +135,105 @@ rt_status nc_settle(rt_comm *c, ncclResult_t r, const char *what) {
   }
 }
 
-// Host wait for the collectives enqueued on st, bounded like nc_settle: a peer that never
-// joins leaves RCCL's kernel spinning, which the abort ends.
+hipEvent_t take_event(rt_comm *c) {
+  if (!c->events.empty()) {
+    hipEvent_t e = c->events.back();
+    c->events.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  return hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess ? e : nullptr;
+}
+
+// The collectives of stream st have completed (or were aborted): their events go back to the pool.
+void retire_marks(rt_comm *c, hipStream_t st) {
+  std::vector<Mark> keep;
+  for (Mark &m : c->marks) {
+    if (m.st != st) {
+      keep.push_back(m);
+      continue;
+    }
+    c->events.push_back(m.pre);
+    c->events.push_back(m.post);
+  }
+  c->marks.swap(keep);
+}
+
+// A collective enqueued on st between two events (Mark): the host waits clock it from the
+// moment the stream reaches it, not from the moment they start.
+template <class F>
+rt_status enqueue_collective(rt_comm *c, hipStream_t st, const char *what, F &&call) {
+  {  // collectives already finished (a caller that never waits through rt_comm) leave the list
+    std::vector<Mark> live;
+    for (Mark &m : c->marks) {
+      if (hipEventQuery(m.post) == hipSuccess) {
+        c->events.push_back(m.pre);
+        c->events.push_back(m.post);
+      } else {
+        live.push_back(m);
+      }
+    }
+    c->marks.swap(live);
+  }
+  Mark m;
+  m.st = st;
+  m.pre = take_event(c);
+  m.post = take_event(c);
+  if (!m.pre || !m.post) {
+    if (m.pre) c->events.push_back(m.pre);
+    if (m.post) c->events.push_back(m.post);
+    return cfail(c, RT_ERR_DEVICE, std::string(what) + ": hipEventCreate failed");
+  }
+  if (hipEventRecord(m.pre, st) != hipSuccess) {
+    c->events.push_back(m.pre);
+    c->events.push_back(m.post);
+    return cfail(c, RT_ERR_DEVICE, std::string(what) + ": hipEventRecord failed");
+  }
+  rt_status r = nc_settle(c, call(), what);
+  if (r == RT_OK && hipEventRecord(m.post, st) != hipSuccess)
+    r = cfail(c, RT_ERR_DEVICE, std::string(what) + ": hipEventRecord failed");
+  if (r != RT_OK) {
+    c->events.push_back(m.pre);
+    c->events.push_back(m.post);
+    return r;
+  }
+  c->marks.push_back(m);
+  return RT_OK;
+}
+
+// Host wait for the collectives enqueued on st.  Only a collective in flight is clocked:
+// the first Mark of st whose `pre` has completed and `post` has not has RTSN_COMM_TIMEOUT_S
+// from the moment a poll first saw it running; a peer that never joins leaves RCCL's kernel
+// spinning, which the abort ends.  Local work ahead of a collective (or after the last) is
+// the handle's own and is not clocked.
 rt_status comm_sync(rt_comm *c, hipStream_t st, const char *what) {
-  const auto t0 = std::chrono::steady_clock::now();
   for (;;) {
     const hipError_t e = hipStreamQuery(st);
-    if (e == hipSuccess) return RT_OK;
+    if (e == hipSuccess) {
+      retire_marks(c, st);
+      return RT_OK;
+    }
     if (e != hipErrorNotReady) return cfail(c, RT_ERR_DEVICE, std::string(what) + ": " + hipGetErrorString(e));
     ncclResult_t as = ncclSuccess;
     if (c->nc && ncclCommGetAsyncError(c->nc, &as) == ncclSuccess && as != ncclSuccess && as != ncclInProgress)
       return abort_comm(c, RT_ERR_DEVICE, std::string(what) + ": " + ncclGetErrorString(as));
-    const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-    if (el > c->timeout_s) {
-      (void)abort_comm(c, RT_ERR_TIMEOUT, "");
-      (void)hipStreamSynchronize(st);  // the aborted kernels have returned
-      return cfail(c, RT_ERR_TIMEOUT, std::string(what) + ": collectives did not complete within RTSN_COMM_TIMEOUT_S = " +
-                                          std::to_string(c->timeout_s) + " s; communicator aborted");
+    const auto now = std::chrono::steady_clock::now();
+    for (Mark &m : c->marks) {
+      if (m.st != st || hipEventQuery(m.post) == hipSuccess) continue;
+      if (hipEventQuery(m.pre) != hipSuccess) break;  // local work ahead of this collective
+      if (!m.started) {
+        m.started = true;
+        m.since = now;
+      }
+      if (std::chrono::duration<double>(now - m.since).count() > c->timeout_s) {
+        (void)abort_comm(c, RT_ERR_TIMEOUT, "");
+        (void)hipStreamSynchronize(st);  // the aborted kernels have returned; only local work remains
+        retire_marks(c, st);
+        return cfail(c, RT_ERR_TIMEOUT, std::string(what) + ": a collective did not complete within "
+                                            "RTSN_COMM_TIMEOUT_S = " + std::to_string(c->timeout_s) +
+                                            " s of starting (a rank is missing or stalled); communicator aborted");
+      }
+      break;
     }
     std::this_thread::sleep_for(std::chrono::microseconds(50));
   }
@@ -137,6 +242,10 @@ rt_status comm_sync(rt_comm *c, hipStream_t st, const char *what) {
 #define NC_TRY(c, expr)                                          \
   do {                                                           \
     if (rt_status st_ = nc_settle((c), (expr), #expr)) return st_; \
+  } while (0)
+#define CO_TRY(c, st, expr)                                                                     \
+  do {                                                                                          \
+    if (rt_status st_ = enqueue_collective((c), (st), #expr, [&] { return (expr); })) return st_; \
   } while (0)
 #define CS_TRY(c, st)                                                         \
   do {                                                                        \
@@ -159,15 +268,14 @@ rt_status comm_sync(rt_comm *c, hipStream_t st, const char *what) {
     if (st_ != RT_OK) return cfail((c), st_, std::string(#expr ": ") + rt_last_error(s));                \
   } while (0)
 
-// Device scratch freed on scope exit (after the stream has drained it).
+// Device scratch, stream-ordered: allocated on the handle's stream and freed on it at scope
+// exit (no host wait).
 struct Scratch {
   void *p = nullptr;
   hipStream_t st = nullptr;
+  hipError_t alloc(size_t bytes) { return hipMallocAsync(&p, bytes, st); }
   ~Scratch() {
-    if (p) {
-      (void)hipStreamSynchronize(st);
-      (void)hipFree(p);
-    }
+    if (p) (void)hipFreeAsync(p, st);
   }
 };
 
@@ -186,10 +294,10 @@ rt_status all_shards(rt_comm *c, rt_solver *s, std::vector<rt_shard> &out, int &
   static_assert(sizeof(rt_shard) == kInts * sizeof(int), "rt_shard is ints only");
   Scratch buf;
   buf.st = st;
-  HC_TRY(c, hipMalloc(&buf.p, sizeof(int) * kInts * (c->nranks + 1)));
+  HC_TRY(c, buf.alloc(sizeof(int) * kInts * (c->nranks + 1)));
   int *d = static_cast<int *>(buf.p);
   HC_TRY(c, hipMemcpyAsync(d, &me, sizeof(rt_shard), hipMemcpyHostToDevice, st));
-  NC_TRY(c, ncclAllGather(d, d + kInts, kInts, ncclInt32, c->nc, st));
+  CO_TRY(c, st, ncclAllGather(d, d + kInts, kInts, ncclInt32, c->nc, st));
   out.resize(c->nranks);
   HC_TRY(c, hipMemcpyAsync(out.data(), d + kInts, sizeof(rt_shard) * c->nranks, hipMemcpyDeviceToHost, st));
   CS_TRY(c, st);
@@ -221,15 +329,15 @@ rt_status combine_vectors(rt_comm *c, rt_solver *s, const std::vector<rt_shard> 
     if (in[j]) layout::apply(layout::vectors_pack(sh.data(), n, c->rank, k, j), in[j], block.data());
   Scratch buf;
   buf.st = st;
-  HC_TRY(c, hipMalloc(&buf.p, sizeof(double) * cnt * (n + 1)));
+  HC_TRY(c, buf.alloc(sizeof(double) * cnt * (n + 1)));
   double *d = static_cast<double *>(buf.p);
   HC_TRY(c, hipMemcpyAsync(d, block.data(), sizeof(double) * cnt, hipMemcpyHostToDevice, st));
   std::vector<double> all(mode == 0 ? cnt * n : cnt);
   if (mode == 0) {
-    NC_TRY(c, ncclAllGather(d, d + cnt, cnt, ncclFloat64, c->nc, st));
+    CO_TRY(c, st, ncclAllGather(d, d + cnt, cnt, ncclFloat64, c->nc, st));
     HC_TRY(c, hipMemcpyAsync(all.data(), d + cnt, sizeof(double) * all.size(), hipMemcpyDeviceToHost, st));
   } else {
-    NC_TRY(c, ncclAllReduce(d, d, cnt, ncclFloat64, ncclSum, c->nc, st));
+    CO_TRY(c, st, ncclAllReduce(d, d, cnt, ncclFloat64, ncclSum, c->nc, st));
     HC_TRY(c, hipMemcpyAsync(all.data(), d, sizeof(double) * cnt, hipMemcpyDeviceToHost, st));
   }
   CS_TRY(c, st);
@@ -283,6 +391,13 @@ extern "C" rt_status rt_comm_rank(rt_comm *c, int *nranks, int *rank) {
   return RT_OK;
 }
 
+extern "C" rt_status rt_comm_count(rt_comm *c, int *count) {
+  if (!c || !count) return cfail(c, RT_ERR_ARG, "rt_comm_count: NULL argument");
+  LIVE(c, "rt_comm_count");
+  NC_TRY(c, ncclCommCount(c->nc, count));
+  return RT_OK;
+}
+
 extern "C" const char *rt_comm_last_error(rt_comm *c) { return c ? c->err.c_str() : g_comm_error.c_str(); }
 
 extern "C" rt_status rt_comm_gather_moments(rt_comm *c, rt_solver *s, double *phi, double *F, double *phi_plus) {
@@ -299,7 +414,7 @@ extern "C" rt_status rt_comm_gather_moments(rt_comm *c, rt_solver *s, double *ph
   hipStream_t st = static_cast<hipStream_t>(rt_stream(s));
   Scratch buf;
   buf.st = st;
-  HC_TRY(c, hipMalloc(&buf.p, sizeof(double) * 3 * blk * (mode == 0 ? n + 1 : 1)));
+  HC_TRY(c, buf.alloc(sizeof(double) * 3 * blk * (mode == 0 ? n + 1 : 1)));
   double *d = static_cast<double *>(buf.p);
   if (Gl == Gm) {  // the local arrays are the wire block (layout::moments_pack is one contiguous copy)
     RT_TRY(c, s, rt_get_moments_device(s, d, d + blk, d + 2 * blk));
@@ -307,7 +422,7 @@ extern "C" rt_status rt_comm_gather_moments(rt_comm *c, rt_solver *s, double *ph
     Scratch tmp;
     tmp.st = st;
     const size_t gn = static_cast<size_t>(N) * Gl;
-    HC_TRY(c, hipMalloc(&tmp.p, sizeof(double) * 3 * gn));
+    HC_TRY(c, tmp.alloc(sizeof(double) * 3 * gn));
     double *t = static_cast<double *>(tmp.p);
     RT_TRY(c, s, rt_get_moments_device(s, t, t + gn, t + 2 * gn));
     HC_TRY(c, hipMemsetAsync(d, 0, sizeof(double) * 3 * blk, st));
@@ -317,9 +432,9 @@ extern "C" rt_status rt_comm_gather_moments(rt_comm *c, rt_solver *s, double *ph
   double *want[3] = {phi, F, phi_plus};
   const double *gathered = d;
   if (mode == 1) {  // every rank holds partial sums over its directions of all G groups
-    NC_TRY(c, ncclAllReduce(d, d, 3 * blk, ncclFloat64, ncclSum, c->nc, st));
+    CO_TRY(c, st, ncclAllReduce(d, d, 3 * blk, ncclFloat64, ncclSum, c->nc, st));
   } else {
-    NC_TRY(c, ncclAllGather(d, d + 3 * blk, 3 * blk, ncclFloat64, c->nc, st));  // [rank][3][N][Gm]
+    CO_TRY(c, st, ncclAllGather(d, d + 3 * blk, 3 * blk, ncclFloat64, c->nc, st));  // [rank][3][N][Gm]
     gathered = d + 3 * blk;
   }
   for (int k = 0; k < 3; ++k)
@@ -390,11 +505,11 @@ extern "C" rt_status rt_comm_gather_psi(rt_comm *c, rt_solver *s, int root, doub
   RT_TRY(c, s, rt_get_psi(s, mine.data()));
   Scratch buf;
   buf.st = st;
-  HC_TRY(c, hipMalloc(&buf.p, sizeof(double) * big * (c->rank == root ? 2 : 1)));
+  HC_TRY(c, buf.alloc(sizeof(double) * big * (c->rank == root ? 2 : 1)));
   double *d = static_cast<double *>(buf.p);
   HC_TRY(c, hipMemcpyAsync(d, mine.data(), sizeof(double) * mine.size(), hipMemcpyHostToDevice, st));
   if (c->rank != root) {
-    NC_TRY(c, ncclSend(d, block(me), ncclFloat64, root, c->nc, st));
+    CO_TRY(c, st, ncclSend(d, block(me), ncclFloat64, root, c->nc, st));
     CS_TRY(c, st);
     return RT_OK;
   }
@@ -402,7 +517,7 @@ extern "C" rt_status rt_comm_gather_psi(rt_comm *c, rt_solver *s, int root, doub
   for (int r = 0; r < c->nranks; ++r) {
     const double *src = d;
     if (r != root) {  // one rank's block at a time through the receive buffer
-      NC_TRY(c, ncclRecv(rx, block(sh[r]), ncclFloat64, r, c->nc, st));
+      CO_TRY(c, st, ncclRecv(rx, block(sh[r]), ncclFloat64, r, c->nc, st));
       src = rx;
     }
     if (rt_status e = run_plan(c, layout::psi_place(sh[r]), src, psi, hipMemcpyDeviceToHost, st)) return e;
@@ -432,10 +547,10 @@ extern "C" rt_status rt_comm_gather_psi_source(rt_comm *c, rt_solver *s, double 
   hipStream_t st = static_cast<hipStream_t>(rt_stream(s));
   Scratch buf;
   buf.st = st;
-  HC_TRY(c, hipMalloc(&buf.p, sizeof(double) * cnt * (c->nranks + 1)));
+  HC_TRY(c, buf.alloc(sizeof(double) * cnt * (c->nranks + 1)));
   double *d = static_cast<double *>(buf.p);
   HC_TRY(c, hipMemcpyAsync(d, mine.data(), sizeof(double) * cnt, hipMemcpyHostToDevice, st));
-  NC_TRY(c, ncclAllGather(d, d + cnt, cnt, ncclFloat64, c->nc, st));
+  CO_TRY(c, st, ncclAllGather(d, d + cnt, cnt, ncclFloat64, c->nc, st));
   std::vector<double> all(cnt * c->nranks);
   HC_TRY(c, hipMemcpyAsync(all.data(), d + cnt, sizeof(double) * all.size(), hipMemcpyDeviceToHost, st));
   CS_TRY(c, st);
@@ -450,7 +565,8 @@ extern "C" rt_status rt_comm_allreduce_absorption(rt_comm *c, rt_solver *s, doub
   int N = 0;
   RT_TRY(c, s, rt_get_dims(s, nullptr, nullptr, &N, nullptr, nullptr));
   RT_TRY(c, s, rt_group_absorption_device(s, d_out));
-  NC_TRY(c, ncclAllReduce(d_out, d_out, N, ncclFloat64, ncclSum, c->nc, static_cast<hipStream_t>(rt_stream(s))));
+  hipStream_t st = static_cast<hipStream_t>(rt_stream(s));
+  CO_TRY(c, st, ncclAllReduce(d_out, d_out, N, ncclFloat64, ncclSum, c->nc, st));
   return RT_OK;
 }
 
@@ -472,7 +588,7 @@ extern "C" rt_status rt_comm_material_step(rt_comm *c, rt_solver *s, int nsteps)
   }
   for (int n = 0; n < nsteps; ++n) {
     RT_TRY(c, s, rt_material_sweep(s, c->q));
-    NC_TRY(c, ncclAllReduce(c->q, c->q, N, ncclFloat64, ncclSum, c->nc, st));
+    CO_TRY(c, st, ncclAllReduce(c->q, c->q, N, ncclFloat64, ncclSum, c->nc, st));
     RT_TRY(c, s, rt_material_update(s, c->q));
   }
   return RT_OK;

@@ -291,7 +291,9 @@ rt_status rtsn_detail::complete(rt_solver *s) {
   if (s->wqueued && (st = wave_flush(s))) return st;
   if (s->Tpipe) {
     const int kw = tail_waves(s, s->Tpipe);
-    if (s->queued && kw && s->queued >= s->Tpipe / kw) {  // the remainder as every position's last block
+    // the remainder as every position's last block; a tail already set is a drain a failed
+    // launch interrupted, which a later call resumes (rt_pipeline_state counts it as queued)
+    if (!s->tail && s->queued && kw && s->queued >= s->Tpipe / kw) {
       s->tail = s->queued;
       s->queued = 0;
     }

@@ -141,6 +141,7 @@ def lib():
         L.rt_comm_destroy.argtypes = [vp]
         L.rt_comm_destroy.restype = None
         L.rt_comm_rank.argtypes = [vp, C.POINTER(C.c_int), C.POINTER(C.c_int)]
+        L.rt_comm_count.argtypes = [vp, C.POINTER(C.c_int)]
         L.rt_comm_gather_moments.argtypes = [vp, vp, dp, dp, dp]
         L.rt_comm_gather_group_ends.argtypes = [vp, vp, dp, dp]
         L.rt_comm_gather_balance.argtypes = [vp, vp, dp, dp, dp]
@@ -631,8 +632,9 @@ class Comm:
 
     uid = Comm.unique_id() on one rank, handed to the others (e.g. by torch.distributed's
     broadcast_object_list or a file); Comm(nranks, rank, uid, device).  Every wait on the
-    communicator is bounded by RTSN_COMM_TIMEOUT_S seconds (default 300): a missing or
-    stalled rank gives RtError status 7 (RT_ERR_TIMEOUT) instead of a hang."""
+    collective is bounded by RTSN_COMM_TIMEOUT_S seconds (default 300) from the moment the
+    stream reaches it: a missing or stalled rank gives RtError status 7 (RT_ERR_TIMEOUT)
+    instead of a hang; the handle's own queued work is not clocked."""
 
     def __init__(self, nranks: int, rank: int, uid: bytes, device: int = 0):
         assert len(uid) == 128
@@ -672,6 +674,13 @@ class Comm:
         n, r = C.c_int(), C.c_int()
         self._check(lib().rt_comm_rank(self._h, C.byref(n), C.byref(r)), "rt_comm_rank")
         return n.value, r.value
+
+    @property
+    def count(self) -> int:
+        """ncclCommCount: the ranks RCCL reports for the communicator."""
+        n = C.c_int()
+        self._check(lib().rt_comm_count(self._h, C.byref(n)), "rt_comm_count")
+        return n.value
 
     def gather_moments(self, solver: "Solver"):
         """phi, F, phi_plus of all groups, (G, N) each, on every rank."""

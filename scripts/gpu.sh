@@ -6,12 +6,14 @@
 #   smoke                 __graft_entry__.smoke()
 #   bench[=ARGS]          python bench.py ARGS (default: the driver's --steps 20 --warmup 5) -> TAG_bench.json
 #   rehearsal             the 2-rank bench on the one GPU over gloo -> TAG_rehearsal2.json
+#   spawn2                the same with no launcher: bench.py --gpus 2 starts its ranks -> TAG_spawn2.json
 #   kt[=ARGS]             rocprofv3 kernel trace + stats of bench.py ARGS (no side legs) -> TAG_kernel_stats.csv,
 #                         TAG_trace_summary.json
 #   pmc[=ARGS]            the four PMC passes of the headline pass -> profiles/pmc_TAG_v0_t20.json
 #   py=SCRIPT[:ARGS]      python SCRIPT ARGS (':' separates arguments), stdout -> TAG_py_N.jsonl
 #   pyk=SCRIPT[:ARGS]     rocprofv3 kernel trace + stats of a python script -> TAG_pyk_N/
 #   pyp=CTRS@SCRIPT[:ARGS] one rocprofv3 PMC pass (CTRS comma-separated) of a python script -> TAG_pyp_N/
+#   pyr=SCRIPT[:ARGS]     rocprofv3 runtime trace (HIP API + kernels + copies) + stats of a python script -> TAG_pyr_N/
 #   env=NAME:VALUE        export NAME=VALUE for the steps after it
 set -o pipefail
 export TMPDIR=/tmp
@@ -66,6 +68,16 @@ s = d.get('schedule', {}); print('schedule', {k: s.get(k) for k in ('end_to_end_
 import json; d=json.load(open('gpurun_out/${TAG}_rehearsal2.json'))
 print('value', d['value'], 'n_gpus', d['n_gpus'], 'comm', d.get('rt_comm_gather'), 'per_rank', d.get('per_rank'))"
       ;;
+    spawn2)
+      # no launcher: bench.py --gpus 2 starts the two rank processes itself (both on cuda:0, gloo)
+      timeout -k 10 600 python bench.py --gpus 2 $DEF_BENCH --backend gloo --share-device --no-cpu-baseline \
+        > $log 2>&1 || { tail -30 $log; exit 1; }
+      grep "^{" $log | tail -1 > gpurun_out/${TAG}_spawn2.json
+      python3 -c "
+import json; d=json.load(open('gpurun_out/${TAG}_spawn2.json'))
+print('value', d['value'], 'n_gpus', d['n_gpus'], 'launcher', d.get('launcher'), 'rccl_nranks', d.get('rccl_nranks'),
+      'per_rank', len(d.get('per_rank') or []))"
+      ;;
     kt)
       [ -z "$arg" ] && arg=$DEF_BENCH
       timeout -k 10 500 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_kt -o run --output-format csv \
@@ -96,10 +108,11 @@ print('value', d['value'], 'n_gpus', d['n_gpus'], 'comm', d.get('rt_comm_gather'
         || { tail -30 $log; tail -5 gpurun_out/${TAG}_py_${n}.jsonl; exit 1; }
       tail -40 gpurun_out/${TAG}_py_${n}.jsonl
       ;;
-    pyk|pyp)
+    pyk|pyp|pyr)
       # pyk=SCRIPT[:ARGS]: kernel trace + stats of a python script -> TAG_pyk_N/;
       # pyp=CTR,CTR,...@SCRIPT[:ARGS]: one PMC pass (counters of one pass only) -> TAG_pyp_N/
       prof="--kernel-trace --stats"
+      [ "$name" = pyr ] && prof="--runtime-trace --stats"
       if [ "$name" = pyp ]; then
         prof="--pmc $(echo "${arg%%@*}" | tr ',' ' ')"
         arg=${arg#*@}
@@ -109,7 +122,7 @@ print('value', d['value'], 'n_gpus', d['n_gpus'], 'comm', d.get('rt_comm_gather'
       [ "$script" != "$arg" ] && rest=$(echo "${arg#*:}" | tr ':' ' ')
       timeout -k 10 -s KILL 400 rocprofv3 $prof -d gpurun_out/${TAG}_${name}_${n} -o run --output-format csv \
         -- python3 $script $rest > $log 2>&1 || { tail -20 $log; exit 1; }
-      rm -f gpurun_out/${TAG}_${name}_${n}/run_kernel_trace.csv
+      [ "$name" = pyr ] || rm -f gpurun_out/${TAG}_${name}_${n}/run_kernel_trace.csv
       ls gpurun_out/${TAG}_${name}_${n}
       ;;
     *)

@@ -16,7 +16,9 @@ from pathlib import Path
 KERNEL = "sweep_block_kernel"
 
 
-def counters(d):
+def counters(d, names=None):
+    """{counter: [values]} over the sweep passes' launches; `names` (a dict) receives
+    {counter: [kernel names]} in the same order."""
     out = {}
     for f in Path(d).rglob("*counter_collection.csv"):
         for r in csv.DictReader(open(f)):
@@ -27,17 +29,22 @@ def counters(d):
             block = KERNEL in name and len(targs) >= 3 and targs[2] in ("0", "2") and "true" not in targs[3:]
             if block or "sweep_split_kernel" in name:
                 out.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
+                if names is not None:
+                    names.setdefault(r["Counter_Name"], []).append(name.split("(")[0].strip())
     return out
 
 
 def main():
     variant, fdir, wdir, *rest = sys.argv[1:]
     # the largest launch is a full pass (pipeline fill/drain launches cover fewer segments)
-    fetch = counters(fdir)["FETCH_SIZE"]
+    names = {}
+    fetch = counters(fdir, names)["FETCH_SIZE"]
     write = counters(wdir)["WRITE_SIZE"]
     rd = max(fetch) * 1024 * 2
     wr = max(write) * 1024
-    res = {"variant": variant, "kernel": KERNEL, "launches": len(fetch),
+    # the kernel of the largest launch (the full pass the bytes are quoted for)
+    kernel = names["FETCH_SIZE"][fetch.index(max(fetch))]
+    res = {"variant": variant, "kernel": kernel, "launches": len(fetch),
            "fetch_size_kib_max": max(fetch), "write_size_kib_max": max(write),
            "hbm_read_bytes_per_launch": rd, "hbm_write_bytes_per_launch": wr,
            "hbm_bytes_per_launch": rd + wr,

@@ -1,4 +1,4 @@
-import json, os, sys
+import json, sys
 sys.path[:0] = ['.', 'radiative-transfer_amd']
 import bench, rtsn
 pdir = bench.REPO / 'tests' / 'golden' / 'prm'
@@ -6,4 +6,4 @@ for name in bench.REFERENCE_CONFIGS:
     ph = rtsn.ParameterHandler(pdir / name, table_dir=str(pdir) + '/')
     q = ph.params
     g = bench.gpu_rate(q, q['ts_method'], 1000)
-    print(json.dumps(dict(config=name, rep=int(sys.argv[1]), waves_max=int(os.environ.get('RTSN_WAVE_WAVES', 8)), **g)), flush=True)
+    print(json.dumps(dict(config=name, rep=int(sys.argv[1]), **g)), flush=True)

@@ -129,3 +129,40 @@ def test_comm_init_without_peer_times_out(tmp_path):
     assert parts[1] == "7", line[0]
     assert 4.5 <= float(parts[2]) <= 60.0, line[0]
     assert "RTSN_COMM_TIMEOUT_S" in line[0]
+
+
+def test_comm_deadline_ignores_local_work_ahead(rtsn_mod, monkeypatch):
+    """the RTSN_COMM_TIMEOUT_S deadline clocks a collective from the moment
+    the stream reaches it, not the host wait.  With a 1 s deadline, a one-rank communicator
+    runs coupled steps whose sweeps take several seconds of local work (material_step: sweep,
+    all-reduce of q, update per step, all stream-ordered) and then a gather whose stream still
+    holds a long rt_advance: both succeed, and ncclCommCount reports the one rank."""
+    import sys
+    import time
+    from conftest import REPO
+    sys.path.insert(0, str(REPO))
+    import bench
+    monkeypatch.setenv("RTSN_COMM_TIMEOUT_S", "1")
+    with rtsn_mod.Comm(1, 0, rtsn_mod.Comm.unique_id(), 0) as c:
+        assert c.count == 1
+        p = bench.material_params(bench.slab_params(16, "v0", N=1_000_000, M=64))
+        with rtsn_mod.Solver(p, device=0) as s:
+            s.material_enable(1.0)
+            s.synchronize()
+            t0 = time.perf_counter()
+            c.material_step(s, 250)      # ~6 ms of sweep per step ahead of each all-reduce
+            c.synchronize(s)
+            dt = time.perf_counter() - t0
+            assert np.isfinite(s.temperature()).all()
+        assert dt > 1.2, f"only {dt:.2f} s of local work: the test does not exercise the deadline"
+        q = dict(bench.slab_params(16, "v0", N=1_000_000, M=64), dt=1e-9)
+        with rtsn_mod.Solver(q, device=0) as s:
+            s.pipeline = 2
+            s.advance(2000)              # ~2 s of pipelined sweeps, enqueued without a host wait
+            t0 = time.perf_counter()
+            left, right = c.gather_group_ends(s)
+            dt = time.perf_counter() - t0
+            l2, r2 = s.compute_group_ends()
+            assert np.array_equal(left, l2) and np.array_equal(right, r2)
+        assert dt > 1.2, f"the gather waited only {dt:.2f} s: the test does not exercise the deadline"
+        assert c.count == 1

@@ -360,3 +360,59 @@ def test_host_cpus_share(monkeypatch):
     assert 1 <= h["threads"] <= h["affinity"] <= h["nproc"]
     monkeypatch.setenv("OMP_NUM_THREADS", "1")
     assert bench.host_cpus()["threads"] == 1
+
+
+def test_launch_mode():
+    """bench.py --gpus N: a plain run with N > 1 starts the ranks itself; under a
+    launcher WORLD_SIZE must equal --gpus."""
+    assert bench.launch_mode(1, {}) == "rank"
+    assert bench.launch_mode(8, {}) == "spawn"
+    assert bench.launch_mode(2, {"WORLD_SIZE": "2"}) == "rank"
+    assert bench.launch_mode(1, {"WORLD_SIZE": "1"}) == "rank"
+    for n, ws in ((8, "1"), (1, "2"), (4, "8")):
+        with pytest.raises(ValueError):
+            bench.launch_mode(n, {"WORLD_SIZE": ws})
+    with pytest.raises(ValueError):
+        bench.launch_mode(0, {})
+
+
+_RANK_CHILD = r"""
+import json, os, sys
+import torch.distributed as dist
+r, n = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+assert os.environ["LOCAL_RANK"] == str(r) and os.environ["MASTER_ADDR"] == "127.0.0.1"
+fail = sys.argv[1] if len(sys.argv) > 1 else ""
+if fail == "rank1" and r == 1:
+    sys.exit(3)
+dist.init_process_group("gloo")
+t = __import__("torch").tensor([float(r)])
+dist.all_reduce(t)
+if r == 0:
+    print("progress line")
+    print(json.dumps({"n_gpus": n if fail != "count" else 1, "sum": float(t), "launcher": os.environ["RTSN_BENCH_LAUNCHER"]}))
+dist.destroy_process_group()
+"""
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_spawn_ranks_relays_rank0(tmp_path, capsys, n):
+    """spawn_ranks starts n fresh rank processes (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_*), they
+    rendezvous (gloo here) and rank 0's JSON line is relayed; status 0."""
+    script = tmp_path / "child.py"
+    script.write_text(_RANK_CHILD)
+    assert bench.spawn_ranks(n, [], script=script) == 0
+    out = capsys.readouterr().out
+    d = json.loads([l for l in out.splitlines() if l.startswith("{")][-1])
+    assert d["n_gpus"] == n and d["sum"] == n * (n - 1) / 2
+    assert d["launcher"] == f"bench.py --gpus {n} (child processes)"
+
+
+@pytest.mark.parametrize("fail,status", [("rank1", 3), ("count", 1)])
+def test_spawn_ranks_fails_loudly(tmp_path, fail, status):
+    """A rank that exits non-zero stops the job (the others, blocked in the rendezvous, are
+    terminated) with that status; a line whose n_gpus is not N is a failure too."""
+    script = tmp_path / "child.py"
+    script.write_text(_RANK_CHILD)
+    t0 = time.time()
+    assert bench.spawn_ranks(2, [fail], script=script, grace_s=5) == status
+    assert time.time() - t0 < 120

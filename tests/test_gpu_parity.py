@@ -545,12 +545,12 @@ def test_level_waves_auto(rtsn_mod):
 
 @pytest.mark.parametrize("tb", [4, 8, 12, 16, 20])
 @pytest.mark.parametrize("bc_left", [0, 2])
-def test_level_split_pass(rtsn_mod, oracle_mod, monkeypatch, tb, bc_left):
+def test_level_split_pass(rtsn_mod, oracle_mod, tb, bc_left):
     """The level-split pipelined pass (sweep_split_kernel: the T levels of a BDF2 pass
     shared by two waves through LDS -- the default at T = 20 -- and by 2 or 4 waves in the
     pipeline's fill and drain launches under the default level_waves 0) is bitwise the
-    one-wave pass (rt_set_level_waves 1, and RTSN_LEVEL_WAVES=1 at creation, whose
-    segment count follows the one-wave occupancy) -- same arithmetic per (cell, level)
+    one-wave pass (rt_set_level_waves 1; also after a handle ran with 2) -- same arithmetic
+    per (cell, level)
     -- over 3 T + 1 steps (fill, steady state, drain, an aligned remainder), and matches
     the oracle over T + 3 steps (the reference's BDF2 grows the random state so fast
     that longer runs amplify rounding past 1e-10); ragged lines (N = 4099:
@@ -571,13 +571,12 @@ def test_level_split_pass(rtsn_mod, oracle_mod, monkeypatch, tb, bc_left):
     orc.set_ends(ends)
     orc.solve()
     out = {}
+    # (first, lw): level_waves set to `first`, then to lw; 0 is the default (fill and drain
+    # launches split over 2 or 4 waves, pipe_launch)
     for env, lw in (("1", 1), ("2", 2), ("2", 1), (None, 0)):
-        if env:
-            monkeypatch.setenv("RTSN_LEVEL_WAVES", env)
-        else:  # the default: fill and drain launches split over 2 or 4 waves (pipe_launch)
-            monkeypatch.delenv("RTSN_LEVEL_WAVES")
         with rtsn_mod.Solver(to_rt(p), g_lo=lo, g_hi=hi) as gpu:
             if env:
+                gpu.level_waves = int(env)
                 assert gpu.level_waves == int(env)
             gpu.level_waves = lw
             with pytest.raises(rtsn_mod.RtError):
