@@ -32,6 +32,7 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <cstdlib>
 
 #include "cell.hpp"
 #include "kernels.hpp"
@@ -657,6 +658,112 @@ __global__ void __launch_bounds__(64) moments_kernel(const double2 *__restrict__
       phi[o] = sphi;
       F[o] = sF;
       phi_plus[o] = splus;
+    }
+  }
+}
+
+// Producer/consumer moments (round 5): the same sums, bitwise, from a workgroup of three
+// waves with fixed roles.  An item is (cell c, 64 groups): half 0's row k = N-1-c and half
+// 1's row k = c, each a contiguous run of 64 H lines (l = i' + H g).  Loader wave h streams
+// half h's run with lane-contiguous 16-byte nt loads (1 KiB per instruction, as the state
+// scan reads) into a register ring of the H loads of one item, so the loads of item p + 1
+// are in flight while item p's values are converted to psi = (e_in + e_out) / 2 and written
+// to an LDS slot [half][group][i'] (row stride H + 1 doubles: conflict-free); its only waits
+// are on its own oldest load.  The summing wave (lane = group) takes the previous item's slot
+// and runs the three sums over i = 0 .. M-1 in the reference's order (solver.cpp:191-237,
+// no FMA contraction; w psi computed once for phi and phi_plus, mu w as one product, as
+// moments_kernel).  The three waves meet at one barrier per item (LDS writes and reads
+// drained, lgkmcnt(0); the barrier itself does not wait for the loads in flight), two slots
+// alternating.  Lines past the item's groups read as zero through the descriptor's bound.
+template <int H>
+__global__ void __launch_bounds__(192) moments_pc_kernel(const double2 *__restrict__ E, const double *__restrict__ mu,
+                                                         const double *__restrict__ wt, double *phi, double *F,
+                                                         double *phi_plus, LineMap m) {
+#pragma clang fp contract(off)
+  static_assert(64 % H == 0 && H >= 8, "a load of 64 lines covers whole groups");
+  constexpr int ST = H + 1;             // doubles per group row in a slot
+  constexpr int SLOT = 2 * 64 * ST;     // one item: [half][64 groups][ST]
+  __shared__ double lds[2 * SLOT + 4 * H];  // two slots, then (w_i, mu_i w_i) for i < 2H
+  double *const wl = lds + 2 * SLOT;
+  const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
+  const int lane = threadIdx.x & 63;
+  const int nchunks = (m.Gl + 63) / 64;
+  const long long items = static_cast<long long>(m.N) * nchunks;
+  const long long first = blockIdx.x, step = gridDim.x;
+  const long long mine = first < items ? (items - 1 - first) / step + 1 : 0;  // this workgroup's items
+  for (int i = threadIdx.x; i < 2 * H; i += blockDim.x) {
+    wl[2 * i] = wt[i];
+    wl[2 * i + 1] = mu[i] * wt[i];
+  }
+  __syncthreads();
+  const auto sync = [] {  // LDS traffic drained, then the workgroup barrier (loads stay in flight)
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+    __builtin_amdgcn_s_barrier();
+  };
+  if (wave < 2) {  // loader of half `wave`
+    const int h = wave;
+    const auto rsrc = [&](long long p) {  // item p's run in half h; past the last item: no records
+      if (p >= mine) return __builtin_amdgcn_make_buffer_rsrc(const_cast<double2 *>(E), 0, 0, 0x00020000);
+      const long long it = first + p * step;
+      const int c = static_cast<int>(it / nchunks), g0 = static_cast<int>(it % nchunks) * 64;
+      const int ng = min(64, m.Gl - g0);
+      const double2 *row = E + m.at(h, h == 0 ? m.N - 1 - c : c, H * g0);
+      return __builtin_amdgcn_make_buffer_rsrc(const_cast<double2 *>(row), 0, ng * H * 16, 0x00020000);
+    };
+    const int voff = lane * 16;
+    double2 v[H];
+    {
+      const __amdgpu_buffer_rsrc_t R = rsrc(0);
+#pragma unroll
+      for (int r = 0; r < H; ++r) {  // in ring order (the loop's waits count on it)
+        v[r] = row_load(R, voff, r * 1024);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    double *const base = lds + h * 64 * ST + (lane / H) * ST + lane % H;
+    for (long long p = 0; p < mine; ++p) {
+      double *const slot = base + (p & 1) * SLOT;
+      const __amdgpu_buffer_rsrc_t Rn = rsrc(p + 1);
+#pragma unroll
+      for (int r = 0; r < H; ++r) {  // line lane + 64 r: group lane / H + 64 r / H, i' = lane % H
+        slot[(64 / H) * r * ST] = 0.5 * (v[r].x + v[r].y);
+        v[r] = row_load(Rn, voff, r * 1024);
+        __builtin_amdgcn_sched_barrier(0);  // a rolling ring: each load waits only for the oldest
+      }
+      sync();
+    }
+    sync();  // the summing wave's last item
+  } else {  // the summing wave: lane = group of the item
+    for (long long p = 0; p <= mine; ++p) {
+      if (p > 0) {
+        const long long it = first + (p - 1) * step;
+        const int c = static_cast<int>(it / nchunks), g0 = static_cast<int>(it % nchunks) * 64;
+        const double *s0 = lds + ((p - 1) & 1) * SLOT + lane * ST;
+        const double *s1 = s0 + 64 * ST;
+        double sphi = 0.0, sF = 0.0, splus = 0.0;
+#pragma unroll
+        for (int i = 0; i < H; ++i) {  // mu < 0: i' = H - 1 - i
+          const double q = s0[H - 1 - i];
+          const double wq = wl[2 * i] * q;
+          sphi += wq;
+          sF += wl[2 * i + 1] * q;
+        }
+#pragma unroll
+        for (int i = 0; i < H; ++i) {  // mu > 0: i = H + i'
+          const double q = s1[i];
+          const double wq = wl[2 * (H + i)] * q;
+          sphi += wq;
+          sF += wl[2 * (H + i) + 1] * q;
+          splus += wq;
+        }
+        if (g0 + lane < m.Gl) {
+          const size_t o = static_cast<size_t>(c) * m.Gl + g0 + lane;
+          __builtin_nontemporal_store(sphi, phi + o);
+          __builtin_nontemporal_store(sF, F + o);
+          __builtin_nontemporal_store(splus, phi_plus + o);
+        }
+      }
+      sync();
     }
   }
 }
@@ -1560,6 +1667,12 @@ hipError_t launch_import_ends(double2 *E, const double *ends, const Geometry &g,
 #ifndef RT_MOM_W
 #define RT_MOM_W 16
 #endif
+// RTSN_MOMENTS_LEGACY=1: the one-wave moments_kernel where the producer/consumer form applies
+// (A/B timing and the bitwise test of the two forms)
+static bool getenv_moments_legacy() {
+  const char *e = std::getenv("RTSN_MOMENTS_LEGACY");
+  return e && e[0] == '1';
+}
 hipError_t launch_moments(const double2 *E, const double *mu, const double *wt, double *phi, double *F,
                           double *phi_plus, const Geometry &g, hipStream_t st) {
   const LineMap m = make_map(g);
@@ -1570,6 +1683,19 @@ hipError_t launch_moments(const double2 *E, const double *mu, const double *wt, 
   static const size_t resident[3] = {resident_blocks(moments_kernel<false, 8>, 64),
                                      resident_blocks(moments_kernel<true, 8>, 64),
                                      resident_blocks(moments_kernel<true, W>, 64)};
+  if (!getenv_moments_legacy() && (m.H == 8 || m.H == 16 || m.H == 32)) {  // producer/consumer form
+    static const size_t pc[3] = {resident_blocks(moments_pc_kernel<8>, 192), resident_blocks(moments_pc_kernel<16>, 192),
+                                 resident_blocks(moments_pc_kernel<32>, 192)};
+    const int k = m.H == 8 ? 0 : (m.H == 16 ? 1 : 2);
+    const dim3 g(static_cast<unsigned>(tasks < pc[k] ? tasks : pc[k]));
+    if (m.H == 8)
+      hipLaunchKernelGGL((moments_pc_kernel<8>), g, dim3(192), 0, st, E, mu, wt, phi, F, phi_plus, m);
+    else if (m.H == 16)
+      hipLaunchKernelGGL((moments_pc_kernel<16>), g, dim3(192), 0, st, E, mu, wt, phi, F, phi_plus, m);
+    else
+      hipLaunchKernelGGL((moments_pc_kernel<32>), g, dim3(192), 0, st, E, mu, wt, phi, F, phi_plus, m);
+    return hipGetLastError();
+  }
   const int kind = m.H % W == 0 ? 2 : (m.H % 8 == 0 ? 1 : 0);
   const dim3 grid(static_cast<unsigned>(tasks < resident[kind] ? tasks : resident[kind]));
   if (kind == 2)

@@ -2,13 +2,26 @@
 // contraction so that the reference's expression order is the arithmetic.
 #include "physics.hpp"
 
+#include <sched.h>
+
 #include <algorithm>
 #include <cfloat>
 #include <cmath>
 #include <limits>
+#include <thread>
+#include <vector>
 
 namespace rtamd {
 namespace phys {
+
+// Threads for host-side setup work: the process's CPU affinity (the lease's share on a
+// shared machine, not hardware_concurrency), at most 8.
+static int host_threads() {
+  cpu_set_t set;
+  int n = 1;
+  if (sched_getaffinity(0, sizeof(set), &set) == 0) n = CPU_COUNT(&set);
+  return std::max(1, std::min(n, 8));
+}
 
 double rad_a_long() {
   return (8.0 * std::pow(kPi, 5) * std::pow(kBoltzmann, 4)) /
@@ -126,16 +139,19 @@ double PlanckIntegrator::tail_series(double z1, double z2, bool dT) const {
     else
       break;
   }
+  // pow(n, 4.0) of an integer n < 2^13 is exact (n^4 < 2^53 and libm's pow errs by < 1 ulp,
+  // so it returns the representable exact value): the product n n n n, bitwise the same
   double s1 = 0.0, s2 = 0.0;
   for (int n = n_terms; n > 0; --n) {
+    const double dn = n, n4 = dn * dn * dn * dn;
     if (dT) {
-      s1 += std::exp(-n * z1) / std::pow(n, 4.0) *
+      s1 += std::exp(-n * z1) / n4 *
             (std::pow(n * z1, 4.0) + 4.0 * std::pow(n * z1, 3.0) + 12.0 * std::pow(n * z1, 2.0) + 24.0 * n * z1 + 24.0);
-      s2 += std::exp(-n * z2) / std::pow(n, 4.0) *
+      s2 += std::exp(-n * z2) / n4 *
             (std::pow(n * z2, 4.0) + 4.0 * std::pow(n * z2, 3.0) + 12.0 * std::pow(n * z2, 2.0) + 24.0 * n * z2 + 24.0);
     } else {
-      s1 += std::exp(-n * z1) / std::pow(n, 4.0) * (std::pow(n * z1, 3.0) + 3.0 * std::pow(n * z1, 2.0) + 6.0 * n * z1 + 6.0);
-      s2 += std::exp(-n * z2) / std::pow(n, 4.0) * (std::pow(n * z2, 3.0) + 3.0 * std::pow(n * z2, 2.0) + 6.0 * n * z2 + 6.0);
+      s1 += std::exp(-n * z1) / n4 * (std::pow(n * z1, 3.0) + 3.0 * std::pow(n * z1, 2.0) + 6.0 * n * z1 + 6.0);
+      s2 += std::exp(-n * z2) / n4 * (std::pow(n * z2, 3.0) + 3.0 * std::pow(n * z2, 2.0) + 6.0 * n * z2 + 6.0);
     }
   }
   return s1 - s2;
@@ -183,14 +199,33 @@ double PlanckIntegrator::integral_dBdT(double T, double e_min, double e_max) con
   return value * 4.0 * kPi;
 }
 
+// The G - 1 integral pairs are independent; only the remainder group's running
+// subtraction is ordered.  With many groups they are evaluated on host threads (each
+// group's arithmetic unchanged, so the table is bitwise the serial one): the Bose series
+// takes >= 32 terms of exp / pow per bound, ~9 us per group on one core, which was most of
+// llnl_slab_test's rt_create (124 groups: 1.1 ms on one core of the build container).
 void PlanckIntegrator::group_integrals(double T, int G, const double *e_lo, const double *e_hi, double *B,
                                        double *dBdT) const {
   double rest_B = rad_a_long() * kLight * std::pow(T, 4.0);
   double rest_dB = 4.0 * rad_a_long() * kLight * std::pow(T, 3.0);
-  for (int g = 0; g < G - 1; ++g) {
-    B[g] = integral_B(T, e_lo[g], e_hi[g]);
+  const auto work = [&](int g0, int g1) {
+    for (int g = g0; g < g1; ++g) {
+      B[g] = integral_B(T, e_lo[g], e_hi[g]);
+      dBdT[g] = integral_dBdT(T, e_lo[g], e_hi[g]);
+    }
+  };
+  const int n = G - 1;
+  const int nt = n < 32 ? 1 : std::min(host_threads(), (n + 15) / 16);
+  if (nt <= 1) {
+    work(0, n);
+  } else {
+    std::vector<std::thread> pool;
+    for (int t = 1; t < nt; ++t) pool.emplace_back(work, n * t / nt, n * (t + 1) / nt);
+    work(0, n / nt);
+    for (std::thread &th : pool) th.join();
+  }
+  for (int g = 0; g < n; ++g) {
     rest_B -= B[g];
-    dBdT[g] = integral_dBdT(T, e_lo[g], e_hi[g]);
     rest_dB -= dBdT[g];
   }
   if (rest_B > 0.0) B[G - 1] = rest_B;

@@ -254,6 +254,11 @@ struct rt_solver {
   void *staging[2] = {nullptr, nullptr};
   size_t staging_bytes = 0, staging_cap[2] = {0, 0};
   hipEvent_t staging_ev[2] = {nullptr, nullptr};
+  // host -> device uploads of the per-line setup (upload()): a pinned arena the copies leave
+  // from asynchronously; reused from its start after a stream synchronisation
+  void *up_arena = nullptr;
+  size_t up_cap = 0, up_used = 0;
+  bool agg_zero_pending = false;  // the aggregates are zeroed before the first segment pass
   std::string err;
 
   ~rt_solver() {  // everything goes back to the resource cache once the stream is idle
@@ -261,6 +266,7 @@ struct rt_solver {
     if (stream) (void)hipStreamSynchronize(stream);  // no kernel may outlive the buffers it uses
     rtsn_detail::ResourcePool &pool = rtsn_detail::ResourcePool::get();
     for (int k = 0; k < 2; ++k) pool.release(true, staging[k], staging_cap[k], 0);
+    pool.release(true, up_arena, up_cap, 0);
     for (hipEvent_t e : staging_ev) pool.release_event(e, false, device);
     for (hipEvent_t e : ev_pool) pool.release_event(e, true, device);
     pool.release_stream(stream, device);
@@ -386,6 +392,8 @@ rt_status check_validation(rt_solver *s);
 rt_status ensure_equilibrium(rt_solver *s);
 rt_status fold_events(rt_solver *s);
 SegArgs seg_args(rt_solver *s);
+// zero the segment aggregates if a (re)allocation left them pending: before any segment pass
+rt_status ensure_segments(rt_solver *s);
 rt_status enqueue_fold(rt_solver *s, int T, bool reflective_outflow);
 rt_status apply_correction(rt_solver *s);
 rt_status enqueue_pass(rt_solver *s, int T, bool coupled = false);

@@ -2,6 +2,8 @@
 // the per-line affine cell map (cell.hpp) and the aligned schedule's segment propagators,
 // boundary inflows, and the segmentation of the lines (segment_lines / resegment).
 
+#include <cstring>
+
 #include "rtsn_internal.hpp"
 
 using namespace rtamd;
@@ -145,8 +147,35 @@ static void matpow(int K, const double *A, long long n, double *out) {
   std::copy(acc.begin(), acc.end(), out);
 }
 
+// Host -> device, asynchronous: `src` may be freed at return.  Up to kArenaMax bytes go
+// through the handle's pinned upload arena (a DMA from page-locked memory, no host wait):
+// the setup of a handle -- line maps and constants, inflows, sources -- is a handful of small
+// copies that a pageable hipMemcpyAsync + stream synchronisation each made a host round trip
+// (round 5, profiles/r05a_*: ~100 us of llnl_slab_test's create).  The arena restarts from
+// its beginning after a stream synchronisation once full; larger copies (the aligned
+// schedule's propagators) go from `src` and wait.
+constexpr size_t kArenaMax = size_t(16) << 20;
 rt_status rtsn_detail::upload(rt_solver *s, DeviceBuf &b, const void *src, size_t bytes) {
-  HIP_TRY(s, hipMemcpyAsync(b.p, src, bytes, hipMemcpyHostToDevice, s->stream));
+  if (bytes > kArenaMax) {
+    HIP_TRY(s, hipMemcpyAsync(b.p, src, bytes, hipMemcpyHostToDevice, s->stream));
+    HIP_TRY(s, hipStreamSynchronize(s->stream));  // src dies at return
+    return RT_OK;
+  }
+  const size_t need = (bytes + 255) & ~size_t(255);
+  if (s->up_used + need > s->up_cap) {
+    if (s->up_used) HIP_TRY(s, hipStreamSynchronize(s->stream));  // earlier uploads have left the arena
+    s->up_used = 0;
+    if (need > s->up_cap) {
+      ResourcePool::get().release(true, s->up_arena, s->up_cap, 0);
+      s->up_arena = nullptr;
+      s->up_cap = 0;
+      HIP_TRY(s, ResourcePool::get().alloc(true, std::max(need, size_t(1) << 20), &s->up_arena, &s->up_cap));
+    }
+  }
+  char *h = static_cast<char *>(s->up_arena) + s->up_used;
+  std::memcpy(h, src, bytes);
+  HIP_TRY(s, hipMemcpyAsync(b.p, h, bytes, hipMemcpyHostToDevice, s->stream));
+  s->up_used += need;
   return RT_OK;
 }
 
@@ -193,7 +222,6 @@ rt_status rtsn_detail::line_maps_s(rt_solver *s, bool unit_B, DeviceBuf &map_dev
   rt_status st;
   if ((st = upload(s, lc_dev, lc.data(), lc.size() * sizeof(double)))) return st;
   if ((st = upload(s, map_dev, map.data(), map.size() * sizeof(double)))) return st;
-  HIP_TRY(s, hipStreamSynchronize(s->stream));  // host vectors die at return
   return RT_OK;
 }
 
@@ -214,7 +242,6 @@ static rt_status setup_lines_s(rt_solver *s) {
   std::copy(s->mu.begin(), s->mu.end(), muwt.begin());
   std::copy(s->wt.begin(), s->wt.end(), muwt.begin() + s->p.M);
   if ((st = upload(s, s->muwt, muwt.data(), muwt.size() * sizeof(double)))) return st;
-  HIP_TRY(s, hipStreamSynchronize(s->stream));  // host vectors die at return
   return RT_OK;
 }
 
@@ -252,7 +279,6 @@ static rt_status build_propagators_s(rt_solver *s, int T) {
   for (std::thread &th : pool) th.join();
   rt_status st = upload(s, s->prop[T], pr.data(), pr.size() * sizeof(double));
   if (st) return st;
-  HIP_TRY(s, hipStreamSynchronize(s->stream));  // pr dies at return
   s->prop_ready[T] = true;
   return RT_OK;
 }
@@ -277,10 +303,7 @@ rt_status rtsn_detail::setup_lines(rt_solver *s) {
 rt_status rtsn_detail::upload_inflow(rt_solver *s) {
   std::vector<double> bd;
   line_inflow(*s, bd);
-  rt_status st = upload(s, s->bdry, bd.data(), bd.size() * sizeof(double));
-  if (st) return st;
-  HIP_TRY(s, hipStreamSynchronize(s->stream));
-  return RT_OK;
+  return upload(s, s->bdry, bd.data(), bd.size() * sizeof(double));
 }
 
 // Segments per line: enough waves (2 Q Sg) to fill the chip at the sweep
@@ -323,10 +346,18 @@ hipError_t rtsn_detail::alloc_segments(rt_solver *h) {
   hipError_t e = dalloc(h->agg[0], sizeof(double) * 2 * h->Sg * kMaxTimeBlock * K * Lp);
   if (!e) e = dalloc(h->agg[1], sizeof(double) * 2 * h->Sg * kMaxTimeBlock * K * Lp);
   if (!e) e = dalloc(h->yseg, sizeof(double) * 2 * (h->Sg + 1) * kMaxAlignedBlock * K * Lp);
-  if (!e) e = hipMemsetAsync(h->agg[0].p, 0, h->agg[0].bytes, h->stream);
-  if (!e) e = hipMemsetAsync(h->agg[1].p, 0, h->agg[1].bytes, h->stream);
+  h->agg_zero_pending = true;  // zeroed before the first segment pass (ensure_segments): a
+                               // wavefront-only handle never touches them
   for (bool &r : h->prop_ready) r = false;
   return e;
+}
+
+rt_status rtsn_detail::ensure_segments(rt_solver *s) {
+  if (!s->agg_zero_pending) return RT_OK;
+  HIP_TRY(s, hipMemsetAsync(s->agg[0].p, 0, s->agg[0].bytes, s->stream));
+  HIP_TRY(s, hipMemsetAsync(s->agg[1].p, 0, s->agg[1].bytes, s->stream));
+  s->agg_zero_pending = false;
+  return RT_OK;
 }
 
 // Segments sized for the pipelined pass of the current time block (its occupancy: one

@@ -219,6 +219,15 @@ extern "C" rt_status rt_get_moments(rt_solver *s, double *phi, double *F, double
   const size_t GN = static_cast<size_t>(s->Gl) * s->p.N;
   const double *m = static_cast<const double *>(s->mom.p);
   double *dst[3] = {phi, F, phi_plus};
+  if (3 * GN <= kStagedPiece) {  // the three fields ([3][GN] in `mom`) in one transfer and one wait
+    if (rt_status st2 = ensure_staging(s, sizeof(double) * 3 * GN)) return st2;
+    HIP_TRY(s, hipMemcpyAsync(s->staging[0], m, sizeof(double) * 3 * GN, hipMemcpyDeviceToHost, s->stream));
+    HIP_TRY(s, hipEventRecord(s->staging_ev[0], s->stream));
+    HIP_TRY(s, hipEventSynchronize(s->staging_ev[0]));
+    for (int k = 0; k < 3; ++k)
+      if (dst[k]) std::memcpy(dst[k], static_cast<const double *>(s->staging[0]) + k * GN, sizeof(double) * GN);
+    return RT_OK;
+  }
   for (int k = 0; k < 3; ++k)
     if (dst[k])
       if (rt_status st2 = staged_d2h(s, dst[k], m + k * GN, GN)) return st2;

@@ -64,6 +64,7 @@ SegArgs rtsn_detail::seg_args(rt_solver *s) {
 // previous pass (agg_prev) -> yseg for the pending correction, or this pass's
 // mu < 0 half (agg_cur) -> yrefl for the reflective mu > 0 heads.
 rt_status rtsn_detail::enqueue_fold(rt_solver *s, int T, bool reflective_outflow) {
+  if (rt_status st = ensure_segments(s)) return st;
   if (rt_status st = ensure_propagators(s, T)) return st;
   FoldArgs f{};
   const int slot = reflective_outflow ? s->agg_cur : (s->agg_cur ^ 1);
@@ -119,6 +120,7 @@ static rt_status event_end(rt_solver *s, hipEvent_t e1) {
 // One pass of T full steps, every segment at the same time level.
 // coupled: the material-coupled sweep (T = 1, per-cell emission).
 rt_status rtsn_detail::enqueue_pass(rt_solver *s, int T, bool coupled) {
+  if (rt_status st = ensure_segments(s)) return st;
   if (s->pending && s->Tp != T) {
     rt_status st = apply_correction(s);
     if (st) return st;
@@ -188,6 +190,7 @@ static rt_status enqueue_steps(rt_solver *s, int nsteps) {
 // runs its last whole block -- one launch more than the drain, instead of aligned passes
 // with the cross-segment correction after it.
 static rt_status pipe_launch(rt_solver *s) {
+  if (rt_status st = ensure_segments(s)) return st;
   const int P = chain_positions(s), T = s->Tpipe;
   const long long end = s->target + s->tail;
   auto block = [&](int c) { return s->tau[c] < s->target ? T : s->tail; };

@@ -29,4 +29,15 @@ for name in ("llnl_slab_test.prm", "single_group.prm", "multi_group_equilibrium.
         if rep:
             for k, v in t.items():
                 best[k] = min(best.get(k, 1e9), v)
-    print(json.dumps({"config": name, **{k: round(1e3 * v, 4) for k, v in best.items()}}), flush=True)
+        else:
+            cold = t
+    print(json.dumps({"config": name, **{k: round(1e3 * v, 4) for k, v in best.items()},
+                      "first_run": {k: round(1e3 * v, 4) for k, v in cold.items()}}), flush=True)
+    # host-only parts of rt_create: the Planck group table (rt_planck_groups) for the .prm's groups
+    if ph.params.get("group_bounds") is not None:
+        ts = []
+        for _ in range(5):
+            t0 = time.perf_counter()
+            rtsn.planck_groups(ph.params["T"], ph.params["group_bounds"])
+            ts.append(time.perf_counter() - t0)
+        print(json.dumps({"config": name, "host_planck_ms": round(1e3 * min(ts), 4)}), flush=True)
