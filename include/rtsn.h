@@ -262,6 +262,11 @@ rt_status rt_get_wavefront(rt_solver *s, int *mode, int *active, int *cells_per_
  * 512 cells).  The chain's lanes per line are ceil(N / C); replaces nothing in the reference
  * (its sweep is serial, solver.cpp:700-717). */
 rt_status rt_set_wavefront_waves(rt_solver *s, int max_waves);
+/* Cells per lane of the chain (1, 2, 4, 8; 0 = wavefront_plan's choice, the default): the
+ * chain then spans ceil(lanes / 64) waves, and a choice whose chain would exceed max_waves
+ * falls back to the plan's.  For measuring the plan's crossovers (tools/chain_plan.py);
+ * bitwise-identical results. */
+rt_status rt_set_wavefront_cells(rt_solver *s, int cells_per_lane);
 /* *max_waves as set; *waves_per_chain: this handle's chain (0: too long).  NULLs skipped. */
 rt_status rt_get_wavefront_waves(rt_solver *s, int *max_waves, int *waves_per_chain);
 /* Waves per segment of a pipelined BDF2 pass of 8, 10, 12, 16 or 20 steps: 1 runs

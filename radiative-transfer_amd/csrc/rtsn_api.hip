@@ -298,6 +298,18 @@ extern "C" rt_status rt_set_wavefront_waves(rt_solver *s, int max_waves) {
   return RT_OK;
 }
 
+extern "C" rt_status rt_set_wavefront_cells(rt_solver *s, int cells_per_lane) {
+  if (!s) return fail(nullptr, RT_ERR_ARG, "rt_set_wavefront_cells: NULL handle");
+  if (cells_per_lane != 0 && cells_per_lane != 1 && cells_per_lane != 2 && cells_per_lane != 4 && cells_per_lane != 8)
+    return fail(s, RT_ERR_ARG, "rt_set_wavefront_cells: 0 (the plan's), 1, 2, 4 or 8");
+  if (s->wqueued) {  // steps queued for the current chain plan run on it first
+    HIP_TRY(s, hipSetDevice(s->device));
+    if (rt_status st = wave_flush(s)) return st;
+  }
+  s->wave_cells = cells_per_lane;
+  return RT_OK;
+}
+
 extern "C" rt_status rt_get_wavefront_waves(rt_solver *s, int *max_waves, int *waves_per_chain) {
   if (!s) return fail(nullptr, RT_ERR_ARG, "rt_get_wavefront_waves: NULL handle");
   if (max_waves) *max_waves = s->wave_max;

@@ -228,6 +228,7 @@ struct rt_solver {
   bool pipe_set = false;         // the caller chose the schedule (rt_set_pipeline)
   int wave = 1;                  // short lines, one launch per advance (rt_set_wavefront): 0 off, 1 auto, 2 on
   int wave_max = kWaveMaxWaves;  // waves a wavefront chain may span (rt_set_wavefront_waves)
+  int wave_cells = 0;            // cells per lane of the chain: 0 the plan's, else 1, 2, 4, 8 (rt_set_wavefront_cells)
   std::vector<long long> tau;    // full steps completed per chain position
   long long target = 0;          // full steps every position must reach
   long long pipe_base = 0;       // tau of every position when the pipeline started

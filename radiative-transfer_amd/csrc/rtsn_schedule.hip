@@ -327,7 +327,13 @@ rt_status rtsn_detail::finalize(rt_solver *s) {
 // workgroup's chain and the caller chose neither a time block nor a schedule, always with
 // rt_set_wavefront 2.
 WavePlan rtsn_detail::wave_plan(const rt_solver *s) {
-  return wavefront_plan(s->p.N, s->p.bc_left_indicator == 2, s->wave_max);
+  const bool refl = s->p.bc_left_indicator == 2;
+  if (s->wave_cells) {  // the caller's cells per lane, where the chain then fits wave_max waves
+    const int C = s->wave_cells, lanes = (s->p.N + C - 1) / C;
+    const int waves = ((refl ? 2 * lanes : lanes) + 63) / 64;
+    if (waves <= s->wave_max) return WavePlan{C, waves, lanes};
+  }
+  return wavefront_plan(s->p.N, refl, s->wave_max);
 }
 
 // Auto (mode 1) takes a chain of several waves while the chains need at most two waves per

@@ -127,6 +127,7 @@ def lib():
         L.rt_get_wavefront.argtypes = [vp, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)]
         L.rt_set_wavefront_waves.argtypes = [vp, C.c_int]
         L.rt_get_wavefront_waves.argtypes = [vp, C.POINTER(C.c_int), C.POINTER(C.c_int)]
+        L.rt_set_wavefront_cells.argtypes = [vp, C.c_int]
         L.rt_material_enable.argtypes = [vp, C.c_double, dp]
         L.rt_material_sweep.argtypes = [vp, vp]
         L.rt_material_update.argtypes = [vp, vp]
@@ -573,6 +574,10 @@ class Solver:
     @wavefront_waves.setter
     def wavefront_waves(self, n):
         _check(lib().rt_set_wavefront_waves(self._h, int(n)), "rt_set_wavefront_waves", self._h)
+
+    def set_wavefront_cells(self, c: int):
+        """Cells per lane of the wavefront chain (rt_set_wavefront_cells): 0 the plan's, 1, 2, 4, 8."""
+        _check(lib().rt_set_wavefront_cells(self._h, int(c)), "rt_set_wavefront_cells", self._h)
 
     def wavefront_state(self) -> dict:
         """{"mode", "active" (the next advance takes the wavefront), "cells_per_lane" (0: too

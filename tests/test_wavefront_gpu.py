@@ -201,3 +201,29 @@ def test_wavefront_deferred_small_advances(rtsn_mod, oracle_mod, N, bc_left):
         if done < steps:
             s.advance(steps - done)
         assert np.array_equal(s.ends(), ref)
+
+
+@pytest.mark.parametrize("N,bc_left", [(300, 0), (300, 2), (700, 0), (129, 2), (1000, 1)])
+@pytest.mark.parametrize("ts", [2, 3])
+def test_wavefront_cells_choice_bitwise(rtsn_mod, oracle_mod, N, bc_left, ts):
+    """rt_set_wavefront_cells: every cells-per-lane choice (one wave, or chains of 2-8 waves;
+    a choice past the wave cap falls back to the plan's) runs the same arithmetic per (cell,
+    level): the node arrays after 40 steps from a random state are bitwise equal."""
+    p, q = _params(oracle_mod, N, ts, bc_left, 1 if bc_left == 2 else bc_left)
+    lo, hi = 20, 26
+    B = oracle_mod.OracleSolver(p, g_lo=lo, g_hi=hi).groups()["B"][lo:hi]
+    ends0 = _random_ends(q, lo, hi, B, 77 + N + ts)
+    out, seen = [], set()
+    for C in (0, 1, 2, 4, 8):
+        with rtsn_mod.Solver(q, g_lo=lo, g_hi=hi) as s:
+            s.wavefront = 2
+            s.set_wavefront_cells(C)
+            st = s.wavefront_state()
+            assert st["active"]
+            seen.add((st["cells_per_lane"], st["waves"]))
+            s.set_ends(ends0)
+            s.advance(40)
+            out.append(s.ends())
+    assert len(seen) >= 2
+    for o in out[1:]:
+        assert np.array_equal(out[0], o)
