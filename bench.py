@@ -1003,8 +1003,14 @@ def main():
                                             f"{5.994 if other == 'corr' else 0.0}, v/c correction "
                                             f"{'on' if other == 'corr' else 'inactive'}), same timing", dirs)
     if args.material_steps > 0:
-        line["material"] = run_material(p, info, world, device, local, args.material_steps, dirs, rank,
-                                        comm, comm_error)
+        try:
+            line["material"] = run_material(p, info, world, device, local, args.material_steps, dirs, rank,
+                                            comm, comm_error)
+        except rtsn.RtError as e:  # an rt_comm wait expired or RCCL failed: the side leg is skipped
+            if comm is not None:   # (every rank raises: the collectives are the same on all)
+                comm.close()
+                comm = None
+            line["material"] = {"skipped": ("timeout: " if e.status == 7 else "") + str(e)}
     if comm is not None:
         comm.close()
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -322,14 +322,12 @@ inline int fill_level_waves(const rt_solver *s, int grid) {
   return best;
 }
 
-// Waves per segment for a drain launch carrying the run's remainder as a tail block
-// (launch_split_tail; any split is bitwise the same), or 0 when the pipeline cannot:
-// reflective chains (the mu > 0 heads take the mu < 0 outflow), other schemes, blocks
-// without a tail kernel.  complete() takes a tail of at least T / waves steps, so that wave
-// 0 (which streams the rows in) runs the plain body.
 // Waves of the tail launch (launch_split_tail): the most waves with a tail kernel for T,
 // whatever rt_set_level_waves fixed for the whole blocks -- the split of the shortest tails
-// that can ride the drain (T / waves levels), and a layout the whole blocks share.
+// that can ride the drain (T / waves levels), and a layout the whole blocks share; 0 when
+// the pipeline cannot carry a tail: reflective chains (the mu > 0 heads take the mu < 0
+// outflow), other schemes, blocks without a tail kernel.  complete() takes a tail of at
+// least T / waves steps, so that wave 0 (which streams the rows in) runs the plain body.
 inline int tail_waves(const rt_solver *s, int T) {
   if (s->scheme != SCHEME_BDF2 || s->p.bc_left_indicator == 2) return 0;
   for (int k : {4, 2})

@@ -189,6 +189,24 @@ static rt_status enqueue_steps(rt_solver *s, int nsteps) {
 // blocks): position c runs it once position c - 1 has, in the launch where position c + 1
 // runs its last whole block -- one launch more than the drain, instead of aligned passes
 // with the cross-segment correction after it.
+// Positions per launch of the fill and drain ramps (round 5).  A ramp launch of k < P
+// positions takes four waves per segment (fill_level_waves), and at two 4-wave workgroups per
+// CU the chip holds the workgroups of m = resident / (workgroups per position) positions:
+// beyond m (the SL slab's T = 20 pipeline: m = 4 of 8 positions) the rest ran as a second
+// round on half the SIMDs (k = 5 / 6: 149 / 151 ms against shares of 104 / 125 ms,
+// profiles/r04ag_trace_summary.json).  Positions of one launch never exchange data (each
+// reads what its predecessor published in the previous launch), so such a launch is cut into
+// consecutive launches of at most m positions, each with its own waves per segment.  The
+// full launch (k = P), a caller-set level split and other schemes keep one launch.
+static int ramp_chunk(const rt_solver *s, int k, int grid_per_pos) {
+  const int T = s->Tpipe, P = chain_positions(s);
+  if (k >= P || s->level_waves || s->scheme != SCHEME_BDF2 || !split_block(T) || T % 4) return k;
+  int wpc = 0;
+  if (split_occupancy(T, 4, &wpc) != hipSuccess || wpc < 1) return k;
+  const long long m = static_cast<long long>(wpc) * s->cus / grid_per_pos;
+  return m >= 1 && m < k ? static_cast<int>(m) : k;
+}
+
 static rt_status pipe_launch(rt_solver *s) {
   if (rt_status st = ensure_segments(s)) return st;
   const int P = chain_positions(s), T = s->Tpipe;
@@ -206,27 +224,32 @@ static rt_status pipe_launch(rt_solver *s) {
   for (int c = lo; c <= hi; ++c)
     if (s->tau[c] != s->tau[lo] - static_cast<long long>(c - lo) * T || (c > lo && block(c) != T))
       return fail(s, RT_ERR_PARAM, "pipeline: positions out of step");
-  SegArgs a = seg_args(s);
-  a.aggs[0] = static_cast<double *>(s->agg[0].p);
-  a.aggs[1] = static_cast<double *>(s->agg[1].p);
-  a.pending = 0;
-  a.pos_lo = lo;
-  a.npos = hi - lo + 1;
-  a.pass_lo = static_cast<int>(((s->tau[lo] - s->pipe_base) / T) & 1);
-  const int grid = (a.reflective ? 1 : 2) * a.npos * s->Q;
-  a.level_waves = fill_level_waves(s, grid);
-  a.tail_levels = block(lo) == T ? 0 : s->tail;
-  hipEvent_t e1;
-  rt_status st = event_begin(s, &e1);
-  if (st) return st;
-  if (a.tail_levels) {
-    a.level_waves = tail_waves(s, T);  // (complete: wave 0 runs whole levels)
-    HIP_TRY(s, launch_split_tail(T, a.level_waves, a, grid, s->stream));
-  } else {
-    HIP_TRY(s, launch_sweep(s->scheme, T, SWEEP_PIPELINED, a, grid, s->stream));
+  const int per_pos = (s->p.bc_left_indicator == 2 ? 1 : 2) * s->Q;  // workgroups per position
+  const int m = ramp_chunk(s, hi - lo + 1, per_pos);
+  for (int c0 = lo; c0 <= hi; c0 += m) {
+    const int c1 = std::min(hi, c0 + m - 1);
+    SegArgs a = seg_args(s);
+    a.aggs[0] = static_cast<double *>(s->agg[0].p);
+    a.aggs[1] = static_cast<double *>(s->agg[1].p);
+    a.pending = 0;
+    a.pos_lo = c0;
+    a.npos = c1 - c0 + 1;
+    a.pass_lo = static_cast<int>(((s->tau[c0] - s->pipe_base) / T) & 1);
+    const int grid = a.npos * per_pos;
+    a.level_waves = fill_level_waves(s, grid);
+    a.tail_levels = block(c0) == T ? 0 : s->tail;  // only the first position can run the tail
+    hipEvent_t e1;
+    rt_status st = event_begin(s, &e1);
+    if (st) return st;
+    if (a.tail_levels) {
+      a.level_waves = tail_waves(s, T);  // (complete: wave 0 runs whole levels)
+      HIP_TRY(s, launch_split_tail(T, a.level_waves, a, grid, s->stream));
+    } else {
+      HIP_TRY(s, launch_sweep(s->scheme, T, SWEEP_PIPELINED, a, grid, s->stream));
+    }
+    if ((st = event_end(s, e1))) return st;
   }
   ++s->state_version;
-  if ((st = event_end(s, e1))) return st;
   for (int c = lo; c <= hi; ++c) s->tau[c] += block(c);
   return RT_OK;
 }

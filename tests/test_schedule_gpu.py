@@ -178,3 +178,32 @@ def test_moments_producer_consumer_bitwise(rtsn_mod, oracle_mod, monkeypatch, M,
     for a, b in zip(out[1], orc.moments()):
         scale = np.maximum(np.abs(b).max(axis=1, keepdims=True), 1e-300)
         assert (np.abs(a - b) / scale).max() <= 1e-13
+
+
+def test_ramp_launches_cut_into_rounds(rtsn_mod, oracle_mod):
+    """Ramp launches of more positions than one round of four-wave workgroups holds (128 groups
+    x S64: 128 workgroups per position, 4 positions per round on 256 CUs) run as consecutive
+    launches of at most a round's positions (ramp_chunk); positions never exchange data
+    within a launch, so the node array equals the one-launch ramps' (level_waves 4, and 2)
+    bitwise, through the fill and the drain of 10 passes over 16 positions."""
+    import sys
+    from conftest import REPO
+    sys.path.insert(0, str(REPO))
+    import bench
+    p = dict(bench.slab_params(128, "v0", N=2000, M=64), dt=1e-9)
+    rng = np.random.default_rng(5)
+    out = {}
+    for lw in (0, 4, 2):
+        with rtsn_mod.Solver(p) as s:
+            s.time_block = 20
+            s.pipeline = 2
+            s.set_segmentation(8)
+            s.level_waves = lw
+            assert s.sweep_geometry()[1] >= 10
+            if lw == 0:
+                ends = rng.uniform(0.5, 1.5, size=(64, 128, 2000, 2)) * 1e-3
+            s.set_ends(ends)
+            s.advance(200)
+            out[lw] = s.ends()
+    assert np.isfinite(out[0]).all()
+    assert np.array_equal(out[0], out[4]) and np.array_equal(out[0], out[2])
