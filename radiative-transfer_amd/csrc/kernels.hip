@@ -662,25 +662,32 @@ __global__ void __launch_bounds__(64) moments_kernel(const double2 *__restrict__
   }
 }
 
-// Producer/consumer moments (round 5): the same sums, bitwise, from a workgroup of three
+// Producer/consumer moments (round 5): the same sums, bitwise, from a workgroup of five
 // waves with fixed roles.  An item is (cell c, 64 groups): half 0's row k = N-1-c and half
-// 1's row k = c, each a contiguous run of 64 H lines (l = i' + H g).  Loader wave h streams
-// half h's run with lane-contiguous 16-byte nt loads (1 KiB per instruction, as the state
-// scan reads) into a register ring of the H loads of one item, so the loads of item p + 1
-// are in flight while item p's values are converted to psi = (e_in + e_out) / 2 and written
-// to an LDS slot [half][group][i'] (row stride H + 1 doubles: conflict-free); its only waits
-// are on its own oldest load.  The summing wave (lane = group) takes the previous item's slot
-// and runs the three sums over i = 0 .. M-1 in the reference's order (solver.cpp:191-237,
-// no FMA contraction; w psi computed once for phi and phi_plus, mu w as one product, as
-// moments_kernel).  The three waves meet at one barrier per item (LDS writes and reads
-// drained, lgkmcnt(0); the barrier itself does not wait for the loads in flight), two slots
-// alternating.  Lines past the item's groups read as zero through the descriptor's bound.
+// 1's row k = c, each a contiguous run of 64 H lines (l = i' + H g).  Four loader waves
+// (two per half, half the run's 1 KiB load instructions each) stream the runs with
+// lane-contiguous 16-byte nt loads, as the state scan reads, into a register ring two items
+// deep: while item p's values are converted to psi = (e_in + e_out) / 2 and written to an LDS
+// slot [half][group][i'] (row stride H + 1 doubles: conflict-free), the loads of items p + 1
+// and p + 2 are in flight, and a loader's only waits are on its own oldest load.  The
+// summing wave (lane = group) takes the previous item's slot and runs the three sums over
+// i = 0 .. M-1 in the reference's order (solver.cpp:191-237, no FMA contraction; w psi
+// computed once for phi and phi_plus, mu w as one product, as moments_kernel).  The five
+// waves meet at one barrier per item (LDS traffic drained, lgkmcnt(0); the barrier does not
+// wait for the loads in flight), two slots alternating.  Lines past the item's groups, and
+// items past the workgroup's last, read as zero through the descriptor's bound (no traffic).
+// Bytes in flight per CU (two workgroups: 68.6 KB of LDS each, <= 168 VGPRs for three waves
+// per SIMD): 4 x 2 x 32 KB = 256 KB -- the first form (one loader per half, one item deep,
+// 128 KB) read at 5.94 TB/s (22.1 ms on SL, profiles/r05b_*), the state scan at 6.86.
+constexpr int kMomLoadersPerHalf = 2;
 template <int H>
-__global__ void __launch_bounds__(192) moments_pc_kernel(const double2 *__restrict__ E, const double *__restrict__ mu,
+__global__ void __launch_bounds__(320) moments_pc_kernel(const double2 *__restrict__ E, const double *__restrict__ mu,
                                                          const double *__restrict__ wt, double *phi, double *F,
                                                          double *phi_plus, LineMap m) {
 #pragma clang fp contract(off)
-  static_assert(64 % H == 0 && H >= 8, "a load of 64 lines covers whole groups");
+  constexpr int NL = kMomLoadersPerHalf;
+  static_assert(64 % H == 0 && H % NL == 0 && H >= 8, "a load of 64 lines covers whole groups");
+  constexpr int R = H / NL;             // loads per item of one loader
   constexpr int ST = H + 1;             // doubles per group row in a slot
   constexpr int SLOT = 2 * 64 * ST;     // one item: [half][64 groups][ST]
   __shared__ double lds[2 * SLOT + 4 * H];  // two slots, then (w_i, mu_i w_i) for i < 2H
@@ -691,6 +698,7 @@ __global__ void __launch_bounds__(192) moments_pc_kernel(const double2 *__restri
   const long long items = static_cast<long long>(m.N) * nchunks;
   const long long first = blockIdx.x, step = gridDim.x;
   const long long mine = first < items ? (items - 1 - first) / step + 1 : 0;  // this workgroup's items
+  const long long phases = (mine + 1) & ~1LL;  // loaders run whole pairs of items (a zero item pads)
   for (int i = threadIdx.x; i < 2 * H; i += blockDim.x) {
     wl[2 * i] = wt[i];
     wl[2 * i + 1] = mu[i] * wt[i];
@@ -700,8 +708,8 @@ __global__ void __launch_bounds__(192) moments_pc_kernel(const double2 *__restri
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
     __builtin_amdgcn_s_barrier();
   };
-  if (wave < 2) {  // loader of half `wave`
-    const int h = wave;
+  if (wave < 2 * NL) {  // loader `part` of half h: the run's loads r = part R .. part R + R - 1
+    const int h = wave / NL, part = wave % NL;
     const auto rsrc = [&](long long p) {  // item p's run in half h; past the last item: no records
       if (p >= mine) return __builtin_amdgcn_make_buffer_rsrc(const_cast<double2 *>(E), 0, 0, 0x00020000);
       const long long it = first + p * step;
@@ -711,44 +719,55 @@ __global__ void __launch_bounds__(192) moments_pc_kernel(const double2 *__restri
       return __builtin_amdgcn_make_buffer_rsrc(const_cast<double2 *>(row), 0, ng * H * 16, 0x00020000);
     };
     const int voff = lane * 16;
-    double2 v[H];
+    double2 v0[R], v1[R];  // the ring: items p (v0) and p + 1 (v1), p even
     {
-      const __amdgpu_buffer_rsrc_t R = rsrc(0);
+      const __amdgpu_buffer_rsrc_t R0 = rsrc(0), R1 = rsrc(1);
 #pragma unroll
-      for (int r = 0; r < H; ++r) {  // in ring order (the loop's waits count on it)
-        v[r] = row_load(R, voff, r * 1024);
+      for (int r = 0; r < R; ++r) {  // in ring order (the loop's waits count on it)
+        v0[r] = row_load(R0, voff, (part * R + r) * 1024);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        v1[r] = row_load(R1, voff, (part * R + r) * 1024);
         __builtin_amdgcn_sched_barrier(0);
       }
     }
-    double *const base = lds + h * 64 * ST + (lane / H) * ST + lane % H;
-    for (long long p = 0; p < mine; ++p) {
+    // line lane + 64 (part R + r): group lane / H + (64 / H)(part R + r), i' = lane % H
+    double *const base = lds + h * 64 * ST + (lane / H) * ST + lane % H + (64 / H) * part * R * ST;
+    const auto consume = [&](double2 (&v)[R], long long p) {  // item p in, item p + 2 issued
       double *const slot = base + (p & 1) * SLOT;
-      const __amdgpu_buffer_rsrc_t Rn = rsrc(p + 1);
+      const __amdgpu_buffer_rsrc_t Rn = rsrc(p + 2);
 #pragma unroll
-      for (int r = 0; r < H; ++r) {  // line lane + 64 r: group lane / H + 64 r / H, i' = lane % H
+      for (int r = 0; r < R; ++r) {
         slot[(64 / H) * r * ST] = 0.5 * (v[r].x + v[r].y);
-        v[r] = row_load(Rn, voff, r * 1024);
+        v[r] = row_load(Rn, voff, (part * R + r) * 1024);
         __builtin_amdgcn_sched_barrier(0);  // a rolling ring: each load waits only for the oldest
       }
+    };
+    for (long long p = 0; p < phases; p += 2) {
+      consume(v0, p);
+      sync();
+      consume(v1, p + 1);
       sync();
     }
     sync();  // the summing wave's last item
   } else {  // the summing wave: lane = group of the item
-    for (long long p = 0; p <= mine; ++p) {
-      if (p > 0) {
+    for (long long p = 0; p <= phases; ++p) {
+      if (p > 0 && p - 1 < mine) {
         const long long it = first + (p - 1) * step;
         const int c = static_cast<int>(it / nchunks), g0 = static_cast<int>(it % nchunks) * 64;
         const double *s0 = lds + ((p - 1) & 1) * SLOT + lane * ST;
         const double *s1 = s0 + 64 * ST;
         double sphi = 0.0, sF = 0.0, splus = 0.0;
-#pragma unroll
+#pragma unroll 8
         for (int i = 0; i < H; ++i) {  // mu < 0: i' = H - 1 - i
           const double q = s0[H - 1 - i];
           const double wq = wl[2 * i] * q;
           sphi += wq;
           sF += wl[2 * i + 1] * q;
         }
-#pragma unroll
+#pragma unroll 8
         for (int i = 0; i < H; ++i) {  // mu > 0: i = H + i'
           const double q = s1[i];
           const double wq = wl[2 * (H + i)] * q;
@@ -1684,16 +1703,17 @@ hipError_t launch_moments(const double2 *E, const double *mu, const double *wt, 
                                      resident_blocks(moments_kernel<true, 8>, 64),
                                      resident_blocks(moments_kernel<true, W>, 64)};
   if (!getenv_moments_legacy() && (m.H == 8 || m.H == 16 || m.H == 32)) {  // producer/consumer form
-    static const size_t pc[3] = {resident_blocks(moments_pc_kernel<8>, 192), resident_blocks(moments_pc_kernel<16>, 192),
-                                 resident_blocks(moments_pc_kernel<32>, 192)};
+    constexpr int TH = 64 * (2 * kMomLoadersPerHalf + 1);
+    static const size_t pc[3] = {resident_blocks(moments_pc_kernel<8>, TH), resident_blocks(moments_pc_kernel<16>, TH),
+                                 resident_blocks(moments_pc_kernel<32>, TH)};
     const int k = m.H == 8 ? 0 : (m.H == 16 ? 1 : 2);
     const dim3 g(static_cast<unsigned>(tasks < pc[k] ? tasks : pc[k]));
     if (m.H == 8)
-      hipLaunchKernelGGL((moments_pc_kernel<8>), g, dim3(192), 0, st, E, mu, wt, phi, F, phi_plus, m);
+      hipLaunchKernelGGL((moments_pc_kernel<8>), g, dim3(TH), 0, st, E, mu, wt, phi, F, phi_plus, m);
     else if (m.H == 16)
-      hipLaunchKernelGGL((moments_pc_kernel<16>), g, dim3(192), 0, st, E, mu, wt, phi, F, phi_plus, m);
+      hipLaunchKernelGGL((moments_pc_kernel<16>), g, dim3(TH), 0, st, E, mu, wt, phi, F, phi_plus, m);
     else
-      hipLaunchKernelGGL((moments_pc_kernel<32>), g, dim3(192), 0, st, E, mu, wt, phi, F, phi_plus, m);
+      hipLaunchKernelGGL((moments_pc_kernel<32>), g, dim3(TH), 0, st, E, mu, wt, phi, F, phi_plus, m);
     return hipGetLastError();
   }
   const int kind = m.H % W == 0 ? 2 : (m.H % 8 == 0 ? 1 : 0);

@@ -186,12 +186,18 @@ def _check(st: int, what: str, handle=None):
         raise RtError(st, f"{what} ({msg})")
 
 
+_DEFAULTS = None
+
+
 def params_default() -> dict:
-    p = rt_params()
-    lib().rt_params_default(C.byref(p))
-    d = {f: getattr(p, f) for f in _SCALARS}
-    d.update(psi_source=None, group_bounds=None, group_kappa=None)
-    return d
+    """rt_params_default as a dict (a fresh copy; the library's values are read once)."""
+    global _DEFAULTS
+    if _DEFAULTS is None:
+        p = rt_params()
+        lib().rt_params_default(C.byref(p))
+        _DEFAULTS = {f: getattr(p, f) for f in _SCALARS}
+        _DEFAULTS.update(psi_source=None, group_bounds=None, group_kappa=None)
+    return dict(_DEFAULTS)
 
 
 def quadrature(M: int):
