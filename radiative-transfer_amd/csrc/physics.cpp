@@ -7,7 +7,11 @@
 #include <algorithm>
 #include <cfloat>
 #include <cmath>
+#include <atomic>
+#include <condition_variable>
+#include <functional>
 #include <limits>
+#include <mutex>
 #include <thread>
 #include <vector>
 
@@ -22,6 +26,73 @@ static int host_threads() {
   if (sched_getaffinity(0, sizeof(set), &set) == 0) n = CPU_COUNT(&set);
   return std::max(1, std::min(n, 8));
 }
+
+// Persistent host workers for rt_create's setup loops: started on first use and kept for the
+// process (a thread start costs 30-40 us, which the per-create work of a .prm-sized handle
+// does not amortise); a job wakes them, the caller takes a share, and run() returns when
+// every index is done.  One job at a time.
+namespace {
+class HostPool {
+ public:
+  static HostPool &get() {
+    static HostPool *pool = new HostPool(host_threads() - 1);  // never destroyed: workers sleep at exit
+    return *pool;
+  }
+  int size() const { return static_cast<int>(workers_.size()) + 1; }
+  void run(int n, const std::function<void(int)> &fn) {
+    std::lock_guard<std::mutex> one(job_m_);
+    if (workers_.empty() || n <= 1) {
+      for (int i = 0; i < n; ++i) fn(i);
+      return;
+    }
+    {
+      std::lock_guard<std::mutex> lk(m_);
+      fn_ = &fn;
+      n_ = n;
+      next_.store(0);
+      busy_ = static_cast<int>(workers_.size());
+      ++gen_;
+    }
+    cv_.notify_all();
+    drain();
+    std::unique_lock<std::mutex> lk(m_);
+    done_.wait(lk, [&] { return busy_ == 0; });
+    fn_ = nullptr;
+  }
+
+ private:
+  explicit HostPool(int workers) {
+    for (int w = 0; w < workers; ++w) workers_.emplace_back([this] { loop(); });
+    for (std::thread &t : workers_) t.detach();
+  }
+  void drain() {
+    for (int i = next_.fetch_add(1); i < n_; i = next_.fetch_add(1)) (*fn_)(i);
+  }
+  void loop() {
+    unsigned long long seen = 0;
+    for (;;) {
+      {
+        std::unique_lock<std::mutex> lk(m_);
+        cv_.wait(lk, [&] { return gen_ != seen; });
+        seen = gen_;
+      }
+      drain();
+      std::lock_guard<std::mutex> lk(m_);
+      if (--busy_ == 0) done_.notify_one();
+    }
+  }
+  std::vector<std::thread> workers_;
+  std::mutex job_m_, m_;
+  std::condition_variable cv_, done_;
+  const std::function<void(int)> *fn_ = nullptr;
+  int n_ = 0, busy_ = 0;
+  std::atomic<int> next_{0};
+  unsigned long long gen_ = 0;
+};
+}  // namespace
+
+int host_workers() { return HostPool::get().size(); }
+void parallel_for(int n, const std::function<void(int)> &fn) { HostPool::get().run(n, fn); }
 
 double rad_a_long() {
   return (8.0 * std::pow(kPi, 5) * std::pow(kBoltzmann, 4)) /
@@ -121,7 +192,7 @@ double PlanckIntegrator::gauss(double T, double mid, double half_width, bool dT)
 // Bose series of the integral from z1 to z2 (Planck.cpp:94-118, 170-193):
 // the number of terms is the first n > 32 whose next term drops below the
 // accuracy relative to the leading term.
-double PlanckIntegrator::tail_series(double z1, double z2, bool dT) const {
+int PlanckIntegrator::series_terms(double z1, bool dT) const {
   int n_terms = 32;
   double lead = dT ? std::exp(-z1) * (std::pow(z1, 4.0) + 4.0 * std::pow(z1, 3.0) + 12.0 * z1 * z1 + 24.0 * z1 + 24.0)
                    : std::exp(-z1) * (z1 * z1 * z1 + 3.0 * z1 * z1 + 6.0 * z1 + 6.0);
@@ -139,64 +210,79 @@ double PlanckIntegrator::tail_series(double z1, double z2, bool dT) const {
     else
       break;
   }
-  // pow(n, 4.0) of an integer n < 2^13 is exact (n^4 < 2^53 and libm's pow errs by < 1 ulp,
-  // so it returns the representable exact value): the product n n n n, bitwise the same
+  return n_terms;
+}
+
+// Term n of the series at z, the reference's expression.  pow(n, 4.0) of an integer
+// n < 2^13 is exact (n^4 < 2^53 and libm's pow errs by < 1 ulp, so it returns the
+// representable exact value): the product n n n n, bitwise the same.
+double PlanckIntegrator::series_term(int n, double z, bool dT) {
+  const double dn = n, n4 = dn * dn * dn * dn;
+  if (dT)
+    return std::exp(-n * z) / n4 *
+           (std::pow(n * z, 4.0) + 4.0 * std::pow(n * z, 3.0) + 12.0 * std::pow(n * z, 2.0) + 24.0 * n * z + 24.0);
+  return std::exp(-n * z) / n4 * (std::pow(n * z, 3.0) + 3.0 * std::pow(n * z, 2.0) + 6.0 * n * z + 6.0);
+}
+
+// The terms 1 .. n at z from the cache c (recomputed when it holds another z, extended when
+// it holds fewer).
+const std::vector<double> &PlanckIntegrator::terms(Terms &c, double z, int n, bool dT) const {
+  if (c.z != z) {
+    c.z = z;
+    c.b.assign(1, 0.0);
+    c.d.assign(1, 0.0);
+  }
+  std::vector<double> &t = dT ? c.d : c.b;
+  for (int k = static_cast<int>(t.size()); k <= n; ++k) t.push_back(series_term(k, z, dT));
+  return t;
+}
+
+double PlanckIntegrator::tail_series(double z1, double z2, bool dT, Terms *c1, Terms *c2) const {
+  const int n_terms = series_terms(z1, dT);
+  Terms l1, l2;
+  const std::vector<double> &t1 = terms(c1 ? *c1 : l1, z1, n_terms, dT);
+  const std::vector<double> &t2 = terms(c2 ? *c2 : l2, z2, n_terms, dT);
   double s1 = 0.0, s2 = 0.0;
-  for (int n = n_terms; n > 0; --n) {
-    const double dn = n, n4 = dn * dn * dn * dn;
-    if (dT) {
-      s1 += std::exp(-n * z1) / n4 *
-            (std::pow(n * z1, 4.0) + 4.0 * std::pow(n * z1, 3.0) + 12.0 * std::pow(n * z1, 2.0) + 24.0 * n * z1 + 24.0);
-      s2 += std::exp(-n * z2) / n4 *
-            (std::pow(n * z2, 4.0) + 4.0 * std::pow(n * z2, 3.0) + 12.0 * std::pow(n * z2, 2.0) + 24.0 * n * z2 + 24.0);
-    } else {
-      s1 += std::exp(-n * z1) / n4 * (std::pow(n * z1, 3.0) + 3.0 * std::pow(n * z1, 2.0) + 6.0 * n * z1 + 6.0);
-      s2 += std::exp(-n * z2) / n4 * (std::pow(n * z2, 3.0) + 3.0 * std::pow(n * z2, 2.0) + 6.0 * n * z2 + 6.0);
-    }
+  for (int n = n_terms; n > 0; --n) {  // the reference's order: n descending
+    s1 += t1[n];
+    s2 += t2[n];
   }
   return s1 - s2;
 }
 
-// Planck.cpp:85-154: Gauss below z = 0.7, series above z = 0.5, split at 0.6.
-double PlanckIntegrator::integral_B(double T, double e_min, double e_max) const {
+// Planck.cpp:85-154 (B) and :161-229 (dB/dT): Gauss below z = 0.7, series above z = 0.5,
+// split at 0.6.  c1 / c2: term caches of the bounds (NULL: none).
+double PlanckIntegrator::integral(double T, double e_min, double e_max, bool dT, Terms *c1, Terms *c2) const {
   if (nearly_equal(T, 0.0) || nearly_equal(e_min, e_max)) return 0.0;
   const double kT = kBoltzmann * T;
   double z1 = e_min / kT;
   const double z2 = e_max / kT;
+  // the series part in the reference's expression order (B: Planck.cpp:100-103, dB/dT: :176-179)
+  const auto series = [&](double a, Terms *ca) {
+    return dT ? 2.0 * std::pow(kBoltzmann, 4.0) * std::pow(T, 3.0) * tail_series(a, z2, true, ca, c2) /
+                    (std::pow(kPlanck, 3.0) * std::pow(kLight, 2.0))
+              : 2.0 * std::pow(kBoltzmann * T, 4.0) * tail_series(a, z2, false, ca, c2) /
+                    (std::pow(kPlanck, 3.0) * std::pow(kLight, 2.0));
+  };
   double value;
   if (z2 <= 0.7) {
-    value = gauss(T, 0.5 * (e_max + e_min), 0.5 * (e_max - e_min), false);
+    value = gauss(T, 0.5 * (e_max + e_min), 0.5 * (e_max - e_min), dT);
   } else if (z1 >= 0.5) {
-    value = 2.0 * std::pow(kBoltzmann * T, 4.0) * tail_series(z1, z2, false) /
-            (std::pow(kPlanck, 3.0) * std::pow(kLight, 2.0));
+    value = series(z1, c1);
   } else {
     z1 = 0.6;
-    const double lo = gauss(T, 0.5 * (z1 * kBoltzmann * T + e_min), 0.5 * (z1 * kBoltzmann * T - e_min), false);
-    value = lo + 2.0 * std::pow(kBoltzmann * T, 4.0) * tail_series(z1, z2, false) /
-                     (std::pow(kPlanck, 3.0) * std::pow(kLight, 2.0));
+    const double lo = gauss(T, 0.5 * (z1 * kBoltzmann * T + e_min), 0.5 * (z1 * kBoltzmann * T - e_min), dT);
+    value = lo + series(z1, nullptr);
   }
   return value * 4.0 * kPi;
 }
 
-// Planck.cpp:161-229
+double PlanckIntegrator::integral_B(double T, double e_min, double e_max) const {
+  return integral(T, e_min, e_max, false, nullptr, nullptr);
+}
+
 double PlanckIntegrator::integral_dBdT(double T, double e_min, double e_max) const {
-  if (nearly_equal(T, 0.0) || nearly_equal(e_min, e_max)) return 0.0;
-  const double kT = kBoltzmann * T;
-  double z1 = e_min / kT;
-  const double z2 = e_max / kT;
-  double value;
-  if (z2 <= 0.7) {
-    value = gauss(T, 0.5 * (e_max + e_min), 0.5 * (e_max - e_min), true);
-  } else if (z1 >= 0.5) {
-    value = 2.0 * std::pow(kBoltzmann, 4.0) * std::pow(T, 3.0) * tail_series(z1, z2, true) /
-            (std::pow(kPlanck, 3.0) * std::pow(kLight, 2.0));
-  } else {
-    z1 = 0.6;
-    const double lo = gauss(T, 0.5 * (z1 * kBoltzmann * T + e_min), 0.5 * (z1 * kBoltzmann * T - e_min), true);
-    value = lo + 2.0 * std::pow(kBoltzmann, 4.0) * std::pow(T, 3.0) * tail_series(z1, z2, true) /
-                     (std::pow(kPlanck, 3.0) * std::pow(kLight, 2.0));
-  }
-  return value * 4.0 * kPi;
+  return integral(T, e_min, e_max, true, nullptr, nullptr);
 }
 
 // The G - 1 integral pairs are independent; only the remainder group's running
@@ -209,21 +295,19 @@ void PlanckIntegrator::group_integrals(double T, int G, const double *e_lo, cons
   double rest_B = rad_a_long() * kLight * std::pow(T, 4.0);
   double rest_dB = 4.0 * rad_a_long() * kLight * std::pow(T, 3.0);
   const auto work = [&](int g0, int g1) {
+    Terms lo, hi;  // the terms at z1 and z2 of the group; a group's z2 is the next group's z1
     for (int g = g0; g < g1; ++g) {
-      B[g] = integral_B(T, e_lo[g], e_hi[g]);
-      dBdT[g] = integral_dBdT(T, e_lo[g], e_hi[g]);
+      B[g] = integral(T, e_lo[g], e_hi[g], false, &lo, &hi);
+      dBdT[g] = integral(T, e_lo[g], e_hi[g], true, &lo, &hi);
+      std::swap(lo, hi);
     }
   };
   const int n = G - 1;
-  const int nt = n < 32 ? 1 : std::min(host_threads(), (n + 15) / 16);
-  if (nt <= 1) {
+  const int nt = n < 32 ? 1 : std::min(HostPool::get().size(), (n + 15) / 16);
+  if (nt <= 1)
     work(0, n);
-  } else {
-    std::vector<std::thread> pool;
-    for (int t = 1; t < nt; ++t) pool.emplace_back(work, n * t / nt, n * (t + 1) / nt);
-    work(0, n / nt);
-    for (std::thread &th : pool) th.join();
-  }
+  else
+    HostPool::get().run(nt, [&](int t) { work(n * t / nt, n * (t + 1) / nt); });
   for (int g = 0; g < n; ++g) {
     rest_B -= B[g];
     rest_dB -= dBdT[g];

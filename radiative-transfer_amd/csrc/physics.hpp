@@ -8,6 +8,7 @@
 // bit for bit on the same machine.  The O(M G N) work happens on the GPU.
 #pragma once
 
+#include <functional>
 #include <vector>
 
 #include "../../include/rtsn.h"
@@ -25,6 +26,11 @@ constexpr double kFourPi = 4.0 * kPi;
 constexpr double kRadA = 1.3653104e-2;        // jk/(cm^3-keV^4)
 constexpr double kValidationTol = 1.E-6;
 double rad_a_long();                          // Constants.h:22-23
+
+// Host setup loops on the process's persistent workers (physics.cpp): fn(i) for i in [0, n),
+// the caller taking a share; host_workers() threads in all (the caller included).
+int host_workers();
+void parallel_for(int n, const std::function<void(int)> &fn);
 
 // GLQuad::build (GLQuad.cpp:4-44): mu ascending, weights scaled to `norm`.
 void gauss_legendre(int M, double norm, double *mu, double *wt);
@@ -48,8 +54,19 @@ class PlanckIntegrator {
   }
 
  private:
+  // Bose-series terms f(n, z), n = 1 .. size - 1, of one bound z (B and dB/dT), kept so that
+  // adjacent groups, whose shared edge is one group's z2 and the next one's z1, evaluate them
+  // once (group_integrals)
+  struct Terms {
+    double z = -1.0;
+    std::vector<double> b, d;
+  };
   double gauss(double T, double mid, double half_width, bool dBdT) const;
-  double tail_series(double z1, double z2, bool dBdT) const;
+  int series_terms(double z1, bool dBdT) const;
+  static double series_term(int n, double z, bool dBdT);
+  const std::vector<double> &terms(Terms &c, double z, int n, bool dBdT) const;
+  double tail_series(double z1, double z2, bool dBdT, Terms *c1 = nullptr, Terms *c2 = nullptr) const;
+  double integral(double T, double e_min, double e_max, bool dBdT, Terms *c1, Terms *c2) const;
   long double node_[12];
   long double weight_[12];
   double accuracy_;

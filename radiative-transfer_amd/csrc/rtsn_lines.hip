@@ -2,6 +2,7 @@
 // the per-line affine cell map (cell.hpp) and the aligned schedule's segment propagators,
 // boundary inflows, and the segmentation of the lines (segment_lines / resegment).
 
+#include <atomic>
 #include <cstring>
 
 #include "rtsn_internal.hpp"
@@ -207,18 +208,25 @@ rt_status rtsn_detail::line_maps_s(rt_solver *s, bool unit_B, DeviceBuf &map_dev
   std::vector<double> lc(2 * LC_COUNT * Lp, 0.0), unit_map;
   std::vector<double> &map = unit_B ? unit_map : s->map_host;
   map.assign(2 * WN * Lp, 0.0);
-  double W[WN];
-  for (int half = 0; half < 2; ++half)
-    for (int gl = 0; gl < s->Gl; ++gl)
-      for (int ip = 0; ip < s->H; ++ip) {
-        const int i = line_direction(s->H, half, ip), g = s->g_lo + gl;
-        const size_t ell = ip + static_cast<size_t>(s->H) * gl;
-        const LineConst L = line_constants(*s, i, g, unit_B);
-        for (int n = 0; n < LC_COUNT; ++n) lc[(half * LC_COUNT + n) * Lp + ell] = L.c[n];
-        if (!cell_map<S>(L, hd, half == 0, W))
-          return fail(s, RT_ERR_PARAM, "cell map: a structurally zero coefficient is not zero");
-        for (int n = 0; n < WN; ++n) map[(half * WN + n) * Lp + ell] = W[n];
-      }
+  // lines are independent: chunks of them on the host workers (phys::parallel_for)
+  const long long lines = 2LL * s->Gl * s->H;
+  const int chunks = static_cast<int>(std::min<long long>(phys::host_workers(), (lines + 63) / 64));
+  std::atomic<bool> bad{false};
+  phys::parallel_for(chunks, [&](int t) {
+    double W[WN];
+    for (long long x = lines * t / chunks; x < lines * (t + 1) / chunks; ++x) {
+      const int half = static_cast<int>(x / (static_cast<long long>(s->Gl) * s->H));
+      const int rem = static_cast<int>(x % (static_cast<long long>(s->Gl) * s->H));
+      const int gl = rem / s->H, ip = rem % s->H;
+      const int i = line_direction(s->H, half, ip), g = s->g_lo + gl;
+      const size_t ell = ip + static_cast<size_t>(s->H) * gl;
+      const LineConst L = line_constants(*s, i, g, unit_B);
+      for (int n = 0; n < LC_COUNT; ++n) lc[(half * LC_COUNT + n) * Lp + ell] = L.c[n];
+      if (!cell_map<S>(L, hd, half == 0, W)) bad = true;
+      for (int n = 0; n < WN; ++n) map[(half * WN + n) * Lp + ell] = W[n];
+    }
+  });
+  if (bad) return fail(s, RT_ERR_PARAM, "cell map: a structurally zero coefficient is not zero");
   rt_status st;
   if ((st = upload(s, lc_dev, lc.data(), lc.size() * sizeof(double)))) return st;
   if ((st = upload(s, map_dev, map.data(), map.size() * sizeof(double)))) return st;

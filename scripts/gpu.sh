@@ -14,6 +14,7 @@
 #   pyk=SCRIPT[:ARGS]     rocprofv3 kernel trace + stats of a python script -> TAG_pyk_N/
 #   pyp=CTRS@SCRIPT[:ARGS] one rocprofv3 PMC pass (CTRS comma-separated) of a python script -> TAG_pyp_N/
 #   pyr=SCRIPT[:ARGS]     rocprofv3 runtime trace (HIP API + kernels + copies) + stats of a python script -> TAG_pyr_N/
+#   exe=PATH[:ARGS]       run a prebuilt host program (tools/), stdout -> TAG_exe_N.jsonl
 #   env=NAME:VALUE        export NAME=VALUE for the steps after it
 set -o pipefail
 export TMPDIR=/tmp
@@ -99,6 +100,13 @@ print('value', d['value'], 'n_gpus', d['n_gpus'], 'launcher', d.get('launcher'),
       python3 scripts/pmc_summary.py ${TAG}_v0_t20 gpurun_out/${TAG}_pmc_1 gpurun_out/${TAG}_pmc_2 \
         gpurun_out/${TAG}_pmc_3 gpurun_out/${TAG}_pmc_4
       cp profiles/pmc_${TAG}_v0_t20.json gpurun_out/ 2>/dev/null || true
+      ;;
+    exe)
+      prog=${arg%%:*}
+      rest=""
+      [ "$prog" != "$arg" ] && rest=$(echo "${arg#*:}" | tr ':' ' ')
+      timeout -k 10 120 ./$prog $rest > gpurun_out/${TAG}_exe_${n}.jsonl 2> $log || { tail -20 $log; exit 1; }
+      tail -5 gpurun_out/${TAG}_exe_${n}.jsonl
       ;;
     py)
       script=${arg%%:*}
