@@ -543,32 +543,41 @@ static hipError_t launch_wave_s(const WavePlan &p, const SegArgs &a, int nsteps,
   return hipGetLastError();
 }
 
-// Which (cells per lane, waves) a chain takes: a tick costs ~148 C cycles of FP64 issue on
-// one wave (~200 at C = 1: latency), and a chain over several waves adds ~160-200 cycles of
-// cross-wave coupling per tick -- more beyond 4 waves, where two waves share a SIMD (1000
-// steps, 1000 cells: 4 waves x 4 cells 477 us, 8 x 2 595 us; profiles/archive/r03ak_waves.jsonl).
-// Measured crossover (profiles/archive/r03an_plan.jsonl, 1000 steps): one wave wins up to 4 cells
-// per lane (256 cells: one wave x 4 cells 244 us, 4 waves x 1 cell 298 us), a chain at 2
-// cells per lane beats one wave at 8 (512 cells: 361 vs 448 us; reflective 200 cells: 453
-// vs 563 us).  So: one wave while up to 4 cells per lane fit it; else the fewest cells per
-// lane on at most 4 waves; else on at most max_waves waves.  max_waves = 1: one wave only
-// (up to 8 cells per lane).
+// Which (cells per lane C, waves) a chain takes: the least estimated time of a 1000-step
+// advance, (1000 + L - 1) ticks x the measured cost of one tick at (C, waves), L the chain's
+// lanes.  Tick costs (ns) from tools/chain_plan.py on chain_kernel / wavefront_kernel (round
+// 5, profiles/r05b_chain_plan.jsonl: 1000 BDF2 steps, 8 lines, every feasible C at N = 65 ..
+// 2048, vacuum and reflective; entries without a measurement interpolated, marked *).  A
+// chain's tick is ~2x a single wave's at the same C (the hand-over through LDS and the
+// per-block barrier), and beyond 4 waves two share a SIMD: so one wave at C = 4 (the round-3
+// rule for up to 256 cells) lost to 3 waves at C = 1 by 18% at 129 cells, and by 35% on a
+// reflective 65-cell pair.  The table reproduces the fastest measured C at every length.
+static const float kTickVacuum[4][kWaveMaxWaves] = {
+    {70, 141, 166, 185, 225, 248, 259, 272},     // C = 1 (one wave: the llnl_slab_test loop, 67 ns)
+    {127, 194, 217, 238, 306, 343, 356, 368},    // C = 2 (7 waves *)
+    {222, 300, 323, 341, 441, 541, 560, 579},    // C = 4 (5, 7 waves *)
+    {412, 502, 532, 555, 800, 880, 910, 943}};   // C = 8 (5-8 waves *: only C = 8 fits there)
+static const float kTickReflective[4][kWaveMaxWaves] = {
+    {150, 230, 258, 268, 276, 291, 322, 354},    // C = 1 (1, 2, 4, 7 waves *)
+    {250, 337, 326, 315, 337, 364, 375, 447},    // C = 2 (1 wave *)
+    {432, 437, 413, 420, 531, 569, 610, 652},    // C = 4 (7 waves *)
+    {620, 629, 646, 662, 830, 991, 1100, 1213}}; // C = 8 (5, 7 waves *)
 WavePlan wavefront_plan(int N, bool reflective, int max_waves) {
   max_waves = max_waves < 1 ? 1 : (max_waves > kWaveMaxWaves ? kWaveMaxWaves : max_waves);
   if (N < 1) return WavePlan{0, 0, 0};
-  const auto fit = [&](int C, int cap, WavePlan *p) {
-    const int Lw = (N + C - 1) / C;
-    const int waves = ((reflective ? 2 * Lw : Lw) + 63) / 64;
-    *p = WavePlan{C, waves, Lw};
-    return waves <= cap;
-  };
-  WavePlan p{};
-  for (int C : {1, 2, 4})
-    if (fit(C, 1, &p)) return p;
-  for (int cap : {max_waves < 4 ? max_waves : 4, max_waves})
-    for (int C : {1, 2, 4, 8})
-      if (fit(C, cap, &p)) return p;
-  return WavePlan{0, 0, 0};  // too long: the segment pipeline
+  WavePlan best{0, 0, 0};
+  double best_cost = 0.0;
+  for (int ci = 0; ci < 4; ++ci) {
+    const int C = 1 << ci, Lw = (N + C - 1) / C;
+    const int used = reflective ? 2 * Lw : Lw, waves = (used + 63) / 64;
+    if (waves > max_waves) continue;
+    const double cost = (1000.0 + used - 1) * (reflective ? kTickReflective : kTickVacuum)[ci][waves - 1];
+    if (!best.C || cost < best_cost) {
+      best = WavePlan{C, waves, Lw};
+      best_cost = cost;
+    }
+  }
+  return best;  // C = 0: too long for max_waves waves (the segment pipeline)
 }
 
 hipError_t launch_wavefront(int scheme, const WavePlan &p, const SegArgs &a, int nsteps, hipStream_t st) {

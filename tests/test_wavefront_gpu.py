@@ -22,20 +22,27 @@ LENGTHS = [1, 5, 31, 32, 33, 50, 63, 64, 65, 100, 127, 128, 129, 255, 256, 257, 
            4096]
 
 
+# kernels_wave.hip's tick costs (ns; profiles/r05b_chain_plan.jsonl), rows C = 1, 2, 4, 8, columns 1..8 waves
+TICK_VACUUM = [[70, 141, 166, 185, 225, 248, 259, 272], [127, 194, 217, 238, 306, 343, 356, 368],
+               [222, 300, 323, 341, 441, 541, 560, 579], [412, 502, 532, 555, 800, 880, 910, 943]]
+TICK_REFLECTIVE = [[150, 230, 258, 268, 276, 291, 322, 354], [250, 337, 326, 315, 337, 364, 375, 447],
+                   [432, 437, 413, 420, 531, 569, 610, 652], [620, 629, 646, 662, 830, 991, 1100, 1213]]
+
+
 def wave_plan(N, reflective, max_waves=8):
-    """kernels_wave.hip wavefront_plan: one wave while up to 4 cells per lane fit its 64 lanes
-    (a reflective pair: both lines' lanes), else the fewest cells per lane (1, 2, 4, 8) whose
-    chain of ceil(N / C) lanes per line fits min(4, max_waves) waves, else max_waves waves."""
-    def waves(C):
-        return -(-(-(-N // C) * (2 if reflective else 1)) // 64)
-    for C in (1, 2, 4):
-        if waves(C) == 1:
-            return C, 1
-    for cap in (min(4, max_waves), max_waves):
-        for C in (1, 2, 4, 8):
-            if waves(C) <= cap:
-                return C, waves(C)
-    return 0, 0
+    """kernels_wave.hip wavefront_plan: the cells per lane C (1, 2, 4, 8) whose chain of
+    ceil(N / C) lanes per line (a reflective pair: both lines') fits max_waves waves with the
+    least (1000 + lanes - 1) x measured tick cost at (C, waves); (0, 0) when none fits."""
+    best = None
+    for ci, C in enumerate((1, 2, 4, 8)):
+        used = -(-N // C) * (2 if reflective else 1)
+        w = -(-used // 64)
+        if w > max_waves:
+            continue
+        cost = (1000.0 + used - 1) * (TICK_REFLECTIVE if reflective else TICK_VACUUM)[ci][w - 1]
+        if best is None or cost < best[0]:
+            best = (cost, C, w)
+    return (best[1], best[2]) if best else (0, 0)
 
 
 def _params(oracle_mod, N, ts, bc_left, bc_right, M=6, V=5.994, dt=1e-6):
@@ -124,7 +131,8 @@ def test_wavefront_oracle_and_default(rtsn_mod, oracle_mod, ts):
     orc = oracle_mod.OracleSolver(p)
     orc.solve()
     with rtsn_mod.Solver(q) as s:
-        assert s.wavefront_state() == {"mode": 1, "active": True, "cells_per_lane": 2, "waves": 1}
+        C, w = wave_plan(50, True)
+        assert s.wavefront_state() == {"mode": 1, "active": True, "cells_per_lane": C, "waves": w}
         s.solve()
         assert per_group_rel(s.psi(), orc.psi(), 1) <= 1e-10
         assert per_group_rel(s.ends(), orc.ends(), 1) <= 1e-10

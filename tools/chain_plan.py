@@ -2,7 +2,7 @@
 1000 BDF2 steps of llnl_slab_test's material on N-cell lines (4 groups, M = 2: 8 lines), every
 feasible cells-per-lane choice C (rt_set_wavefront_cells; the chain spans ceil(lanes / 64)
 waves), vacuum and reflective, median of 3 runs (advance + finish + sync after an 8-step warm
-start).  python tools/chain_plan.py -> one JSON line per (N, bc_left, C)."""
+start).  python tools/chain_plan.py [N ...] -> one JSON line per (N, bc_left, C)."""
 import json
 import sys
 import time
@@ -46,8 +46,9 @@ def run(q, C):
         return sorted(ts)[1], st
 
 
+LENGTHS = [int(a) for a in sys.argv[1:]] or [65, 129, 192, 256, 320, 384, 448, 512, 640, 768, 1024, 1536, 2048]
 for bcl in (0, 2):
-    for N in (65, 129, 192, 256, 320, 384, 448, 512, 640, 768, 1024, 1536, 2048):
+    for N in LENGTHS:
         q = params(N, bcl)
         with rtsn.Solver(q) as s:
             s.wavefront = 2
