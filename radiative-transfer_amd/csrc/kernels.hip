@@ -674,8 +674,7 @@ __global__ void __launch_bounds__(64) moments_kernel(const double2 *__restrict__
 // i = 0 .. M-1 in the reference's order (solver.cpp:191-237, no FMA contraction; w psi
 // computed once for phi and phi_plus, mu w as one product, as moments_kernel).  The five
 // waves meet at one barrier per item (LDS traffic drained, lgkmcnt(0); the barrier does not
-// wait for the loads in flight), two slots alternating.  Lines past the item's groups, and
-// items past the workgroup's last, read as zero through the descriptor's bound (no traffic).
+// wait for the loads in flight), two slots alternating.
 // Bytes in flight per CU (two workgroups: 68.6 KB of LDS each, <= 168 VGPRs for three waves
 // per SIMD): 4 x 2 x 32 KB = 256 KB -- the first form (one loader per half, one item deep,
 // 128 KB) read at 5.94 TB/s (22.1 ms on SL, profiles/r05b_*), the state scan at 6.86.
@@ -710,26 +709,39 @@ __global__ void __launch_bounds__(320) moments_pc_kernel(const double2 *__restri
   };
   if (wave < 2 * NL) {  // loader `part` of half h: the run's loads r = part R .. part R + R - 1
     const int h = wave / NL, part = wave % NL;
-    const auto rsrc = [&](long long p) {  // item p's run in half h; past the last item: no records
-      if (p >= mine) return __builtin_amdgcn_make_buffer_rsrc(const_cast<double2 *>(E), 0, 0, 0x00020000);
+    typedef double d2v __attribute__((ext_vector_type(2)));
+    // item p's run in half h and its lines; lines past them (a partial group chunk) re-read
+    // the run's last line, and an item past the workgroup's last reads line 0 of the state:
+    // the slot rows they fill belong to no summed group or item
+    const auto run = [&](long long p, int &lim) -> const d2v * {
+      if (p >= mine) {
+        lim = 1;
+        return reinterpret_cast<const d2v *>(E);
+      }
       const long long it = first + p * step;
       const int c = static_cast<int>(it / nchunks), g0 = static_cast<int>(it % nchunks) * 64;
-      const int ng = min(64, m.Gl - g0);
-      const double2 *row = E + m.at(h, h == 0 ? m.N - 1 - c : c, H * g0);
-      return __builtin_amdgcn_make_buffer_rsrc(const_cast<double2 *>(row), 0, ng * H * 16, 0x00020000);
+      lim = min(64, m.Gl - g0) * H;
+      return reinterpret_cast<const d2v *>(E + m.at(h, h == 0 ? m.N - 1 - c : c, H * g0));
     };
-    const int voff = lane * 16;
+    // global (not buffer) loads, nt: the buffer form kept the texture addresser busy for the
+    // whole kernel (TA_BUSY 4.28e7 cycles per dispatch against 1.98e7 for the state scan's
+    // global loads of the same bytes and requests, profiles/r05d_moments_pmc.json)
+    const auto load = [&](const d2v *row, int lim, int r) {
+      const d2v v = __builtin_nontemporal_load(row + min(lane + 64 * (part * R + r), lim - 1));
+      return make_double2(v.x, v.y);
+    };
     double2 v0[R], v1[R];  // the ring: items p (v0) and p + 1 (v1), p even
     {
-      const __amdgpu_buffer_rsrc_t R0 = rsrc(0), R1 = rsrc(1);
+      int l0, l1;
+      const d2v *r0 = run(0, l0), *r1 = run(1, l1);
 #pragma unroll
       for (int r = 0; r < R; ++r) {  // in ring order (the loop's waits count on it)
-        v0[r] = row_load(R0, voff, (part * R + r) * 1024);
+        v0[r] = load(r0, l0, r);
         __builtin_amdgcn_sched_barrier(0);
       }
 #pragma unroll
       for (int r = 0; r < R; ++r) {
-        v1[r] = row_load(R1, voff, (part * R + r) * 1024);
+        v1[r] = load(r1, l1, r);
         __builtin_amdgcn_sched_barrier(0);
       }
     }
@@ -737,11 +749,12 @@ __global__ void __launch_bounds__(320) moments_pc_kernel(const double2 *__restri
     double *const base = lds + h * 64 * ST + (lane / H) * ST + lane % H + (64 / H) * part * R * ST;
     const auto consume = [&](double2 (&v)[R], long long p) {  // item p in, item p + 2 issued
       double *const slot = base + (p & 1) * SLOT;
-      const __amdgpu_buffer_rsrc_t Rn = rsrc(p + 2);
+      int ln;
+      const d2v *rn = run(p + 2, ln);
 #pragma unroll
       for (int r = 0; r < R; ++r) {
         slot[(64 / H) * r * ST] = 0.5 * (v[r].x + v[r].y);
-        v[r] = row_load(Rn, voff, (part * R + r) * 1024);
+        v[r] = load(rn, ln, r);
         __builtin_amdgcn_sched_barrier(0);  // a rolling ring: each load waits only for the oldest
       }
     };

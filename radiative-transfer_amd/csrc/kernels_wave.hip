@@ -545,23 +545,26 @@ static hipError_t launch_wave_s(const WavePlan &p, const SegArgs &a, int nsteps,
 
 // Which (cells per lane C, waves) a chain takes: the least estimated time of a 1000-step
 // advance, (1000 + L - 1) ticks x the measured cost of one tick at (C, waves), L the chain's
-// lanes.  Tick costs (ns) from tools/chain_plan.py on chain_kernel / wavefront_kernel (round
-// 5, profiles/r05b_chain_plan.jsonl: 1000 BDF2 steps, 8 lines, every feasible C at N = 65 ..
-// 2048, vacuum and reflective; entries without a measurement interpolated, marked *).  A
-// chain's tick is ~2x a single wave's at the same C (the hand-over through LDS and the
-// per-block barrier), and beyond 4 waves two share a SIMD: so one wave at C = 4 (the round-3
-// rule for up to 256 cells) lost to 3 waves at C = 1 by 18% at 129 cells, and by 35% on a
-// reflective 65-cell pair.  The table reproduces the fastest measured C at every length.
+// lanes.  Tick costs (ns, medians) from tools/chain_plan.py on chain_kernel / wavefront_kernel
+// (round 5, profiles/r05d_chain_plan.jsonl: 1000 BDF2 steps, 8 lines, every feasible C at
+// N = 16 .. 2048, vacuum and reflective; * = interpolated, no length measured there).  A
+// reflective pair whose N is not a multiple of C runs the padded kernel (the mu < 0 line's
+// padding cells pass the state through by a select): ~1.3x the tick (C = 4: 430 vs 346 ns at
+// one wave).  A chain's tick is ~2x a single wave's at the same C (the hand-over through LDS
+// and the per-block barrier), and beyond 4 waves two share a SIMD, so round 3's rule -- one
+// wave up to 4 cells per lane -- lost to 3 waves at C = 1 by 18% at 129 cells, and by 35% on
+// a reflective 65-cell pair.
 static const float kTickVacuum[4][kWaveMaxWaves] = {
-    {70, 141, 166, 185, 225, 248, 259, 272},     // C = 1 (one wave: the llnl_slab_test loop, 67 ns)
-    {127, 194, 217, 238, 306, 343, 356, 368},    // C = 2 (7 waves *)
-    {222, 300, 323, 341, 441, 541, 560, 579},    // C = 4 (5, 7 waves *)
-    {412, 502, 532, 555, 800, 880, 910, 943}};   // C = 8 (5-8 waves *: only C = 8 fits there)
-static const float kTickReflective[4][kWaveMaxWaves] = {
-    {150, 230, 258, 268, 276, 291, 322, 354},    // C = 1 (1, 2, 4, 7 waves *)
-    {250, 337, 326, 315, 337, 364, 375, 447},    // C = 2 (1 wave *)
-    {432, 437, 413, 420, 531, 569, 610, 652},    // C = 4 (7 waves *)
-    {620, 629, 646, 662, 830, 991, 1100, 1213}}; // C = 8 (5, 7 waves *)
+    {79, 141, 166, 185, 225, 248, 259, 272},     // C = 1
+    {126, 194, 217, 238, 306, 343, 356, 368},    // C = 2 (7 waves *)
+    {220, 300, 323, 341, 441, 541, 560, 579},    // C = 4 (5, 7 waves *)
+    {410, 500, 532, 555, 800, 880, 910, 943}};   // C = 8 (5-8 waves *: only C = 8 fits there)
+static const float kTickReflective[4][kWaveMaxWaves] = {  // N a multiple of C
+    {201, 242, 258, 268, 276, 291, 322, 354},    // C = 1 (4, 7 waves *)
+    {250, 270, 304, 315, 337, 364, 375, 447},    // C = 2 (2 waves *)
+    {346, 396, 413, 420, 531, 569, 610, 652},    // C = 4 (7 waves *)
+    {533, 630, 646, 662, 830, 991, 1100, 1213}}; // C = 8 (5, 7 waves *)
+constexpr double kTickPadded = 1.3;
 WavePlan wavefront_plan(int N, bool reflective, int max_waves) {
   max_waves = max_waves < 1 ? 1 : (max_waves > kWaveMaxWaves ? kWaveMaxWaves : max_waves);
   if (N < 1) return WavePlan{0, 0, 0};
@@ -571,7 +574,8 @@ WavePlan wavefront_plan(int N, bool reflective, int max_waves) {
     const int C = 1 << ci, Lw = (N + C - 1) / C;
     const int used = reflective ? 2 * Lw : Lw, waves = (used + 63) / 64;
     if (waves > max_waves) continue;
-    const double cost = (1000.0 + used - 1) * (reflective ? kTickReflective : kTickVacuum)[ci][waves - 1];
+    double cost = (1000.0 + used - 1) * (reflective ? kTickReflective : kTickVacuum)[ci][waves - 1];
+    if (reflective && N % C) cost *= kTickPadded;
     if (!best.C || cost < best_cost) {
       best = WavePlan{C, waves, Lw};
       best_cost = cost;

@@ -22,17 +22,18 @@ LENGTHS = [1, 5, 31, 32, 33, 50, 63, 64, 65, 100, 127, 128, 129, 255, 256, 257, 
            4096]
 
 
-# kernels_wave.hip's tick costs (ns; profiles/r05b_chain_plan.jsonl), rows C = 1, 2, 4, 8, columns 1..8 waves
-TICK_VACUUM = [[70, 141, 166, 185, 225, 248, 259, 272], [127, 194, 217, 238, 306, 343, 356, 368],
-               [222, 300, 323, 341, 441, 541, 560, 579], [412, 502, 532, 555, 800, 880, 910, 943]]
-TICK_REFLECTIVE = [[150, 230, 258, 268, 276, 291, 322, 354], [250, 337, 326, 315, 337, 364, 375, 447],
-                   [432, 437, 413, 420, 531, 569, 610, 652], [620, 629, 646, 662, 830, 991, 1100, 1213]]
+# kernels_wave.hip's tick costs (ns; profiles/r05d_chain_plan.jsonl), rows C = 1, 2, 4, 8, columns 1..8 waves
+TICK_VACUUM = [[79, 141, 166, 185, 225, 248, 259, 272], [126, 194, 217, 238, 306, 343, 356, 368],
+               [220, 300, 323, 341, 441, 541, 560, 579], [410, 500, 532, 555, 800, 880, 910, 943]]
+TICK_REFLECTIVE = [[201, 242, 258, 268, 276, 291, 322, 354], [250, 270, 304, 315, 337, 364, 375, 447],
+                   [346, 396, 413, 420, 531, 569, 610, 652], [533, 630, 646, 662, 830, 991, 1100, 1213]]
 
 
 def wave_plan(N, reflective, max_waves=8):
     """kernels_wave.hip wavefront_plan: the cells per lane C (1, 2, 4, 8) whose chain of
     ceil(N / C) lanes per line (a reflective pair: both lines') fits max_waves waves with the
-    least (1000 + lanes - 1) x measured tick cost at (C, waves); (0, 0) when none fits."""
+    least (1000 + lanes - 1) x measured tick cost at (C, waves) (x 1.3 for a reflective pair
+    whose N is not a multiple of C); (0, 0) when none fits."""
     best = None
     for ci, C in enumerate((1, 2, 4, 8)):
         used = -(-N // C) * (2 if reflective else 1)
@@ -40,6 +41,8 @@ def wave_plan(N, reflective, max_waves=8):
         if w > max_waves:
             continue
         cost = (1000.0 + used - 1) * (TICK_REFLECTIVE if reflective else TICK_VACUUM)[ci][w - 1]
+        if reflective and N % C:
+            cost *= 1.3  # the padded kernel
         if best is None or cost < best[0]:
             best = (cost, C, w)
     return (best[1], best[2]) if best else (0, 0)
