@@ -549,7 +549,7 @@ __global__ void import_ends_kernel(double2 *E, const double *ends, LineMap m, in
 // are wave-uniform (scalar loads).
 // MOM_W directions per chunk: 8 x 16 B = one 128 B line per group, 16 = two (16 KB of the
 // state in flight per wave instead of 8: round 4).  23.0 ms on SL (5.7 TB/s of the 131 GB
-// state, profiles/r04q_*).  Round 4 measured and removed, all within +-5% of this kernel on
+// state, profiles/archive/r04q_*).  Round 4 measured and removed, all within +-5% of this kernel on
 // one box while a plain scan of the same state runs at 6.9 TB/s: 32-direction chunks; a
 // register ring of 2-4 chunks in flight per wave; LDS-DMA rings (global_load_lds) of 2-3
 // 32 KB units; two passes in row order (half 0's partial sums through the outputs); whole

@@ -194,7 +194,7 @@ static rt_status enqueue_steps(rt_solver *s, int nsteps) {
 // CU the chip holds the workgroups of m = resident / (workgroups per position) positions:
 // beyond m (the SL slab's T = 20 pipeline: m = 4 of 8 positions) the rest ran as a second
 // round on half the SIMDs (k = 5 / 6: 149 / 151 ms against shares of 104 / 125 ms,
-// profiles/r04ag_trace_summary.json).  Positions of one launch never exchange data (each
+// profiles/archive/r04ag_trace_summary.json).  Positions of one launch never exchange data (each
 // reads what its predecessor published in the previous launch), so such a launch is cut into
 // consecutive launches of at most m positions, each with its own waves per segment.  The
 // full launch (k = P), a caller-set level split and other schemes keep one launch.
@@ -524,7 +524,7 @@ struct Schedule {
 
 static Schedule plan_schedule(const RunGeom &g, long long nsteps) {
   // T = 4 over four waves (no remainder for n % 4 == 0) measured slower than T = 8 with its
-  // aligned remainder (16-group shard, 100 steps: 181 vs 167 ms, profiles/r04d_solve_plan.jsonl)
+  // aligned remainder (16-group shard, 100 steps: 181 vs 167 ms, profiles/archive/r04d_solve_plan.jsonl)
   static const int kBlocks[] = {40, 32, 24, 20, 16, 8}, kWgs[] = {4, 8, 16, 32};
   Schedule best;
   for (int T : kBlocks)
