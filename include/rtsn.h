@@ -246,14 +246,15 @@ rt_status rt_get_time_block(rt_solver *s, int *steps_per_pass);
  * line (with the reflective left boundary: a mu < 0 line and its mirror) is a chain of lanes
  * of one workgroup, C cells per lane in registers, every step of an advance in one launch (up
  * to 65536 steps per launch), the upwind recurrence carried lane to lane by a DPP shift each
- * tick: one wave with the fewest cells per lane (C = 1, 2, 4, 8) while the line fits 64 C
- * cells (reflective: 32 C), else a chain of up to rt_set_wavefront_waves' waves (default 8,
- * lines of up to 4096 cells, reflective 2048) handing the carried state from wave to wave
- * through LDS.  Results are bitwise those of the pipelined segment schedule, whatever C and
- * the waves per chain.  mode 0: off; 1 (default): used when the line fits, the caller set
- * neither a time block (rt_set_time_block) nor a schedule (rt_set_pipeline), and -- for a
- * chain of several waves -- the chains need at most two waves per SIMD; 2: used whenever the
- * line fits.  RTSN_WAVEFRONT=0|2 at creation sets 0 or 2. */
+ * tick: C cells per lane (1, 2, 4, 8) on ceil(lanes / 64) waves -- one wave, or a chain of up
+ * to rt_set_wavefront_waves' waves (default 8, lines of up to 4096 cells, reflective 2048)
+ * handing the carried state from wave to wave through LDS -- with C the least estimated time
+ * of a 1000-step advance from measured tick costs (kernels_wave.hip wavefront_plan;
+ * rt_set_wavefront_cells overrides).  Results are bitwise those of the pipelined segment
+ * schedule, whatever C and the waves per chain.  mode 0: off; 1 (default): used when the line
+ * fits, the caller set neither a time block (rt_set_time_block) nor a schedule
+ * (rt_set_pipeline), and -- for a chain of several waves -- the chains need at most two waves
+ * per SIMD; 2: used whenever the line fits. */
 rt_status rt_set_wavefront(rt_solver *s, int mode);
 /* *mode as set; *active: the next rt_advance takes the wavefront; *cells_per_lane: C for
  * this handle's lines (0: too long for a wave).  Any NULL skipped. */

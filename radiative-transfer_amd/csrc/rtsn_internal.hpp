@@ -202,7 +202,7 @@ struct rt_solver {
   int Sg = 1, Ls = 16;           // segments per line and cells per segment
   int seg_T = 0;                 // the time block the segments were sized for (0: none)
   int seg_w = 0;                 // ... and the workgroups per CU they were sized for
-  bool T_set = false;            // the caller chose the time block (rt_set_time_block / RTSN_TIME_BLOCK)
+  bool T_set = false;            // the caller chose the time block (rt_set_time_block)
   int level_waves = 0;           // pipelined BDF2 passes: 0 auto (level_waves_of), 1 one wave, 2 levels shared by two
   bool lw_set = false;           // the caller chose the waves per segment (rt_set_level_waves)
   int seg_wgs = 0;               // segments sized for this many workgroups per CU (0: the pass's occupancy)
