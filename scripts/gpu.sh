@@ -6,7 +6,7 @@
 #   smoke                 __graft_entry__.smoke()
 #   bench[=ARGS]          python bench.py ARGS (default: the driver's --steps 20 --warmup 5) -> TAG_bench.json
 #   rehearsal             the 2-rank bench on the one GPU over gloo -> TAG_rehearsal2.json
-#   spawn2                the same with no launcher: bench.py --gpus 2 starts its ranks -> TAG_spawn2.json
+#   spawn2, spawn4        the same with no launcher: bench.py --gpus 2|4 starts its ranks -> TAG_spawnN.json
 #   kt[=ARGS]             rocprofv3 kernel trace + stats of bench.py ARGS (no side legs) -> TAG_kernel_stats.csv,
 #                         TAG_trace_summary.json
 #   pmc[=ARGS]            the four PMC passes of the headline pass -> profiles/pmc_TAG_v0_t20.json
@@ -69,13 +69,14 @@ s = d.get('schedule', {}); print('schedule', {k: s.get(k) for k in ('end_to_end_
 import json; d=json.load(open('gpurun_out/${TAG}_rehearsal2.json'))
 print('value', d['value'], 'n_gpus', d['n_gpus'], 'comm', d.get('rt_comm_gather'), 'per_rank', d.get('per_rank'))"
       ;;
-    spawn2)
-      # no launcher: bench.py --gpus 2 starts the two rank processes itself (both on cuda:0, gloo)
-      timeout -k 10 600 python bench.py --gpus 2 $DEF_BENCH --backend gloo --share-device --no-cpu-baseline \
+    spawn2|spawn4)
+      # no launcher: bench.py --gpus N starts the N rank processes itself (all on cuda:0, gloo)
+      nr=${name#spawn}
+      timeout -k 10 600 python bench.py --gpus $nr $DEF_BENCH --backend gloo --share-device --no-cpu-baseline \
         > $log 2>&1 || { tail -30 $log; exit 1; }
-      grep "^{" $log | tail -1 > gpurun_out/${TAG}_spawn2.json
+      grep "^{" $log | tail -1 > gpurun_out/${TAG}_${name}.json
       python3 -c "
-import json; d=json.load(open('gpurun_out/${TAG}_spawn2.json'))
+import json; d=json.load(open('gpurun_out/${TAG}_${name}.json'))
 print('value', d['value'], 'n_gpus', d['n_gpus'], 'launcher', d.get('launcher'), 'rccl_nranks', d.get('rccl_nranks'),
       'per_rank', len(d.get('per_rank') or []))"
       ;;
