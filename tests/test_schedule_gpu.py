@@ -155,10 +155,11 @@ def test_solve_remainder_tail(rtsn_mod, oracle_mod):
 @pytest.mark.parametrize("M,G,N", [(64, 128, 300), (64, 100, 257), (32, 70, 129), (16, 64, 64), (16, 3, 50),
                                    (64, 1, 17), (12, 40, 33)])
 def test_moments_producer_consumer_bitwise(rtsn_mod, oracle_mod, monkeypatch, M, G, N):
-    """The producer/consumer moments kernel (moments_pc_kernel: H = M/2 of 8, 16, 32) equals the
-    one-wave moments_kernel bitwise (RTSN_MOMENTS_LEGACY=1) on a random state -- whole and
-    partial 64-group chunks, fewer items than workgroups -- and both the oracle's sums of the
-    same state (M = 12 has no producer/consumer form: both runs take the one-wave kernel)."""
+    """The moments forms (RTSN_MOMENTS_FORM): the two-pass moments_half_kernel (the default),
+    the one-pass producer/consumer moments_pc_kernel and the one-wave moments_kernel, where
+    H = M/2 is 8, 16 or 32, are bitwise equal on a random state -- whole and partial 64-group
+    chunks, fewer items than workgroups -- and match the oracle's sums of the same state
+    (M = 12 has neither producer/consumer form: every run takes the one-wave kernel)."""
     p = oracle_mod.parse_prm(PRM_DIR / "llnl_slab_test.prm", table_dir=PRM_DIR)
     p.update(M=M, N=N, G=G, group_bounds=None, group_kappa=None, dt=1e-9, max_timesteps=1, bc_left=0, bc_right=0)
     p["dx"] = p["X"] / p["N"]
@@ -167,15 +168,16 @@ def test_moments_producer_consumer_bitwise(rtsn_mod, oracle_mod, monkeypatch, M,
     ends = rng.uniform(-1.0, 2.0, size=(M, G, N, 2))
     out = []
     with rtsn_mod.Solver(to_rt(p)) as gpu:
-        for legacy in ("1", "0"):
-            monkeypatch.setenv("RTSN_MOMENTS_LEGACY", legacy)
+        for form in ("0", "1", "2"):
+            monkeypatch.setenv("RTSN_MOMENTS_FORM", form)
             gpu.set_ends(ends)  # a new state version: the moments are recomputed
             out.append(gpu.moments())
-    for a, b in zip(out[0], out[1]):
-        assert np.array_equal(a, b)
+    for o in out[1:]:
+        for a, b in zip(out[0], o):
+            assert np.array_equal(a, b)
     orc = oracle_mod.OracleSolver(p)
     orc.set_ends(ends)
-    for a, b in zip(out[1], orc.moments()):
+    for a, b in zip(out[2], orc.moments()):
         scale = np.maximum(np.abs(b).max(axis=1, keepdims=True), 1e-300)
         assert (np.abs(a - b) / scale).max() <= 1e-13
 
