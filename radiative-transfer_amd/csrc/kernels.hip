@@ -800,147 +800,6 @@ __global__ void __launch_bounds__(320) moments_pc_kernel(const double2 *__restri
   }
 }
 
-// Two-pass moments (round 5): the producer/consumer structure of moments_pc_kernel over ONE
-// half per launch, rows ascending.  moments_pc_kernel pairs half 0's row N-1-c with half 1's
-// row c, two address streams walking toward each other; its PMC (profiles/r05d_moments_pmc.json)
-// has the same requests and L1 stalls as the state scan, which walks ONE ascending stream at
-// 6.84 TB/s against 6.24, i.e. the memory returns the two-stream order more slowly.  Here
-// pass 0 sweeps half 0 (rows ascending: cells descending) and stores the partial sums over
-// i < H (phi, F) in the outputs; pass 1 sweeps half 1 (rows ascending) and continues each
-// sum from its partial -- the reference's sequential order over i = 0 .. M-1 unchanged
-// (solver.cpp:191-237), so bitwise the one-pass kernels -- at 2 x 8 B more traffic per
-// (cell, group) for the partials (4 GB on SL, +3%).  An item is (row, 64 groups): one run of
-// 64 H lines; four loader waves take a quarter of its load instructions each into a register
-// ring two items deep, one summing wave (lane = group).  LDS: two slots of one half (33.8 KB),
-// so four workgroups per CU hold 4 x 4 x 2 x 8 KB = 256 KB of loads in flight.
-template <int H, int PASS>
-__global__ void __launch_bounds__(320) moments_half_kernel(const double2 *__restrict__ E, const double *__restrict__ mu,
-                                                           const double *__restrict__ wt, double *phi, double *F,
-                                                           double *phi_plus, LineMap m) {
-#pragma clang fp contract(off)
-  constexpr int NL = 4;                 // loader waves
-  static_assert(64 % H == 0 && H % NL == 0 && H >= 8, "a load of 64 lines covers whole groups");
-  constexpr int R = H / NL;             // loads per item of one loader
-  constexpr int ST = H + 1;             // doubles per group row in a slot
-  constexpr int SLOT = 64 * ST;         // one item: [64 groups][ST]
-  __shared__ double lds[2 * SLOT + 2 * H];  // two slots, then (w_i, mu_i w_i) for this half's i
-  double *const wl = lds + 2 * SLOT;
-  const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
-  const int lane = threadIdx.x & 63;
-  const int nchunks = (m.Gl + 63) / 64;
-  const long long items = static_cast<long long>(m.N) * nchunks;
-  const long long first = blockIdx.x, step = gridDim.x;
-  const long long mine = first < items ? (items - 1 - first) / step + 1 : 0;
-  const long long phases = (mine + 1) & ~1LL;
-  const int i0 = PASS == 0 ? 0 : H;  // this pass's directions i0 .. i0 + H - 1, ascending
-  for (int i = threadIdx.x; i < H; i += blockDim.x) {
-    wl[2 * i] = wt[i0 + i];
-    wl[2 * i + 1] = mu[i0 + i] * wt[i0 + i];
-  }
-  __syncthreads();
-  const auto sync = [] {
-    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
-    __builtin_amdgcn_s_barrier();
-  };
-  // item p: row k = it / nchunks ascending (pass 0: cell N-1-k), groups (it % nchunks) * 64..
-  const auto cell_of = [&](long long it) {
-    const int k = static_cast<int>(it / nchunks);
-    return PASS == 0 ? m.N - 1 - k : k;
-  };
-  if (wave < NL) {
-    const int part = wave;
-    typedef double d2v __attribute__((ext_vector_type(2)));
-    const auto run = [&](long long p, int &lim) -> const d2v * {  // past the last item: line 0
-      if (p >= mine) {
-        lim = 1;
-        return reinterpret_cast<const d2v *>(E);
-      }
-      const long long it = first + p * step;
-      const int k = static_cast<int>(it / nchunks), g0 = static_cast<int>(it % nchunks) * 64;
-      lim = min(64, m.Gl - g0) * H;
-      return reinterpret_cast<const d2v *>(E + m.at(PASS, k, H * g0));
-    };
-    const auto load = [&](const d2v *row, int lim, int r) {
-      const d2v v = __builtin_nontemporal_load(row + min(lane + 64 * (part * R + r), lim - 1));
-      return make_double2(v.x, v.y);
-    };
-    double2 v0[R], v1[R];
-    {
-      int l0, l1;
-      const d2v *r0 = run(0, l0), *r1 = run(1, l1);
-#pragma unroll
-      for (int r = 0; r < R; ++r) {
-        v0[r] = load(r0, l0, r);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-#pragma unroll
-      for (int r = 0; r < R; ++r) {
-        v1[r] = load(r1, l1, r);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    }
-    double *const base = lds + (lane / H) * ST + lane % H + (64 / H) * part * R * ST;
-    const auto consume = [&](double2 (&v)[R], long long p) {
-      double *const slot = base + (p & 1) * SLOT;
-      int ln;
-      const d2v *rn = run(p + 2, ln);
-#pragma unroll
-      for (int r = 0; r < R; ++r) {
-        slot[(64 / H) * r * ST] = 0.5 * (v[r].x + v[r].y);
-        v[r] = load(rn, ln, r);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    };
-    for (long long p = 0; p < phases; p += 2) {
-      consume(v0, p);
-      sync();
-      consume(v1, p + 1);
-      sync();
-    }
-    sync();
-  } else {  // the summing wave
-    // pass 1: the partial sums of the next item, loaded one phase ahead
-    double nphi = 0.0, nF = 0.0;
-    const auto partials = [&](long long p) {
-      if (PASS == 1 && p < mine) {
-        const long long it = first + p * step;
-        const int g = static_cast<int>(it % nchunks) * 64 + lane;
-        if (g < m.Gl) {
-          const size_t o = static_cast<size_t>(cell_of(it)) * m.Gl + g;
-          nphi = phi[o];
-          nF = F[o];
-        }
-      }
-    };
-    partials(0);
-    for (long long p = 0; p <= phases; ++p) {
-      if (p > 0 && p - 1 < mine) {
-        const long long it = first + (p - 1) * step;
-        const int c = cell_of(it), g0 = static_cast<int>(it % nchunks) * 64;
-        double sphi = nphi, sF = nF;
-        partials(p);
-        const double *sl = lds + ((p - 1) & 1) * SLOT + lane * ST;
-        double splus = 0.0;
-#pragma unroll 8
-        for (int i = 0; i < H; ++i) {  // pass 0: i' = H - 1 - i (mu < 0); pass 1: i' = i (mu > 0)
-          const double q = sl[PASS == 0 ? H - 1 - i : i];
-          const double wq = wl[2 * i] * q;
-          sphi += wq;
-          sF += wl[2 * i + 1] * q;
-          if (PASS == 1) splus += wq;
-        }
-        if (g0 + lane < m.Gl) {
-          const size_t o = static_cast<size_t>(c) * m.Gl + g0 + lane;
-          __builtin_nontemporal_store(sphi, phi + o);
-          __builtin_nontemporal_store(sF, F + o);
-          if (PASS == 1) __builtin_nontemporal_store(splus, phi_plus + o);
-        }
-      }
-      sync();
-    }
-  }
-}
-
 // NaN/Inf scan of the state: a block per row of the real cells (padding rows and
 // lanes hold zeros), one ballot per wave, one flag store per offending wave.
 __global__ void finite_scan_kernel(const double2 *E, int *flag, int N, int Nrow, int Lpad) {
@@ -1841,11 +1700,13 @@ hipError_t launch_import_ends(double2 *E, const double *ends, const Geometry &g,
 #define RT_MOM_W 16
 #endif
 // The moments form where M/2 is 8, 16 or 32 (RTSN_MOMENTS_FORM, for A/B timing and the bitwise
-// tests of the forms): 0 the one-wave moments_kernel, 1 moments_pc_kernel (one pass), 2 (the
-// default) moments_half_kernel's two passes
+// test of the forms): 0 the one-wave moments_kernel, 1 (the default) moments_pc_kernel.  A
+// two-pass form (each half's rows in one ascending stream, the partial sums through the
+// outputs) was measured slower and removed: 11.4 + 12.3 ms against 22.4 on one box
+// (profiles/r05g_*), refuting the two-address-stream explanation of the gap to the scan.
 static int moments_form() {
   const char *e = std::getenv("RTSN_MOMENTS_FORM");
-  return e && e[0] >= '0' && e[0] <= '2' ? e[0] - '0' : 2;
+  return e && e[0] == '0' ? 0 : 1;
 }
 hipError_t launch_moments(const double2 *E, const double *mu, const double *wt, double *phi, double *F,
                           double *phi_plus, const Geometry &g, hipStream_t st) {
@@ -1858,24 +1719,6 @@ hipError_t launch_moments(const double2 *E, const double *mu, const double *wt, 
                                      resident_blocks(moments_kernel<true, 8>, 64),
                                      resident_blocks(moments_kernel<true, W>, 64)};
   const int form = moments_form();
-  if (form == 2 && (m.H == 8 || m.H == 16 || m.H == 32)) {  // two passes, one ascending stream each
-    constexpr int TH = 64 * 5;
-#define RT_MOM_HALF(h)                                                                                         \
-  {                                                                                                            \
-    static const size_t res = resident_blocks(moments_half_kernel<h, 0>, TH);                                  \
-    const dim3 g(static_cast<unsigned>(tasks < res ? tasks : res));                                            \
-    hipLaunchKernelGGL((moments_half_kernel<h, 0>), g, dim3(TH), 0, st, E, mu, wt, phi, F, phi_plus, m);        \
-    hipLaunchKernelGGL((moments_half_kernel<h, 1>), g, dim3(TH), 0, st, E, mu, wt, phi, F, phi_plus, m);        \
-  }
-    if (m.H == 8)
-      RT_MOM_HALF(8)
-    else if (m.H == 16)
-      RT_MOM_HALF(16)
-    else
-      RT_MOM_HALF(32)
-#undef RT_MOM_HALF
-    return hipGetLastError();
-  }
   if (form >= 1 && (m.H == 8 || m.H == 16 || m.H == 32)) {  // producer/consumer form
     constexpr int TH = 64 * (2 * kMomLoadersPerHalf + 1);
     static const size_t pc[3] = {resident_blocks(moments_pc_kernel<8>, TH), resident_blocks(moments_pc_kernel<16>, TH),

@@ -155,9 +155,9 @@ def test_solve_remainder_tail(rtsn_mod, oracle_mod):
 @pytest.mark.parametrize("M,G,N", [(64, 128, 300), (64, 100, 257), (32, 70, 129), (16, 64, 64), (16, 3, 50),
                                    (64, 1, 17), (12, 40, 33)])
 def test_moments_producer_consumer_bitwise(rtsn_mod, oracle_mod, monkeypatch, M, G, N):
-    """The moments forms (RTSN_MOMENTS_FORM): the two-pass moments_half_kernel (the default),
-    the one-pass producer/consumer moments_pc_kernel and the one-wave moments_kernel, where
-    H = M/2 is 8, 16 or 32, are bitwise equal on a random state -- whole and partial 64-group
+    """The moments forms (RTSN_MOMENTS_FORM): the producer/consumer moments_pc_kernel (the
+    default) and the one-wave moments_kernel, where H = M/2 is 8, 16 or 32, are bitwise equal
+    on a random state -- whole and partial 64-group
     chunks, fewer items than workgroups -- and match the oracle's sums of the same state
     (M = 12 has neither producer/consumer form: every run takes the one-wave kernel)."""
     p = oracle_mod.parse_prm(PRM_DIR / "llnl_slab_test.prm", table_dir=PRM_DIR)
@@ -168,7 +168,7 @@ def test_moments_producer_consumer_bitwise(rtsn_mod, oracle_mod, monkeypatch, M,
     ends = rng.uniform(-1.0, 2.0, size=(M, G, N, 2))
     out = []
     with rtsn_mod.Solver(to_rt(p)) as gpu:
-        for form in ("0", "1", "2"):
+        for form in ("0", "1"):
             monkeypatch.setenv("RTSN_MOMENTS_FORM", form)
             gpu.set_ends(ends)  # a new state version: the moments are recomputed
             out.append(gpu.moments())
@@ -177,7 +177,7 @@ def test_moments_producer_consumer_bitwise(rtsn_mod, oracle_mod, monkeypatch, M,
             assert np.array_equal(a, b)
     orc = oracle_mod.OracleSolver(p)
     orc.set_ends(ends)
-    for a, b in zip(out[2], orc.moments()):
+    for a, b in zip(out[1], orc.moments()):
         scale = np.maximum(np.abs(b).max(axis=1, keepdims=True), 1e-300)
         assert (np.abs(a - b) / scale).max() <= 1e-13
 
