@@ -800,113 +800,6 @@ __global__ void __launch_bounds__(320) moments_pc_kernel(const double2 *__restri
   }
 }
 
-// Shallow form of moments_pc_kernel (round 5 A/B): NL loader waves per half, each keeping only
-// D loads (D KiB) in flight in a rolling ring that runs across item boundaries -- the state
-// scan's shape (one 1 KiB load per wave in flight, ~32 waves per CU, 6.84 TB/s with ~32 KB per
-// CU in flight: a Little's-law latency of ~1.2 us against ~10.5 us for moments_pc_kernel's
-// 256 KB, i.e. its deep queues add latency, not bandwidth).  Same slots, barriers and sums.
-template <int H, int NL, int D>
-__global__ void __launch_bounds__(64 * (2 * NL + 1)) moments_roll_kernel(const double2 *__restrict__ E,
-                                                                         const double *__restrict__ mu,
-                                                                         const double *__restrict__ wt, double *phi,
-                                                                         double *F, double *phi_plus, LineMap m) {
-#pragma clang fp contract(off)
-  static_assert(64 % H == 0 && H % NL == 0 && H >= 8, "a load of 64 lines covers whole groups");
-  constexpr int R = H / NL;             // loads per item of one loader
-  static_assert(D >= 1 && D <= R && R % D == 0, "the ring's slots repeat every item");
-  constexpr int ST = H + 1, SLOT = 2 * 64 * ST;
-  __shared__ double lds[2 * SLOT + 4 * H];
-  double *const wl = lds + 2 * SLOT;
-  const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
-  const int lane = threadIdx.x & 63;
-  const int nchunks = (m.Gl + 63) / 64;
-  const long long items = static_cast<long long>(m.N) * nchunks;
-  const long long first = blockIdx.x, step = gridDim.x;
-  const long long mine = first < items ? (items - 1 - first) / step + 1 : 0;
-  for (int i = threadIdx.x; i < 2 * H; i += blockDim.x) {
-    wl[2 * i] = wt[i];
-    wl[2 * i + 1] = mu[i] * wt[i];
-  }
-  __syncthreads();
-  const auto sync = [] {
-    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
-    __builtin_amdgcn_s_barrier();
-  };
-  if (wave < 2 * NL) {
-    const int h = wave / NL, part = wave % NL;
-    typedef double d2v __attribute__((ext_vector_type(2)));
-    const auto run = [&](long long p, int &lim) -> const d2v * {
-      if (p >= mine) {
-        lim = 1;
-        return reinterpret_cast<const d2v *>(E);
-      }
-      const long long it = first + p * step;
-      const int c = static_cast<int>(it / nchunks), g0 = static_cast<int>(it % nchunks) * 64;
-      lim = min(64, m.Gl - g0) * H;
-      return reinterpret_cast<const d2v *>(E + m.at(h, h == 0 ? m.N - 1 - c : c, H * g0));
-    };
-    const auto load = [&](const d2v *row, int lim, int r) {
-      const d2v v = __builtin_nontemporal_load(row + min(lane + 64 * (part * R + r), lim - 1));
-      return make_double2(v.x, v.y);
-    };
-    double2 v[D];
-    int lc, ln;
-    const d2v *rc = run(0, lc);
-#pragma unroll
-    for (int r = 0; r < D; ++r) {
-      v[r] = load(rc, lc, r);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    double *const base = lds + h * 64 * ST + (lane / H) * ST + lane % H + (64 / H) * part * R * ST;
-    for (long long p = 0; p < mine; ++p) {
-      double *const slot = base + (p & 1) * SLOT;
-      const d2v *rn = run(p + 1, ln);
-#pragma unroll
-      for (int r = 0; r < R; ++r) {  // consume load r of item p, issue load r + D (of item p or p + 1)
-        slot[(64 / H) * r * ST] = 0.5 * (v[r % D].x + v[r % D].y);
-        v[r % D] = r + D < R ? load(rc, lc, r + D) : load(rn, ln, r + D - R);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      rc = rn;
-      lc = ln;
-      sync();
-    }
-    sync();
-  } else {
-    for (long long p = 0; p <= mine; ++p) {
-      if (p > 0) {
-        const long long it = first + (p - 1) * step;
-        const int c = static_cast<int>(it / nchunks), g0 = static_cast<int>(it % nchunks) * 64;
-        const double *s0 = lds + ((p - 1) & 1) * SLOT + lane * ST;
-        const double *s1 = s0 + 64 * ST;
-        double sphi = 0.0, sF = 0.0, splus = 0.0;
-#pragma unroll 8
-        for (int i = 0; i < H; ++i) {
-          const double q = s0[H - 1 - i];
-          const double wq = wl[2 * i] * q;
-          sphi += wq;
-          sF += wl[2 * i + 1] * q;
-        }
-#pragma unroll 8
-        for (int i = 0; i < H; ++i) {
-          const double q = s1[i];
-          const double wq = wl[2 * (H + i)] * q;
-          sphi += wq;
-          sF += wl[2 * (H + i) + 1] * q;
-          splus += wq;
-        }
-        if (g0 + lane < m.Gl) {
-          const size_t o = static_cast<size_t>(c) * m.Gl + g0 + lane;
-          __builtin_nontemporal_store(sphi, phi + o);
-          __builtin_nontemporal_store(sF, F + o);
-          __builtin_nontemporal_store(splus, phi_plus + o);
-        }
-      }
-      sync();
-    }
-  }
-}
-
 // NaN/Inf scan of the state: a block per row of the real cells (padding rows and
 // lanes hold zeros), one ballot per wave, one flag store per offending wave.
 __global__ void finite_scan_kernel(const double2 *E, int *flag, int N, int Nrow, int Lpad) {
@@ -1813,7 +1706,7 @@ hipError_t launch_import_ends(double2 *E, const double *ends, const Geometry &g,
 // (profiles/r05g_*), refuting the two-address-stream explanation of the gap to the scan.
 static int moments_form() {
   const char *e = std::getenv("RTSN_MOMENTS_FORM");
-  return e && e[0] >= '0' && e[0] <= '4' ? e[0] - '0' : 1;
+  return e && e[0] == '0' ? 0 : 1;
 }
 hipError_t launch_moments(const double2 *E, const double *mu, const double *wt, double *phi, double *F,
                           double *phi_plus, const Geometry &g, hipStream_t st) {
@@ -1826,23 +1719,6 @@ hipError_t launch_moments(const double2 *E, const double *mu, const double *wt, 
                                      resident_blocks(moments_kernel<true, 8>, 64),
                                      resident_blocks(moments_kernel<true, W>, 64)};
   const int form = moments_form();
-  if (form >= 2 && m.H == 32) {  // A/B: the shallow rolling-ring loaders
-#define RT_MOM_ROLL(nl, d)                                                                                      \
-  {                                                                                                             \
-    static const size_t res = resident_blocks(moments_roll_kernel<32, nl, d>, 64 * (2 * nl + 1));              \
-    const dim3 g(static_cast<unsigned>(tasks < res ? tasks : res));                                             \
-    hipLaunchKernelGGL((moments_roll_kernel<32, nl, d>), g, dim3(64 * (2 * nl + 1)), 0, st, E, mu, wt, phi, F,  \
-                       phi_plus, m);                                                                            \
-  }
-    if (form == 2)
-      RT_MOM_ROLL(2, 4)
-    else if (form == 3)
-      RT_MOM_ROLL(4, 4)
-    else
-      RT_MOM_ROLL(2, 16)
-#undef RT_MOM_ROLL
-    return hipGetLastError();
-  }
   if (form >= 1 && (m.H == 8 || m.H == 16 || m.H == 32)) {  // producer/consumer form
     constexpr int TH = 64 * (2 * kMomLoadersPerHalf + 1);
     static const size_t pc[3] = {resident_blocks(moments_pc_kernel<8>, TH), resident_blocks(moments_pc_kernel<16>, TH),
