@@ -3,6 +3,7 @@
 #include "physics.hpp"
 
 #include <sched.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <cfloat>
@@ -40,6 +41,11 @@ class HostPool {
   }
   int size() const { return static_cast<int>(workers_.size()) + 1; }
   void run(int n, const std::function<void(int)> &fn) {
+    // a forked child has the pool's bookkeeping but none of its threads: it works alone
+    if (getpid() != pid_) {
+      for (int i = 0; i < n; ++i) fn(i);
+      return;
+    }
     std::lock_guard<std::mutex> one(job_m_);
     if (workers_.empty() || n <= 1) {
       for (int i = 0; i < n; ++i) fn(i);
@@ -61,7 +67,7 @@ class HostPool {
   }
 
  private:
-  explicit HostPool(int workers) {
+  explicit HostPool(int workers) : pid_(getpid()) {
     for (int w = 0; w < workers; ++w) workers_.emplace_back([this] { loop(); });
     for (std::thread &t : workers_) t.detach();
   }
@@ -81,6 +87,7 @@ class HostPool {
       if (--busy_ == 0) done_.notify_one();
     }
   }
+  const pid_t pid_;  // the process the workers run in
   std::vector<std::thread> workers_;
   std::mutex job_m_, m_;
   std::condition_variable cv_, done_;

@@ -242,3 +242,29 @@ def test_c_client_solves_against_oracle(oracle_mod, tmp_path, name):
     assert np.allclose(left, l_o, rtol=1e-10, atol=0) and np.allclose(right, r_o, rtol=1e-10, atol=0)
     assert np.allclose(bal, o.balance(), rtol=1e-9, atol=1e-12)
     assert np.array_equal(e_ave, o.groups()["e_ave"])
+
+
+def test_host_workers_survive_fork(rtsn_mod):
+    """The Planck table runs on persistent host workers (physics.cpp HostPool); a child forked
+    after they started has none of their threads and must compute the same table alone,
+    not wait for workers that do not exist (a bounded wait here)."""
+    import os
+    import time
+    from conftest import PRM_DIR
+    ph = rtsn_mod.ParameterHandler(PRM_DIR / "llnl_slab_test.prm", table_dir=PRM_DIR)
+    e = ph.params["group_bounds"]
+    B, dB = rtsn_mod.planck_groups(1.0, e)
+    pid = os.fork()
+    if pid == 0:  # the child: same table, then exit with the verdict
+        B2, dB2 = rtsn_mod.planck_groups(1.0, e)
+        os._exit(0 if (B2 == B).all() and (dB2 == dB).all() else 3)
+    t0 = time.time()
+    while time.time() - t0 < 60:
+        done, status = os.waitpid(pid, os.WNOHANG)
+        if done:
+            assert os.waitstatus_to_exitcode(status) == 0
+            return
+        time.sleep(0.05)
+    os.kill(pid, 9)
+    os.waitpid(pid, 0)
+    raise AssertionError("the forked child hung in the host worker pool")
