@@ -209,3 +209,22 @@ def test_ramp_launches_cut_into_rounds(rtsn_mod, oracle_mod):
             out[lw] = s.ends()
     assert np.isfinite(out[0]).all()
     assert np.array_equal(out[0], out[4]) and np.array_equal(out[0], out[2])
+
+
+def test_experiment_env_ignored(rtsn_mod, oracle_mod, monkeypatch):
+    """the round-3/4 experiment variables no longer change a handle's schedule
+    (rt_set_* are the only way): created with RTSN_TIME_BLOCK=4, RTSN_WAVEFRONT=0,
+    RTSN_WAVE_WAVES=1 and RTSN_LEVEL_WAVES=4 in the environment, a handle reports the same
+    time block, wavefront state and waves per segment as one created without them."""
+    p = _params(oracle_mod, 5000, 10)
+    with rtsn_mod.Solver(to_rt(p)) as s:
+        want = (s.time_block, s.level_waves, s.wavefront_state())
+    q = _params(oracle_mod, 300, 10)
+    with rtsn_mod.Solver(to_rt(q)) as s:
+        want_w = s.wavefront_state()
+    for k, v in (("RTSN_TIME_BLOCK", "4"), ("RTSN_WAVEFRONT", "0"), ("RTSN_WAVE_WAVES", "1"), ("RTSN_LEVEL_WAVES", "4")):
+        monkeypatch.setenv(k, v)
+    with rtsn_mod.Solver(to_rt(p)) as s:
+        assert (s.time_block, s.level_waves, s.wavefront_state()) == want
+    with rtsn_mod.Solver(to_rt(q)) as s:
+        assert s.wavefront_state() == want_w and want_w["active"]
