@@ -807,14 +807,15 @@ def _free_port() -> int:
         return so.getsockname()[1]
 
 
-def spawn_ranks(n: int, argv, script=None, env=None, grace_s: float = 20.0) -> int:
+def spawn_ranks(n: int, argv, script=None, env=None, grace_s: float = 20.0, straggle_s: float = 300.0) -> int:
     """Start n rank processes of `script` (default: this file) with `argv`, one per GPU
     (LOCAL_RANK r -> cuda:r), rendezvous on 127.0.0.1 at a free port.  Each child is a fresh
     interpreter started by fork+exec from this process, which has not initialised the GPU (it
     imports neither torch nor librtsn).  Rank 0's stdout is relayed line by line; the other
     ranks' output and every stderr pass through.  When a rank exits non-zero the others are
     terminated (their own PIDs: SIGTERM, then SIGKILL after grace_s) and that status is
-    returned; 0 when all ranks succeed and rank 0 printed a JSON line whose n_gpus is n."""
+    returned; 0 when all ranks succeed and rank 0 printed a JSON line whose n_gpus is n.  Ranks
+    still running straggle_s after the first one finished cleanly are stopped (status 1)."""
     import signal
     import subprocess
     import threading
@@ -853,12 +854,21 @@ def spawn_ranks(n: int, argv, script=None, env=None, grace_s: float = 20.0) -> i
         reader = threading.Thread(target=relay, args=(procs[0].stdout,), daemon=True)
         reader.start()
         status = 0
+        first_done = None  # when the first rank finished cleanly: the rest get straggle_s more
         while [q.poll() for q in procs].count(None):
             bad = [q.returncode for q in procs if q.returncode not in (None, 0)]
             if bad:
                 status = bad[0]
                 print(f"bench.py: a rank exited with status {status}; stopping the others", file=sys.stderr)
                 stop_all()
+                break
+            if first_done is None and any(q.returncode == 0 for q in procs):
+                first_done = time.time()
+            if first_done is not None and time.time() - first_done > straggle_s:
+                print(f"bench.py: ranks still running {straggle_s:.0f} s after the first finished; stopping them",
+                      file=sys.stderr)
+                stop_all()
+                status = 1
                 break
             time.sleep(0.2)
         reader.join(timeout=30)

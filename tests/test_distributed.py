@@ -391,6 +391,8 @@ if r == 0:
     print("progress line")
     print(json.dumps({"n_gpus": n if fail != "count" else 1, "sum": float(t), "launcher": os.environ["RTSN_BENCH_LAUNCHER"]}))
 dist.destroy_process_group()
+if fail == "straggle" and r == 1:  # finishes its work, then never exits
+    __import__("time").sleep(600)
 """
 
 
@@ -407,12 +409,13 @@ def test_spawn_ranks_relays_rank0(tmp_path, capsys, n):
     assert d["launcher"] == f"bench.py --gpus {n} (child processes)"
 
 
-@pytest.mark.parametrize("fail,status", [("rank1", 3), ("count", 1)])
+@pytest.mark.parametrize("fail,status", [("rank1", 3), ("count", 1), ("straggle", 1)])
 def test_spawn_ranks_fails_loudly(tmp_path, fail, status):
     """A rank that exits non-zero stops the job (the others, blocked in the rendezvous, are
-    terminated) with that status; a line whose n_gpus is not N is a failure too."""
+    terminated) with that status; a line whose n_gpus is not N is a failure too, and so is a
+    rank still running long after the others finished (straggle_s)."""
     script = tmp_path / "child.py"
     script.write_text(_RANK_CHILD)
     t0 = time.time()
-    assert bench.spawn_ranks(2, [fail], script=script, grace_s=5) == status
+    assert bench.spawn_ranks(2, [fail], script=script, grace_s=5, straggle_s=10) == status
     assert time.time() - t0 < 120
