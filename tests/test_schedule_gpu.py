@@ -228,3 +228,32 @@ def test_experiment_env_ignored(rtsn_mod, oracle_mod, monkeypatch):
         assert (s.time_block, s.level_waves, s.wavefront_state()) == want
     with rtsn_mod.Solver(to_rt(q)) as s:
         assert s.wavefront_state() == want_w and want_w["active"]
+
+
+@pytest.mark.parametrize("bc_left", [0, 2])
+def test_segmentation_bitwise(rtsn_mod, oracle_mod, bc_left):
+    """Results do not depend on the segmentation (rt_set_segmentation: the segments sized for
+    1, 2, 4 workgroups per CU, against the default): every segment of the pipelined schedule
+    starts from its predecessor's exact exit state, so the node array is bitwise the same for
+    every cut of the lines (6000 cells in ~50 to ~375 chain positions), through the fill and
+    drain of 2 passes at T = 20 (vacuum and reflective chains) -- and matches the oracle."""
+    steps, M, G = 40, 8, 8
+    p = _params(oracle_mod, 6000, steps, bc_left=bc_left, G=G)
+    p["M"] = M
+    p["psi_source"] = np.full((M, G), 0.5)
+    orc = _oracle(oracle_mod, p)
+    ends, positions = {}, {}
+    for w in (0, 1, 2, 4):
+        with rtsn_mod.Solver(to_rt(p)) as gpu:
+            gpu.time_block = 20
+            gpu.pipeline = 2
+            if w:
+                gpu.set_segmentation(w)
+            positions[w] = gpu.sweep_geometry()[1]
+            gpu.advance(steps)
+            ends[w] = gpu.ends()
+            if w == 0:
+                compare_all(gpu, orc)
+    assert len(set(positions.values())) >= 3, positions  # the cuts really differ
+    for w in (1, 2, 4):
+        assert np.array_equal(ends[0], ends[w]), (w, positions)
