@@ -235,6 +235,14 @@ __host__ __device__ constexpr int map_count() {
   return map_slot<S>(K, K + 2) + 1;
 }
 
+// The reflective mu > 0 head cell's map (cell_step_maybe_head probed the same way) differs
+// from its line's map only from this slot on: BDF2's last two rows (the BDF substep reads the
+// mirror's last-substep outflow as its prev and half upwind nodes); BE / CN: nowhere.
+template <int S>
+__host__ __device__ constexpr int head_map_first() {
+  return S == SCHEME_BDF2 ? map_slot<S>(SchemeDim<S>::K - 1, 0) : map_count<S>();
+}
+
 // Apply the map (CONST: with the affine constants; otherwise its linear part).
 // cs scales the constants: the material-coupled sweep stores them for B = 1
 // and passes the cell's B_g(T(x)) (with the correction off they are linear in

@@ -381,7 +381,7 @@ __global__ __launch_bounds__(64) void sweep_block_kernel(SegArgs a) {
 #pragma unroll
       for (int r = 0; r < K; ++r) X[t][r] = 0.0;
   }
-  const double *lcp = a.lc + static_cast<size_t>(half) * LC_COUNT * stride + ell;
+  const double *hmp = a.hmap + ell;  // the head cell's map (refl_head only)
 
   // ---- stream the segment in C-row chunks ----
   const int row_bytes = a.Lpad * static_cast<int>(sizeof(double2));
@@ -434,7 +434,7 @@ __global__ __launch_bounds__(64) void sweep_block_kernel(SegArgs a) {
   if (refl_head) {
     h_oi = ein[0];
     h_oo = eout[0];
-    head_cell<S, T>(lcp, stride, a.hd, b, X, h_oi, h_oo, bv[0]);
+    head_cell<S, T>(hmp, stride, X, h_oi, h_oo, bv[0]);
   }
 
   // ---- the line's cell map ----

@@ -54,7 +54,7 @@ constexpr int prop_count(int K, int T) { return (T * K) * (T * K + 1); }
 struct SegArgs {
   double2 *E;                 // [2][Nrow][Lpad] (e_in, e_out)
   const double *map;          // [2][map_count<S>][Lpad] per-line affine cell map (cell.hpp)
-  const double *lc;           // [2][LC_COUNT][Lpad] line constants (reflective head cell only)
+  const double *hmap;         // [map_count<S>][Lpad] the reflective mu > 0 head cell's map (half 1 lines)
   const double *bdry;         // [2][Lpad] inflow value per line (non-reflective)
   const double *yseg;         // [2][Sg+1][T K][Lpad] true incoming state per segment (fold_kernel)
   const double *yrefl;        // [T K][Lpad] this pass's mu < 0 line outflow state (reflective)

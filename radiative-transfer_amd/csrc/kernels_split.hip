@@ -203,7 +203,7 @@ __device__ __forceinline__ void split_role(const SegArgs &a, double2 (*hand)[2][
   // reflective head cell: wave r runs its levels on wave r - 1's result, in turn
   double h_oi = 0.0, h_oo = 0.0;
   if (refl_head) {  // workgroup-uniform: every wave passes the KW - 1 barriers
-    const double *lcp = a.lc + static_cast<size_t>(half) * LC_COUNT * stride + ell;
+    const double *hmp = a.hmap + ell;
     if constexpr (IN) {
       h_oi = ein[0];
       h_oo = eout[0];
@@ -216,7 +216,7 @@ __device__ __forceinline__ void split_role(const SegArgs &a, double2 (*hand)[2][
           h_oi = v.x;
           h_oo = v.y;
         }
-        head_cell<S, TW>(lcp, stride, a.hd, b, X, h_oi, h_oo, 1.0);
+        head_cell<S, TW>(hmp, stride, X, h_oi, h_oo, 1.0);
         hhead[lane] = make_double2(h_oi, h_oo);
       }
       __syncthreads();
@@ -225,7 +225,7 @@ __device__ __forceinline__ void split_role(const SegArgs &a, double2 (*hand)[2][
       const double2 v = hhead[lane];
       h_oi = v.x;
       h_oo = v.y;
-      head_cell<S, TW>(lcp, stride, a.hd, b, X, h_oi, h_oo, 1.0);
+      head_cell<S, TW>(hmp, stride, X, h_oi, h_oo, 1.0);
     }
   }
 

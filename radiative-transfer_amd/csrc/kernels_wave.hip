@@ -20,8 +20,8 @@
 // wavefront_plan's choice, from measured tick costs (profiles/r05*_plan.jsonl).
 //
 // Same arithmetic per (cell, level) as the pipelined segment pass (the per-line affine map
-// of cell.hpp, exact carries; the reflective mu > 0 head cell by the reference's algebra
-// with the mirror's per-substep outflows, sweep_device.hpp head_cell): bitwise equal to it,
+// of cell.hpp, exact carries; the reflective mu > 0 head cell by its own map of the
+// reference's head algebra, as sweep_device.hpp head_cell runs it): bitwise equal to it,
 // whatever the cells per lane and waves per chain.
 #include <hip/hip_runtime.h>
 
@@ -87,6 +87,42 @@ __device__ unsigned long long g_block_stamps[kWaveMaxWaves * kBlockStamps * 2];
   } while (0)
 #endif
 
+// The lane's cell maps.  A pair chain's mu > 0 head lane runs its cell 0 on the head cell's
+// own map (rtsn_lines.hip cell_map<S, true>: the reference's head algebra with the mirror's
+// per-substep outflows, probed into the same FMA rows), so every lane runs the same
+// instructions every tick -- round 4 branched into the reference's algebra there, and the
+// exec-mask divergence roughly doubled a reflective chain's tick.  The head map differs from
+// the line's only in its last rows (BDF2: the BDF substep's output and oin, which read the
+// mirror's last-substep outflow; the host checks the others are bitwise the line's; BE / CN:
+// nowhere), so a lane holds just those: W gets them on the head lane where a lane has one
+// cell; with more, cell 0 reads W0 = W with them replaced (the rest are W's own registers).
+template <int S, int C, bool PAIR>
+__device__ __forceinline__ void head_maps(const SegArgs &a, int half, int ell, size_t stride, bool refl_head,
+                                          double (&W)[map_count<S>()], double (&W0)[map_count<S>()]) {
+  constexpr int WN = map_count<S>(), F = head_map_first<S>();
+#pragma unroll
+  for (int n = 0; n < WN; ++n) W[n] = a.map[(static_cast<size_t>(half) * WN + n) * stride + ell];
+  double T[WN - F > 0 ? WN - F : 1];
+  if constexpr (PAIR) {
+#pragma unroll
+    for (int n = F; n < WN; ++n) {
+      const double h = a.hmap[n * stride + ell];  // every lane (ell < Lpad): a select, no branch
+      T[n - F] = refl_head ? h : W[n];
+    }
+    if constexpr (C == 1) {
+#pragma unroll
+      for (int n = F; n < WN; ++n) W[n] = T[n - F];
+    }
+  }
+  // a wave-uniform line map would live in SGPRs, and gfx9's one scalar operand per VALU op
+  // then costs an accumulator copy per row and cell: keep it in VGPRs (after all the loads
+  // are issued, so that they are in flight together)
+#pragma unroll
+  for (int n = 0; n < WN; ++n) asm volatile("" : "+v"(W[n]));
+#pragma unroll
+  for (int n = 0; n < WN; ++n) W0[n] = (PAIR && C > 1 && n >= F) ? T[n - F] : W[n];
+}
+
 // grid: one workgroup per line (mu < 0 lines then mu > 0 lines, ell < H Gl) -- or, PAIR (the
 // reflective left boundary), one per line pair ell (chain lanes [0, Lw) the mu < 0 line,
 // [Lw, 2 Lw) its mirror).  Lw = lanes per line = ceil(N / C); the chain fills one wave.
@@ -126,21 +162,9 @@ __global__ __launch_bounds__(64) void wavefront_kernel(SegArgs a, int nsteps, in
       eout[c] = v.y;
     }
   }
-  double W[WN];
-#pragma unroll
-  for (int n = 0; n < WN; ++n) W[n] = a.map[(static_cast<size_t>(half) * WN + n) * stride + ell];
-  // a wave-uniform line map would live in SGPRs, and gfx9's one scalar operand per VALU op
-  // then costs an accumulator copy per row and cell: keep it in VGPRs (after all the loads
-  // are issued, so that they are in flight together)
-#pragma unroll
-  for (int n = 0; n < WN; ++n) asm volatile("" : "+v"(W[n]));
   const bool refl_head = PAIR && half == 1 && j == 0;  // one lane of a pair chain
-  LineConst L{};
-  if (refl_head) {
-    const double *lcp = a.lc + static_cast<size_t>(half) * LC_COUNT * stride + ell;
-#pragma unroll
-    for (int n = 0; n < LC_COUNT; ++n) L.c[n] = lcp[n * stride];
-  }
+  double W[WN], W0[WN];
+  head_maps<S, C, PAIR>(a, half, ell, stride, refl_head, W, W0);
 
   // Xin: the state each lane receives at its tick -- lane - 1's exit state of the same level;
   // chain lane 0's is the chain head's inflow state (solver.cpp:695-697), the mu < 0 line's
@@ -195,13 +219,7 @@ __global__ __launch_bounds__(64) void wavefront_kernel(SegArgs a, int nsteps, in
 #pragma unroll
       for (int c = 0; c < C; ++c) {
         double Xn[K], oi, oo;
-        if (PAIR && c == 0 && refl_head) {  // reflective head: the reference's algebra, distinct inflows
-          cell_step_maybe_head<S>(L, a.hd, false, ein[0], eout[0], X, true, X[K - 1], oi, oo);
-#pragma unroll
-          for (int r = 0; r < K; ++r) Xn[r] = X[r];
-        } else {
-          map_apply<S, true>(W, X, ein[c], eout[c], Xn, oi, oo);
-        }
+        map_apply<S, true>(PAIR && C > 1 && c == 0 ? W0 : W, X, ein[c], eout[c], Xn, oi, oo);
         if constexpr (PAD) {
           const bool pad = j * C + c >= a.N;
 #pragma unroll
@@ -318,18 +336,9 @@ __global__ __launch_bounds__(64 * (WIDE ? kWaveMaxWaves : 4)) void chain_kernel(
       eout[c] = v.y;
     }
   }
-  double W[WN];
-#pragma unroll
-  for (int n = 0; n < WN; ++n) W[n] = a.map[(static_cast<size_t>(half) * WN + n) * stride + ell];
-#pragma unroll
-  for (int n = 0; n < WN; ++n) asm volatile("" : "+v"(W[n]));  // VGPR-resident map (wavefront_kernel)
   const bool refl_head = PAIR && half == 1 && j == 0;
-  LineConst L{};
-  if (refl_head) {
-    const double *lcp = a.lc + static_cast<size_t>(half) * LC_COUNT * stride + ell;
-#pragma unroll
-    for (int n = 0; n < LC_COUNT; ++n) L.c[n] = lcp[n * stride];
-  }
+  double W[WN], W0[WN];
+  head_maps<S, C, PAIR>(a, half, ell, stride, refl_head, W, W0);  // VGPR-resident maps
   double Xin[K], X[K];
   {
     const double bv = a.bdry[static_cast<size_t>(PAIR ? 0 : half) * stride + ell];
@@ -367,13 +376,7 @@ __global__ __launch_bounds__(64 * (WIDE ? kWaveMaxWaves : 4)) void chain_kernel(
 #pragma unroll
     for (int c = 0; c < C; ++c) {
       double Xn[K], oi, oo;
-      if (PAIR && c == 0 && refl_head) {
-        cell_step_maybe_head<S>(L, a.hd, false, ein[0], eout[0], X, true, X[K - 1], oi, oo);
-#pragma unroll
-        for (int r = 0; r < K; ++r) Xn[r] = X[r];
-      } else {
-        map_apply<S, true>(W, X, ein[c], eout[c], Xn, oi, oo);
-      }
+      map_apply<S, true>(PAIR && C > 1 && c == 0 ? W0 : W, X, ein[c], eout[c], Xn, oi, oo);
       if constexpr (PAD) {
         const bool pad = j * C + c >= a.N;
 #pragma unroll
@@ -547,7 +550,9 @@ static hipError_t launch_wave_s(const WavePlan &p, const SegArgs &a, int nsteps,
 // advance, (1000 + L - 1) ticks x the measured cost of one tick at (C, waves), L the chain's
 // lanes.  Tick costs (ns, medians) from tools/chain_plan.py on chain_kernel / wavefront_kernel
 // (round 5, profiles/r05d_chain_plan.jsonl: 1000 BDF2 steps, 8 lines, every feasible C at
-// N = 16 .. 2048, vacuum and reflective; * = interpolated, no length measured there).  A
+// N = 16 .. 2048, vacuum and reflective; * = interpolated, no length measured there; the
+// reflective rows re-measured after the head cell took its own map, r05p_chain_plan_refl.jsonl:
+// N = 32 .. 2048 in steps filling each wave count).  A
 // reflective pair whose N is not a multiple of C runs the padded kernel (the mu < 0 line's
 // padding cells pass the state through by a select): ~1.3x the tick (C = 4: 430 vs 346 ns at
 // one wave).  A chain's tick is ~2x a single wave's at the same C (the hand-over through LDS
@@ -560,10 +565,10 @@ static const float kTickVacuum[4][kWaveMaxWaves] = {
     {220, 300, 323, 341, 441, 541, 560, 579},    // C = 4 (5, 7 waves *)
     {410, 500, 532, 555, 800, 880, 910, 943}};   // C = 8 (5-8 waves *: only C = 8 fits there)
 static const float kTickReflective[4][kWaveMaxWaves] = {  // N a multiple of C
-    {201, 242, 258, 268, 276, 291, 322, 354},    // C = 1 (4, 7 waves *)
-    {250, 270, 304, 315, 337, 364, 375, 447},    // C = 2 (2 waves *)
-    {346, 396, 413, 420, 531, 569, 610, 652},    // C = 4 (7 waves *)
-    {533, 630, 646, 662, 830, 991, 1100, 1213}}; // C = 8 (5, 7 waves *)
+    {83, 156, 173, 191, 230, 255, 266, 278},     // C = 1 (round 5 before the head map: 201 .. 354)
+    {131, 203, 222, 244, 321, 349, 363, 388},    // C = 2
+    {227, 307, 330, 351, 515, 551, 570, 587},    // C = 4
+    {421, 529, 559, 579, 1032, 1070, 1089, 1113}};  // C = 8
 constexpr double kTickPadded = 1.3;
 WavePlan wavefront_plan(int N, bool reflective, int max_waves) {
   max_waves = max_waves < 1 ? 1 : (max_waves > kWaveMaxWaves ? kWaveMaxWaves : max_waves);

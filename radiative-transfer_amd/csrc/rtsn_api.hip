@@ -217,7 +217,7 @@ static rt_status create_impl(const rt_params *pin, int g_lo, int g_hi, int d_lo,
   hipError_t e = hipSuccess;
   const size_t Nrow = static_cast<size_t>(h->J) * kSweepTile;  // cells padded to whole tiles
   if (!e) e = dalloc(h->E, sizeof(double2) * 2 * Nrow * Lp);
-  if (!e) e = dalloc(h->lc, sizeof(double) * 2 * LC_COUNT * Lp);
+  if (!e) e = dalloc(h->hmap, sizeof(double) * map_count_of(h->scheme) * Lp);
   if (!e) e = dalloc(h->map, sizeof(double) * 2 * map_count_of(h->scheme) * Lp);
   for (int T = 1; T <= kMaxAlignedBlock; ++T)
     if (!e) e = dalloc(h->prop[T], sizeof(double) * 2 * prop_count(K, T) * Lp);

@@ -214,7 +214,7 @@ struct rt_solver {
   int device = 0, cus = 0;
   hipStream_t stream = nullptr;
   // device state
-  rtsn_detail::DeviceBuf E, map, lc, prop[kMaxAlignedBlock + 1], bdry, agg[2], yseg, yrefl, lineB, muwt, mom, rows, sigma;
+  rtsn_detail::DeviceBuf E, map, hmap, prop[kMaxAlignedBlock + 1], bdry, agg[2], yseg, yrefl, lineB, muwt, mom, rows, sigma;
   std::vector<double> map_host;  // [2][WN][Lpad], kept for the lazily built propagators
   bool prop_ready[kMaxAlignedBlock + 1] = {};
   int agg_cur = 0;               // aggregates of the last pass live in agg[agg_cur ^ 1]
@@ -239,7 +239,7 @@ struct rt_solver {
   // material-temperature coupling (rt_material_enable)
   bool material = false;
   double rho_cv = 0.0, wsum = 0.0;
-  rtsn_detail::DeviceBuf Tcell, Bcell, qbuf, edges, map_unit, lc_unit, phi_part;
+  rtsn_detail::DeviceBuf Tcell, Bcell, qbuf, edges, map_unit, hmap_unit, phi_part;
   rtsn_detail::DeviceBuf corr_pow;            // A^Lsub per line for phi_correction_kernel's sub-segments
   int corr_pow_L = 0;            // the Lsub it holds (0: none)
   rtsn_detail::DeviceBuf corr_rows;           // BDF2: rows b A^j and A^64 per line (phi_correction_rows_kernel)
@@ -376,7 +376,7 @@ inline Geometry geometry(const rt_solver *s) { return Geometry{s->p.M, s->Gl, s-
 // rtsn_lines.hip
 rt_status upload(rt_solver *s, DeviceBuf &b, const void *src, size_t bytes);
 template <int S>
-rt_status line_maps_s(rt_solver *s, bool unit_B, DeviceBuf &map_dev, DeviceBuf &lc_dev);
+rt_status line_maps_s(rt_solver *s, bool unit_B, DeviceBuf &map_dev, DeviceBuf &hmap_dev);
 rt_status ensure_propagators(rt_solver *s, int T);
 rt_status setup_lines(rt_solver *s);
 rt_status upload_inflow(rt_solver *s);

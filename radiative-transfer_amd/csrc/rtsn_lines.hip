@@ -71,7 +71,11 @@ static LineConst line_constants(const rt_solver &s, int i, int g, bool unit_B = 
 // cell_step<S> on unit inputs (constants and data zeroed), constants from
 // cell_step<S> on zero inputs.  Every coefficient outside the structural
 // pattern must come out exactly zero; false otherwise.
-template <int S>
+// HEAD: the reflective mu > 0 head cell's map instead (cell_step_maybe_head with the
+// mirror's last-substep outflow b3 = X[K-1], the carried state being head_state(b): a map
+// of the same structure, so the kernels run the head cell as the same FMA rows as every
+// other cell -- no divergent per-tick branch into the reference's algebra).
+template <int S, bool HEAD = false>
 static bool cell_map(const LineConst &Lin, double hd, bool neg, double *W) {
   constexpr int K = SchemeDim<S>::K;
   double dense[K + 1][K + 3];  // [row][input 0..K+1, constant K+2]
@@ -84,7 +88,10 @@ static bool cell_map(const LineConst &Lin, double hd, bool neg, double *W) {
     if (col == K) pin = 1.0;
     if (col == K + 1) pout = 1.0;
     double oi, oo;
-    cell_step<S>(L, hd, neg, pin, pout, X, oi, oo);
+    if constexpr (HEAD)
+      cell_step_maybe_head<S>(L, hd, neg, pin, pout, X, true, X[K - 1], oi, oo);
+    else
+      cell_step<S>(L, hd, neg, pin, pout, X, oi, oo);
     for (int r = 0; r < K; ++r) dense[r][col] = X[r];
     dense[K][col] = oi;
     if (X[K - 1] != oo) return false;  // oout is X'[K-1]
@@ -198,14 +205,15 @@ static void line_inflow(const rt_solver &s, std::vector<double> &bd) {
   (void)M;
 }
 
-// Per-line maps and constants into (map, lc); unit_B: sources for B_g = 1
-// (material coupling), leaving map_host (the propagators' source) alone.
+// Per-line maps into map_dev, and the mu > 0 lines' head-cell maps into hmap_dev (used by
+// reflective chains only); unit_B: sources for B_g = 1 (material coupling), leaving
+// map_host (the propagators' source) alone.
 template <int S>
-rt_status rtsn_detail::line_maps_s(rt_solver *s, bool unit_B, DeviceBuf &map_dev, DeviceBuf &lc_dev) {
+rt_status rtsn_detail::line_maps_s(rt_solver *s, bool unit_B, DeviceBuf &map_dev, DeviceBuf &hmap_dev) {
   constexpr int WN = map_count<S>();
   const double hd = 0.5 * (s->p.X / s->p.N);
   const size_t Lp = s->Lpad;
-  std::vector<double> lc(2 * LC_COUNT * Lp, 0.0), unit_map;
+  std::vector<double> hmap(WN * Lp, 0.0), unit_map;
   std::vector<double> &map = unit_B ? unit_map : s->map_host;
   map.assign(2 * WN * Lp, 0.0);
   // lines are independent: chunks of them on the host workers (phys::parallel_for)
@@ -221,14 +229,20 @@ rt_status rtsn_detail::line_maps_s(rt_solver *s, bool unit_B, DeviceBuf &map_dev
       const int i = line_direction(s->H, half, ip), g = s->g_lo + gl;
       const size_t ell = ip + static_cast<size_t>(s->H) * gl;
       const LineConst L = line_constants(*s, i, g, unit_B);
-      for (int n = 0; n < LC_COUNT; ++n) lc[(half * LC_COUNT + n) * Lp + ell] = L.c[n];
       if (!cell_map<S>(L, hd, half == 0, W)) bad = true;
       for (int n = 0; n < WN; ++n) map[(half * WN + n) * Lp + ell] = W[n];
+      if (half == 1) {
+        double Wh[WN];
+        if (!cell_map<S, true>(L, hd, false, Wh)) bad = true;
+        for (int n = 0; n < head_map_first<S>(); ++n)  // the kernels keep only the rest apart
+          if (Wh[n] != W[n]) bad = true;
+        for (int n = 0; n < WN; ++n) hmap[n * Lp + ell] = Wh[n];
+      }
     }
   });
-  if (bad) return fail(s, RT_ERR_PARAM, "cell map: a structurally zero coefficient is not zero");
+  if (bad) return fail(s, RT_ERR_PARAM, "cell map: a structurally zero coefficient is not zero (or a head-cell row differs from its line map)");
   rt_status st;
-  if ((st = upload(s, lc_dev, lc.data(), lc.size() * sizeof(double)))) return st;
+  if ((st = upload(s, hmap_dev, hmap.data(), hmap.size() * sizeof(double)))) return st;
   if ((st = upload(s, map_dev, map.data(), map.size() * sizeof(double)))) return st;
   return RT_OK;
 }
@@ -237,7 +251,7 @@ template <int S>
 static rt_status setup_lines_s(rt_solver *s) {
   const size_t Lp = s->Lpad;
   rt_status st;
-  if ((st = line_maps_s<S>(s, false, s->map, s->lc))) return st;
+  if ((st = line_maps_s<S>(s, false, s->map, s->hmap))) return st;
   std::vector<double> lineB(2 * Lp, 0.0);
   for (int half = 0; half < 2; ++half)
     for (int gl = 0; gl < s->Gl; ++gl)

@@ -12,7 +12,7 @@ using namespace rtsn_detail;
 
 template <int S>
 static rt_status unit_maps_s(rt_solver *s) {
-  return line_maps_s<S>(s, true, s->map_unit, s->lc_unit);
+  return line_maps_s<S>(s, true, s->map_unit, s->hmap_unit);
 }
 
 static rt_status material_planck(rt_solver *s) {
@@ -64,7 +64,7 @@ extern "C" rt_status rt_material_enable(rt_solver *s, double rho_cv, const doubl
     if (!e) e = dalloc(s->qbuf, sizeof(double) * N);
     if (!e) e = dalloc(s->edges, sizeof(double) * (s->p.G + 1));
     if (!e) e = dalloc(s->map_unit, s->map.bytes);
-    if (!e) e = dalloc(s->lc_unit, s->lc.bytes);
+    if (!e) e = dalloc(s->hmap_unit, s->hmap.bytes);
     s->phi_fused = 64 % s->H == 0;  // a group's lines never straddle a wave
     if (!e && s->phi_fused) e = dalloc(s->phi_part, sizeof(double) * 4 * NG);  // [half sums, corrections][half]
     if (e) return fail(s, RT_ERR_NOMEM, std::string("material buffers: ") + hipGetErrorString(e));

@@ -41,7 +41,7 @@ SegArgs rtsn_detail::seg_args(rt_solver *s) {
   SegArgs a{};
   a.E = static_cast<double2 *>(s->E.p);
   a.map = static_cast<const double *>(s->map.p);
-  a.lc = static_cast<const double *>(s->lc.p);
+  a.hmap = static_cast<const double *>(s->hmap.p);
   a.bdry = static_cast<const double *>(s->bdry.p);
   a.yseg = static_cast<const double *>(s->yseg.p);
   a.yrefl = static_cast<const double *>(s->yrefl.p);
@@ -129,7 +129,7 @@ rt_status rtsn_detail::enqueue_pass(rt_solver *s, int T, bool coupled) {
   SegArgs a = seg_args(s);
   if (coupled) {
     a.map = static_cast<const double *>(s->map_unit.p);
-    a.lc = static_cast<const double *>(s->lc_unit.p);
+    a.hmap = static_cast<const double *>(s->hmap_unit.p);
     a.bcell = static_cast<const double *>(s->Bcell.p);
     a.Gl = s->Gl;
     a.H = s->H;

@@ -40,20 +40,25 @@ __device__ __forceinline__ void row_store(__amdgpu_buffer_rsrc_t r, int voff, in
 }
 
 // Reflective mu > 0 head cell (cell 0 of segment 0) with distinct per-substep
-// inflows: the reference's algebra with cell_step_maybe_head (cell.hpp),
-// level by level.  Rare (one cell per line per pass): line constants are
-// read from memory here instead of being kept in registers.
+// inflows, level by level: the head cell's own affine map (the host's probe of the
+// reference's algebra, cell_step_maybe_head, rtsn_lines.hip cell_map<S, true>) on the
+// carried state head_state(b), whose last component is the mirror's last-substep outflow --
+// the same FMA rows the wavefront kernels run for it.  Rare (one cell per line per pass):
+// the map is read from memory here instead of being kept in registers.  bs scales the map's
+// constants (material coupling: the cell's B_g(T(x)); 1 otherwise).
 template <int S, int T>
-__device__ __forceinline__ void head_cell(const double *lcp, size_t stride, double hd, const double (&b)[T][4],
-                                          double (&X)[T][SchemeDim<S>::K], double &oi, double &oo, double bs) {
-  LineConst L;
+__device__ __forceinline__ void head_cell(const double *hmp, size_t stride, double (&X)[T][SchemeDim<S>::K],
+                                          double &oi, double &oo, double bs) {
+  constexpr int K = SchemeDim<S>::K, WN = map_count<S>();
+  double Wh[WN];
 #pragma unroll
-  for (int n = 0; n < LC_COUNT; ++n) L.c[n] = lcp[n * stride];
-  L.c[LC_SC] *= bs;  // material coupling: the cell's B_g(T(x)) (1 otherwise)
+  for (int n = 0; n < WN; ++n) Wh[n] = hmp[n * stride];
 #pragma unroll
   for (int t = 0; t < T; ++t) {
-    double a, c;
-    cell_step_maybe_head<S>(L, hd, false, oi, oo, X[t], true, b[t][3], a, c);
+    double Xn[K], a, c;
+    map_apply<S, true>(Wh, X[t], oi, oo, Xn, a, c, bs);
+#pragma unroll
+    for (int r = 0; r < K; ++r) X[t][r] = Xn[r];
     oi = a;
     oo = c;
   }

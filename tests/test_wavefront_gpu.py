@@ -2,7 +2,8 @@
 rt_set_wavefront): lanes over cells, every step of an advance in one launch.
 
 Same arithmetic per (cell, level) as the pipelined segment pass -- the per-line affine map
-with exact carries, the reflective mu > 0 head by the reference's algebra -- so its node
+with exact carries, the reflective mu > 0 head by its own map (rtsn_lines.hip
+cell_map<S, true>, the reference's head algebra probed into the same rows) -- so its node
 array must equal the pipelined schedule's BITWISE (the segment kernels are pinned to the
 oracle by test_gpu_parity.py), for every scheme, boundary pair and line length around the
 lane-count edges (C = 1, 2, 4, 8 cells per lane; a chain of up to 8 waves handing over
@@ -25,8 +26,8 @@ LENGTHS = [1, 5, 31, 32, 33, 50, 63, 64, 65, 100, 127, 128, 129, 255, 256, 257, 
 # kernels_wave.hip's tick costs (ns; profiles/r05d_chain_plan.jsonl), rows C = 1, 2, 4, 8, columns 1..8 waves
 TICK_VACUUM = [[79, 141, 166, 185, 225, 248, 259, 272], [126, 194, 217, 238, 306, 343, 356, 368],
                [220, 300, 323, 341, 441, 541, 560, 579], [410, 500, 532, 555, 800, 880, 910, 943]]
-TICK_REFLECTIVE = [[201, 242, 258, 268, 276, 291, 322, 354], [250, 270, 304, 315, 337, 364, 375, 447],
-                   [346, 396, 413, 420, 531, 569, 610, 652], [533, 630, 646, 662, 830, 991, 1100, 1213]]
+TICK_REFLECTIVE = [[83, 156, 173, 191, 230, 255, 266, 278], [131, 203, 222, 244, 321, 349, 363, 388],
+                   [227, 307, 330, 351, 515, 551, 570, 587], [421, 529, 559, 579, 1032, 1070, 1089, 1113]]
 
 
 def wave_plan(N, reflective, max_waves=8):

@@ -2,7 +2,7 @@
 1000 BDF2 steps of llnl_slab_test's material on N-cell lines (4 groups, M = 2: 8 lines), every
 feasible cells-per-lane choice C (rt_set_wavefront_cells; the chain spans ceil(lanes / 64)
 waves), vacuum and reflective, median of 3 runs (advance + finish + sync after an 8-step warm
-start).  python tools/chain_plan.py [N ...] -> one JSON line per (N, bc_left, C)."""
+start).  python tools/chain_plan.py [vacuum|reflective] [N ...] -> one JSON line per (N, bc_left, C)."""
 import json
 import sys
 import time
@@ -46,8 +46,12 @@ def run(q, C):
         return sorted(ts)[1], st
 
 
-LENGTHS = [int(a) for a in sys.argv[1:]] or [65, 129, 192, 256, 320, 384, 448, 512, 640, 768, 1024, 1536, 2048]
-for bcl in (0, 2):
+ARGS = sys.argv[1:]
+KINDS = {"vacuum": (0,), "reflective": (2,)}.get(ARGS[0] if ARGS else "", (0, 2))
+if ARGS and ARGS[0] in ("vacuum", "reflective"):
+    ARGS = ARGS[1:]
+LENGTHS = [int(a) for a in ARGS] or [65, 129, 192, 256, 320, 384, 448, 512, 640, 768, 1024, 1536, 2048]
+for bcl in KINDS:
     for N in LENGTHS:
         q = params(N, bcl)
         with rtsn.Solver(q) as s:
