@@ -249,14 +249,16 @@ __host__ __device__ constexpr int head_map_first() {
 // the source); 1.0 elsewhere, which the compiler folds away.  For the correction
 // walks, which move a state with no data delta: NODATA skips the din/dout columns
 // (both 0.0; fma(w, 0.0, acc) is not folded by the compiler), ZERO0 also skips X[0]
-// (0.0 after one cell where row 0 copies dout: CN, BDF2) -- the same values.
-template <int S, bool CONST, bool NODATA = false, bool ZERO0 = false>
+// (0.0 after one cell where row 0 copies dout: CN, BDF2) -- the same values.  ROW_LO > 0:
+// only rows ROW_LO .. K (Xn below ROW_LO untouched), each the same FMA sequence as in the
+// whole map -- the reflective head lane redoing the rows where its map differs.
+template <int S, bool CONST, bool NODATA = false, bool ZERO0 = false, int ROW_LO = 0>
 __host__ __device__ __forceinline__ void map_apply(const double *W, const double *X, double din, double dout,
                                                    double *Xn, double &oin, double &oout, double cs = 1.0) {
   constexpr int K = SchemeDim<S>::K;
   static_assert(!ZERO0 || (NODATA && map_copy_row0<S>()), "X[0] vanishes only where row 0 copies a zero dout");
 #pragma unroll
-  for (int r = 0; r <= K; ++r) {
+  for (int r = ROW_LO; r <= K; ++r) {
     if (map_copy_row0<S>() && r == 0) {
       Xn[0] = dout;
       continue;

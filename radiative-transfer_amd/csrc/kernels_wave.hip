@@ -92,22 +92,38 @@ __device__ unsigned long long g_block_stamps[kWaveMaxWaves * kBlockStamps * 2];
 // per-substep outflows, probed into the same FMA rows), so every lane runs the same
 // instructions every tick -- round 4 branched into the reference's algebra there, and the
 // exec-mask divergence roughly doubled a reflective chain's tick.  The head map differs from
-// the line's only in its last rows (BDF2: the BDF substep's output and oin, which read the
-// mirror's last-substep outflow; the host checks the others are bitwise the line's; BE / CN:
-// nowhere), so a lane holds just those: W gets them on the head lane where a lane has one
-// cell; with more, cell 0 reads W0 = W with them replaced (the rest are W's own registers).
-template <int S, int C, bool PAIR>
+// the line's only from slot head_map_first on (BDF2: the BDF substep's output and oin, which
+// read the mirror's last-substep outflow; the host checks the others are bitwise the line's;
+// BE / CN: nowhere), so a lane holds just those: W gets them on the head lane where a lane has
+// one cell; with 2-4 cells, cell 0 reads W0 = W with them replaced (the rest are W's own
+// registers).  In the 5-8-wave chains at 8 cells per lane (which spilled already) the head
+// lane instead redoes those rows for its cell 0 with the head map's coefficients,
+// wave-uniform in Wh (the pair's line is the workgroup's): 16 FMAs under an exec mask in the
+// head's wave only -- 927-1046 ns per tick at 5-8 waves against 1032-1113 with W0, while up to
+// 4 waves W0 is 0-8% the faster (profiles/r05t_chain_plan_c8.jsonl).
+template <int S, int C, bool WIDE>
+__device__ __forceinline__ constexpr bool head_redo() {
+  return WIDE && C >= 8 && head_map_first<S>() < map_count<S>();
+}
+
+template <int S, int C, bool PAIR, bool REDO>
 __device__ __forceinline__ void head_maps(const SegArgs &a, int half, int ell, size_t stride, bool refl_head,
-                                          double (&W)[map_count<S>()], double (&W0)[map_count<S>()]) {
+                                          double (&W)[map_count<S>()], double (&W0)[map_count<S>()],
+                                          double (&Wh)[map_count<S>()]) {
   constexpr int WN = map_count<S>(), F = head_map_first<S>();
 #pragma unroll
   for (int n = 0; n < WN; ++n) W[n] = a.map[(static_cast<size_t>(half) * WN + n) * stride + ell];
   double T[WN - F > 0 ? WN - F : 1];
+#pragma unroll
+  for (int n = 0; n < WN; ++n) Wh[n] = 0.0;  // (REDO reads slots >= F only)
   if constexpr (PAIR) {
 #pragma unroll
     for (int n = F; n < WN; ++n) {
       const double h = a.hmap[n * stride + ell];  // every lane (ell < Lpad): a select, no branch
-      T[n - F] = refl_head ? h : W[n];
+      if constexpr (REDO)
+        Wh[n] = h;  // a wave-uniform address: scalar loads
+      else
+        T[n - F] = refl_head ? h : W[n];
     }
     if constexpr (C == 1) {
 #pragma unroll
@@ -120,7 +136,21 @@ __device__ __forceinline__ void head_maps(const SegArgs &a, int half, int ell, s
 #pragma unroll
   for (int n = 0; n < WN; ++n) asm volatile("" : "+v"(W[n]));
 #pragma unroll
-  for (int n = 0; n < WN; ++n) W0[n] = (PAIR && C > 1 && n >= F) ? T[n - F] : W[n];
+  for (int n = 0; n < WN; ++n) W0[n] = (PAIR && C > 1 && !REDO && n >= F) ? T[n - F] : W[n];
+}
+
+// Cell c of a lane: the map (W0 for a pair chain's cell 0), and with REDO the head lane's
+// redo of the rows where its map differs (head_maps).
+template <int S, int C, bool PAIR, bool REDO>
+__device__ __forceinline__ void lane_cell(int c, bool refl_head, const double (&W)[map_count<S>()],
+                                          const double (&W0)[map_count<S>()], const double (&Wh)[map_count<S>()],
+                                          const double *X, double din, double dout, double *Xn, double &oi,
+                                          double &oo) {
+  constexpr int K = SchemeDim<S>::K;
+  map_apply<S, true>(PAIR && C > 1 && c == 0 ? W0 : W, X, din, dout, Xn, oi, oo);
+  if constexpr (PAIR && REDO) {
+    if (c == 0 && refl_head) map_apply<S, true, false, false, K - 1>(Wh, X, din, dout, Xn, oi, oo);
+  }
 }
 
 // grid: one workgroup per line (mu < 0 lines then mu > 0 lines, ell < H Gl) -- or, PAIR (the
@@ -163,8 +193,8 @@ __global__ __launch_bounds__(64) void wavefront_kernel(SegArgs a, int nsteps, in
     }
   }
   const bool refl_head = PAIR && half == 1 && j == 0;  // one lane of a pair chain
-  double W[WN], W0[WN];
-  head_maps<S, C, PAIR>(a, half, ell, stride, refl_head, W, W0);
+  double W[WN], W0[WN], Wh[WN];
+  head_maps<S, C, PAIR, false>(a, half, ell, stride, refl_head, W, W0, Wh);
 
   // Xin: the state each lane receives at its tick -- lane - 1's exit state of the same level;
   // chain lane 0's is the chain head's inflow state (solver.cpp:695-697), the mu < 0 line's
@@ -219,7 +249,7 @@ __global__ __launch_bounds__(64) void wavefront_kernel(SegArgs a, int nsteps, in
 #pragma unroll
       for (int c = 0; c < C; ++c) {
         double Xn[K], oi, oo;
-        map_apply<S, true>(PAIR && C > 1 && c == 0 ? W0 : W, X, ein[c], eout[c], Xn, oi, oo);
+        lane_cell<S, C, PAIR, false>(c, refl_head, W, W0, Wh, X, ein[c], eout[c], Xn, oi, oo);
         if constexpr (PAD) {
           const bool pad = j * C + c >= a.N;
 #pragma unroll
@@ -337,8 +367,9 @@ __global__ __launch_bounds__(64 * (WIDE ? kWaveMaxWaves : 4)) void chain_kernel(
     }
   }
   const bool refl_head = PAIR && half == 1 && j == 0;
-  double W[WN], W0[WN];
-  head_maps<S, C, PAIR>(a, half, ell, stride, refl_head, W, W0);  // VGPR-resident maps
+  constexpr bool REDO = head_redo<S, C, WIDE>();
+  double W[WN], W0[WN], Wh[WN];
+  head_maps<S, C, PAIR, REDO>(a, half, ell, stride, refl_head, W, W0, Wh);  // VGPR-resident maps
   double Xin[K], X[K];
   {
     const double bv = a.bdry[static_cast<size_t>(PAIR ? 0 : half) * stride + ell];
@@ -376,7 +407,7 @@ __global__ __launch_bounds__(64 * (WIDE ? kWaveMaxWaves : 4)) void chain_kernel(
 #pragma unroll
     for (int c = 0; c < C; ++c) {
       double Xn[K], oi, oo;
-      map_apply<S, true>(PAIR && C > 1 && c == 0 ? W0 : W, X, ein[c], eout[c], Xn, oi, oo);
+      lane_cell<S, C, PAIR, REDO>(c, refl_head, W, W0, Wh, X, ein[c], eout[c], Xn, oi, oo);
       if constexpr (PAD) {
         const bool pad = j * C + c >= a.N;
 #pragma unroll
@@ -568,7 +599,7 @@ static const float kTickReflective[4][kWaveMaxWaves] = {  // N a multiple of C
     {83, 156, 173, 191, 230, 255, 266, 278},     // C = 1 (round 5 before the head map: 201 .. 354)
     {131, 203, 222, 244, 321, 349, 363, 388},    // C = 2
     {227, 307, 330, 351, 515, 551, 570, 587},    // C = 4
-    {421, 529, 559, 579, 1032, 1070, 1089, 1113}};  // C = 8
+    {421, 529, 559, 579, 927, 977, 1001, 1046}};  // C = 8 (5-8 waves: the head's redo, r05t_chain_plan_c8)
 constexpr double kTickPadded = 1.3;
 WavePlan wavefront_plan(int N, bool reflective, int max_waves) {
   max_waves = max_waves < 1 ? 1 : (max_waves > kWaveMaxWaves ? kWaveMaxWaves : max_waves);

@@ -27,7 +27,7 @@ LENGTHS = [1, 5, 31, 32, 33, 50, 63, 64, 65, 100, 127, 128, 129, 255, 256, 257, 
 TICK_VACUUM = [[79, 141, 166, 185, 225, 248, 259, 272], [126, 194, 217, 238, 306, 343, 356, 368],
                [220, 300, 323, 341, 441, 541, 560, 579], [410, 500, 532, 555, 800, 880, 910, 943]]
 TICK_REFLECTIVE = [[83, 156, 173, 191, 230, 255, 266, 278], [131, 203, 222, 244, 321, 349, 363, 388],
-                   [227, 307, 330, 351, 515, 551, 570, 587], [421, 529, 559, 579, 1032, 1070, 1089, 1113]]
+                   [227, 307, 330, 351, 515, 551, 570, 587], [421, 529, 559, 579, 927, 977, 1001, 1046]]
 
 
 def wave_plan(N, reflective, max_waves=8):
