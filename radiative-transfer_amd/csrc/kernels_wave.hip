@@ -59,6 +59,8 @@ static_assert(kWaveUnroll >= 2 && kWaveUnroll % 2 == 0, "renames cancel over an 
 #ifdef RT_WAVE_STAMPS
 constexpr int kStampWaves = 16384;
 __device__ unsigned long long g_wave_stamps[kStampWaves * 6];
+// (slot 0 also records the wave's HW_ID register: SIMD, CU and SE it runs on)
+__device__ unsigned int g_wave_hwid[kStampWaves];
 #define RT_STAMP(slot)                                                                              \
   do {                                                                                              \
     const unsigned long long t_ = __builtin_amdgcn_s_memtime();                                     \
@@ -67,6 +69,7 @@ __device__ unsigned long long g_wave_stamps[kStampWaves * 6];
     if ((threadIdx.x & 63) == 0 && wv_ < kStampWaves) {                                             \
       g_wave_stamps[wv_ * 6 + 2 * (slot)] = t_;                                                     \
       g_wave_stamps[wv_ * 6 + 2 * (slot) + 1] = r_;                                                 \
+      if ((slot) == 0) g_wave_hwid[wv_] = __builtin_amdgcn_s_getreg((31 << 11) | 4);                \
     }                                                                                               \
   } while (0)
 // chain_kernel, workgroup 0 only: every wave's s_memtime before and after each block's barrier
@@ -651,6 +654,13 @@ extern "C" int rt_debug_wave_stamps(unsigned long long *out, int waves) {
   if (hipDeviceSynchronize() != hipSuccess) return -1;
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(rtamd::g_wave_stamps), sizeof(unsigned long long) * 6 * waves) != hipSuccess)
     return -1;
+  return waves;
+}
+// the HW_ID register of each wave of the last launch (diagnostic builds only)
+extern "C" int rt_debug_wave_hwid(unsigned int *out, int waves) {
+  if (waves > rtamd::kStampWaves) waves = rtamd::kStampWaves;
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(rtamd::g_wave_hwid), sizeof(unsigned int) * waves) != hipSuccess) return -1;
   return waves;
 }
 // per-block stamps of chain_kernel's workgroup 0: [wave][block][before, after the barrier]
