@@ -1,5 +1,6 @@
 // rtsn_lines.hip -- per-line setup of a handle: the line constants of the reference algebra,
-// the per-line affine cell map (cell.hpp) and the aligned schedule's segment propagators,
+// the per-line affine cell map (cell.hpp) and the reflective head cell's own map (probed from
+// the same algebra), the aligned schedule's segment propagators,
 // boundary inflows, and the segmentation of the lines (segment_lines / resegment).
 
 #include <atomic>
