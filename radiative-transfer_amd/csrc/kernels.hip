@@ -678,9 +678,12 @@ __global__ void __launch_bounds__(64) moments_kernel(const double2 *__restrict__
 // Bytes in flight per CU (two workgroups: 68.6 KB of LDS each, <= 168 VGPRs for three waves
 // per SIMD): 4 x 2 x 32 KB = 256 KB -- the first form (one loader per half, one item deep,
 // 128 KB) read at 5.94 TB/s (22.1 ms on SL, profiles/r05b_*), the state scan at 6.86.
-constexpr int kMomLoadersPerHalf = 2;
+#ifndef RT_MOM_LOADERS
+#define RT_MOM_LOADERS 2  // loader waves per half (timing experiments)
+#endif
+constexpr int kMomLoadersPerHalf = RT_MOM_LOADERS;
 template <int H>
-__global__ void __launch_bounds__(320) moments_pc_kernel(const double2 *__restrict__ E, const double *__restrict__ mu,
+__global__ void __launch_bounds__(64 * (2 * kMomLoadersPerHalf + 1)) moments_pc_kernel(const double2 *__restrict__ E, const double *__restrict__ mu,
                                                          const double *__restrict__ wt, double *phi, double *F,
                                                          double *phi_plus, LineMap m) {
 #pragma clang fp contract(off)
