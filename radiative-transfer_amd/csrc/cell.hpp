@@ -279,4 +279,47 @@ __host__ __device__ __forceinline__ void map_apply(const double *W, const double
   oout = Xn[K - 1];
 }
 
+// The per-line affine cell map (cell.hpp, map_apply): coefficients from
+// cell_step<S> on unit inputs (constants and data zeroed), constants from
+// cell_step<S> on zero inputs.  Every coefficient outside the structural
+// pattern must come out exactly zero; false otherwise.
+// (host code: rtsn_lines.hip builds every line's maps with it, tools/cell_map_check.cpp tests it.)
+// HEAD: the reflective mu > 0 head cell's map instead (cell_step_maybe_head with the
+// mirror's last-substep outflow b3 = X[K-1], the carried state being head_state(b): a map
+// of the same structure, so the kernels run the head cell as the same FMA rows as every
+// other cell -- no divergent per-tick branch into the reference's algebra).
+template <int S, bool HEAD = false>
+inline bool cell_map(const LineConst &Lin, double hd, bool neg, double *W) {
+  constexpr int K = SchemeDim<S>::K;
+  double dense[K + 1][K + 3];  // [row][input 0..K+1, constant K+2]
+  for (int col = 0; col <= K + 2; ++col) {
+    LineConst L = Lin;
+    if (col != K + 2) L.c[LC_SC] = 0.0;
+    double X[K] = {};
+    double pin = 0.0, pout = 0.0;
+    if (col < K) X[col] = 1.0;
+    if (col == K) pin = 1.0;
+    if (col == K + 1) pout = 1.0;
+    double oi, oo;
+    if constexpr (HEAD)
+      cell_step_maybe_head<S>(L, hd, neg, pin, pout, X, true, X[K - 1], oi, oo);
+    else
+      cell_step<S>(L, hd, neg, pin, pout, X, oi, oo);
+    for (int r = 0; r < K; ++r) dense[r][col] = X[r];
+    dense[K][col] = oi;
+    if (X[K - 1] != oo) return false;  // oout is X'[K-1]
+  }
+  for (int r = 0; r <= K; ++r)
+    for (int col = 0; col <= K + 2; ++col) {
+      const bool copy = map_copy_row0<S>() && r == 0;
+      const bool used = !copy && (col == K + 2 || map_dep<S>(r, col));
+      if (used) {
+        W[map_slot<S>(r, col)] = dense[r][col];
+      } else if (dense[r][col] != (copy && col == K + 1 ? 1.0 : 0.0)) {
+        return false;
+      }
+    }
+  return true;
+}
+
 }  // namespace rtamd

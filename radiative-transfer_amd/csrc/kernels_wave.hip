@@ -91,7 +91,7 @@ __device__ unsigned long long g_block_stamps[kWaveMaxWaves * kBlockStamps * 2];
 #endif
 
 // The lane's cell maps.  A pair chain's mu > 0 head lane runs its cell 0 on the head cell's
-// own map (rtsn_lines.hip cell_map<S, true>: the reference's head algebra with the mirror's
+// own map (cell.hpp cell_map<S, true>: the reference's head algebra with the mirror's
 // per-substep outflows, probed into the same FMA rows), so every lane runs the same
 // instructions every tick -- round 4 branched into the reference's algebra there, and the
 // exec-mask divergence roughly doubled a reflective chain's tick.  The head map differs from

@@ -41,7 +41,7 @@ __device__ __forceinline__ void row_store(__amdgpu_buffer_rsrc_t r, int voff, in
 
 // Reflective mu > 0 head cell (cell 0 of segment 0) with distinct per-substep
 // inflows, level by level: the head cell's own affine map (the host's probe of the
-// reference's algebra, cell_step_maybe_head, rtsn_lines.hip cell_map<S, true>) on the
+// reference's algebra, cell_step_maybe_head, cell.hpp cell_map<S, true>) on the
 // carried state head_state(b), whose last component is the mirror's last-substep outflow --
 // the same FMA rows the wavefront kernels run for it.  Rare (one cell per line per pass):
 // the map is read from memory here instead of being kept in registers.  bs scales the map's
