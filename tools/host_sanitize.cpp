@@ -1,6 +1,7 @@
 // host_sanitize -- the host-side code of librtsn (the .prm reader, Planck /
-// GLQuad / correction tables, equilibrium sources, affine cell maps of
-// cell.hpp) under AddressSanitizer + UBSan, over every .prm in a directory.
+// GLQuad / correction tables, equilibrium sources) under AddressSanitizer +
+// UBSan, over every .prm in a directory (the affine cell maps of cell.hpp:
+// tools/cell_map_check.cpp).
 // Host code only: GPU sanitizers are not available on this pool.
 //   g++ -std=c++17 -O1 -g -fsanitize=address,undefined -fno-omit-frame-pointer \
 //       -I radiative-transfer_amd/csrc tools/host_sanitize.cpp \
