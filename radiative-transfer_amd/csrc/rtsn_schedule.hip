@@ -444,13 +444,14 @@ extern "C" rt_status rt_synchronize(rt_solver *s) {
 // per segment, segmentation), a BDF2 run takes the pipelined schedule with the least
 // estimated whole-run time (plan_schedule): time block T of 8-40 steps, four waves per
 // segment (sweep_split_kernel<3, T, 4>, every launch of the run) and segments sized for w of
-// 4-32 workgroups per CU.  The model (fitted to the finite-state whole-run
+// 1-32 workgroups per CU (1 and 2 only when clearly ahead, plan_schedule).  The model (fitted to the finite-state whole-run
 // grids profiles/archive/r03l_grid{16,128}.jsonl: mean error 3%): a run of n steps is P = n / T
 // passes over a chain of C segment positions, launched as P + C - 1 launches whose active
 // positions form a band (ramp up, plateau of min(P, C), ramp down); a launch of W workgroups
 // runs in rounds of the resident 2 per CU, and a round's time is one segment's Ls x T / 4
 // cell-levels per wave at the per-level cost of its block (t_T) times the workgroups the
-// busiest CU holds (ceil(W / CUs): a wave per SIMD each).  n mod T steps more ride the drain as
+// busiest CU holds (ceil(W / CUs): a wave per SIMD each), stretched by the workgroup's own
+// wave pipeline fill over a short segment.  n mod T steps more ride the drain as
 // every position's last block (one launch more, pipe_launch) when they are at least T / 4;
 // else, on reflective chains and at T = 40 (whose tail kernel would spill) they run
 // as aligned passes with the cross-segment correction (~3 steps' cost each, ~3 ms of folds
@@ -490,7 +491,12 @@ static double run_ms_model(const RunGeom &g, long long n, int T, int w) {
   const long long C = g.reflective ? 2 * Sg : Sg, R = g.reflective ? Q : 2 * Q;
   const long long P = n / T, rem = n % T;
   if (P == 0) return 1e300;
-  const double tf = level_ns(T) * 1e-9, tl = 0.99 * tf, unit = static_cast<double>(Ls) * T / kw;
+  // a segment's cell-levels per wave, and the workgroup's own pipeline fill: wave w of kw
+  // starts 2 w chunk intervals after wave 0 (kernels_split.hip), which short segments feel
+  // (round 5, late: 48-cell segments ran ~2x the model without it, profiles/r05zf_*)
+  const long long nch = (Ls + split_chunk_cells() - 1) / split_chunk_cells();
+  const double fill = static_cast<double>(nch + 2 * (kw - 1)) / static_cast<double>(nch);
+  const double tf = level_ns(T) * 1e-9, tl = 0.99 * tf, unit = static_cast<double>(Ls) * T / kw * fill;
   const long long S = static_cast<long long>(occ) * g.cus;
   auto launch = [&](long long a) {  // seconds
     const long long W = a * R, full = W / S, part = W % S;
@@ -525,13 +531,20 @@ struct Schedule {
 static Schedule plan_schedule(const RunGeom &g, long long nsteps) {
   // T = 4 over four waves (no remainder for n % 4 == 0) measured slower than T = 8 with its
   // aligned remainder (16-group shard, 100 steps: 181 vs 167 ms, profiles/archive/r04d_solve_plan.jsonl)
-  static const int kBlocks[] = {40, 32, 24, 20, 16, 8}, kWgs[] = {4, 8, 16, 32};
-  Schedule best;
+  // Segments for 1 or 2 workgroups per CU (round 5, late) serve lines too few to fill the chip
+  // at any segmentation (few groups, long lines: 4 groups x 5000 cells, 1000 steps, 4.6 ms at
+  // one workgroup per CU against 7.3 at the old plan's four, profiles/r05zf_*); they are taken
+  // only when the model puts them 3% ahead of the best of 4-32 (its error on these runs), so
+  // that chip-filling runs (the SL slab: < 1% either way) keep the measured schedules.
+  static const int kBlocks[] = {40, 32, 24, 20, 16, 8}, kWgs[] = {1, 2, 4, 8, 16, 32};
+  Schedule best, few;
   for (int T : kBlocks)
     for (int w : kWgs) {
       const double ms = run_ms_model(g, nsteps, T, w);
-      if (ms < 1e300 && (!best.T || ms < best.ms)) best = {T, w, ms};
+      Schedule &b = w >= 4 ? best : few;
+      if (ms < 1e300 && (!b.T || ms < b.ms)) b = {T, w, ms};
     }
+  if (few.T && (!best.T || few.ms < 0.97 * best.ms)) return few;
   return best;
 }
 
