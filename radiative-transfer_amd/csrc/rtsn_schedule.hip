@@ -444,8 +444,10 @@ extern "C" rt_status rt_synchronize(rt_solver *s) {
 // per segment, segmentation), a BDF2 run takes the pipelined schedule with the least
 // estimated whole-run time (plan_schedule): time block T of 8-40 steps, four waves per
 // segment (sweep_split_kernel<3, T, 4>, every launch of the run) and segments sized for w of
-// 1-32 workgroups per CU (1 and 2 only when clearly ahead, plan_schedule).  The model (fitted to the finite-state whole-run
-// grids profiles/archive/r03l_grid{16,128}.jsonl: mean error 3%): a run of n steps is P = n / T
+// 1-32 workgroups per CU (1 and 2 only when clearly ahead, plan_schedule).  The model
+// (fitted to the finite-state whole-run grids
+// profiles/archive/r03l_grid{16,128}.jsonl, mean error 3%, and refit in round 5 on few-group
+// long lines, profiles/r05zf_* / r05zg_*, 4% over 120 forced runs): a run of n steps is P = n / T
 // passes over a chain of C segment positions, launched as P + C - 1 launches whose active
 // positions form a band (ramp up, plateau of min(P, C), ramp down); a launch of W workgroups
 // runs in rounds of the resident 2 per CU, and a round's time is one segment's Ls x T / 4
