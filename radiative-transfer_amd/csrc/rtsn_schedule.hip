@@ -530,6 +530,9 @@ struct Schedule {
   double ms = 0.0;
 };
 
+#ifndef RT_PLAN_FEW_GUARD
+#define RT_PLAN_FEW_GUARD 0.97  // 1-2 workgroups per CU must beat the best of 4-32 by this factor
+#endif
 static Schedule plan_schedule(const RunGeom &g, long long nsteps) {
   // T = 4 over four waves (no remainder for n % 4 == 0) measured slower than T = 8 with its
   // aligned remainder (16-group shard, 100 steps: 181 vs 167 ms, profiles/archive/r04d_solve_plan.jsonl)
@@ -546,7 +549,7 @@ static Schedule plan_schedule(const RunGeom &g, long long nsteps) {
       Schedule &b = w >= 4 ? best : few;
       if (ms < 1e300 && (!b.T || ms < b.ms)) b = {T, w, ms};
     }
-  if (few.T && (!best.T || few.ms < 0.97 * best.ms)) return few;
+  if (few.T && (!best.T || few.ms < RT_PLAN_FEW_GUARD * best.ms)) return few;
   return best;
 }
 
