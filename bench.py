@@ -67,6 +67,7 @@ import time
 from pathlib import Path
 
 REPO = Path(__file__).resolve().parent
+T_PROCESS0 = time.perf_counter()  # the process's own clock: process_wall_s in the line
 sys.path.insert(0, str(REPO / "radiative-transfer_amd"))
 
 import numpy as np  # noqa: E402
@@ -503,6 +504,9 @@ def run_rank(solver, p: dict, steps: int, warmup: int, world: int, device, shard
     solver.synchronize()
     barrier()
     t_end = time.perf_counter()
+    # device memory in use with the state resident (the handle's hipMallocs are not torch's,
+    # so the device's own count: total - free)
+    free_b, total_b = torch.cuda.mem_get_info(device) if device.type == "cuda" else (0, 0)
 
     # group-summed absorption all-reduce, outside the timed region
     absorb = torch.zeros(p["N"], dtype=torch.float64, device=device)
@@ -602,6 +606,7 @@ def run_rank(solver, p: dict, steps: int, warmup: int, world: int, device, shard
                      "pass is HBM-bound: see hbm_pass_t1") if tb > 1 else "HBM-bound pass",
         },
         "state_finite": finite,
+        "device_memory_gb": {"used": (total_b - free_b) / 1e9, "total": total_b / 1e9},
     }
     if per_rank is not None:
         line["per_rank"] = per_rank
@@ -650,7 +655,8 @@ def side_leg(p: dict, info, world: int, device, local: int, scaling: str, tb: in
 def material_params(p: dict) -> dict:
     """The material leg's configuration from the sweep's: BE, the v/c correction inactive
     (V = 0) as rt_material_enable requires -- for either SL variant -- and SURVEY's dt = 1e-3
-    (the BE coupling stays finite; stability number 1.22 at rho_cv = 1)."""
+    (stiffness number 1.22 at 1 keV and rho_cv = 1; ~1e5 with the material at 50 keV, where the
+    explicit emission of rounds 1-5 diverged and the linearised implicit one is stable)."""
     return dict(p, ts_method=1, V=0.0, dt=1e-3)
 
 
@@ -722,7 +728,7 @@ def rccl_gather_check(comm, solver, gathered, dirs) -> dict:
 
 
 def run_material(p: dict, info, world: int, device, local: int, steps: int, dirs=None, rank: int = 0,
-                 comm=None, comm_error=None) -> dict:
+                 comm=None, comm_error=None, T0_keV=None) -> dict:
     """The material-temperature coupling (rt_material_*, beyond the reference) on
     the same SL shard: BE steps (the reference's BDF2 diverges on SL within a few
     steps, DESIGN.md §4, which would leave T meaningless; the v/c correction off, as
@@ -745,8 +751,8 @@ def run_material(p: dict, info, world: int, device, local: int, steps: int, dirs
     if comm is None:
         path = f"torch.distributed all-reduce on the handle's stream (rt_comm unavailable: {comm_error})"
     with make_solver(q, local, info, dirs) as s:  # q(x): each rank's groups or directions, summed
-        number = s.material_enable(1.0)
-        buf = torch.zeros(q["N"], dtype=torch.float64, device=device)
+        number = s.material_enable(1.0, None if T0_keV is None else np.full(q["N"], float(T0_keV)))
+        buf = torch.zeros(2 * q["N"], dtype=torch.float64, device=device)
 
         def step(n):
             if comm is not None:
@@ -780,10 +786,11 @@ def run_material(p: dict, info, world: int, device, local: int, steps: int, dirs
     if world > 1:
         dist.all_reduce(u)
     upd = float(u[0])
-    return {"what": "material-temperature coupling (beyond the reference): BE step with per-cell Planck "
-                    "emission, q(x) all-reduce over ranks, T update",
+    return {"what": "material-temperature coupling (beyond the reference): BE step with the per-cell Planck "
+                    "emission linearised implicit in T, [q, b] all-reduce over ranks, T update",
+            "T0_keV": float(T0_keV if T0_keV is not None else q["T"]),
             "ts_method": 1, "steps": steps, "warmup": 1, "ms_per_step": 1e3 * wall / steps,
-            "updates_per_s": upd / wall, "allreduce_bytes_per_step": 8 * q["N"], "allreduce": path,
+            "updates_per_s": upd / wall, "allreduce_bytes_per_step": 16 * q["N"], "allreduce": path,
             "rccl": rtsn.comm_version(),  # the RCCL rt_comm ran on (the process's librccl.so.1)
             "stability_number": number, "rho_cv": 1.0, "T_range_keV": [float(T.min()), float(T.max())],
             "state_finite": bool(np.isfinite(T).all())}
@@ -1020,6 +1027,9 @@ def main():
         try:
             line["material"] = run_material(p, info, world, device, local, args.material_steps, dirs, rank,
                                             comm, comm_error)
+            # the same at 50 keV: emission stiffness ~1e5, beyond any explicit step
+            line["material_hot"] = run_material(p, info, world, device, local, args.material_steps, dirs, rank,
+                                                comm, comm_error, T0_keV=50.0)
         except rtsn.RtError as e:  # an rt_comm wait expired or RCCL failed: the side leg is skipped
             if comm is not None:   # (every rank raises: the collectives are the same on all)
                 comm.close()
@@ -1033,6 +1043,7 @@ def main():
     if rank == 0:
         line["llnl_slab_test"] = llnl_slab_test_rate(line.get("reference_config"))
     if rank == 0:
+        line["process_wall_s"] = time.perf_counter() - T_PROCESS0
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

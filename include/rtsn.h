@@ -45,8 +45,8 @@ typedef enum {
   RT_ERR_TIMEOUT = 7,     /* an rt_comm wait passed RTSN_COMM_TIMEOUT_S: the communicator was aborted */
   RT_ERR_ARG = 8,         /* NULL handle / bad argument */
   RT_ERR_STATE = 9,       /* call not valid in the handle's mode (e.g. rt_advance with material coupling on) */
-  RT_WARN_UNSTABLE = 10   /* a warning, not a failure: rt_material_enable turned coupling on, but its explicit
-                             emission step is above the stability limit (rt_material_stability) */
+  RT_WARN_UNSTABLE = 10   /* not returned since round 6 (the coupling's T update is implicit in its emission);
+                             kept so that the values of the codes do not change */
 } rt_status;
 
 /* Every .prm key (ParameterHandler.cpp:100-212) with the reference's meaning.
@@ -294,42 +294,80 @@ rt_status rt_get_level_waves(rt_solver *s, int *waves);
  * and segment) and segments per line. */
 rt_status rt_sweep_geometry(rt_solver *s, int *workgroups, long long *tiles);
 
+/* ---- test and A/B hooks -------------------------------------------------
+ * Kernel forms the tests compare bitwise and the measurements time against each other
+ * (the library reads no environment variable to pick a kernel or a schedule; the variables
+ * read are RTSN_COMM_TIMEOUT_S, RTSN_POOL_MB, RTSN_EXPORT_CHUNK -- cells per chunk of the
+ * rt_get_psi / rt_get_ends / rt_set_ends transfers, for testing the chunk edges -- and, in
+ * bin/transfer and bin/test_gray, TRANSFER_DIR, RT_TABLE_DIR, RTSN_QUIET and the rank
+ * variables RTSN_RANKS, RTSN_DEVICE_BASE and RTSN_FAULT_STALL_RANK, a test hook).
+ * Moments kernel where M/2 is 8, 16 or 32: 1 (default) the producer/consumer
+ * moments_pc_kernel, 0 the one-wave moments_kernel; bitwise-identical results. */
+rt_status rt_set_moments_form(rt_solver *s, int form);
+/* The material coupling's cross-segment correction of the fused angular sums: 0 (default)
+ * the closed forms (phi_correction_geo_kernel for BE / CN, phi_correction_rows_kernel for
+ * BDF2), 1 the cell-by-cell walk; equal to rounding. */
+rt_status rt_set_phi_correction_form(rt_solver *s, int form);
+/* Fault injection: the pipelined sub-launch after `after` more successful ones fails with
+ * RT_ERR_DEVICE without starting a kernel (-1: off, the default).  A launch cut into
+ * sub-launches commits each sub-launch's chain positions as soon as it is in the stream, so
+ * the next call (rt_advance, rt_finish, a read-out) runs exactly the positions still owed. */
+rt_status rt_debug_fail_launch(rt_solver *s, int after);
+
 /* ---- material-temperature coupling (beyond the reference) ---------------
  * The reference holds T constant (solver.cpp:157).  With coupling enabled the
  * handle carries a cell temperature T(x) and, per full time step n (duration
- * dt; ts_method 3's four substeps form one step):
- *   1. sweep with the per-cell emission B_g(T^n(x)) (Planck group integrals
- *      on the device, Planck.cpp:44-337's algorithm; the last group is the
- *      grey remainder a c T^4 - integral over groups 0..G-2, when positive);
- *   2. q(x) = sum_g sigma_g (phi_g^{n+1}(x) - W B_g(T^n(x))), W = sum_i w_i:
- *      this handle's groups only -- with sharded groups the callers sum the
- *      ranks' q (one all-reduce of N doubles per step, e.g. RCCL);
- *   3. T^{n+1}(x) = T^n(x) + dt q(x) / rho_cv.
- * With ts_method 1 (BE) the total energy sum_x dx (sum_g phi_g / c + rho_cv T)
- * changes by exactly -dt x (net boundary outflow) per step (up to rounding).
- * Requires the v/c correction to be inactive (V == 0 or use_correction == 0). */
+ * dt; ts_method 3's four substeps form one step), with sigma_g = rho kappa_g and
+ * W = sum_i w_i over all directions:
+ *   1. sweep with the per-cell emission Beff_g = B_g(T^n) + p_g (Planck group
+ *      integrals on the device, Planck.cpp:44-337's algorithm; the last group is
+ *      the grey remainder a c T^4 - integral over groups 0..G-2, when positive),
+ *      p_g the share of the owed emission (below) paid in this sweep;
+ *   2. q(x) = sum_g sigma_g (phi_g^{n+1} - W B_g(T^n)) and b(x) = sum_g sigma_g
+ *      dB_g/dT(T^n): this handle's groups only -- with sharded groups the callers
+ *      sum both over the ranks (ONE all-reduce of 2N doubles per step, e.g. RCCL);
+ *   3. T^{n+1} = T^n + dT with dT = dt q / (rho_cv + dt W b): the update implicit
+ *      in the material's own emission (B(T^{n+1}) linearised about T^n), which
+ *      relaxes T toward the radiation's temperature at any dt / rho_cv (linear grey
+ *      analysis; the explicit dT = dt q / rho_cv of rounds 1-5 needed
+ *      dt W b / rho_cv < 2 + sigma c dt) and keeps T > 0 for BE (dT > -T since
+ *      B_g <= T dB_g/dT);
+ *   4. the material thereby emitted dt W sigma_g dB_g/dT dT per group beyond the
+ *      sweep's B: it joins the group's owed emission, paid in the next sweeps as
+ *      p_g = max(owed_g, -B_g) (Beff >= 0; all of it unless the material cooled by
+ *      a large fraction of T in one step).
+ * With ts_method 1 (BE) radiation + material + owed energy,
+ * sum_x dx (sum_g phi_g / c + rho_cv T + rt_get_material_transit), changes by
+ * exactly -dt x (net boundary outflow) per step (up to rounding).  Requires the
+ * v/c correction to be inactive (V == 0 or use_correction == 0). */
 /* Turn coupling on: rho_cv > 0 (material energy per volume per keV), T_cells
- * (N, host) the initial T(x), NULL for the uniform p.T.  The state psi is kept.
- * Returns RT_WARN_UNSTABLE (coupling is on) when the explicit emission's stability
- * number at the hottest cell exceeds 2 -- see rt_material_stability. */
+ * (N, host) the initial T(x), NULL for the uniform p.T.  The state psi is kept; nothing
+ * is owed.  (RT_WARN_UNSTABLE is no longer returned: the update is implicit in T.) */
 rt_status rt_material_enable(rt_solver *s, double rho_cv, const double *T_cells);
-/* Stability number of the explicit emission at the current T(x): linearising step 3
- * around the hottest cell, T' = T - dt (W sum_g rho kappa_g dB_g/dT) / rho_cv T + ...,
- * so forward-Euler stability needs  number = dt W sum_g rho kappa_g dB_g/dT(T_max) /
- * rho_cv < 2  (W = sum of all quadrature weights, the sum over ALL G groups -- a shard
- * reports the whole configuration's number).  Blocks (reads T(x) back). */
+/* The emission's stiffness at the current T(x): number = dt W sum_g rho kappa_g
+ * dB_g/dT(T_max) / rho_cv over ALL G groups (a shard reports the whole configuration's
+ * number); the implicit update scales the explicit change by 1 / (1 + number) at the
+ * hottest cell, and number < 2 was the explicit emission's limit.  Blocks (reads T(x)). */
 rt_status rt_material_stability(rt_solver *s, double *number);
-/* Steps 1-2: one coupled sweep, then this handle's q into d_q (DEVICE, N
- * doubles; NULL: an internal buffer), on the handle's stream, asynchronous. */
+/* Steps 1-2: one coupled sweep, then this handle's [q, b] into d_q (DEVICE, 2N
+ * doubles: q(x) then b(x); NULL: an internal buffer), on the handle's stream,
+ * asynchronous. */
 rt_status rt_material_sweep(rt_solver *s, double *d_q);
-/* Step 3 from the (group-summed) q in d_q (DEVICE, N; NULL: the internal
- * buffer), then B_g(T(x)) for the next step; handle's stream, asynchronous. */
+/* Steps 3-4 from the group-summed [q, b] in d_q (DEVICE, 2N; NULL: the internal
+ * buffer), then B_g, dB_g/dT, the owed emission and Beff_g at the new T(x) for the next
+ * step; handle's stream, asynchronous. */
 rt_status rt_material_update(rt_solver *s, const double *d_q);
 /* nsteps x (sweep + update) for a handle that holds all G groups. */
 rt_status rt_material_step(rt_solver *s, int nsteps);
-/* T(x) (N) and the per-cell emission B (G_local*N, g + G_local*c) to host memory. */
+/* T(x) (N), the per-cell B_g(T(x)) and the next step's emission Beff (G_local*N each,
+ * g + G_local*c) to host memory. */
 rt_status rt_get_temperature(rt_solver *s, double *T_cells);
 rt_status rt_get_cell_planck(rt_solver *s, double *B);
+rt_status rt_get_cell_emission(rt_solver *s, double *Beff);
+/* Energy per volume the material owes the radiation, per cell (N, host): dt W sum over
+ * the handle's groups of sigma_g (p_g + owed_g) -- the next sweep's payment and the rest;
+ * sum it over group shards. */
+rt_status rt_get_material_transit(rt_solver *s, double *E);
 
 /* ---- multi-GPU: RCCL behind the ABI (one process per GPU, xGMI) -----------
  * The reference is single-process (main.cc:79-133).  Energy groups are independent for
@@ -347,7 +385,11 @@ rt_status rt_get_cell_planck(rt_solver *s, double *B);
  * moment the stream reaches that collective: the handle's own work queued before it (a long
  * rt_advance, the sweeps of rt_comm_material_step) is waited for without the deadline.  On
  * expiry -- a rank missing or stalled -- the communicator is aborted, the call returns
- * RT_ERR_TIMEOUT and later collectives on it RT_ERR_STATE. */
+ * RT_ERR_TIMEOUT and later collectives on it RT_ERR_STATE.  The stream-ordered collectives
+ * (rt_comm_allreduce_absorption, rt_comm_material_step) return before their all-reduces ran:
+ * retire them with rt_comm_synchronize before any other host wait on the handle (a host
+ * read-out such as rt_get_temperature, rt_synchronize, an upload that waits for the stream),
+ * whose own waits carry no deadline -- only then does the bound hold for a missing peer. */
 typedef struct rt_comm rt_comm;
 #define RT_COMM_ID_BYTES 128
 /* ncclGetUniqueId: on one rank, then handed to every rank (file, pipe, MPI, ...). */
@@ -382,7 +424,7 @@ rt_status rt_comm_gather_psi_source(rt_comm *c, rt_solver *s, double *psi_source
  * DEVICE buffer d_out, stream-ordered, no host synchronisation. */
 rt_status rt_comm_allreduce_absorption(rt_comm *c, rt_solver *s, double *d_out);
 /* nsteps coupled steps (rt_material_*) across the shards: per step the shard's sweep and
- * q(x), one ncclAllReduce(sum) of q (N doubles) on the handle's stream, then the T
+ * [q, b], one ncclAllReduce(sum) of those 2N doubles on the handle's stream, then the T
  * update -- stream-ordered, no host synchronisation; every rank ends with the same T(x). */
 rt_status rt_comm_material_step(rt_comm *c, rt_solver *s, int nsteps);
 /* Host wait for everything enqueued on the handle's stream (its sweeps and c's stream-

@@ -83,12 +83,18 @@ def lib():
         L.orc_material_sweep.argtypes = [C.c_void_p, dp]
         L.orc_material_update.argtypes = [C.c_void_p, dp]
         L.orc_material_update.restype = None
+        L.orc_get_material_transit.argtypes = [C.c_void_p, dp]
+        L.orc_get_material_transit.restype = None
         L.orc_get_temperature.argtypes = [C.c_void_p, dp]
         L.orc_get_temperature.restype = None
         L.orc_get_cell_planck.argtypes = [C.c_void_p, dp]
         L.orc_get_cell_planck.restype = None
+        L.orc_get_cell_emission.argtypes = [C.c_void_p, dp]
+        L.orc_get_cell_emission.restype = None
         L.orc_planck_cell.argtypes = [C.c_double, C.c_int, dp, C.c_int]
         L.orc_planck_cell.restype = C.c_double
+        L.orc_planck_cell_dBdT.argtypes = [C.c_double, C.c_int, dp, C.c_int]
+        L.orc_planck_cell_dBdT.restype = C.c_double
         _lib = L
     return _lib
 
@@ -179,7 +185,8 @@ class OracleSolver:
         lib().orc_set_parallel_copies(self._h, 1 if on else 0)
 
     def set_threads(self, n: int):
-        """OpenMP threads over the lines of a direction (results do not depend on it)."""
+        """OpenMP threads over the (direction, group) lines of a run of same-sign directions
+        (results do not depend on it).."""
         lib().orc_set_threads(self._h, int(n))
 
     def solve(self):
@@ -264,8 +271,9 @@ class OracleSolver:
             raise OracleError(f"material_enable -> {ORC_ERRORS.get(st, st)}")
 
     def material_sweep(self) -> np.ndarray:
-        """One coupled full step; returns this solver's q (N)."""
-        q = np.empty(self.N)
+        """One coupled full step; returns this solver's [q, b] (2N: q(x), then
+        sum over its groups of sigma_g dB_g/dT(x)) -- sum it over group shards."""
+        q = np.empty(2 * self.N)
         st = lib().orc_material_sweep(self._h, _dp(q))
         if st:
             raise OracleError(f"material_sweep -> {ORC_ERRORS.get(st, st)}")
@@ -284,10 +292,22 @@ class OracleSolver:
         lib().orc_get_temperature(self._h, _dp(out))
         return out
 
+    def material_transit(self) -> np.ndarray:
+        """(N) energy per volume the material owes the radiation (this solver's groups)."""
+        out = np.empty(self.N)
+        lib().orc_get_material_transit(self._h, _dp(out))
+        return out
+
     def cell_planck(self) -> np.ndarray:
-        """(G_local, N) per-cell emission."""
+        """(G_local, N) B_g(T(x))."""
         out = np.empty(self.N * self.Gl)
         lib().orc_get_cell_planck(self._h, _dp(out))
+        return out.reshape(self.N, self.Gl).T.copy()
+
+    def cell_emission(self) -> np.ndarray:
+        """(G_local, N) the next step's emission B_g(T) + dB_g/dT(T_prev) dT_prev."""
+        out = np.empty(self.N * self.Gl)
+        lib().orc_get_cell_emission(self._h, _dp(out))
         return out.reshape(self.N, self.Gl).T.copy()
 
 
@@ -312,6 +332,12 @@ def planck_cell(T: float, e_edge, g: int) -> float:
     """kcon x B_g(T) per the material coupling's definition (rt_oracle.c orc_planck_cell)."""
     e = np.ascontiguousarray(e_edge, dtype=np.float64)
     return lib().orc_planck_cell(float(T), len(e) - 1, _dp(e), int(g))
+
+
+def planck_cell_dBdT(T: float, e_edge, g: int) -> float:
+    """kcon x dB_g/dT(T) (rt_oracle.c orc_planck_cell_dBdT)."""
+    e = np.ascontiguousarray(e_edge, dtype=np.float64)
+    return lib().orc_planck_cell_dBdT(float(T), len(e) - 1, _dp(e), int(g))
 
 
 def eigen_inverse2(m) -> np.ndarray:

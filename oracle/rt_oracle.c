@@ -537,7 +537,7 @@ struct orc_solver {
   int M, G, N, g_lo, Gl;
   double dx, dt;
   int literal_half;
-  int threads;        /* OpenMP threads over the lines of a direction (orc_set_threads); 1 = serial */
+  int threads;        /* OpenMP threads over the lines of a same-sign direction run (orc_set_threads); 1 = serial */
   int par_copies;     /* CPU baseline: the whole-array snapshot copies split over the threads */
   double ac;          /* RADIATION_CONSTANT_A * c (solver.h:29, correction.h:25) */
   double *mu, *wt;
@@ -554,14 +554,19 @@ struct orc_solver {
   double *psi, *ends, *prev_ends, *half_ends;
   /* material-temperature coupling (not in the reference; orc_material_*) */
   double *Tcell;      /* N */
-  double *Bcell;      /* N x Gl, c*Gl + gl; NULL = the reference's constant-T B_g */
+  double *Bcell;      /* N x Gl, c*Gl + gl: B_g(T(c)); NULL = the reference's constant-T B_g */
+  double *dBcell;     /* N x Gl: dB_g/dT(T(c)) */
+  double *Beff;       /* N x Gl: the step's emission B_g(T^n) + the owed emission paid in it */
+  double *owed;       /* N x Gl: emission the material owes the radiation, not yet paid (B units) */
+  double *dTlast;     /* N: the last update's temperature change (0 before the first) */
+  double *bpart;      /* N: sum over the local groups of sigma_g dB_g/dT(T(c)) */
   double rho_cv, wsum;
   int mat_it;         /* substep counter of the coupled steps (_it of solve()) */
   int equil_done;
 };
 
 /* emission of cell c, local group gl: per cell when coupled, else B_g (solver.cpp:338,...) */
-#define SRC_B(s, gl, c) ((s)->Bcell ? (s)->Bcell[(size_t)(c) * (s)->Gl + (size_t)(gl)] : (s)->B[(s)->g_lo + (gl)])
+#define SRC_B(s, gl, c) ((s)->Beff ? (s)->Beff[(size_t)(c) * (s)->Gl + (size_t)(gl)] : (s)->B[(s)->g_lo + (gl)])
 #define PSI(s, i, g, c) ((s)->psi[(size_t)(i) + (size_t)(s)->M * ((size_t)(g) + (size_t)(s)->Gl * (size_t)(c))])
 #define TC(s, i, g, c) ((s)->total_correction[(size_t)(i) + (size_t)(s)->M * ((size_t)(g) + (size_t)(s)->Gl * (size_t)(c))])
 #define E4(arr, s, i, g, c, k) \
@@ -806,7 +811,7 @@ void orc_destroy(orc_solver *s) {
   free(s->cB); free(s->cdBdT); free(s->kappa_edge); free(s->dEB); free(s->dsigEdE); free(s->dkapEB);
   free(s->cor1); free(s->cor2); free(s->cor3); free(s->total_correction);
   free(s->psi); free(s->ends); free(s->prev_ends); free(s->half_ends);
-  free(s->Tcell); free(s->Bcell);
+  free(s->Tcell); free(s->Bcell); free(s->dBcell); free(s->Beff); free(s->owed); free(s->dTlast); free(s->bpart);
   free(s);
 }
 
@@ -1032,23 +1037,30 @@ static int solve_iteration(orc_solver *s, int it) {
   if (ts != 3 || it % 4 == 0) par_copy(s->prev_ends, s->ends, ends_bytes(s), s->par_copies ? s->threads : 1); /* :620-625 */
 
   int half_copy_pending = 0;
-  for (int i = 0; i < M; ++i) {
-    double mu = s->mu[i];
+  for (int i = 0; i < M;) {
+    const int neg = s->mu[i] < 0.;
     /* Lazy form of :733: the surviving copy is the one after the last mu<0 CN cell. */
-    if (half_copy_pending && mu >= 0.) {
+    if (half_copy_pending && !neg) {
       par_copy(s->half_ends, s->ends, ends_bytes(s), s->par_copies ? s->threads : 1);
       half_copy_pending = 0;
     }
+    /* A run [i, i1) of directions of one sign: its lines (i, g) are independent --
+     * groups never couple (T constant), a mu<0 line reads only the right BC, a mu>0
+     * line at most the mu<0 outflow of this substep (reflective left BC, :677-684),
+     * final before the run starts, and the lazy :733 copy falls between runs. */
+    int i1 = i + 1;
+    while (i1 < M && (s->mu[i1] < 0.) == neg) ++i1;
     int err = 0, pend = 0;
-    /* lines (i, g) of one direction are independent (groups never couple, T constant) */
+    const int nl = (i1 - i) * s->Gl;
 #pragma omp parallel for schedule(static) num_threads(s->threads) reduction(| : err, pend) if (s->threads > 1 && !s->literal_half)
-    for (int gl = 0; gl < s->Gl; ++gl) {
+    for (int l = 0; l < nl; ++l) {
       int hp = 0;
-      err |= sweep_line(s, it, i, gl, &hp);
+      err |= sweep_line(s, it, i + l / s->Gl, l % s->Gl, &hp);
       pend |= hp;
     }
     if (err) return ORC_ERR_PARAM;
     if (pend) half_copy_pending = 1;
+    i = i1;
   }
   if (half_copy_pending) par_copy(s->half_ends, s->ends, ends_bytes(s), s->par_copies ? s->threads : 1);
   return ORC_OK;
@@ -1093,21 +1105,79 @@ double orc_planck_cell(double T, int G, const double *e_edge, int g) {
   return planck_cell(&P, T, G, e_edge, g);
 }
 
-static void material_planck(orc_solver *s) {
-#pragma omp parallel for schedule(static) num_threads(s->threads) if (s->threads > 1)
-  for (int c = 0; c < s->N; ++c)
-    for (int gl = 0; gl < s->Gl; ++gl)
-      s->Bcell[(size_t)c * s->Gl + gl] = planck_cell(&s->planck, s->Tcell[c], s->G, s->e_edge, s->g_lo + gl);
+/* kcon dB_g/dT(T) for one group g: Planck::integrate_dBdT (Planck.cpp:161-229) for g < G-1;
+ * the last group the remainder 4 a c T^3 minus the integral over [e_0, e_{G-1}] (the
+ * derivative of planck_cell's remainder, Planck.cpp:156-159), when positive, else 0. */
+static double planck_cell_dBdT(const planck_t *P, double T, int G, const double *e_edge, int g) {
+  if (!(T > 0.0) || !isfinite(T)) return 0.0;
+  if (g < G - 1) return C_BOLTZ_JPK * planck_integrate_dBdT(P, T, e_edge[g], e_edge[g + 1]);
+  double rest = 4.0 * rad_a_long() * C_LIGHT * pow(T, 3.0) - planck_integrate_dBdT(P, T, e_edge[0], e_edge[G - 1]);
+  return rest > 0.0 ? C_BOLTZ_JPK * rest : 0.0;
 }
 
+double orc_planck_cell_dBdT(double T, int G, const double *e_edge, int g) {
+  planck_t P;
+  planck_setup(&P);
+  return planck_cell_dBdT(&P, T, G, e_edge, g);
+}
+
+/* Per cell at the new T(c), per local group: the owed emission grows by dB_g/dT(T_old) dT
+ * (what the last implicit update let the material emit beyond the sweep's B); B_g(T); the
+ * next sweep pays p_g = max(owed_g, -B_g) of it -- Beff_g = B_g + p_g >= 0 -- and owed_g
+ * keeps the rest; then dB_g/dT(T) and bpart(c) = sum over the local groups (ascending) of
+ * sigma_g dB_g/dT. */
+static void material_planck(orc_solver *s) {
+#pragma omp parallel for schedule(static) num_threads(s->threads) if (s->threads > 1)
+  for (int c = 0; c < s->N; ++c) {
+    double b = 0.0;
+    for (int gl = 0; gl < s->Gl; ++gl) {
+      const int g = s->g_lo + gl;
+      const size_t o = (size_t)c * s->Gl + gl;
+      const double owed = s->owed[o] + s->dBcell[o] * s->dTlast[c];
+      const double B = planck_cell(&s->planck, s->Tcell[c], s->G, s->e_edge, g);
+      const double dB = planck_cell_dBdT(&s->planck, s->Tcell[c], s->G, s->e_edge, g);
+      const double pay = owed > -B ? owed : -B;
+      s->Bcell[o] = B;
+      s->Beff[o] = B + pay;
+      s->owed[o] = owed - pay;
+      s->dBcell[o] = dB;
+      b = b + s->rho[g] * s->kappa[g] * dB;
+    }
+    s->bpart[c] = b;
+  }
+}
+
+/* The coupling (include/rtsn.h "material"): the temperature update implicit in the
+ * material's own emission, the emission change it implies paid to the radiation in the
+ * following sweeps.  Per full step, with W = sum_i w_i and sigma_g = rho kappa_g:
+ *   sweep with the emission Beff_g = B_g(T^n) + p_g (p_g: the owed emission paid now);
+ *   q = sum_g sigma_g (phi_g^{n+1} - W B_g(T^n)) and b = sum_g sigma_g dB_g/dT(T^n) over ALL
+ *     groups (the callers sum both over the shards: one all-reduce of 2N doubles);
+ *   dT = dt q / (rho_cv + dt W b) -- rho_cv dT = dt sum_g sigma_g (phi_g - W B_g(T^{n+1})) with
+ *     B(T^{n+1}) linearised about T^n -- and T^{n+1} = T^n + dT;
+ *   the material thereby emitted dt W sum_g sigma_g dB_g/dT dT beyond the sweep's B: each
+ *     group's share joins its owed emission, paid in the next sweeps as far as the emission
+ *     stays >= 0 (all of it unless the material cooled by a large fraction of T).
+ * Radiation + material + owed energy changes only by the boundary flows (BE: to rounding;
+ * orc_get_material_transit).  Linear grey analysis: stable at any dt / rho_cv;
+ * BE keeps T > 0 (dT > -T when phi >= 0, since B_g / dB_g/dT <= T). */
 int orc_material_enable(orc_solver *s, double rho_cv, const double *T_cells) {
   if (!(rho_cv > 0.0)) return ORC_ERR_PARAM;
   if (s->p.use_correction && s->p.V != 0.0) return ORC_ERR_PARAM;
   int ok = 1;
   if (!s->Tcell) s->Tcell = (double *)xcalloc(s->N, sizeof(double), &ok);
+  if (!s->dTlast) s->dTlast = (double *)xcalloc(s->N, sizeof(double), &ok);
+  if (!s->bpart) s->bpart = (double *)xcalloc(s->N, sizeof(double), &ok);
   if (!s->Bcell) s->Bcell = (double *)xcalloc((size_t)s->N * s->Gl, sizeof(double), &ok);
+  if (!s->dBcell) s->dBcell = (double *)xcalloc((size_t)s->N * s->Gl, sizeof(double), &ok);
+  if (!s->Beff) s->Beff = (double *)xcalloc((size_t)s->N * s->Gl, sizeof(double), &ok);
+  if (!s->owed) s->owed = (double *)xcalloc((size_t)s->N * s->Gl, sizeof(double), &ok);
   if (!ok) return ORC_ERR_NOMEM;
-  for (int c = 0; c < s->N; ++c) s->Tcell[c] = T_cells ? T_cells[c] : s->p.T;
+  for (int c = 0; c < s->N; ++c) {
+    s->Tcell[c] = T_cells ? T_cells[c] : s->p.T;
+    s->dTlast[c] = 0.0;
+    for (int gl = 0; gl < s->Gl; ++gl) s->owed[(size_t)c * s->Gl + gl] = 0.0;
+  }
   s->rho_cv = rho_cv;
   s->wsum = 0.0;
   for (int i = 0; i < s->M; ++i) s->wsum += s->wt[i];
@@ -1115,10 +1185,10 @@ int orc_material_enable(orc_solver *s, double rho_cv, const double *T_cells) {
   return ORC_OK;
 }
 
-/* One full step with the per-cell emission (ts 3: four substeps), then
- * q(c) = sum_gl sigma_g (phi_g(c) - W B_g(c)) over the local groups. */
-int orc_material_sweep(orc_solver *s, double *q) {
-  if (!s->Bcell) return ORC_ERR_PARAM;
+/* One full step with the per-cell emission Beff (ts 3: four substeps), then into qb (2N):
+ * q(c) = sum_gl sigma_g (phi_g(c) - W B_g(c)) and b(c) = bpart(c), local groups. */
+int orc_material_sweep(orc_solver *s, double *qb) {
+  if (!s->Beff) return ORC_ERR_PARAM;
   if (s->p.use_mg_equilib && !s->equil_done) {
     int st = equilibrium_sources(s);
     if (st) return st;
@@ -1139,16 +1209,39 @@ int orc_material_sweep(orc_solver *s, double *q) {
       double sigma = s->rho[g] * s->kappa[g];
       acc += sigma * (phi[(size_t)c * s->Gl + gl] - s->wsum * s->Bcell[(size_t)c * s->Gl + gl]);
     }
-    q[c] = acc;
+    qb[c] = acc;
+    qb[(size_t)s->N + c] = s->bpart[c];
   }
   free(phi);
   return ORC_OK;
 }
 
-/* T(c) += dt q(c) / rho_cv (q summed over all groups), then B_g(T(c)). */
-void orc_material_update(orc_solver *s, const double *q) {
-  for (int c = 0; c < s->N; ++c) s->Tcell[c] = s->Tcell[c] + s->dt * q[c] / s->rho_cv;
+/* From qb (2N: q and b summed over all groups): dT = dt q / (rho_cv + dt W b), T += dT,
+ * then the Planck terms at the new T and the next emission (see orc_material_enable). */
+void orc_material_update(orc_solver *s, const double *qb) {
+  const double W = s->wsum, dt = s->dt, rc = s->rho_cv;
+  for (int c = 0; c < s->N; ++c) {
+    const double q = qb[c], b = qb[(size_t)s->N + c];
+    const double dT = dt * q / (rc + dt * W * b);
+    s->Tcell[c] = s->Tcell[c] + dT;
+    s->dTlast[c] = dT;
+  }
   material_planck(s);
+}
+
+/* Energy per volume the material owes the radiation, per cell: dt W sum_gl sigma_g (p_g +
+ * owed_g) -- the next sweep's payment and the rest (this solver's groups). */
+void orc_get_material_transit(const orc_solver *s, double *E) {
+  for (int c = 0; c < s->N; ++c) {
+    double e = 0.0;
+    if (s->owed)
+      for (int gl = 0; gl < s->Gl; ++gl) {
+        const int g = s->g_lo + gl;
+        const size_t o = (size_t)c * s->Gl + gl;
+        e += s->rho[g] * s->kappa[g] * ((s->Beff[o] - s->Bcell[o]) + s->owed[o]);
+      }
+    E[c] = s->dt * s->wsum * e;
+  }
 }
 
 void orc_get_temperature(const orc_solver *s, double *T) {
@@ -1157,6 +1250,10 @@ void orc_get_temperature(const orc_solver *s, double *T) {
 
 void orc_get_cell_planck(const orc_solver *s, double *B) {
   if (s->Bcell) memcpy(B, s->Bcell, sizeof(double) * (size_t)s->N * s->Gl);
+}
+
+void orc_get_cell_emission(const orc_solver *s, double *Beff) {
+  if (s->Beff) memcpy(Beff, s->Beff, sizeof(double) * (size_t)s->N * s->Gl);
 }
 
 int orc_num_groups_local(const orc_solver *s) { return s->Gl; }

@@ -104,18 +104,25 @@ void orc_get_psi_source(const orc_solver *s, double *out);
 int orc_validate(orc_solver *s);
 
 /* Material-temperature coupling (NOT in the reference: the product's
- * rt_material_* of include/rtsn.h restated on the CPU).  Per full step:
- * orc_material_sweep runs the step with the per-cell emission B_g(T(c)) and
- * writes this solver's q(c) = sum_g sigma_g (phi_g - W B_g) (N); the caller
- * sums q over group shards and calls orc_material_update (T += dt q / rho_cv,
- * then B_g(T)).  Requires the v/c correction off. */
+ * rt_material_* of include/rtsn.h restated on the CPU): T updated implicitly in
+ * the material's own emission, the emission change carried into the next sweep.
+ * Per full step: orc_material_sweep runs the step with the per-cell emission
+ * Beff_g = B_g(T^n) + dB_g/dT(T^{n-1}) dT^{n-1} and writes this solver's
+ * q(c) = sum_g sigma_g (phi_g - W B_g(T^n)) and b(c) = sum_g sigma_g dB_g/dT(T^n)
+ * (2N: q then b); the caller sums both over group shards and calls
+ * orc_material_update (dT = dt q / (rho_cv + dt W b), T += dT, the Planck terms
+ * at the new T).  Requires the v/c correction off. */
 int orc_material_enable(orc_solver *s, double rho_cv, const double *T_cells /* N or NULL */);
-int orc_material_sweep(orc_solver *s, double *q);
-void orc_material_update(orc_solver *s, const double *q);
+int orc_material_sweep(orc_solver *s, double *qb /* 2N */);
+void orc_material_update(orc_solver *s, const double *qb /* 2N */);
+/* energy per volume the material owes the radiation (dt W sum_g sigma_g owed_g, this solver's groups) */
+void orc_get_material_transit(const orc_solver *s, double *E);
 void orc_get_temperature(const orc_solver *s, double *T);
-void orc_get_cell_planck(const orc_solver *s, double *B); /* N x Gl, c*Gl + gl */
-/* kcon x B_g(T) of one group, the last one the grey remainder (see .c) */
+void orc_get_cell_planck(const orc_solver *s, double *B);     /* N x Gl, c*Gl + gl: B_g(T(c)) */
+void orc_get_cell_emission(const orc_solver *s, double *Beff); /* N x Gl: the next step's emission */
+/* kcon x B_g(T) / kcon x dB_g/dT(T) of one group, the last one the grey remainder (see .c) */
 double orc_planck_cell(double T, int G, const double *e_edge, int g);
+double orc_planck_cell_dBdT(double T, int G, const double *e_edge, int g);
 
 /* Stand-alone building blocks exposed for unit tests. */
 void orc_glquad(int M, double norm, double *mu, double *wt);

@@ -678,10 +678,7 @@ __global__ void __launch_bounds__(64) moments_kernel(const double2 *__restrict__
 // Bytes in flight per CU (two workgroups: 68.6 KB of LDS each, <= 168 VGPRs for three waves
 // per SIMD): 4 x 2 x 32 KB = 256 KB -- the first form (one loader per half, one item deep,
 // 128 KB) read at 5.94 TB/s (22.1 ms on SL, profiles/r05b_*), the state scan at 6.86.
-#ifndef RT_MOM_LOADERS
-#define RT_MOM_LOADERS 2  // loader waves per half (timing experiments)
-#endif
-constexpr int kMomLoadersPerHalf = RT_MOM_LOADERS;
+constexpr int kMomLoadersPerHalf = 2;  // loader waves per half
 template <int H>
 __global__ void __launch_bounds__(64 * (2 * kMomLoadersPerHalf + 1)) moments_pc_kernel(const double2 *__restrict__ E, const double *__restrict__ mu,
                                                          const double *__restrict__ wt, double *phi, double *F,
@@ -919,6 +916,31 @@ __device__ double planck_series(double z1, double z2, double accuracy, const dou
   return s1 - s2;
 }
 
+// The dB/dT series (Planck.cpp:170-193): the same walk with the quartic
+// P4(k z) / k^4 = z^4 + r (4 z^3 + r (12 z^2 + r (24 z + 24 r))), r = 1/k.
+__device__ double planck_series_dBdT(double z1, double z2, double accuracy, const double *rk) {
+  const double e1 = exp(-z1), f1 = exp(-z2);
+  const double a1 = (z1 * z1) * (z1 * z1), b1 = 4.0 * (z1 * z1 * z1), c1 = 12.0 * (z1 * z1), d1 = 24.0 * z1;
+  const double a2 = (z2 * z2) * (z2 * z2), b2 = 4.0 * (z2 * z2 * z2), c2 = 12.0 * (z2 * z2), d2 = 24.0 * z2;
+  auto pr = [](double r, double a, double b, double c, double d) { return a + r * (b + r * (c + r * (d + 24.0 * r))); };
+  auto recip = [rk](int k) { return k <= 64 ? rk[k] : 1.0 / k; };
+  const double lead = fmax(e1 * (a1 + b1 + c1 + d1 + 24.0), 2.220446049250313e-16);
+  const double stop = accuracy * (1.0 - e1) * lead;
+  int n = 32;
+  for (double em = exp(-33.0 * z1); n < 4096; ++n, em *= e1)
+    if (!(em * pr(recip(n + 1), a1, b1, c1, d1) > stop)) break;
+  double s1 = 0.0, s2 = 0.0, p1 = 1.0, p2 = 1.0;
+  for (int k = 1; k <= n; ++k) {
+    p1 *= e1;
+    p2 *= f1;
+    if (p1 == 0.0) break;
+    const double r = recip(k);
+    s1 += p1 * pr(r, a1, b1, c1, d1);
+    s2 += p2 * pr(r, a2, b2, c2, d2);
+  }
+  return s1 - s2;
+}
+
 // 12-point Gauss-Legendre of the Planck density over [mid - hw, mid + hw]
 // (Planck.cpp:129-140; k_B = 1 keV/keV)
 __device__ double planck_gauss(const PlanckCells &pc, double inv_T, double mid, double hw, double pre) {
@@ -929,6 +951,38 @@ __device__ double planck_gauss(const PlanckCells &pc, double inv_T, double mid, 
     acc += hw * pc.weight[r] * (pre * (E * E * E) / (exp(E * inv_T) - 1.0));
   }
   return acc;
+}
+
+// ... of its temperature derivative (Planck.h:113-125)
+__device__ double planck_gauss_dBdT(const PlanckCells &pc, double inv_T, double mid, double hw, double pre) {
+  double acc = 0.0;
+#pragma unroll
+  for (int r = 0; r < 12; ++r) {
+    const double E = mid + hw * pc.node[r];
+    const double ex = exp(E * inv_T), em1 = ex - 1.0;
+    acc += hw * pc.weight[r] * (pre * ((E * E) * (E * E)) * (inv_T * inv_T) * ex / (em1 * em1));
+  }
+  return acc;
+}
+
+// Planck::integrate_dBdT (Planck.cpp:161-229) for T > 0, the branches of planck_integral
+__device__ double planck_integral_dBdT(const PlanckCells &pc, double T, double e_min, double e_max, double pre,
+                                       const double *rk) {
+  if (nearly_equal(e_min, e_max)) return 0.0;
+  const double inv_T = 1.0 / T;
+  const double z1 = e_min * inv_T, z2 = e_max * inv_T;
+  const double t3 = (T * T) * T;
+  double v;
+  if (z2 <= 0.7) {
+    v = planck_gauss_dBdT(pc, inv_T, 0.5 * (e_max + e_min), 0.5 * (e_max - e_min), pre);
+  } else if (z1 >= 0.5) {
+    v = pre * t3 * planck_series_dBdT(z1, z2, pc.accuracy, rk);
+  } else {
+    const double e6 = 0.6 * T;
+    v = planck_gauss_dBdT(pc, inv_T, 0.5 * (e6 + e_min), 0.5 * (e6 - e_min), pre) +
+        pre * t3 * planck_series_dBdT(0.6, z2, pc.accuracy, rk);
+  }
+  return v * 4.0 * 3.1415926546;
 }
 
 // Planck::integrate_B (Planck.cpp:85-154) for T > 0: Gauss below z = 0.7,
@@ -956,15 +1010,21 @@ __device__ double planck_integral(const PlanckCells &pc, double T, double e_min,
 // the grey remainder a c T^4 - (integral over groups 0..G-2) when positive
 // (Planck.cpp:73-76; the sum of the other groups as one integral over their
 // joint range, so no shard needs another shard's groups).  T <= 0 (or
-// nearly 0, Planck.h:84-90) or not finite: 0.
+// nearly 0, Planck.h:84-90) or not finite: 0.  With the same branches dB/dT
+// (the last group 4 a c T^3 - the joint integral).  The coupling's owed emission
+// (include/rtsn.h "material", rt_oracle.c material_planck): owed grows by the old
+// dB/dT times the last update's dT[x], the next sweep pays pay = max(owed, -B) of it,
+// Beff[x][gl] = B + pay, and bpart[x] = b_scale sum_gl sigma_gl dB/dT.  owed and dB/dT
+// are the kernel's own, group-major [gl][x] (a wave's 64 cells contiguous).
 //
 // A block owns 64 cells (one per lane) and walks the groups wave by wave, so
 // a wave evaluates ONE group at 64 temperatures -- the branch (Gauss / series
 // / split) and the series length are then nearly uniform across the wave --
-// and stages the tile in LDS to write it back as contiguous [x][g] rows.
-constexpr int kPlanckCells = 64, kPlanckGroups = 64;
-__global__ __launch_bounds__(256) void planck_cells_kernel(PlanckCells pc, const double *Tc, double *B) {
-  __shared__ double tile[kPlanckCells * (kPlanckGroups + 1)];
+// and stages the tiles in LDS to write them back as contiguous [x][g] rows.
+constexpr int kPlanckCells = 64, kPlanckGroups = 64, kPlanckThreads = 256;
+__global__ __launch_bounds__(kPlanckThreads) void planck_cells_kernel(PlanckCells pc, const double *Tc, double *B) {
+  __shared__ double tile[2][kPlanckCells * (kPlanckGroups + 1)];
+  __shared__ double bsum[kPlanckThreads / 64][kPlanckCells];
   __shared__ double rk[65];
   const double hc = 4.141895e-10, c = 299.792458;
   const double pre = 2.0 / ((hc * hc * hc) * (c * c));
@@ -974,29 +1034,55 @@ __global__ __launch_bounds__(256) void planck_cells_kernel(PlanckCells pc, const
   for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
     const int x0 = t * kPlanckCells, nx = min(kPlanckCells, pc.N - x0);
     const double T = lane < nx ? Tc[x0 + lane] : 0.0;
+    const double dT = lane < nx ? pc.dTlast[x0 + lane] : 0.0;
     const bool hot = T > 0.0 && isfinite(T) && !nearly_equal(T, 0.0);
+    double bacc = 0.0;  // this wave's groups of sigma_g dB_g/dT at cell lane
     for (int g0 = 0; g0 < pc.Gl; g0 += kPlanckGroups) {
       const int ng = min(kPlanckGroups, pc.Gl - g0);
-      __syncthreads();  // rk ready; the previous chunk's tile written out
+      __syncthreads();  // rk ready; the previous chunk's tiles written out
       for (int j = wave; j < ng; j += nwave) {
         const int g = pc.g_lo + g0 + j;
-        double b = 0.0;
+        double b = 0.0, db = 0.0;
         if (hot) {
           if (g < pc.G - 1) {
             b = pc.kcon * planck_integral(pc, T, pc.e_edge[g], pc.e_edge[g + 1], pre, rk);
+            db = pc.kcon * planck_integral_dBdT(pc, T, pc.e_edge[g], pc.e_edge[g + 1], pre, rk);
           } else {
             const double rest =
                 pc.a_c * ((T * T) * (T * T)) - planck_integral(pc, T, pc.e_edge[0], pc.e_edge[pc.G - 1], pre, rk);
             b = rest > 0.0 ? pc.kcon * rest : 0.0;
+            const double drest = 4.0 * pc.a_c * ((T * T) * T) -
+                                 planck_integral_dBdT(pc, T, pc.e_edge[0], pc.e_edge[pc.G - 1], pre, rk);
+            db = drest > 0.0 ? pc.kcon * drest : 0.0;
           }
         }
-        tile[lane * (kPlanckGroups + 1) + j] = b;
+        double pay = 0.0;
+        if (lane < nx) {
+#pragma clang fp contract(off)
+          const size_t o = static_cast<size_t>(g0 + j) * pc.N + x0 + lane;
+          const double owed = pc.owed[o] + pc.dB[o] * dT;
+          pay = owed > -b ? owed : -b;
+          pc.owed[o] = owed - pay;
+          pc.dB[o] = db;
+        }
+        tile[0][lane * (kPlanckGroups + 1) + j] = b;
+        tile[1][lane * (kPlanckGroups + 1) + j] = b + pay;
+        bacc += pc.sigma[g0 + j] * db;
       }
       __syncthreads();
       for (int i = threadIdx.x; i < nx * ng; i += blockDim.x) {
         const int xl = i / ng, j = i - xl * ng;
-        B[static_cast<size_t>(x0 + xl) * pc.Gl + g0 + j] = tile[xl * (kPlanckGroups + 1) + j];
+        const size_t o = static_cast<size_t>(x0 + xl) * pc.Gl + g0 + j;
+        B[o] = tile[0][xl * (kPlanckGroups + 1) + j];
+        pc.Beff[o] = tile[1][xl * (kPlanckGroups + 1) + j];
       }
+    }
+    bsum[wave][lane] = bacc;
+    __syncthreads();
+    if (wave == 0 && lane < nx) {
+      double b = 0.0;
+      for (int w = 0; w < nwave; ++w) b += bsum[w][lane];
+      pc.bpart[x0 + lane] = pc.b_scale * b;
     }
   }
 }
@@ -1060,10 +1146,7 @@ __global__ void correction_power_kernel(const double *map, double *pow, int L, i
 }
 
 // cells per LDS tile of the correction's sums (the tile bounds the waves a CU holds)
-#ifndef RT_PHI_CHUNK
-#define RT_PHI_CHUNK 16
-#endif
-constexpr int kPhiChunk = RT_PHI_CHUNK;
+constexpr int kPhiChunk = 16;
 
 template <int S>
 __global__ __launch_bounds__(64) void phi_correction_kernel(SegArgs a, int nsub, int Lsub, const double *pow) {
@@ -1505,7 +1588,7 @@ __global__ __launch_bounds__(64 * kRowsWaves) void phi_correction_rows_kernel(Se
 // [part][x][g] (the fused halves and their corrections, or one full phi):
 // one wave per cell, lanes over groups, then a butterfly over the wave
 __global__ void material_q_kernel(const double *phi, int nparts, const double *B, const double *sigma, double W,
-                                  double *q, int Gl, int N) {
+                                  const double *bpart, double *q, int Gl, int N) {
   const int lane = threadIdx.x & 63;
   const int nw = (gridDim.x * blockDim.x) >> 6;
   const size_t NG = static_cast<size_t>(N) * Gl;
@@ -1518,14 +1601,40 @@ __global__ void material_q_kernel(const double *phi, int nparts, const double *B
       acc += sigma[g] * (ph - W * B[o + g]);
     }
     for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off);
-    if (lane == 0) q[x] = acc;
+    if (lane == 0) {
+      q[x] = acc;
+      q[N + x] = bpart[x];  // the exchange buffer's second half: this handle's sum sigma dB/dT
+    }
   }
 }
 
-__global__ void material_update_kernel(double *T, const double *q, double dt, double rho_cv, int N) {
+// dT = dt q / (rho_cv + dt W b), T += dT (rt_oracle.c orc_material_update, the same
+// expressions unfused); dT kept for the next Planck pass's owed emission
+__global__ void material_update_kernel(double *T, const double *qb, double *dTlast, double dt, double rho_cv, double W,
+                                       int N) {
 #pragma clang fp contract(off)
-  for (int x = blockIdx.x * blockDim.x + threadIdx.x; x < N; x += gridDim.x * blockDim.x)
-    T[x] = T[x] + dt * q[x] / rho_cv;
+  for (int x = blockIdx.x * blockDim.x + threadIdx.x; x < N; x += gridDim.x * blockDim.x) {
+    const double q = qb[x], b = qb[N + x];
+    const double dT = dt * q / (rho_cv + dt * W * b);
+    T[x] = T[x] + dT;
+    dTlast[x] = dT;
+  }
+}
+
+// E[x] = dt W sum_gl sigma_gl ((Beff - B) + owed): the energy per volume the material owes
+// the radiation (rt_get_material_transit); one wave per cell, lanes over groups
+__global__ void material_transit_kernel(const double *B, const double *Beff, const double *owed, const double *sigma,
+                                        double scale, double *E, int Gl, int N) {
+  const int lane = threadIdx.x & 63;
+  const int nw = (gridDim.x * blockDim.x) >> 6;
+  for (int x = (blockIdx.x * blockDim.x + threadIdx.x) >> 6; x < N; x += nw) {
+    const size_t o = static_cast<size_t>(x) * Gl;
+    double acc = 0.0;
+    for (int g = lane; g < Gl; g += 64)
+      acc += sigma[g] * ((Beff[o + g] - B[o + g]) + owed[static_cast<size_t>(g) * N + x]);
+    for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off);
+    if (lane == 0) E[x] = scale * acc;
+  }
 }
 
 // ------------------------------------------------------------------------
@@ -1699,29 +1808,21 @@ hipError_t launch_import_ends(double2 *E, const double *ends, const Geometry &g,
   return hipGetLastError();
 }
 
-#ifndef RT_MOM_W
-#define RT_MOM_W 16
-#endif
-// The moments form where M/2 is 8, 16 or 32 (RTSN_MOMENTS_FORM, for A/B timing and the bitwise
+// The moments form where M/2 is 8, 16 or 32 (rt_set_moments_form, for A/B timing and the bitwise
 // test of the forms): 0 the one-wave moments_kernel, 1 (the default) moments_pc_kernel.  A
 // two-pass form (each half's rows in one ascending stream, the partial sums through the
 // outputs) was measured slower and removed: 11.4 + 12.3 ms against 22.4 on one box
 // (profiles/r05g_*), refuting the two-address-stream explanation of the gap to the scan.
-static int moments_form() {
-  const char *e = std::getenv("RTSN_MOMENTS_FORM");
-  return e && e[0] == '0' ? 0 : 1;
-}
 hipError_t launch_moments(const double2 *E, const double *mu, const double *wt, double *phi, double *F,
-                          double *phi_plus, const Geometry &g, hipStream_t st) {
+                          double *phi_plus, const Geometry &g, int form, hipStream_t st) {
   const LineMap m = make_map(g);
   const size_t tasks = static_cast<size_t>(g.N) * ((g.Gl + 63) / 64);
   // as many waves as the chip holds at once; each walks its tasks with a one-chunk prefetch:
   // 16-direction chunks where the half's directions come in whole ones, else 8
-  constexpr int W = RT_MOM_W;
+  constexpr int W = 16;
   static const size_t resident[3] = {resident_blocks(moments_kernel<false, 8>, 64),
                                      resident_blocks(moments_kernel<true, 8>, 64),
                                      resident_blocks(moments_kernel<true, W>, 64)};
-  const int form = moments_form();
   if (form >= 1 && (m.H == 8 || m.H == 16 || m.H == 32)) {  // producer/consumer form
     constexpr int TH = 64 * (2 * kMomLoadersPerHalf + 1);
     static const size_t pc[3] = {resident_blocks(moments_pc_kernel<8>, TH), resident_blocks(moments_pc_kernel<16>, TH),
@@ -1849,16 +1950,24 @@ hipError_t launch_phi_correction_rows(int scheme, const SegArgs &a, const double
   return hipGetLastError();
 }
 
-hipError_t launch_material_q(const double *phi, int nparts, const double *B, const double *sigma, double W, double *q,
-                             int Gl, int N, hipStream_t st) {
+hipError_t launch_material_q(const double *phi, int nparts, const double *B, const double *sigma, double W,
+                             const double *bpart, double *q, int Gl, int N, hipStream_t st) {
   hipLaunchKernelGGL(material_q_kernel, dim3(grid_for(static_cast<size_t>(N) * 64, 256)), dim3(256), 0, st, phi, nparts,
-                     B, sigma, W, q, Gl, N);
+                     B, sigma, W, bpart, q, Gl, N);
   return hipGetLastError();
 }
 
-hipError_t launch_material_update(double *T, const double *q, double dt, double rho_cv, int N, hipStream_t st) {
-  hipLaunchKernelGGL(material_update_kernel, dim3(grid_for(static_cast<size_t>(N), 256)), dim3(256), 0, st, T, q, dt,
-                     rho_cv, N);
+hipError_t launch_material_update(double *T, const double *qb, double *dTlast, double dt, double rho_cv, double W,
+                                  int N, hipStream_t st) {
+  hipLaunchKernelGGL(material_update_kernel, dim3(grid_for(static_cast<size_t>(N), 256)), dim3(256), 0, st, T, qb,
+                     dTlast, dt, rho_cv, W, N);
+  return hipGetLastError();
+}
+
+hipError_t launch_material_transit(const double *B, const double *Beff, const double *owed, const double *sigma,
+                                   double scale, double *E, int Gl, int N, hipStream_t st) {
+  hipLaunchKernelGGL(material_transit_kernel, dim3(grid_for(static_cast<size_t>(N) * 64, 256)), dim3(256), 0, st, B,
+                     Beff, owed, sigma, scale, E, Gl, N);
   return hipGetLastError();
 }
 

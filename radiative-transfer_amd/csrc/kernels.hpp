@@ -5,28 +5,13 @@
 
 namespace rtamd {
 
-// Build-time tunables (defaults are the measured best).
-#ifndef RT_SWEEP_CELLS
-#define RT_SWEEP_CELLS 16     // cells per wave held in registers
-#endif
-
-constexpr int kSweepCells = RT_SWEEP_CELLS;             // segment lengths are multiples of this
+// Register-tiling constants (the measured best).
+constexpr int kSweepCells = 16;  // cells per wave held in registers; segment lengths are multiples of this
 // rows per chunk held in registers (prefetch depth) for scheme S fusing T steps:
-// measured on SL, BDF2 T = 16: 4 rows 8.67, 8 rows 8.33, 16 rows 8.15 ms/step
-#ifndef RT_CHUNK_BDF2_T2
-#define RT_CHUNK_BDF2_T2 8
-#endif
-#ifndef RT_CHUNK_BDF2_T12
-#define RT_CHUNK_BDF2_T12 16
-#endif
-// T = 20: 16 rows spill to scratch; 8 rows fit 256 VGPRs + 126 AGPRs
-#ifndef RT_CHUNK_BDF2_T20
-#define RT_CHUNK_BDF2_T20 8
-#endif
+// measured on SL, BDF2 T = 16: 4 rows 8.67, 8 rows 8.33, 16 rows 8.15 ms/step;
+// T = 20: 16 rows spill to scratch, 8 rows fit 256 VGPRs + 126 AGPRs
 constexpr int chunk_cells(int S, int T) {
-  return S == 3 && T >= 20   ? RT_CHUNK_BDF2_T20
-         : S == 3 && T >= 12 ? RT_CHUNK_BDF2_T12
-                             : (S == 3 && T >= 2 ? RT_CHUNK_BDF2_T2 : RT_SWEEP_CELLS);
+  return S == 3 && T >= 20 ? 8 : S == 3 && T >= 12 ? 16 : (S == 3 && T >= 2 ? 8 : kSweepCells);
 }
 // pipelined passes whose T levels two waves can share (sweep_split_kernel):
 // BDF2, where the carried states (5 per level) are what overflows 256 registers
@@ -37,10 +22,7 @@ constexpr bool level_split_supported(int S, int T) {
 // states would spill; those run split over four waves)
 constexpr bool one_wave_block(int S, int T) { return S != 3 || T <= 20; }
 // rows per chunk of the level-split pass (16 rows with T/2 = 8 levels spill past 256 registers)
-#ifndef RT_CHUNK_SPLIT
-#define RT_CHUNK_SPLIT 8
-#endif
-constexpr int split_chunk_cells() { return RT_CHUNK_SPLIT; }
+constexpr int split_chunk_cells() { return 8; }
 constexpr int kXcds = 8;                                // gfx950: workgroups are dealt to 8 XCDs round-robin
 constexpr int kSweepTile = 64;                          // cells are padded to whole tiles of 64 rows
 
@@ -115,10 +97,7 @@ hipError_t launch_fold(int KC, const FoldArgs &f, hipStream_t st);
 // long for kWaveMaxWaves waves); waves > 1 hand the chain over through LDS once per tick
 // and meet at a barrier every kWaveBlockTicks ticks
 constexpr int kWaveMaxWaves = 8;
-#ifndef RT_WAVE_BLOCK
-#define RT_WAVE_BLOCK 8
-#endif
-constexpr int kWaveBlockTicks = RT_WAVE_BLOCK;
+constexpr int kWaveBlockTicks = 8;
 struct WavePlan {
   int C, waves, lanes;
 };
@@ -129,8 +108,10 @@ hipError_t launch_init_state(double2 *E, const double *lineB, const Geometry &g,
 hipError_t launch_export_psi(const double2 *E, double *psi, const Geometry &g, int c0, int nc, hipStream_t st);
 hipError_t launch_export_ends(const double2 *E, double *ends, const Geometry &g, int c0, int nc, hipStream_t st);
 hipError_t launch_import_ends(double2 *E, const double *ends, const Geometry &g, int c0, int nc, hipStream_t st);
+// form (rt_set_moments_form): 1 the producer/consumer moments_pc_kernel where M/2 is 8, 16 or
+// 32, 0 the one-wave moments_kernel; bitwise-identical results
 hipError_t launch_moments(const double2 *E, const double *mu, const double *wt, double *phi, double *F,
-                          double *phi_plus, const Geometry &g, hipStream_t st);
+                          double *phi_plus, const Geometry &g, int form, hipStream_t st);
 hipError_t launch_boundary_rows(const double2 *E, double2 *rows, const Geometry &g, hipStream_t st);
 // *flag |= 1 if any node of the N real rows of either half is not finite (flag zeroed by the caller)
 hipError_t launch_finite_scan(const double2 *E, int *flag, const Geometry &g, hipStream_t st);
@@ -151,7 +132,17 @@ struct PlanckCells {
   double a_c;                   // rad_a_long() * c (Constants.h:22-23)
   double kcon;                  // jk per keV (correction.cpp:25-36)
   double accuracy;              // series tolerance (Planck.h:96, DBL_EPSILON)
+  // the coupling's owed emission (rtsn_material.hip): the last update's dT per cell in;
+  // owed and dB (group-major [Gl][N], the kernel's own) updated; Beff = B + the paid share
+  // and bpart = b_scale sum_gl sigma[gl] dB/dT out
+  const double *sigma;          // [Gl] rho kappa of the handle's groups
+  const double *dTlast;         // [N]
+  double *owed, *dB;            // [Gl][N]
+  double *Beff;                 // [N][Gl]
+  double *bpart;                // [N]
+  double b_scale;               // 1, or 0 on a direction shard without pair 0 (b counted once)
 };
+// B[N][Gl] = B_g(T(x)) and the fields above
 hipError_t launch_planck_cells(const PlanckCells &pc, const double *T, double *B, hipStream_t st);
 // the correction's share of the fused angular sums (SegArgs.phi) after a
 // coupled pass with segments started from X = 0 (T = 1; each segment walked as
@@ -170,11 +161,15 @@ size_t corr_rows_doubles(int scheme, int Lpad);
 hipError_t launch_corr_rows(int scheme, const double *map, double *rows, int Lpad, hipStream_t st);
 hipError_t launch_phi_correction_rows(int scheme, const SegArgs &a, const double *rows, hipStream_t st);
 hipError_t launch_correction_power(int scheme, const double *map, double *pow, int L, int Lpad, hipStream_t st);
-// q(x) = sum_g sigma_g (phi_g(x) - W B_g(x)) over the handle's groups, phi the
-// sum of nparts [N][Gl] arrays at phi (the fused parts, or one full phi)
-hipError_t launch_material_q(const double *phi, int nparts, const double *B, const double *sigma, double W, double *q,
-                             int Gl, int N, hipStream_t st);
-// T(x) += dt q(x) / rho_cv
-hipError_t launch_material_update(double *T, const double *q, double dt, double rho_cv, int N, hipStream_t st);
+// q[x] = sum_g sigma_g (phi_g(x) - W B_g(x)) over the handle's groups, phi the
+// sum of nparts [N][Gl] arrays at phi (the fused parts, or one full phi); q[N + x] = bpart[x]
+hipError_t launch_material_q(const double *phi, int nparts, const double *B, const double *sigma, double W,
+                             const double *bpart, double *q, int Gl, int N, hipStream_t st);
+// from qb = [q, b] summed over all groups: dT = dt q / (rho_cv + dt W b), T(x) += dT, dTlast = dT
+hipError_t launch_material_update(double *T, const double *qb, double *dTlast, double dt, double rho_cv, double W,
+                                  int N, hipStream_t st);
+// E[x] = scale sum_gl sigma[gl] ((Beff - B) + owed[gl][x]) (rt_get_material_transit)
+hipError_t launch_material_transit(const double *B, const double *Beff, const double *owed, const double *sigma,
+                                   double scale, double *E, int Gl, int N, hipStream_t st);
 
 }  // namespace rtamd

@@ -7,10 +7,6 @@
 #include "kernels.hpp"
 #include "sweep_device.hpp"
 
-#ifndef RT_SPLIT_PIN_LOADS
-#define RT_SPLIT_PIN_LOADS 1
-#endif
-
 namespace rtamd {
 
 // ------------------------------------------------------------------------
@@ -67,7 +63,6 @@ __device__ __forceinline__ void split_chunk(const double *W, double (&ein)[C], d
     else  // hand the nodes at this wave's last level to the next wave
       lout[c * 64 + lane] = make_double2(oi, oo);
     if constexpr (IN_HBM) {
-#if RT_SPLIT_PIN_LOADS
       // refill from HBM one cell late: row c - 1 with the next chunk's (row C - 1 of THIS
       // chunk at cell 0).  The upwind node of cell c - 1 (row c - 1's e_out) is the carried
       // state's component 0 until cell c's first level, so an earlier load could not reuse
@@ -83,13 +78,6 @@ __device__ __forceinline__ void split_chunk(const double *W, double (&ein)[C], d
       // each load after its cell's FMAs (left alone, the scheduler sinks them to the end)
       __builtin_amdgcn_sched_group_barrier(0x002, TW * 28, 0);  // VALU
       __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);        // VMEM read
-#else
-      if constexpr (!LASTCH) {
-        const double2 v = row_load(Rn, voff, c * row_bytes);
-        ein[c] = v.x;
-        eout[c] = v.y;
-      }
-#endif
     } else if constexpr (!LASTCH) {  // refill with the next chunk from the previous wave
       const double2 v = lin[c * 64 + lane];
       ein[c] = v.x;
@@ -190,9 +178,8 @@ __device__ __forceinline__ void split_role(const SegArgs &a, double2 (*hand)[2][
   if constexpr (IN) {
     const __amdgpu_buffer_rsrc_t R0 = rows(k_begin);
 #pragma unroll
-    for (int c = 0; c < C; ++c) {  // (RT_SPLIT_PIN_LOADS: row C - 1 by the first chunk's cell 0)
-      const double2 v =
-          (c + 1 < C || !RT_SPLIT_PIN_LOADS) ? row_load(R0, voff, c * row_bytes) : make_double2(0.0, 0.0);
+    for (int c = 0; c < C; ++c) {  // (row C - 1 comes with the first chunk's cell 0)
+      const double2 v = c + 1 < C ? row_load(R0, voff, c * row_bytes) : make_double2(0.0, 0.0);
       ein[c] = v.x;
       eout[c] = v.y;
     }
@@ -232,13 +219,11 @@ __device__ __forceinline__ void split_role(const SegArgs &a, double2 (*hand)[2][
   double W[WN];
 #pragma unroll
   for (int n = 0; n < WN; ++n) W[n] = a.map[(static_cast<size_t>(half) * WN + n) * stride + ell];
-#if RT_SPLIT_PIN_LOADS
   // every prologue load (map, carried states, chunk 0) complete before the chunks start:
   // the wait-count pass merges the loop's entry into its head, and a map load still
   // pending there made EVERY chunk start wait for all loads in flight (vmcnt(0)) -- the
   // next chunk's rows, issued just before
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0) expcnt(7) lgkmcnt(15)
-#endif
 
   // ---- chunk intervals: nch + 2 (KW - 1) of them, one barrier after each, for every wave ----
   const int nch = (k_end - k_begin + C - 1) / C;
@@ -275,9 +260,7 @@ __device__ __forceinline__ void split_role(const SegArgs &a, double2 (*hand)[2][
   for (int I = 0; I < 2 * (KW - 1 - w); ++I) __syncthreads();  // the later waves drain it
 }
 
-#ifndef RT_SPLIT_PRIO
-#define RT_SPLIT_PRIO 1  // 1 + the wave given issue priority 1; 0: none (timing experiments)
-#endif
+constexpr int kSplitPrioWave = 0;  // the wave given issue priority 1 (wave 0 streams the rows in)
 // Wave w's role; with `tail`, the waves whose levels reach past the tail's take the TAIL body,
 // the others the plain one -- correct only when wave 0's levels all lie inside the tail
 // (tail_levels >= split_tw of wave 0), which launch_split_tail enforces.
@@ -324,7 +307,7 @@ __global__ __launch_bounds__(64 * KW) __attribute__((amdgpu_waves_per_eu(2, 2)))
   // (profiles/archive/r03ap_prio.jsonl); on another box 8.17-8.18 vs 8.36-8.41, and the four-wave
   // T = 40 pass 7.85-7.88 vs 7.90-7.91 (r03aq_prio.jsonl; MI355X_MICROARCH.md, two waves per
   // SIMD, item 4).
-  if (RT_SPLIT_PRIO > 0 && w == RT_SPLIT_PRIO - 1) __builtin_amdgcn_s_setprio(1);
+  if (w == kSplitPrioWave) __builtin_amdgcn_s_setprio(1);
   split_roles<S, T, KW, false>(a, hand, hhead, w);
 }
 
@@ -340,7 +323,7 @@ __global__ __launch_bounds__(64 * KW) __attribute__((amdgpu_waves_per_eu(2, 2)))
   __shared__ double2 hand[KW - 1][2][split_chunk_cells() * 64];
   __shared__ double2 hhead[64];
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  if (RT_SPLIT_PRIO > 0 && w == RT_SPLIT_PRIO - 1) __builtin_amdgcn_s_setprio(1);
+  if (w == kSplitPrioWave) __builtin_amdgcn_s_setprio(1);
   // The waves that run all their levels take the plain body: with the tail's level count a
   // runtime bound in the level loop the workgroup ran ~55% slower (the loop's pinned loads
   // lose their place), which set every drain launch's time (16-group shard, 100 steps: 237

@@ -46,49 +46,10 @@ __device__ __forceinline__ double lane_shift_up(double old, double v) {
                                         static_cast<unsigned int>(lo));
 }
 
-// Ticks per loop iteration of the single-wave kernel (even; timing experiments: RT_WAVE_UNROLL)
-#ifndef RT_WAVE_UNROLL
-#define RT_WAVE_UNROLL 8
-#endif
-constexpr int kWaveUnroll = RT_WAVE_UNROLL;
+// Ticks per loop iteration of the single-wave kernel (even)
+constexpr int kWaveUnroll = 8;
 static_assert(kWaveUnroll >= 2 && kWaveUnroll % 2 == 0, "renames cancel over an even number of ticks");
 
-// Diagnostic builds only (make variant V=stamps RT_DEFS=-DRT_WAVE_STAMPS): lane 0 of every wave
-// records (s_memtime, s_memrealtime) at entry, before and after its tick stream; the product
-// never reads them.  rt_debug_wave_stamps copies them out (tools/wave_clock.py).
-#ifdef RT_WAVE_STAMPS
-constexpr int kStampWaves = 16384;
-__device__ unsigned long long g_wave_stamps[kStampWaves * 6];
-// (slot 0 also records the wave's HW_ID register: SIMD, CU and SE it runs on)
-__device__ unsigned int g_wave_hwid[kStampWaves];
-#define RT_STAMP(slot)                                                                              \
-  do {                                                                                              \
-    const unsigned long long t_ = __builtin_amdgcn_s_memtime();                                     \
-    const unsigned long long r_ = __builtin_amdgcn_s_memrealtime();                                 \
-    const int wv_ = static_cast<int>(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));          \
-    if ((threadIdx.x & 63) == 0 && wv_ < kStampWaves) {                                             \
-      g_wave_stamps[wv_ * 6 + 2 * (slot)] = t_;                                                     \
-      g_wave_stamps[wv_ * 6 + 2 * (slot) + 1] = r_;                                                 \
-      if ((slot) == 0) g_wave_hwid[wv_] = __builtin_amdgcn_s_getreg((31 << 11) | 4);                \
-    }                                                                                               \
-  } while (0)
-// chain_kernel, workgroup 0 only: every wave's s_memtime before and after each block's barrier
-constexpr int kBlockStamps = 2048;
-__device__ unsigned long long g_block_stamps[kWaveMaxWaves * kBlockStamps * 2];
-#define RT_BLOCK_STAMP(b, k)                                                                        \
-  do {                                                                                              \
-    const unsigned long long t_ = __builtin_amdgcn_s_memtime();                                     \
-    if (blockIdx.x == 0 && (threadIdx.x & 63) == 0 && (b) < kBlockStamps)                           \
-      g_block_stamps[((threadIdx.x >> 6) * kBlockStamps + (b)) * 2 + (k)] = t_;                     \
-  } while (0)
-#else
-#define RT_STAMP(slot) \
-  do {                 \
-  } while (0)
-#define RT_BLOCK_STAMP(b, k) \
-  do {                       \
-  } while (0)
-#endif
 
 // The lane's cell maps.  A pair chain's mu > 0 head lane runs its cell 0 on the head cell's
 // own map (cell.hpp cell_map<S, true>: the reference's head algebra with the mirror's
@@ -166,7 +127,6 @@ __device__ __forceinline__ void lane_cell(int c, bool refl_head, const double (&
 template <int S, int C, bool PAIR, bool PAD>
 __global__ __launch_bounds__(64) void wavefront_kernel(SegArgs a, int nsteps, int Lw) {
   constexpr int K = SchemeDim<S>::K, WN = map_count<S>();
-  RT_STAMP(0);
   const int g = threadIdx.x & 63;  // chain lane
   const int nl = a.H * a.Gl;
   int half, ell, j;
@@ -277,7 +237,6 @@ __global__ __launch_bounds__(64) void wavefront_kernel(SegArgs a, int nsteps, in
   const int ticks = nsteps + used - 1;
   // the unmasked ticks: every real lane at a level in [1, nsteps)
   const int u_lo = min(63, used - 1) + 1, u_hi = max(u_lo, nsteps);
-  RT_STAMP(1);
   if (u_lo < u_hi && u_hi <= ticks) {
     run(0, u_lo, std::true_type{});
     run(u_lo, u_hi, std::false_type{});
@@ -285,7 +244,6 @@ __global__ __launch_bounds__(64) void wavefront_kernel(SegArgs a, int nsteps, in
   } else {
     run(0, ticks, std::true_type{});
   }
-  RT_STAMP(2);
 #pragma unroll
   for (int c = 0; c < C; ++c) {
     const int k = j * C + c;
@@ -317,12 +275,8 @@ constexpr int kChainBlock = 8;                 // wall ticks per barrier block
 constexpr int kChainSkew = 2 * kChainBlock;    // chain ticks wave w runs behind wave w - 1
 constexpr int kChainRing = 4 * kChainBlock;    // slots per boundary (and region 0)
 constexpr int kChainSlot = 6;                  // doubles per slot (48 B: 16-byte aligned)
-#ifndef RT_CHAIN_MASKED_UNROLL
-#define RT_CHAIN_MASKED_UNROLL 1  // masked blocks (a wave's fill and drain ramps) unrolled too (2-6%: r04r)
-#endif
-#ifndef RT_CHAIN_FENCE
-#define RT_CHAIN_FENCE 1  // scheduling fences at each tick's start (4-8 cells per lane) and after its ring read
-#endif
+// masked blocks (a wave's fill and drain ramps) are unrolled too (2-6%: r04r); scheduling
+// fences at each tick's start (4-8 cells per lane) and after its ring read
 static_assert(kChainSkew >= kChainBlock + 2 && kChainSkew + kChainBlock <= kChainRing, "ring too short for the skew");
 static_assert(kChainSkew % kChainBlock == 0 && kChainRing % kChainBlock == 0, "blocks align with the ring");
 
@@ -338,7 +292,6 @@ template <int S, int C, bool PAIR, bool PAD, bool WIDE>
 __global__ __launch_bounds__(64 * (WIDE ? kWaveMaxWaves : 4)) void chain_kernel(SegArgs a, int nsteps, int Lw) {
   constexpr int K = SchemeDim<S>::K, WN = map_count<S>();
   static_assert(K <= kChainSlot - 1, "a slot holds the carried state");
-  RT_STAMP(0);
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
   const int nw = static_cast<int>(blockDim.x >> 6);
@@ -458,7 +411,6 @@ __global__ __launch_bounds__(64 * (WIDE ? kWaveMaxWaves : 4)) void chain_kernel(
 #pragma unroll
   for (int r = 0; r < K; ++r) nx[r] = 0.0;
   read_slot(rd_region, nx, true);  // chain tick 0 (slot 0)
-  RT_STAMP(1);
   for (int b = 0; b < nblocks; ++b) {
     const int t0 = b * kChainBlock - wsk;  // chain tick of the block's first wall tick (= 0 mod the block)
     if (K > 1 && t0 >= u_lo && t0 + kChainBlock <= u_hi) {
@@ -471,7 +423,7 @@ __global__ __launch_bounds__(64 * (WIDE ? kWaveMaxWaves : 4)) void chain_kernel(
       for (int i = 0; i < kChainBlock; ++i) {
         // ticks are not interleaved: at 8 cells per lane an 8-tick block would not fit
         // the registers
-        if (RT_CHAIN_FENCE && C >= 4) __builtin_amdgcn_sched_barrier(0);
+        if (C >= 4) __builtin_amdgcn_sched_barrier(0);
         const double x0 = Xin[K - 1];
         Xin[K - 1] = lane_shift_up(nx[K - 1], X[K - 1]);
 #pragma unroll
@@ -494,7 +446,7 @@ __global__ __launch_bounds__(64 * (WIDE ? kWaveMaxWaves : 4)) void chain_kernel(
           for (int r = 0; r < K; ++r) prev[r] = X[r];
         }
         read_slot(i + 1 < kChainBlock ? rb + (i + 1) * kChainSlot : rn, nx, false);
-        if (RT_CHAIN_FENCE) __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int r = 0; r < K; ++r) X[r] = Xin[r];
         cells(true);
@@ -504,9 +456,7 @@ __global__ __launch_bounds__(64 * (WIDE ? kWaveMaxWaves : 4)) void chain_kernel(
         }
       }
     } else {
-#if RT_CHAIN_MASKED_UNROLL
 #pragma unroll
-#endif
       for (int i = 0; i < kChainBlock; ++i) {
         const int t = t0 + i;
         if (t < 0 || t >= ticks) continue;  // wall ticks before or after this wave's chain
@@ -525,11 +475,8 @@ __global__ __launch_bounds__(64 * (WIDE ? kWaveMaxWaves : 4)) void chain_kernel(
         if (writer) write_slot(wr_region + ((t + 1) & RM) * kChainSlot, X, true);
       }
     }
-    RT_BLOCK_STAMP(b, 0);
     __syncthreads();
-    RT_BLOCK_STAMP(b, 1);
   }
-  RT_STAMP(2);
 #pragma unroll
   for (int c = 0; c < C; ++c) {
     const int k = j * C + c;
@@ -646,29 +593,3 @@ hipError_t launch_wavefront(int scheme, const WavePlan &p, const SegArgs &a, int
 }
 
 }  // namespace rtamd
-
-#ifdef RT_WAVE_STAMPS
-// diagnostic builds only: the stamps of the last wavefront launch, 6 per wave
-extern "C" int rt_debug_wave_stamps(unsigned long long *out, int waves) {
-  if (waves > rtamd::kStampWaves) waves = rtamd::kStampWaves;
-  if (hipDeviceSynchronize() != hipSuccess) return -1;
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(rtamd::g_wave_stamps), sizeof(unsigned long long) * 6 * waves) != hipSuccess)
-    return -1;
-  return waves;
-}
-// the HW_ID register of each wave of the last launch (diagnostic builds only)
-extern "C" int rt_debug_wave_hwid(unsigned int *out, int waves) {
-  if (waves > rtamd::kStampWaves) waves = rtamd::kStampWaves;
-  if (hipDeviceSynchronize() != hipSuccess) return -1;
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(rtamd::g_wave_hwid), sizeof(unsigned int) * waves) != hipSuccess) return -1;
-  return waves;
-}
-// per-block stamps of chain_kernel's workgroup 0: [wave][block][before, after the barrier]
-extern "C" int rt_debug_block_stamps(unsigned long long *out) {
-  if (hipDeviceSynchronize() != hipSuccess) return -1;
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(rtamd::g_block_stamps),
-                          sizeof(unsigned long long) * 2 * rtamd::kWaveMaxWaves * rtamd::kBlockStamps) != hipSuccess)
-    return -1;
-  return rtamd::kBlockStamps;
-}
-#endif

@@ -376,6 +376,28 @@ extern "C" rt_status rt_get_level_waves(rt_solver *s, int *waves) {
   return RT_OK;
 }
 
+extern "C" rt_status rt_set_moments_form(rt_solver *s, int form) {
+  if (!s) return fail(nullptr, RT_ERR_ARG, "rt_set_moments_form: NULL handle");
+  if (form != 0 && form != 1) return fail(s, RT_ERR_ARG, "rt_set_moments_form: 0 (one wave) or 1 (producer/consumer)");
+  s->moments_form = form;
+  s->mom_version = 0;  // the next read-out runs the chosen kernel
+  return RT_OK;
+}
+
+extern "C" rt_status rt_set_phi_correction_form(rt_solver *s, int form) {
+  if (!s) return fail(nullptr, RT_ERR_ARG, "rt_set_phi_correction_form: NULL handle");
+  if (form != 0 && form != 1) return fail(s, RT_ERR_ARG, "rt_set_phi_correction_form: 0 (closed forms) or 1 (walk)");
+  s->phi_corr_form = form;
+  return RT_OK;
+}
+
+extern "C" rt_status rt_debug_fail_launch(rt_solver *s, int after) {
+  if (!s) return fail(nullptr, RT_ERR_ARG, "rt_debug_fail_launch: NULL handle");
+  if (after < -1) return fail(s, RT_ERR_ARG, "rt_debug_fail_launch: -1 (off) or launches before the failure");
+  s->fail_launch_after = after;
+  return RT_OK;
+}
+
 extern "C" rt_status rt_sweep_geometry(rt_solver *s, int *workgroups, long long *tiles) {
   if (!s) return fail(nullptr, RT_ERR_ARG, "rt_sweep_geometry: NULL handle");
   if (workgroups) *workgroups = 2 * s->Q * s->Sg;  // one 64-lane wave per (line group, segment)

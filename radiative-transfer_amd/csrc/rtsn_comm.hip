@@ -4,7 +4,7 @@
 // GPU, each holding a shard handle; groups never exchange data while stepping (T is
 // constant, solver.cpp:157), so the only collectives are the end-of-run reductions of
 // the reference's result arrays and, in the material-coupled mode, one all-reduce of
-// q(x) per step.  Every collective is enqueued on the handle's own stream, so it is
+// [q(x), b(x)] (2N doubles) per step.  Every collective is enqueued on the handle's own stream, so it is
 // ordered after the sweeps that produce its input without a host synchronisation.
 //
 // Layouts on the wire (one all-gather per result, each rank's block padded to the
@@ -60,7 +60,7 @@ struct rt_comm {
   int nranks = 0, rank = 0, device = 0;
   bool aborted = false;  // a wait expired: the communicator was aborted
   double timeout_s = 300.0;
-  double *q = nullptr;  // material coupling: q(x) of the running step (N doubles)
+  double *q = nullptr;  // material coupling: [q(x), b(x)] of the running step (2N doubles)
   size_t q_len = 0;
   std::vector<Mark> marks;         // collectives enqueued since the last completed host wait
   std::vector<hipEvent_t> events;  // recycled event pool
@@ -577,18 +577,19 @@ extern "C" rt_status rt_comm_material_step(rt_comm *c, rt_solver *s, int nsteps)
   int N = 0;
   RT_TRY(c, s, rt_get_dims(s, nullptr, nullptr, &N, nullptr, nullptr));
   hipStream_t st = static_cast<hipStream_t>(rt_stream(s));
-  if (c->q_len < static_cast<size_t>(N)) {
+  const size_t len = 2 * static_cast<size_t>(N);  // q and b: one all-reduce per step
+  if (c->q_len < len) {
     if (c->q) {
       CS_TRY(c, st);
       HC_TRY(c, hipFree(c->q));
       c->q = nullptr;
     }
-    HC_TRY(c, hipMalloc(&c->q, sizeof(double) * N));
-    c->q_len = N;
+    HC_TRY(c, hipMalloc(&c->q, sizeof(double) * len));
+    c->q_len = len;
   }
   for (int n = 0; n < nsteps; ++n) {
     RT_TRY(c, s, rt_material_sweep(s, c->q));
-    CO_TRY(c, st, ncclAllReduce(c->q, c->q, N, ncclFloat64, ncclSum, c->nc, st));
+    CO_TRY(c, st, ncclAllReduce(c->q, c->q, len, ncclFloat64, ncclSum, c->nc, st));
     RT_TRY(c, s, rt_material_update(s, c->q));
   }
   return RT_OK;

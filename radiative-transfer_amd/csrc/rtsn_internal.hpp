@@ -236,10 +236,18 @@ struct rt_solver {
   long long wqueued = 0;         // requested steps queued for the wavefront kernel (wave_advance)
   int Tpipe = 0;                 // time block of the running pipeline (0: positions aligned)
   int tail = 0;                  // draining: the run's last steps (< Tpipe), each position's final block
+  int resume_lo = -1, resume_hi = -1;  // positions a failed sub-launch still owes (pipe_launch)
+  int fail_launch_after = -1;    // test hook (rt_debug_fail_launch): pipelined sub-launches before one fails
+  int moments_form = 1;          // rt_set_moments_form: 1 producer/consumer, 0 one-wave (bitwise equal)
+  int phi_corr_form = 0;         // rt_set_phi_correction_form: 0 closed forms, 1 the cell-by-cell walk
   // material-temperature coupling (rt_material_enable)
   bool material = false;
-  double rho_cv = 0.0, wsum = 0.0;
-  rtsn_detail::DeviceBuf Tcell, Bcell, qbuf, edges, map_unit, hmap_unit, phi_part;
+  double rho_cv = 0.0, wsum = 0.0;  // wsum: this handle's quadrature weights (its q share)
+  double wsum_all = 0.0;              // all M directions' weights (W of the T update)
+  // Tcell [N]; Bcell [N][Gl] B_g(T); Beff [N][Gl] the step's emission B + the owed share paid;
+  // owed, dBcell [Gl][N] the owed emission and dB_g/dT; dTlast [N] the last update's dT; bpart
+  // [N] sum_gl sigma dB/dT; qbuf [2N] the exchange buffer (q, b)
+  rtsn_detail::DeviceBuf Tcell, Bcell, Beff, owed, dBcell, dTlast, bpart, qbuf, edges, map_unit, hmap_unit, phi_part;
   rtsn_detail::DeviceBuf corr_pow;            // A^Lsub per line for phi_correction_kernel's sub-segments
   int corr_pow_L = 0;            // the Lsub it holds (0: none)
   rtsn_detail::DeviceBuf corr_rows;           // BDF2: rows b A^j and A^64 per line (phi_correction_rows_kernel)

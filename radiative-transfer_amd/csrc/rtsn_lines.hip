@@ -363,16 +363,16 @@ rt_status rtsn_detail::resegment(rt_solver *h, bool aligned) {
   if (2LL * h->Q * h->Sg >= (1LL << 31)) return fail(h, RT_ERR_PARAM, "too many lines for one handle: shard the groups");
   HIP_TRY(h, alloc_segments(h));
   h->tau.assign(chain_positions(h), h->target);  // every position at the same, requested time
+  h->resume_lo = h->resume_hi = -1;
   return RT_OK;
 }
 
 // Workgroups per CU the segments of the current time block are sized for: the caller's
 // (rt_set_segmentation, or the schedule rt_solve planned), else the pipelined pass's
-// occupancy (RTSN_WAVES_PER_CU overrides, for experiments).
+// occupancy.
 rt_status rtsn_detail::segment_target(rt_solver *h, int *w_out) {
   int w = h->seg_wgs;
   if (!w) HIP_TRY(h, sweep_occupancy(h->scheme, h->T, level_waves_of(h, h->T), &w));
-  if (const char *env = std::getenv("RTSN_WAVES_PER_CU")) w = std::atoi(env);  // experiments
   *w_out = std::max(1, std::min(w, 64));
   return RT_OK;
 }

@@ -1,5 +1,6 @@
 // rtsn_material.hip -- material-temperature coupling (include/rtsn.h "material"):
-// per-cell Planck emission, the coupled sweep with fused angular sums and the T update.
+// per-cell Planck emission and its T derivative, the coupled sweep with fused angular sums,
+// the T update implicit in the material's own emission and the owed emission it implies.
 
 #include "rtsn_internal.hpp"
 
@@ -21,7 +22,8 @@ static rt_status material_planck(rt_solver *s) {
   return RT_OK;
 }
 
-// dt W sum_g rho kappa_g dB_g/dT(T_max) / rho_cv over all G groups (rt_material_stability)
+// dt W sum_g rho kappa_g dB_g/dT(T_max) / rho_cv over all G groups (rt_material_stability): the
+// emission's stiffness at the hottest cell, 1 / (1 + number) the Fleck factor there
 static double material_stability_number(const rt_solver *s, double T_max) {
   const int G = s->p.G;
   std::vector<double> lo(s->gt.e_edge.begin(), s->gt.e_edge.begin() + G), hi(s->gt.e_edge.begin() + 1,
@@ -61,7 +63,12 @@ extern "C" rt_status rt_material_enable(rt_solver *s, double rho_cv, const doubl
   if (!s->Tcell.p) {
     hipError_t e = dalloc(s->Tcell, sizeof(double) * N);
     if (!e) e = dalloc(s->Bcell, sizeof(double) * NG);
-    if (!e) e = dalloc(s->qbuf, sizeof(double) * N);
+    if (!e) e = dalloc(s->Beff, sizeof(double) * NG);
+    if (!e) e = dalloc(s->owed, sizeof(double) * NG);
+    if (!e) e = dalloc(s->dBcell, sizeof(double) * NG);
+    if (!e) e = dalloc(s->dTlast, sizeof(double) * N);
+    if (!e) e = dalloc(s->bpart, sizeof(double) * N);
+    if (!e) e = dalloc(s->qbuf, sizeof(double) * 2 * N);
     if (!e) e = dalloc(s->edges, sizeof(double) * (s->p.G + 1));
     if (!e) e = dalloc(s->map_unit, s->map.bytes);
     if (!e) e = dalloc(s->hmap_unit, s->hmap.bytes);
@@ -76,10 +83,11 @@ extern "C" rt_status rt_material_enable(rt_solver *s, double rho_cv, const doubl
   }
   if (st) return st;
   {  // coupled passes are single steps: segments for the coupled kernel's occupancy
-     // (measured on SL: 16 waves per CU instead is slower for BE, even for BDF2)
+     // (measured on SL: 16 waves per CU instead is slower for BE, even for BDF2), or the
+     // caller's rt_set_segmentation
     int w = 0;
     HIP_TRY(s, coupled_occupancy(s->scheme, &w));
-    if (const char *env = std::getenv("RTSN_WAVES_PER_CU")) w = std::atoi(env);
+    if (s->seg_set && s->seg_wgs) w = s->seg_wgs;
     const int sg0 = s->Sg;
     segment_lines(s, w);
     s->seg_T = 0;  // sized for the coupled pass
@@ -88,6 +96,7 @@ extern "C" rt_status rt_material_enable(rt_solver *s, double rho_cv, const doubl
       if (2LL * s->Q * s->Sg >= (1LL << 31)) return fail(s, RT_ERR_PARAM, "too many segments");
       HIP_TRY(s, alloc_segments(s));
       s->tau.assign(chain_positions(s), s->target);  // every position at the same, requested time
+      s->resume_lo = s->resume_hi = -1;
     }
   }
   std::vector<double> T0(N, s->p.T);
@@ -95,6 +104,9 @@ extern "C" rt_status rt_material_enable(rt_solver *s, double rho_cv, const doubl
   if (s->phi_fused)  // the correction sums of segment-0 cells are never written: zero
     HIP_TRY(s, hipMemsetAsync(s->phi_part.p, 0, s->phi_part.bytes, s->stream));
   if ((st = upload(s, s->Tcell, T0.data(), N * sizeof(double)))) return st;
+  HIP_TRY(s, hipMemsetAsync(s->dTlast.p, 0, sizeof(double) * N, s->stream));  // nothing owed yet
+  HIP_TRY(s, hipMemsetAsync(s->owed.p, 0, sizeof(double) * NG, s->stream));
+  HIP_TRY(s, hipMemsetAsync(s->dBcell.p, 0, sizeof(double) * NG, s->stream));
   if ((st = upload(s, s->edges, s->gt.e_edge.data(), (s->p.G + 1) * sizeof(double)))) return st;
   PlanckCells &pc = s->pc;
   phys::PlanckIntegrator().nodes(pc.node, pc.weight);
@@ -106,22 +118,25 @@ extern "C" rt_status rt_material_enable(rt_solver *s, double rho_cv, const doubl
   pc.a_c = phys::rad_a_long() * phys::kLight;
   pc.kcon = phys::kBoltzmannJPK;
   pc.accuracy = std::numeric_limits<double>::epsilon();
+  pc.sigma = static_cast<const double *>(s->sigma.p);
+  pc.dTlast = static_cast<const double *>(s->dTlast.p);
+  pc.owed = static_cast<double *>(s->owed.p);
+  pc.dB = static_cast<double *>(s->dBcell.p);
+  pc.Beff = static_cast<double *>(s->Beff.p);
+  pc.bpart = static_cast<double *>(s->bpart.p);
+  pc.b_scale = s->d_lo == 0 ? 1.0 : 0.0;  // direction shards: every one holds all groups, count b once
   s->wsum = 0.0;
   for (double w : s->wt) s->wsum += w;
+  {
+    std::vector<double> mu_all(s->M_full), wt_all(s->M_full);
+    phys::gauss_legendre(s->M_full, phys::kFourPi, mu_all.data(), wt_all.data());
+    s->wsum_all = 0.0;
+    for (double w : wt_all) s->wsum_all += w;
+  }
   s->rho_cv = rho_cv;
   if ((st = material_planck(s))) return st;
   HIP_TRY(s, hipStreamSynchronize(s->stream));  // T0 dies at return
   s->material = true;
-  double T_max = 0.0;
-  for (double t : T0)
-    if (std::isfinite(t)) T_max = std::max(T_max, t);
-  const double number = material_stability_number(s, T_max);
-  if (number > 2.0) {
-    char msg[160];
-    std::snprintf(msg, sizeof(msg), "explicit emission stability number %.4g > 2 at T_max = %.4g keV: "
-                                    "reduce dt or raise rho_cv", number, T_max);
-    return fail(s, RT_WARN_UNSTABLE, msg);
-  }
   return RT_OK;
 }
 
@@ -134,6 +149,7 @@ extern "C" rt_status rt_material_sweep(rt_solver *s, double *d_q) {
   if ((st = ensure_equilibrium(s))) return st;
   double *q = d_q ? d_q : static_cast<double *>(s->qbuf.p);
   const double *B = static_cast<const double *>(s->Bcell.p), *sig = static_cast<const double *>(s->sigma.p);
+  const double *bp = static_cast<const double *>(s->bpart.p);
   if (s->phi_fused) {
     // one pass over the state: the pass sums w psi of its provisional cells, the
     // correction kernel adds the cross-segment correction's share (no state
@@ -147,24 +163,24 @@ extern "C" rt_status rt_material_sweep(rt_solver *s, double *d_q) {
       a.H = s->H;
       a.phic = static_cast<double *>(s->phi_part.p) + 2 * static_cast<size_t>(s->p.N) * s->Gl;
       a.wt = static_cast<const double *>(s->muwt.p) + s->p.M;
-      // BE, CN: closed form, lanes over cells (phi_correction_geo_kernel); RTSN_PHI_WALK=1
-      // keeps the walk for comparison
-      const char *walk = std::getenv("RTSN_PHI_WALK");
-      if (phi_correction_geo_supported(s->scheme, a) && !(walk && !std::strcmp(walk, "1"))) {
+      // BE, CN: closed form, lanes over cells (phi_correction_geo_kernel); rt_set_phi_correction_form
+      // 1 keeps the walk for comparison
+      const bool walk = s->phi_corr_form == 1;
+      if (phi_correction_geo_supported(s->scheme, a) && !walk) {
         HIP_TRY(s, launch_phi_correction_geo(s->scheme, a, s->stream));
-        HIP_TRY(s, launch_material_q(static_cast<const double *>(s->phi_part.p), 4, B, sig, s->wsum, q, s->Gl,
+        HIP_TRY(s, launch_material_q(static_cast<const double *>(s->phi_part.p), 4, B, sig, s->wsum, bp, q, s->Gl,
                                      s->p.N, s->stream));
         return RT_OK;
       }
       // BDF2: closed form by tabulated rows (phi_correction_rows_kernel)
-      if (phi_correction_rows_supported(s->scheme, a) && !(walk && !std::strcmp(walk, "1"))) {
+      if (phi_correction_rows_supported(s->scheme, a) && !walk) {
         if (!s->corr_rows.p) {
           HIP_TRY(s, dalloc(s->corr_rows, sizeof(double) * corr_rows_doubles(s->scheme, s->Lpad)));
           HIP_TRY(s, launch_corr_rows(s->scheme, static_cast<const double *>(s->map.p),
                                       static_cast<double *>(s->corr_rows.p), s->Lpad, s->stream));
         }
         HIP_TRY(s, launch_phi_correction_rows(s->scheme, a, static_cast<const double *>(s->corr_rows.p), s->stream));
-        HIP_TRY(s, launch_material_q(static_cast<const double *>(s->phi_part.p), 4, B, sig, s->wsum, q, s->Gl,
+        HIP_TRY(s, launch_material_q(static_cast<const double *>(s->phi_part.p), 4, B, sig, s->wsum, bp, q, s->Gl,
                                      s->p.N, s->stream));
         return RT_OK;
       }
@@ -183,14 +199,14 @@ extern "C" rt_status rt_material_sweep(rt_solver *s, double *d_q) {
       HIP_TRY(s, launch_phi_correction(s->scheme, a, nsub, Lsub, static_cast<const double *>(s->corr_pow.p),
                                        s->stream));
     }
-    HIP_TRY(s, launch_material_q(static_cast<const double *>(s->phi_part.p), s->pending ? 4 : 2, B, sig, s->wsum, q,
-                                 s->Gl, s->p.N, s->stream));
+    HIP_TRY(s, launch_material_q(static_cast<const double *>(s->phi_part.p), s->pending ? 4 : 2, B, sig, s->wsum, bp,
+                                 q, s->Gl, s->p.N, s->stream));
     return RT_OK;
   }
   if ((st = finalize(s))) return st;
   if ((st = enqueue_pass(s, 1, true))) return st;
   if ((st = compute_moments(s))) return st;  // finalizes the pass
-  HIP_TRY(s, launch_material_q(static_cast<const double *>(s->mom.p), 1, B, sig, s->wsum, q, s->Gl, s->p.N,
+  HIP_TRY(s, launch_material_q(static_cast<const double *>(s->mom.p), 1, B, sig, s->wsum, bp, q, s->Gl, s->p.N,
                                s->stream));
   return RT_OK;
 }
@@ -200,7 +216,8 @@ extern "C" rt_status rt_material_update(rt_solver *s, const double *d_q) {
   if (!s->material) return fail(s, RT_ERR_STATE, "rt_material_update: call rt_material_enable first");
   HIP_TRY(s, hipSetDevice(s->device));
   HIP_TRY(s, launch_material_update(static_cast<double *>(s->Tcell.p), d_q ? d_q : static_cast<const double *>(s->qbuf.p),
-                                    s->p.dt, s->rho_cv, s->p.N, s->stream));
+                                    static_cast<double *>(s->dTlast.p), s->p.dt, s->rho_cv, s->wsum_all, s->p.N,
+                                    s->stream));
   return material_planck(s);
 }
 
@@ -217,13 +234,13 @@ extern "C" rt_status rt_material_step(rt_solver *s, int nsteps) {
   return RT_OK;
 }
 
-// which: 0 T(x), 1 B per cell
+// which: 0 T(x), 1 B per cell, 2 the next step's emission per cell
 static rt_status material_fetch(rt_solver *s, int which, double *out, const char *what) {
   if (!s || !out) return fail(s, RT_ERR_ARG, std::string(what) + ": bad argument");
   if (!s->material) return fail(s, RT_ERR_STATE, std::string(what) + ": material coupling is off");
   HIP_TRY(s, hipSetDevice(s->device));
   const size_t count = which == 0 ? s->p.N : static_cast<size_t>(s->p.N) * s->Gl;
-  const void *src = which == 0 ? s->Tcell.p : s->Bcell.p;
+  const void *src = which == 0 ? s->Tcell.p : (which == 1 ? s->Bcell.p : s->Beff.p);
   HIP_TRY(s, hipMemcpyAsync(out, src, sizeof(double) * count, hipMemcpyDeviceToHost, s->stream));
   HIP_TRY(s, hipStreamSynchronize(s->stream));
   return RT_OK;
@@ -234,3 +251,24 @@ extern "C" rt_status rt_get_temperature(rt_solver *s, double *T_cells) {
 }
 
 extern "C" rt_status rt_get_cell_planck(rt_solver *s, double *B) { return material_fetch(s, 1, B, "rt_get_cell_planck"); }
+
+extern "C" rt_status rt_get_cell_emission(rt_solver *s, double *Beff) {
+  return material_fetch(s, 2, Beff, "rt_get_cell_emission");
+}
+
+extern "C" rt_status rt_get_material_transit(rt_solver *s, double *E) {
+  if (!s || !E) return fail(s, RT_ERR_ARG, "rt_get_material_transit: bad argument");
+  if (!s->material) return fail(s, RT_ERR_STATE, "rt_get_material_transit: material coupling is off");
+  HIP_TRY(s, hipSetDevice(s->device));
+  DeviceBuf d;
+  HIP_TRY(s, dalloc(d, sizeof(double) * s->p.N));
+  hipError_t e = launch_material_transit(static_cast<const double *>(s->Bcell.p), static_cast<const double *>(s->Beff.p),
+                                         static_cast<const double *>(s->owed.p), static_cast<const double *>(s->sigma.p),
+                                         s->p.dt * s->wsum, static_cast<double *>(d.p), s->Gl, s->p.N, s->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(E, d.p, sizeof(double) * s->p.N, hipMemcpyDeviceToHost, s->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
+  (void)hipStreamSynchronize(s->stream);
+  d.reset();
+  if (e != hipSuccess) return fail(s, RT_ERR_DEVICE, std::string("rt_get_material_transit: ") + hipGetErrorString(e));
+  return RT_OK;
+}

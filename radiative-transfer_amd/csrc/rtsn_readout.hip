@@ -206,7 +206,7 @@ rt_status rtsn_detail::compute_moments(rt_solver *s) {
   double *m = static_cast<double *>(s->mom.p);
   const double *muwt = static_cast<const double *>(s->muwt.p);
   HIP_TRY(s, launch_moments(static_cast<const double2 *>(s->E.p), muwt, muwt + s->p.M, m, m + GN, m + 2 * GN, g,
-                            s->stream));
+                            s->moments_form, s->stream));
   s->mom_version = s->state_version;
   return RT_OK;
 }

@@ -108,6 +108,11 @@ static rt_status event_begin(rt_solver *s, hipEvent_t *e1) {
   return RT_OK;
 }
 
+// a launch that failed after event_begin: its pair is returned unused (e1 never recorded)
+static void event_abort(rt_solver *s, hipEvent_t e1) {
+  if (e1) s->ev_used -= 2;
+}
+
 static rt_status event_end(rt_solver *s, hipEvent_t e1) {
   if (e1) {
     HIP_TRY(s, hipEventRecord(e1, s->stream));
@@ -130,7 +135,7 @@ rt_status rtsn_detail::enqueue_pass(rt_solver *s, int T, bool coupled) {
   if (coupled) {
     a.map = static_cast<const double *>(s->map_unit.p);
     a.hmap = static_cast<const double *>(s->hmap_unit.p);
-    a.bcell = static_cast<const double *>(s->Bcell.p);
+    a.bcell = static_cast<const double *>(s->Beff.p);  // the step's linearised emission
     a.Gl = s->Gl;
     a.H = s->H;
     a.phi = s->phi_fused ? static_cast<double *>(s->phi_part.p) : nullptr;
@@ -207,18 +212,31 @@ static int ramp_chunk(const rt_solver *s, int k, int grid_per_pos) {
   return m >= 1 && m < k ? static_cast<int>(m) : k;
 }
 
+// One pipelined launch: every position that can advance a block does.  A launch cut into
+// sub-launches (ramp_chunk) commits each sub-launch's positions (tau, state_version) as soon as
+// it is in the stream, and until the whole launch is, the handle remembers the positions still
+// owed (resume_lo..resume_hi): a call after a failed sub-launch (a non-sticky launch error, or
+// the profiling pool's event wait) runs exactly those, never a position twice.
 static rt_status pipe_launch(rt_solver *s) {
   if (rt_status st = ensure_segments(s)) return st;
   const int P = chain_positions(s), T = s->Tpipe;
   const long long end = s->target + s->tail;
   auto block = [&](int c) { return s->tau[c] < s->target ? T : s->tail; };
+  auto ready = [&](int c) { return s->tau[c] < end && (c == 0 || s->tau[c - 1] >= s->tau[c] + block(c)); };
   int lo = -1, hi = -1;
-  for (int c = 0; c < P; ++c) {
-    const bool ready = s->tau[c] < end && (c == 0 || s->tau[c - 1] >= s->tau[c] + block(c));
-    if (!ready) continue;
-    if (lo < 0) lo = c;
-    if (hi >= 0 && hi != c - 1) return fail(s, RT_ERR_PARAM, "pipeline: active positions not contiguous");
-    hi = c;
+  if (s->resume_lo >= 0) {  // the rest of an interrupted launch
+    lo = s->resume_lo;
+    hi = s->resume_hi;
+    if (hi >= P || lo > hi) return fail(s, RT_ERR_STATE, "pipeline: interrupted launch out of range");
+    for (int c = lo; c <= hi; ++c)
+      if (!ready(c)) return fail(s, RT_ERR_STATE, "pipeline: interrupted launch no longer ready");
+  } else {
+    for (int c = 0; c < P; ++c) {
+      if (!ready(c)) continue;
+      if (lo < 0) lo = c;
+      if (hi >= 0 && hi != c - 1) return fail(s, RT_ERR_PARAM, "pipeline: active positions not contiguous");
+      hi = c;
+    }
   }
   if (lo < 0) return fail(s, RT_ERR_PARAM, "pipeline: no position can advance");  // loops below rely on progress
   for (int c = lo; c <= hi; ++c)
@@ -228,6 +246,8 @@ static rt_status pipe_launch(rt_solver *s) {
   const int m = ramp_chunk(s, hi - lo + 1, per_pos);
   for (int c0 = lo; c0 <= hi; c0 += m) {
     const int c1 = std::min(hi, c0 + m - 1);
+    s->resume_lo = c0;  // owed until this sub-launch is in the stream
+    s->resume_hi = hi;
     SegArgs a = seg_args(s);
     a.aggs[0] = static_cast<double *>(s->agg[0].p);
     a.aggs[1] = static_cast<double *>(s->agg[1].p);
@@ -241,16 +261,29 @@ static rt_status pipe_launch(rt_solver *s) {
     hipEvent_t e1;
     rt_status st = event_begin(s, &e1);
     if (st) return st;
-    if (a.tail_levels) {
-      a.level_waves = tail_waves(s, T);  // (complete: wave 0 runs whole levels)
-      HIP_TRY(s, launch_split_tail(T, a.level_waves, a, grid, s->stream));
+    hipError_t e = hipSuccess;
+    if (s->fail_launch_after == 0) {  // test hook (rt_debug_fail_launch): this launch fails, nothing runs
+      s->fail_launch_after = -1;
+      e = hipErrorLaunchFailure;
     } else {
-      HIP_TRY(s, launch_sweep(s->scheme, T, SWEEP_PIPELINED, a, grid, s->stream));
+      if (s->fail_launch_after > 0) --s->fail_launch_after;
+      if (a.tail_levels) {
+        a.level_waves = tail_waves(s, T);  // (complete: wave 0 runs whole levels)
+        e = launch_split_tail(T, a.level_waves, a, grid, s->stream);
+      } else {
+        e = launch_sweep(s->scheme, T, SWEEP_PIPELINED, a, grid, s->stream);
+      }
     }
+    if (e != hipSuccess) {
+      event_abort(s, e1);
+      return fail(s, RT_ERR_DEVICE, std::string("pipelined launch: ") + hipGetErrorString(e));
+    }
+    for (int c = c0; c <= c1; ++c) s->tau[c] += block(c);
+    ++s->state_version;
+    s->resume_lo = c1 < hi ? c1 + 1 : -1;
+    s->resume_hi = c1 < hi ? hi : -1;
     if ((st = event_end(s, e1))) return st;
   }
-  ++s->state_version;
-  for (int c = lo; c <= hi; ++c) s->tau[c] += block(c);
   return RT_OK;
 }
 
@@ -530,9 +563,7 @@ struct Schedule {
   double ms = 0.0;
 };
 
-#ifndef RT_PLAN_FEW_GUARD
-#define RT_PLAN_FEW_GUARD 0.97  // 1-2 workgroups per CU must beat the best of 4-32 by this factor
-#endif
+constexpr double kPlanFewGuard = 0.97;  // 1-2 workgroups per CU must beat the best of 4-32 by this factor
 static Schedule plan_schedule(const RunGeom &g, long long nsteps) {
   // T = 4 over four waves (no remainder for n % 4 == 0) measured slower than T = 8 with its
   // aligned remainder (16-group shard, 100 steps: 181 vs 167 ms, profiles/archive/r04d_solve_plan.jsonl)
@@ -549,7 +580,7 @@ static Schedule plan_schedule(const RunGeom &g, long long nsteps) {
       Schedule &b = w >= 4 ? best : few;
       if (ms < 1e300 && (!b.T || ms < b.ms)) b = {T, w, ms};
     }
-  if (few.T && (!best.T || few.ms < RT_PLAN_FEW_GUARD * best.ms)) return few;
+  if (few.T && (!best.T || few.ms < kPlanFewGuard * best.ms)) return few;
   return best;
 }
 

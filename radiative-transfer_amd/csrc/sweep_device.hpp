@@ -24,19 +24,13 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rows_rsrc(const double2 *base,
 // Cache policy of the state stream (the buffer aux operand): nt (2).  Every row is
 // read and written once per pass and the state (131 GB on SL) is far beyond L2 and
 // MALL: nt loads and stores measured 1.8% faster on the HBM-bound T = 1 pass (41.9 vs
-// 42.7 ms) and 0.2-0.8% on the T = 16 pass.  Override for timing experiments.
-#ifndef RT_ROW_LOAD_AUX
-#define RT_ROW_LOAD_AUX 2
-#endif
-#ifndef RT_ROW_STORE_AUX
-#define RT_ROW_STORE_AUX 2
-#endif
+// 42.7 ms) and 0.2-0.8% on the T = 16 pass.
+constexpr int kRowAuxNT = 2;
 __device__ __forceinline__ double2 row_load(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
-  return __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, RT_ROW_LOAD_AUX));
+  return __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, kRowAuxNT));
 }
 __device__ __forceinline__ void row_store(__amdgpu_buffer_rsrc_t r, int voff, int soff, double x, double y) {
-  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, make_double2(x, y)), r, voff, soff,
-                                         RT_ROW_STORE_AUX);
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, make_double2(x, y)), r, voff, soff, kRowAuxNT);
 }
 
 // Reflective mu > 0 head cell (cell 0 of segment 0) with distinct per-substep

@@ -18,7 +18,7 @@ HEADER = REPO_ROOT / "include" / "rtsn.h"
 
 STATUS = {0: "ok", 1: "io error", 2: "parse error", 3: "invalid parameter", 4: "correction validation failed",
           5: "out of memory", 6: "device error", 7: "timeout (communicator aborted)", 8: "bad argument",
-          9: "not valid in the handle's mode", 10: "warning: explicit emission above its stability limit"}
+          9: "not valid in the handle's mode", 10: "warning (not returned since round 6)"}
 
 
 class RtError(RuntimeError):
@@ -122,6 +122,9 @@ def lib():
         L.rt_plan_schedule.argtypes = [vp, C.c_longlong, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int),
                                        dp]
         L.rt_set_segmentation.argtypes = [vp, C.c_int]
+        L.rt_set_moments_form.argtypes = [vp, C.c_int]
+        L.rt_set_phi_correction_form.argtypes = [vp, C.c_int]
+        L.rt_debug_fail_launch.argtypes = [vp, C.c_int]
         L.rt_get_level_waves.argtypes = [vp, C.POINTER(C.c_int)]
         L.rt_set_wavefront.argtypes = [vp, C.c_int]
         L.rt_get_wavefront.argtypes = [vp, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)]
@@ -133,6 +136,8 @@ def lib():
         L.rt_material_update.argtypes = [vp, vp]
         L.rt_material_step.argtypes = [vp, C.c_int]
         L.rt_material_stability.argtypes = [vp, dp]
+        L.rt_get_cell_emission.argtypes = [vp, dp]
+        L.rt_get_material_transit.argtypes = [vp, dp]
         L.rt_get_temperature.argtypes = [vp, dp]
         L.rt_get_cell_planck.argtypes = [vp, dp]
         L.rt_get_shard.argtypes = [vp] + [C.POINTER(C.c_int)] * 6
@@ -464,16 +469,14 @@ class Solver:
         T = None if T_cells is None else np.ascontiguousarray(T_cells, dtype=np.float64)
         if T is not None and T.size != self.N:
             raise ValueError("material_enable: T_cells must hold N values")
-        st = lib().rt_material_enable(self._h, float(rho_cv), None if T is None else _dp(T))
-        if st == 10:  # RT_WARN_UNSTABLE: coupling is on, above the explicit emission's limit
-            import warnings
-            warnings.warn(lib().rt_last_error(self._h).decode(errors="replace"), RuntimeWarning, stacklevel=2)
-        else:
-            _check(st, "rt_material_enable", self._h)
+        _check(lib().rt_material_enable(self._h, float(rho_cv), None if T is None else _dp(T)),
+               "rt_material_enable", self._h)
         return self.material_stability()
 
     def material_stability(self) -> float:
-        """dt W sum_g rho kappa_g dB_g/dT(T_max) / rho_cv: < 2 for a stable explicit emission."""
+        """dt W sum_g rho kappa_g dB_g/dT(T_max) / rho_cv: the emission's stiffness at the hottest
+        cell (the implicit update scales the explicit change by 1 / (1 + number); < 2 was the
+        explicit emission's limit)."""
         v = C.c_double()
         _check(lib().rt_material_stability(self._h, C.byref(v)), "rt_material_stability", self._h)
         return v.value
@@ -489,14 +492,15 @@ class Solver:
         return t.data_ptr()
 
     def material_sweep(self, q=None):
-        """One coupled full step; this handle's q (N) into the CUDA tensor q (None:
-        kept inside the handle), ordered on the handle's stream."""
-        _check(lib().rt_material_sweep(self._h, self._device_vec(q, self.N, "material_sweep")),
+        """One coupled full step; this handle's [q, b] (2N: q(x), then sum_g sigma_g dB_g/dT(x))
+        into the CUDA tensor q (None: kept inside the handle), ordered on the handle's stream."""
+        _check(lib().rt_material_sweep(self._h, self._device_vec(q, 2 * self.N, "material_sweep")),
                "rt_material_sweep", self._h)
 
     def material_update(self, q=None):
-        """T += dt q / rho_cv from the group-summed q (CUDA tensor, or None: the handle's own)."""
-        _check(lib().rt_material_update(self._h, self._device_vec(q, self.N, "material_update")),
+        """T += dt q / (rho_cv + dt W b), then the owed emission and the next step's emission,
+        from the group-summed [q, b] (CUDA tensor of 2N, or None: the handle's own)."""
+        _check(lib().rt_material_update(self._h, self._device_vec(q, 2 * self.N, "material_update")),
                "rt_material_update", self._h)
 
     def material_step(self, nsteps: int = 1):
@@ -508,10 +512,22 @@ class Solver:
         return out
 
     def cell_planck(self) -> np.ndarray:
-        """(G_local, N) per-cell emission B_g(T(x)) used by the next coupled step."""
+        """(G_local, N) per-cell B_g(T(x))."""
         out = np.empty(self.N * self.G)
         _check(lib().rt_get_cell_planck(self._h, _dp(out)), "rt_get_cell_planck", self._h)
         return out.reshape(self.N, self.G).T.copy()
+
+    def cell_emission(self) -> np.ndarray:
+        """(G_local, N) the next coupled step's emission B_g + the owed share it pays."""
+        out = np.empty(self.N * self.G)
+        _check(lib().rt_get_cell_emission(self._h, _dp(out)), "rt_get_cell_emission", self._h)
+        return out.reshape(self.N, self.G).T.copy()
+
+    def material_transit(self) -> np.ndarray:
+        """(N) energy per volume the material owes the radiation (rt_get_material_transit)."""
+        out = np.empty(self.N)
+        _check(lib().rt_get_material_transit(self._h, _dp(out)), "rt_get_material_transit", self._h)
+        return out
 
     # ---- measurement ----
     def set_profiling(self, on: bool):
@@ -605,6 +621,18 @@ class Solver:
         """rt_set_segmentation: segments sized for wgs_per_cu workgroups per CU (0: occupancy)."""
         _check(lib().rt_set_segmentation(self._h, int(wgs_per_cu)), "rt_set_segmentation", self._h)
 
+    def set_moments_form(self, form: int):
+        """rt_set_moments_form: 1 producer/consumer (default), 0 one-wave moments kernel."""
+        _check(lib().rt_set_moments_form(self._h, int(form)), "rt_set_moments_form", self._h)
+
+    def set_phi_correction_form(self, form: int):
+        """rt_set_phi_correction_form: 0 closed forms (default), 1 the cell-by-cell walk."""
+        _check(lib().rt_set_phi_correction_form(self._h, int(form)), "rt_set_phi_correction_form", self._h)
+
+    def debug_fail_launch(self, after: int):
+        """rt_debug_fail_launch: the pipelined sub-launch after `after` more fails (-1: off)."""
+        _check(lib().rt_debug_fail_launch(self._h, int(after)), "rt_debug_fail_launch", self._h)
+
     def pipeline_state(self) -> dict:
         """{"lag_steps", "queued_steps", "pending"} (rt_pipeline_state)."""
         lag, q, pend = C.c_longlong(), C.c_int(), C.c_int()
@@ -645,7 +673,10 @@ class Comm:
     broadcast_object_list or a file); Comm(nranks, rank, uid, device).  Every wait on the
     collective is bounded by RTSN_COMM_TIMEOUT_S seconds (default 300) from the moment the
     stream reaches it: a missing or stalled rank gives RtError status 7 (RT_ERR_TIMEOUT)
-    instead of a hang; the handle's own queued work is not clocked."""
+    instead of a hang; the handle's own queued work is not clocked.  allreduce_absorption and
+    material_step leave their all-reduces on the handle's stream: retire them with
+    synchronize() before any other host wait on the handle (Solver.temperature(),
+    Solver.synchronize(), a read-out), whose waits have no deadline."""
 
     def __init__(self, nranks: int, rank: int, uid: bytes, device: int = 0):
         assert len(uid) == 128

@@ -419,3 +419,59 @@ def test_spawn_ranks_fails_loudly(tmp_path, fail, status):
     t0 = time.time()
     assert bench.spawn_ranks(2, [fail], script=script, grace_s=5, straggle_s=10) == status
     assert time.time() - t0 < 120
+
+
+_BENCH_RANK_CHILD = r"""
+import json, os, sys
+sys.path[:0] = [{repo!r}, {tests!r}, {oracle!r}]
+import torch
+import torch.distributed as dist
+import bench
+from test_distributed import OracleShard, small_params
+r, n = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+fail = sys.argv[1] if len(sys.argv) > 1 else ""
+dist.init_process_group("gloo")
+if fail == "rank5" and r == 5:  # dies after the rendezvous: the others wait in the first barrier
+    sys.exit(5)
+groups = 128
+info = bench.shard("strong", groups, n, r)
+p = small_params(info[0])
+shards = [bench.shard("strong", groups, n, k)[1:] for k in range(n)]
+line, _, gathered = bench.run_rank(OracleShard(p, info[1], info[2]), p, 2, 1, n, torch.device("cpu"), info,
+                                   "strong", shards)
+line["shards"] = shards
+line["gathered_groups"] = int(gathered["phi"].shape[1])
+if r == 0:
+    print(json.dumps(line), flush=True)
+dist.destroy_process_group()
+"""
+
+
+def test_spawn_ranks_eight_rank_rehearsal(tmp_path, capsys):
+    """VERDICT r05 #2a: the driver's SCALE shape on CPU -- bench.spawn_ranks(8, ...) starts eight
+    rank processes (fresh interpreters, gloo), each runs bench.run_rank on its 16-group shard of
+    the 128-group slab (a tiny slab: N = 48, S8, the oracle stand-in), and rank 0's line says
+    n_gpus 8 with eight per_rank entries, the shard table [0, 16), [16, 32), ..., [112, 128),
+    and the end-of-run gather holding all 128 groups."""
+    script = tmp_path / "bench_rank.py"
+    script.write_text(_BENCH_RANK_CHILD.format(repo=str(REPO), tests=str(REPO / "tests"), oracle=str(REPO / "oracle")))
+    assert bench.spawn_ranks(8, [], script=script) == 0
+    out = capsys.readouterr().out
+    d = json.loads([l for l in out.splitlines() if l.startswith("{")][-1])
+    assert d["n_gpus"] == 8 and len(d["per_rank"]) == 8
+    assert [e["rank"] for e in d["per_rank"]] == list(range(8))
+    assert d["shards"] == [[16 * k, 16 * k + 16] for k in range(8)]
+    assert d["config"]["groups_per_gpu"] == 16 and d["config"]["groups_total"] == 128
+    assert d["gathered_groups"] == 128
+    assert d["value"] > 0 and d["state_finite"]
+
+
+def test_spawn_ranks_eight_ranks_failing_rank_stops_all(tmp_path):
+    """... and rank 5 dying after the rendezvous stops the other seven (blocked in the first
+    barrier): a non-zero job status -- rank 5's 5, or the status of a peer whose gloo
+    connection to it broke in the same poll interval -- well inside the grace period."""
+    script = tmp_path / "bench_rank.py"
+    script.write_text(_BENCH_RANK_CHILD.format(repo=str(REPO), tests=str(REPO / "tests"), oracle=str(REPO / "oracle")))
+    t0 = time.time()
+    assert bench.spawn_ranks(8, ["rank5"], script=script, grace_s=5, straggle_s=30) != 0
+    assert time.time() - t0 < 120

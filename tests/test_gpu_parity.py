@@ -709,6 +709,110 @@ def test_full_size_sl_properties(rtsn_mod, shard_tb):
     assert err <= 1e-12, err
 
 
+def test_full_size_sl_oracle_groups(rtsn_mod):
+    """The driver's exact workload checked against values (verdict r05, item 1): ONE handle
+    of the SL slab at its full size -- N = 1e6 cells x S64 x 128 groups, 131 GB of state, the
+    half and line-group row offsets far past 2^31 bytes -- run pipelined at T = 20 with the
+    default level split (sweep_split_kernel<3,20,2> and its fill / drain launches) for
+    T + 2 = 22 BDF2 steps (fill and drain over every segment position, then the 2-step
+    remainder), dt = 1e-7 (Courant number 64: the upwind carry crosses segment after
+    segment).  phi, F and phi_plus (rt_get_moments_device), the group ends and the balance
+    of groups 0, 63 and 127 -- the lowest and highest line rows of each half and the
+    middle -- against one-group oracle runs of those groups (solver.cpp:590-823 restated,
+    rt_oracle.c), which run on the host's CPU share while the GPU works.  Tolerance 1e-10:
+    phi and phi_plus per group against the group's max; F against its summands' scale
+    (parity.flux_rel); the group ends (sums of the M/2 lines' exit nodes) against the sum of
+    those lines' magnitudes, max |ends| per line -- at dt = 1e-7 the reference's BDF2 grows a
+    steep line's interior to ~1e15 x its inflow while its exit node stays ~B, so the exit node
+    carries the rounding of the line's magnitude in both codes (profiles/r06c_ends_probe.json:
+    group 0, exit nodes 1e-2 apart relative to themselves, 2e-17 relative to their line's
+    max; the 1-group and 128-group handles' ends bitwise equal); the balance against its
+    terms' magnitudes (sum |rho kappa phi dx| + the boundary currents: the grown modes
+    alternate in sign, so sum rho kappa phi dx cancels to rounding in both codes)."""
+    import sys
+    import time
+    from concurrent.futures import ThreadPoolExecutor
+
+    import torch
+    sys.path.insert(0, str(REPO))
+    import bench
+    import oracle
+
+    p = bench.slab_params(128, "v0")
+    p["dt"] = 1e-7
+    steps, tb, groups = 22, 20, (0, 63, 127)
+    q = dict(p, bc_left=0, bc_right=0, dx=p["X"] / p["N"], have_group_bounds=0, have_group_kappa=1, prm_found=1,
+             max_timesteps=steps)
+    threads = max(1, bench.host_cpus()["threads"] // len(groups))
+
+    def orc_run(g):
+        t0 = time.perf_counter()
+        o = oracle.OracleSolver(q, g_lo=g, g_hi=g + 1)
+        o.set_threads(threads)
+        o.solve()
+        mu, wt = o.quad()
+        gr = o.groups()
+        ends = o.ends()  # (M, 1, N, 2)
+        mom = o.moments()
+        den = gr["de_ave"][g] * 299.792458
+        out = {"psi": o.psi(), "moments": mom, "group_ends": o.group_ends(), "balance": o.balance(),
+               "mu": mu, "wt": wt, "s": time.perf_counter() - t0,
+               # the magnitudes the cancelling sums are made of (solver.cpp:240-284, 826-850)
+               "left_abs": float(np.abs(ends[mu < 0, 0]).max(axis=(1, 2)).sum() / den),
+               "right_abs": float(np.abs(ends[mu > 0, 0]).max(axis=(1, 2)).sum() / den),
+               "absorption_abs": float(q["rho"] * gr["kappa"][g] * q["dx"] * np.abs(mom[0]).sum()),
+               "currents_abs": float(np.abs(ends[:, 0, [0, -1], :] * (mu * wt)[:, None, None]).sum())}
+        del ends
+        del o
+        return out
+
+    pool = ThreadPoolExecutor(len(groups))
+    futs = {g: pool.submit(orc_run, g) for g in groups}
+    N = p["N"]
+    t0 = time.perf_counter()
+    with rtsn_mod.Solver(p) as s:
+        assert s.G == 128 and s.M == 64 and s.N == N
+        s.pipeline = 2
+        s.time_block = tb
+        assert s.level_waves == 2
+        _, segs = s.sweep_geometry()
+        s.advance(steps)
+        s.finish()
+        mom = [torch.empty(N * s.G, dtype=torch.float64, device="cuda") for _ in range(3)]
+        s.moments_device(*mom)
+        s.synchronize()
+        assert s.state_finite()
+        gpu_mom = [t.view(N, s.G)[:, list(groups)].T.cpu().numpy() for t in mom]  # (3 groups, N) each
+        del mom
+        l_g, r_g = s.compute_group_ends()
+        bal_g, src_g, snk_g = s.compute_balance_terms()
+    gpu_s = time.perf_counter() - t0
+    pool.shutdown(wait=True)
+    errs = {}
+    for k, g in enumerate(groups):
+        ref = futs[g].result()
+        phi_o, F_o, pp_o = ref["moments"]
+        phi_g, F_g, pp_g = (m[k:k + 1] for m in gpu_mom)
+        e = {"phi": per_group_rel(phi_g, phi_o, 0),
+             "F": flux_rel(F_g, F_o, ref["psi"], ref["mu"], ref["wt"]),
+             "phi_plus": per_group_rel(pp_g, pp_o, 0)}
+        l_o, r_o = ref["group_ends"]
+        e["left_ends"] = float(abs(l_g[g] - l_o[0]) / ref["left_abs"])
+        e["right_ends"] = float(abs(r_g[g] - r_o[0]) / ref["right_abs"])
+        e["left_ends_own"] = float(abs(l_g[g] - l_o[0]) / abs(l_o[0]))
+        e["right_ends_own"] = float(abs(r_g[g] - r_o[0]) / abs(r_o[0]))
+        # balance = |sinks - sources| / sources: its error against its terms' magnitudes
+        bscale = (ref["absorption_abs"] + ref["currents_abs"] + abs(src_g[g])) / abs(src_g[g])
+        e["balance"] = float(abs(bal_g[g] - ref["balance"][0]) / bscale)
+        e["balance_own"] = float(abs(bal_g[g] - ref["balance"][0]) / abs(ref["balance"][0]))
+        e["oracle_s"] = ref["s"]
+        errs[g] = e
+    print(f"full-size SL vs oracle: segments {segs}, GPU {gpu_s:.1f} s, oracle threads {threads}: {errs}")
+    for g, e in errs.items():
+        for k in ("phi", "F", "phi_plus", "left_ends", "right_ends", "balance"):
+            assert e[k] <= TOL, (g, k, e)
+
+
 # The timed kernels with several 64-line groups per half (verdict r02, item 1): the
 # workgroup -> (half, segment, line group q) decode of sweep_split_kernel (kernels_split.hip
 # split_role: ell = q * 64 + lane) and sweep_block_kernel, reflective (one chain of 2 Sg

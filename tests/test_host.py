@@ -33,6 +33,27 @@ def test_library_is_gfx950_code(rtsn_mod):
         assert other + b"\x00" not in blob or other == b"sm_"
 
 
+def test_getenv_only_documented():
+    """the shipped library and executables read only the environment
+    variables include/rtsn.h documents (kernel forms and segmentation are ABI setters), and
+    no build-time tuning macro has a branch the tested build does not compile (no
+    #ifndef RT_... overrides, no #if on one)."""
+    import re
+    src = REPO / "radiative-transfer_amd" / "csrc"
+    allowed = {"TRANSFER_DIR", "RT_TABLE_DIR", "RTSN_QUIET", "RTSN_COMM_TIMEOUT_S", "RTSN_POOL_MB",
+               "RTSN_EXPORT_CHUNK", "RTSN_DEVICE_BASE", "RTSN_FAULT_STALL_RANK", "RTSN_RANKS"}
+    read, knobs = set(), []
+    for f in sorted(src.iterdir()):
+        text = f.read_text()
+        read |= set(re.findall(r'getenv\("([A-Z_0-9]+)"\)', text))
+        knobs += [f"{f.name}: {m}" for m in re.findall(r"#\s*(?:ifndef|ifdef|if)\s+(RT_\w+)", text)]
+    assert read <= allowed, read - allowed
+    header = (REPO / "include" / "rtsn.h").read_text()
+    for name in read:
+        assert name in header, name
+    assert not knobs, knobs
+
+
 def _params_equal(ph, ref):
     for k in ("M", "G", "N", "efirst", "elast", "X", "rho", "kappa_grey", "T", "V", "dt", "max_timesteps"):
         assert ph.params[k] == ref[k], k

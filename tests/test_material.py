@@ -2,10 +2,17 @@
 
 The reference holds T constant (solver.cpp:157); SURVEY §8(f)-4 names the
 T(x) update fed by the group-sum all-reduce as the next row.  Its definition
- is restated in the oracle (rt_oracle.c orc_material_*), which
+(the emission linearised implicit in T, include/rtsn.h
+"material") is restated in the oracle (rt_oracle.c orc_material_*), which
 these tests pin by properties the definition guarantees -- there is no
 reference output to pin it against ("parity unpinned" beyond these
 properties):
+  * the per-cell dB_g/dT is the derivative of the per-cell B_g (central
+    differences) and, at a uniform T, the reference's dBdT table
+    (Planck.cpp:161-229);
+  * the coupling stays finite, positive and conservative at emission
+    stiffness up to ~1e8 (50 keV, thin and thick cells), where the explicit
+    emission of rounds 1-5 diverged;
   * the per-cell Planck emission at a uniform T is the reference's group
     table (Planck.cpp:44-77) -- bitwise for every group but the last, whose
     remainder takes the other groups as one integral;
@@ -48,9 +55,10 @@ def t_profile(N, lo=0.7, hi=1.3):
 
 
 def total_energy(s, p, rho_cv):
-    """sum_x dx (sum_g phi_g / c + rho_cv T) over the solver's groups and T."""
+    """sum_x dx (sum_g phi_g / c + rho_cv T + the emission in transit) over the solver's
+    groups and T (the transit: dt W b dT of the last update, owed to the next sweep)."""
     phi, _, _ = s.moments()
-    return p["dx"] * float((phi.sum(axis=0) / C_LIGHT + rho_cv * s.temperature()).sum())
+    return p["dx"] * float((phi.sum(axis=0) / C_LIGHT + rho_cv * s.temperature() + s.material_transit()).sum())
 
 
 def net_outflow(s, p):
@@ -84,6 +92,58 @@ def test_cell_planck_uniform_equals_group_table(oracle_mod):
         assert abs(B[-1, 0] - table["B"][-1]) <= 1e-14 * acT4
         for g in (0, 5, 11):
             assert oracle_mod.planck_cell(T, e, g) == B[g, 0]
+
+
+def test_cell_dbdt_is_derivative_of_cell_planck(oracle_mod):
+    """kcon dB_g/dT per cell (orc_planck_cell_dBdT: Planck::integrate_dBdT, the last group the
+    remainder 4 a c T^3 - the joint integral) against central differences of planck_cell, on
+    every branch of the integral (Gauss z2 <= 0.7, series z1 >= 0.5, split), and at a
+    uniform T the reference's dBdT table (Planck.cpp:161-229) bitwise but the last group."""
+    e = np.array([0.0, 0.01, 0.1, 0.5, 1.0, 3.0, 10.0, 30.0])
+    G = len(e) - 1
+    for T in (0.05, 0.4, 1.0, 7.0, 50.0):
+        h = T * 1e-5
+        for g in range(G):
+            d = oracle_mod.planck_cell_dBdT(T, e, g)
+            fd = (oracle_mod.planck_cell(T + h, e, g) - oracle_mod.planck_cell(T - h, e, g)) / (2 * h)
+            # the last group's remainder cancels against the grey total 4 a c T^3, and so does
+            # its difference quotient (rounding of B_total / h): an absolute term of that scale
+            grey = oracle_mod.planck_cell_dBdT(T, np.array([0.0, 30.0]), 0)
+            assert abs(d - fd) <= 1e-6 * abs(fd) + 1e-9 * grey, (T, g, d, fd, grey)
+    p = params(oracle_mod, G=12, efirst=0.01, elast=30.0)
+    s = oracle_mod.OracleSolver(p)
+    table = s.groups()
+    kcon = table["B"][0] / oracle_mod.planck_groups(1.0, table["e_edge"][:-1], table["e_edge"][1:])[0][0]
+    for g in range(11):
+        assert oracle_mod.planck_cell_dBdT(1.0, table["e_edge"], g) == table["dBdT"][g]
+    for T in (0.0, -1.0, float("nan")):
+        assert oracle_mod.planck_cell_dBdT(T, e, 3) == 0.0
+    assert kcon > 0
+
+
+@pytest.mark.parametrize("kappa", [0.1, 10.0, 1e3])
+@pytest.mark.parametrize("T_rad,T_mat", [(50.0, 55.0), (5.0, 5.5), (1.0, 50.0)])
+def test_stiff_emission_stays_stable(oracle_mod, kappa, T_rad, T_mat):
+    """Material at T_mat against radiation at B(T_rad), BE, vacuum boundaries, rho_cv = 1,
+    dt = 1e-3: emission stiffness dt W sum sigma dB/dT / rho_cv from ~1e-1 to ~1e8 -- the
+    explicit emission of rounds 1-5 diverged from ~2 on.  50 steps: T finite and > 0 in
+    every cell, the emission Beff >= 0, and radiation + material + owed energy balance the
+    boundary outflow to rounding every step."""
+    p = params(oracle_mod, ts=1, G=6, N=40, bc_left=0, bc_right=0, kappa=kappa, dt=1e-3, T=T_rad, efirst=0.1,
+               elast=100.0)
+    p["psi_source"] = np.zeros((p["M"], p["G"]))
+    s = oracle_mod.OracleSolver(p)
+    rho_cv = 1.0
+    s.material_enable(rho_cv, T_mat * (1.0 + 0.1 * np.sin(2 * np.pi * (np.arange(p["N"]) + 0.5) / p["N"])))
+    for n in range(50):
+        e0 = total_energy(s, p, rho_cv)
+        s.material_step(1)
+        e1 = total_energy(s, p, rho_cv)
+        T = s.temperature()
+        assert np.isfinite(T).all() and np.all(T > 0.0), (n, T.min(), T.max())
+        assert np.all(s.cell_emission() >= 0.0), n
+        resid = (e1 - e0) + p["dt"] * net_outflow(s, p)
+        assert abs(resid) <= 1e-12 * max(abs(e0), abs(e1)), (n, resid, e0)
 
 
 def test_cell_planck_edge_temperatures(oracle_mod):
@@ -156,7 +216,7 @@ def test_group_shards_sum_q(oracle_mod):
         s.material_enable(4.0, T0)
     for _ in range(8):
         full.material_step(1)
-        q = sum(s.material_sweep() for s in parts)
+        q = sum(s.material_sweep() for s in parts)  # [q, b]: one sum of 2N values
         for s in parts:
             s.material_update(q)
     for s in parts:
@@ -203,7 +263,7 @@ def _worker(rank, world, port, outdir):
         lo, hi = ((0, 3), (3, 6))[rank]
         s = oracle.OracleSolver(p, g_lo=lo, g_hi=hi)
         s.material_enable(4.0, t_profile(p["N"]))
-        q = torch.zeros(p["N"], dtype=torch.float64)
+        q = torch.zeros(2 * p["N"], dtype=torch.float64)
         coupled_steps(OracleMaterialShard(s), 6, q, world_size=world)
         np.save(os.path.join(outdir, f"T{rank}.npy"), s.temperature())
         np.save(os.path.join(outdir, f"psi{rank}.npy"), s.psi())

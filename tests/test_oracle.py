@@ -149,19 +149,24 @@ def test_group_subset_is_independent(oracle_mod):
 
 
 def test_threaded_oracle_bitwise(oracle_mod):
-    """orc_set_threads (the multi-core CPU baseline) does not change any bit."""
+    """orc_set_threads (the multi-core CPU baseline, and the one-group oracle runs of the
+    full-size GPU check: lines of a run of same-sign directions over the threads) does not
+    change any bit, reflective left BC included."""
     p = oracle_mod.parse_prm(PRM_DIR / "llnl_slab_test.prm", table_dir=PRM_DIR)
     p.update(M=8, N=200, V=5.994, bc_left=2, max_timesteps=3)
     p["psi_source"] = np.ones((8, p["G"]))
     p["dx"] = p["X"] / p["N"]
-    outs = []
-    for threads in (1, 4):
-        s = oracle_mod.OracleSolver(p)
-        s.set_threads(threads)
-        s.solve()
-        outs.append((s.ends(), s.psi()))
-    np.testing.assert_array_equal(outs[0][0], outs[1][0])
-    np.testing.assert_array_equal(outs[0][1], outs[1][1])
+    for g_lo, g_hi in ((0, 0), (63, 64)):
+        outs = []
+        for threads in (1, 4):
+            s = oracle_mod.OracleSolver(p, g_lo=g_lo, g_hi=g_hi)
+            s.set_threads(threads)
+            s.solve()
+            outs.append((s.ends(), s.psi(), s.moments()))
+        np.testing.assert_array_equal(outs[0][0], outs[1][0])
+        np.testing.assert_array_equal(outs[0][1], outs[1][1])
+        for a, b in zip(outs[0][2], outs[1][2]):
+            np.testing.assert_array_equal(a, b)
 
 
 def test_equilibrium_known_answer(oracle_mod):

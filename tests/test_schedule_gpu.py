@@ -154,8 +154,8 @@ def test_solve_remainder_tail(rtsn_mod, oracle_mod):
 
 @pytest.mark.parametrize("M,G,N", [(64, 128, 300), (64, 100, 257), (32, 70, 129), (16, 64, 64), (16, 3, 50),
                                    (64, 1, 17), (12, 40, 33)])
-def test_moments_producer_consumer_bitwise(rtsn_mod, oracle_mod, monkeypatch, M, G, N):
-    """The moments forms (RTSN_MOMENTS_FORM): the producer/consumer moments_pc_kernel (the
+def test_moments_producer_consumer_bitwise(rtsn_mod, oracle_mod, M, G, N):
+    """The moments forms (rt_set_moments_form): the producer/consumer moments_pc_kernel (the
     default) and the one-wave moments_kernel, where H = M/2 is 8, 16 or 32, are bitwise equal
     on a random state -- whole and partial 64-group
     chunks, fewer items than workgroups -- and match the oracle's sums of the same state
@@ -168,10 +168,14 @@ def test_moments_producer_consumer_bitwise(rtsn_mod, oracle_mod, monkeypatch, M,
     ends = rng.uniform(-1.0, 2.0, size=(M, G, N, 2))
     out = []
     with rtsn_mod.Solver(to_rt(p)) as gpu:
-        for form in ("0", "1"):
-            monkeypatch.setenv("RTSN_MOMENTS_FORM", form)
-            gpu.set_ends(ends)  # a new state version: the moments are recomputed
+        for form in (0, 1):
+            gpu.set_moments_form(form)
+            gpu.set_ends(ends)
             out.append(gpu.moments())
+        gpu.set_moments_form(0)  # the setter drops the cached moments of the same state
+        assert all(np.array_equal(a, b) for a, b in zip(gpu.moments(), out[0]))
+        with pytest.raises(rtsn_mod.RtError):
+            gpu.set_moments_form(2)
     for o in out[1:]:
         for a, b in zip(out[0], o):
             assert np.array_equal(a, b)
@@ -182,50 +186,106 @@ def test_moments_producer_consumer_bitwise(rtsn_mod, oracle_mod, monkeypatch, M,
         assert (np.abs(a - b) / scale).max() <= 1e-13
 
 
-def test_ramp_launches_cut_into_rounds(rtsn_mod, oracle_mod):
+@pytest.mark.parametrize("bc_left", [0, 2])
+def test_ramp_launches_cut_into_rounds(rtsn_mod, oracle_mod, bc_left):
     """Ramp launches of more positions than one round of four-wave workgroups holds (128 groups
-    x S64: 128 workgroups per position, 4 positions per round on 256 CUs) run as consecutive
-    launches of at most a round's positions (ramp_chunk); positions never exchange data
-    within a launch, so the node array equals the one-launch ramps' (level_waves 4, and 2)
-    bitwise, through the fill and the drain of 10 passes over 16 positions."""
+    x S64: 128 workgroups per position, 4 positions per round on 256 CUs; reflective chains of
+    2 Sg positions with 64 workgroups each, 8 per round) run as consecutive launches of at most
+    a round's positions (ramp_chunk); positions never exchange data within a launch, so the
+    node array equals the one-launch ramps' (level_waves 4, and 2) bitwise, through the fill
+    and the drain of 10 passes -- and the default really cut its ramps: more sub-launches
+    (profiled event pairs) than the P + C - 1 launches of the one-launch ramps."""
     import sys
     from conftest import REPO
     sys.path.insert(0, str(REPO))
     import bench
-    p = dict(bench.slab_params(128, "v0", N=2000, M=64), dt=1e-9)
-    rng = np.random.default_rng(5)
-    out = {}
+    p = dict(bench.slab_params(128, "v0", N=2000, M=64), dt=1e-9, bc_left_indicator=bc_left)
+    rng = np.random.default_rng(5 + bc_left)
+    out, launches = {}, {}
     for lw in (0, 4, 2):
         with rtsn_mod.Solver(p) as s:
             s.time_block = 20
             s.pipeline = 2
             s.set_segmentation(8)
             s.level_waves = lw
-            assert s.sweep_geometry()[1] >= 10
+            C = s.sweep_geometry()[1] * (2 if bc_left == 2 else 1)
+            assert C >= 10
             if lw == 0:
                 ends = rng.uniform(0.5, 1.5, size=(64, 128, 2000, 2)) * 1e-3
             s.set_ends(ends)
+            s.set_profiling(True)
             s.advance(200)
+            s.finish()
+            launches[lw] = s.sweep_time()[1]
             out[lw] = s.ends()
     assert np.isfinite(out[0]).all()
     assert np.array_equal(out[0], out[4]) and np.array_equal(out[0], out[2])
+    assert launches[4] == launches[2] == 10 + C - 1, launches
+    assert launches[0] > launches[4], launches
+
+
+@pytest.mark.parametrize("bc_left", [0, 2])
+def test_failed_sub_launch_resumes_exactly(rtsn_mod, bc_left):
+    """a ramp launch cut into sub-launches commits each sub-launch's
+    positions as it enters the stream, so a failure part-way (rt_debug_fail_launch: a
+    sub-launch that returns RT_ERR_DEVICE without running) leaves the handle owing exactly the
+    positions not yet launched; the next call runs those and the run ends bitwise equal to an
+    undisturbed one.  Failures at the first sub-launch, at the second chunk of the first cut
+    ramp launch (vacuum: k = 5 of chunks 4 + 1 is sub-launch 5; reflective: k = 9 of 8 + 1 is
+    sub-launch 9) and later in the fill and the drain."""
+    import sys
+    from conftest import REPO
+    sys.path.insert(0, str(REPO))
+    import bench
+    p = dict(bench.slab_params(128, "v0", N=2000, M=64), dt=1e-9, bc_left_indicator=bc_left)
+    ends = np.random.default_rng(11 + bc_left).uniform(0.5, 1.5, size=(64, 128, 2000, 2)) * 1e-3
+
+    def run(fail_after):
+        with rtsn_mod.Solver(p) as s:
+            s.time_block = 20
+            s.pipeline = 2
+            s.set_segmentation(8)
+            s.set_ends(ends)
+            s.set_profiling(True)  # counts the sub-launches that ran
+            if fail_after is not None:
+                s.debug_fail_launch(fail_after)
+                with pytest.raises(rtsn_mod.RtError) as e:
+                    s.advance(200)
+                    s.finish()
+                assert e.value.status == 6 and "pipelined launch" in str(e.value)
+            else:
+                s.advance(200)
+            s.finish()  # resumes the interrupted launch, then drains
+            assert s.pipeline_state()["lag_steps"] == 0
+            return s.ends(), s.sweep_time()[1]
+
+    want, total = run(None)
+    first_cut = 5 if bc_left == 0 else 9
+    assert total > first_cut + 2
+    for after in (0, first_cut, total // 2, total - 1):
+        got, n = run(after)
+        assert n == total, (after, n, total)  # every sub-launch ran once: none repeated, none lost
+        assert np.array_equal(got, want), after
 
 
 def test_experiment_env_ignored(rtsn_mod, oracle_mod, monkeypatch):
-    """the round-3/4 experiment variables no longer change a handle's schedule
-    (rt_set_* are the only way): created with RTSN_TIME_BLOCK=4, RTSN_WAVEFRONT=0,
-    RTSN_WAVE_WAVES=1 and RTSN_LEVEL_WAVES=4 in the environment, a handle reports the same
-    time block, wavefront state and waves per segment as one created without them."""
+    """the experiment variables of rounds 3-5 no longer change a
+    handle's schedule (rt_set_* are the only way): created with RTSN_TIME_BLOCK=4,
+    RTSN_WAVEFRONT=0, RTSN_WAVE_WAVES=1, RTSN_LEVEL_WAVES=4, RTSN_WAVES_PER_CU=1,
+    RTSN_MOMENTS_FORM=0 and RTSN_PHI_WALK=1 in the environment, a handle reports the same
+    time block, wavefront state, waves per segment and segments as one created without them
+    (the library's getenv calls are listed in test_host.test_getenv_only_documented)."""
     p = _params(oracle_mod, 5000, 10)
     with rtsn_mod.Solver(to_rt(p)) as s:
-        want = (s.time_block, s.level_waves, s.wavefront_state())
+        want = (s.time_block, s.level_waves, s.wavefront_state(), s.sweep_geometry())
     q = _params(oracle_mod, 300, 10)
     with rtsn_mod.Solver(to_rt(q)) as s:
         want_w = s.wavefront_state()
-    for k, v in (("RTSN_TIME_BLOCK", "4"), ("RTSN_WAVEFRONT", "0"), ("RTSN_WAVE_WAVES", "1"), ("RTSN_LEVEL_WAVES", "4")):
+    for k, v in (("RTSN_TIME_BLOCK", "4"), ("RTSN_WAVEFRONT", "0"), ("RTSN_WAVE_WAVES", "1"), ("RTSN_LEVEL_WAVES", "4"),
+                 ("RTSN_WAVES_PER_CU", "1"), ("RTSN_MOMENTS_FORM", "0"), ("RTSN_PHI_WALK", "1")):
         monkeypatch.setenv(k, v)
     with rtsn_mod.Solver(to_rt(p)) as s:
-        assert (s.time_block, s.level_waves, s.wavefront_state()) == want
+        assert (s.time_block, s.level_waves, s.wavefront_state(), s.sweep_geometry()) == want
     with rtsn_mod.Solver(to_rt(q)) as s:
         assert s.wavefront_state() == want_w and want_w["active"]
 
