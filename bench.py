@@ -787,7 +787,7 @@ def run_material(p: dict, info, world: int, device, local: int, steps: int, dirs
         dist.all_reduce(u)
     upd = float(u[0])
     return {"what": "material-temperature coupling (beyond the reference): BE step with the per-cell Planck "
-                    "emission linearised implicit in T, [q, b] all-reduce over ranks, T update",
+                    "emission, [q, b] all-reduce over ranks, T update implicit in the material's emission (the implied emission owed to the next sweeps)",
             "T0_keV": float(T0_keV if T0_keV is not None else q["T"]),
             "ts_method": 1, "steps": steps, "warmup": 1, "ms_per_step": 1e3 * wall / steps,
             "updates_per_s": upd / wall, "allreduce_bytes_per_step": 16 * q["N"], "allreduce": path,

@@ -222,6 +222,7 @@ struct rt_solver {
   // every launch that writes E bumps state_version; the moments kernel's phi, F, phi_plus
   // in `mom` are reused by every read-out (moments, balance, absorption) of the same state
   unsigned long long state_version = 1, mom_version = 0;
+  unsigned long long mom_serial = 0;  // moments kernel launches; mom_host holds launch mom_host_serial's
   // pipelined schedule (rt_set_pipeline): chain positions (segments; half 0 then
   // half 1 when the left boundary is reflective) at staggered time levels
   int pipe = 1;                  // 0 off, 1 auto (runs long enough to fill), 2 always
@@ -263,6 +264,12 @@ struct rt_solver {
   void *staging[2] = {nullptr, nullptr};
   size_t staging_bytes = 0, staging_cap[2] = {0, 0};
   hipEvent_t staging_ev[2] = {nullptr, nullptr};
+  // pinned host copy of `mom` ([3][GN], when it fits one staged piece): every moments read-out
+  // of one state after the first is a host copy (a D2H after the rows' small copies stalled
+  // the first phi_plus read-out of a process ~8 ms, r06j)
+  void *mom_host = nullptr;
+  size_t mom_host_cap = 0;
+  unsigned long long mom_host_serial = 0;
   // host -> device uploads of the per-line setup (upload()): a pinned arena the copies leave
   // from asynchronously; reused from its start after a stream synchronisation
   void *up_arena = nullptr;
@@ -275,6 +282,7 @@ struct rt_solver {
     if (stream) (void)hipStreamSynchronize(stream);  // no kernel may outlive the buffers it uses
     rtsn_detail::ResourcePool &pool = rtsn_detail::ResourcePool::get();
     for (int k = 0; k < 2; ++k) pool.release(true, staging[k], staging_cap[k], 0);
+    pool.release(true, mom_host, mom_host_cap, 0);
     pool.release(true, up_arena, up_cap, 0);
     for (hipEvent_t e : staging_ev) pool.release_event(e, false, device);
     for (hipEvent_t e : ev_pool) pool.release_event(e, true, device);

@@ -208,6 +208,7 @@ rt_status rtsn_detail::compute_moments(rt_solver *s) {
   HIP_TRY(s, launch_moments(static_cast<const double2 *>(s->E.p), muwt, muwt + s->p.M, m, m + GN, m + 2 * GN, g,
                             s->moments_form, s->stream));
   s->mom_version = s->state_version;
+  ++s->mom_serial;
   return RT_OK;
 }
 
@@ -219,13 +220,21 @@ extern "C" rt_status rt_get_moments(rt_solver *s, double *phi, double *F, double
   const size_t GN = static_cast<size_t>(s->Gl) * s->p.N;
   const double *m = static_cast<const double *>(s->mom.p);
   double *dst[3] = {phi, F, phi_plus};
-  if (3 * GN <= kStagedPiece) {  // the three fields ([3][GN] in `mom`) in one transfer and one wait
-    if (rt_status st2 = ensure_staging(s, sizeof(double) * 3 * GN)) return st2;
-    HIP_TRY(s, hipMemcpyAsync(s->staging[0], m, sizeof(double) * 3 * GN, hipMemcpyDeviceToHost, s->stream));
-    HIP_TRY(s, hipEventRecord(s->staging_ev[0], s->stream));
-    HIP_TRY(s, hipEventSynchronize(s->staging_ev[0]));
+  if (3 * GN <= kStagedPiece) {  // the three fields ([3][GN] in `mom`) in one transfer, once per state
+    if (s->mom_host_serial != s->mom_serial) {
+      if (s->mom_host_cap < sizeof(double) * 3 * GN) {
+        ResourcePool::get().release(true, s->mom_host, s->mom_host_cap, 0);
+        s->mom_host = nullptr;
+        s->mom_host_cap = 0;
+        HIP_TRY(s, ResourcePool::get().alloc(true, sizeof(double) * 3 * GN, &s->mom_host, &s->mom_host_cap));
+      }
+      HIP_TRY(s, hipMemcpyAsync(s->mom_host, m, sizeof(double) * 3 * GN, hipMemcpyDeviceToHost, s->stream));
+      HIP_TRY(s, hipEventRecord(s->staging_ev[0], s->stream));
+      HIP_TRY(s, hipEventSynchronize(s->staging_ev[0]));
+      s->mom_host_serial = s->mom_serial;
+    }
     for (int k = 0; k < 3; ++k)
-      if (dst[k]) std::memcpy(dst[k], static_cast<const double *>(s->staging[0]) + k * GN, sizeof(double) * GN);
+      if (dst[k]) std::memcpy(dst[k], static_cast<const double *>(s->mom_host) + k * GN, sizeof(double) * GN);
     return RT_OK;
   }
   for (int k = 0; k < 3; ++k)
@@ -248,15 +257,15 @@ extern "C" rt_status rt_get_moments_device(rt_solver *s, double *d_phi, double *
 }
 
 // boundary rows: [0] half0 k=0, [1] half0 k=N-1, [2] half1 k=0, [3] half1 k=N-1
+// (through the pinned staging pair: a copy into pageable memory makes the runtime pin a
+// staging buffer of its own, ~18 ms on the first read-out of a process, r06g)
 static rt_status fetch_rows(rt_solver *s, std::vector<double> &rows) {
   if (rt_status st = finalize(s)) return st;
   const Geometry g = geometry(s);
   rows.resize(static_cast<size_t>(8) * s->Lpad);
   HIP_TRY(s, launch_boundary_rows(static_cast<const double2 *>(s->E.p), static_cast<double2 *>(s->rows.p), g,
                                   s->stream));
-  HIP_TRY(s, hipMemcpyAsync(rows.data(), s->rows.p, sizeof(double) * rows.size(), hipMemcpyDeviceToHost, s->stream));
-  HIP_TRY(s, hipStreamSynchronize(s->stream));
-  return RT_OK;
+  return staged_d2h(s, rows.data(), static_cast<const double *>(s->rows.p), rows.size());
 }
 
 // physical ends(i, g, c, node) for c in {0, N-1} from the boundary rows

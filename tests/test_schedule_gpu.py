@@ -186,6 +186,42 @@ def test_moments_producer_consumer_bitwise(rtsn_mod, oracle_mod, M, G, N):
         assert (np.abs(a - b) / scale).max() <= 1e-13
 
 
+def test_moments_host_copy_follows_state(rtsn_mod, oracle_mod):
+    """The pinned host copy of the moments (one transfer per state, every later read-out of
+    the same state a host copy): read-outs interleaved with balance and group ends (their
+    own small transfers), then an advance, a new ends state and a moments-form switch -- the
+    moments always those of the current state (oracle; the device read-out bitwise)."""
+    import torch
+    p = _params(oracle_mod, 600, 12, G=4)
+    with rtsn_mod.Solver(to_rt(p)) as gpu:
+        for done, step in ((5, 5), (12, 7)):
+            gpu.advance(step)
+            orc = _oracle(oracle_mod, dict(p, max_timesteps=done))
+            first = gpu.moments()
+            gpu.compute_balance()
+            gpu.compute_group_ends()
+            again = gpu.moments()
+            assert all(np.array_equal(a, b) for a, b in zip(first, again))
+            for a, b in zip(again, orc.moments()):
+                scale = np.maximum(np.abs(b).max(axis=1, keepdims=True), 1e-300)
+                assert (np.abs(a - b) / scale).max() <= 1e-10
+            dev = [torch.empty(gpu.G * gpu.N, dtype=torch.float64, device="cuda") for _ in range(3)]
+            gpu.moments_device(*dev)
+            torch.cuda.synchronize()
+            for a, d in zip(again, dev):
+                assert np.array_equal(a, d.cpu().numpy().reshape(gpu.N, gpu.G).T)
+        rng = np.random.default_rng(7)
+        ends = rng.uniform(0.0, 1.0, size=(p["M"], 4, 600, 2))
+        gpu.set_ends(ends)
+        after = gpu.moments()
+        orc = oracle_mod.OracleSolver(p)
+        orc.set_ends(ends)
+        for a, b in zip(after, orc.moments()):
+            assert (np.abs(a - b) / np.abs(b).max(axis=1, keepdims=True)).max() <= 1e-13
+        gpu.set_moments_form(0)
+        assert all(np.array_equal(a, b) for a, b in zip(gpu.moments(), after))
+
+
 @pytest.mark.parametrize("bc_left", [0, 2])
 def test_ramp_launches_cut_into_rounds(rtsn_mod, oracle_mod, bc_left):
     """Ramp launches of more positions than one round of four-wave workgroups holds (128 groups
