@@ -297,8 +297,7 @@ rt_status rt_sweep_geometry(rt_solver *s, int *workgroups, long long *tiles);
 /* ---- test and A/B hooks -------------------------------------------------
  * Kernel forms the tests compare bitwise and the measurements time against each other
  * (the library reads no environment variable to pick a kernel or a schedule; the variables
- * read are RTSN_COMM_TIMEOUT_S, RTSN_POOL_MB, RTSN_EXPORT_CHUNK -- cells per chunk of the
- * rt_get_psi / rt_get_ends / rt_set_ends transfers, for testing the chunk edges -- and, in
+ * read are RTSN_COMM_TIMEOUT_S, RTSN_POOL_MB and, in
  * bin/transfer and bin/test_gray, TRANSFER_DIR, RT_TABLE_DIR, RTSN_QUIET and the rank
  * variables RTSN_RANKS, RTSN_DEVICE_BASE and RTSN_FAULT_STALL_RANK, a test hook).
  * Moments kernel where M/2 is 8, 16 or 32: 1 (default) the producer/consumer
@@ -313,6 +312,10 @@ rt_status rt_set_phi_correction_form(rt_solver *s, int form);
  * sub-launches commits each sub-launch's chain positions as soon as it is in the stream, so
  * the next call (rt_advance, rt_finish, a read-out) runs exactly the positions still owed. */
 rt_status rt_debug_fail_launch(rt_solver *s, int after);
+/* Host transfers in pieces of at most `doubles` doubles (0: the defaults, 256 MB device
+ * chunks and 16 MB pinned pieces; moments then come in one transfer per state): the chunk
+ * edges of rt_get_psi / rt_get_ends / rt_set_ends and the staged moments, for testing. */
+rt_status rt_debug_set_transfer_chunk(rt_solver *s, long long doubles);
 
 /* ---- material-temperature coupling (beyond the reference) ---------------
  * The reference holds T constant (solver.cpp:157).  With coupling enabled the

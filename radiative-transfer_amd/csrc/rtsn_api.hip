@@ -398,6 +398,13 @@ extern "C" rt_status rt_debug_fail_launch(rt_solver *s, int after) {
   return RT_OK;
 }
 
+extern "C" rt_status rt_debug_set_transfer_chunk(rt_solver *s, long long doubles) {
+  if (!s) return fail(nullptr, RT_ERR_ARG, "rt_debug_set_transfer_chunk: NULL handle");
+  if (doubles < 0) return fail(s, RT_ERR_ARG, "rt_debug_set_transfer_chunk: 0 (default) or doubles per piece");
+  s->transfer_chunk = doubles;
+  return RT_OK;
+}
+
 extern "C" rt_status rt_sweep_geometry(rt_solver *s, int *workgroups, long long *tiles) {
   if (!s) return fail(nullptr, RT_ERR_ARG, "rt_sweep_geometry: NULL handle");
   if (workgroups) *workgroups = 2 * s->Q * s->Sg;  // one 64-lane wave per (line group, segment)

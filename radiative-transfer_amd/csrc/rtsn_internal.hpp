@@ -239,6 +239,7 @@ struct rt_solver {
   int tail = 0;                  // draining: the run's last steps (< Tpipe), each position's final block
   int resume_lo = -1, resume_hi = -1;  // positions a failed sub-launch still owes (pipe_launch)
   int fail_launch_after = -1;    // test hook (rt_debug_fail_launch): pipelined sub-launches before one fails
+  long long transfer_chunk = 0;  // test hook (rt_debug_set_transfer_chunk): doubles per host transfer piece, 0 default
   int moments_form = 1;          // rt_set_moments_form: 1 producer/consumer, 0 one-wave (bitwise equal)
   int phi_corr_form = 0;         // rt_set_phi_correction_form: 0 closed forms, 1 the cell-by-cell walk
   // material-temperature coupling (rt_material_enable)

@@ -40,7 +40,7 @@ constexpr size_t kExportChunk = size_t(1) << 25;  // doubles
 static int chunk_cells(const rt_solver *s) {
   const size_t per_cell = static_cast<size_t>(s->p.M) * s->Gl;
   size_t chunk = kExportChunk;
-  if (const char *env = std::getenv("RTSN_EXPORT_CHUNK")) chunk = std::max(1L, std::atol(env));  // tests
+  if (s->transfer_chunk > 0) chunk = static_cast<size_t>(s->transfer_chunk);  // rt_debug_set_transfer_chunk
   return static_cast<int>(std::max<size_t>(1, std::min<size_t>(s->p.N, chunk / per_cell)));
 }
 
@@ -83,7 +83,7 @@ constexpr size_t kStagedPiece = size_t(1) << 21;  // 16 MB
 static rt_status staged_d2h(rt_solver *s, double *host, const double *dev, size_t count) {
   if (rt_status st = ensure_staging(s, sizeof(double) * std::min(count, kStagedPiece))) return st;
   size_t piece = std::min(kStagedPiece, s->staging_bytes / sizeof(double));
-  if (const char *env = std::getenv("RTSN_EXPORT_CHUNK")) piece = std::min(piece, size_t(std::max(1L, std::atol(env))));  // tests
+  if (s->transfer_chunk > 0) piece = std::min(piece, static_cast<size_t>(s->transfer_chunk));  // rt_debug_set_transfer_chunk
   hipError_t e = hipSuccess;
   size_t k = 0, prev = 0, prev_n = 0;
   for (size_t o = 0; o < count && e == hipSuccess; o += piece, ++k) {
@@ -220,7 +220,7 @@ extern "C" rt_status rt_get_moments(rt_solver *s, double *phi, double *F, double
   const size_t GN = static_cast<size_t>(s->Gl) * s->p.N;
   const double *m = static_cast<const double *>(s->mom.p);
   double *dst[3] = {phi, F, phi_plus};
-  if (3 * GN <= kStagedPiece) {  // the three fields ([3][GN] in `mom`) in one transfer, once per state
+  if (3 * GN <= kStagedPiece && s->transfer_chunk == 0) {  // the three fields ([3][GN] in `mom`) in one transfer, once per state
     if (s->mom_host_serial != s->mom_serial) {
       if (s->mom_host_cap < sizeof(double) * 3 * GN) {
         ResourcePool::get().release(true, s->mom_host, s->mom_host_cap, 0);

@@ -125,6 +125,7 @@ def lib():
         L.rt_set_moments_form.argtypes = [vp, C.c_int]
         L.rt_set_phi_correction_form.argtypes = [vp, C.c_int]
         L.rt_debug_fail_launch.argtypes = [vp, C.c_int]
+        L.rt_debug_set_transfer_chunk.argtypes = [vp, C.c_longlong]
         L.rt_get_level_waves.argtypes = [vp, C.POINTER(C.c_int)]
         L.rt_set_wavefront.argtypes = [vp, C.c_int]
         L.rt_get_wavefront.argtypes = [vp, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)]
@@ -632,6 +633,11 @@ class Solver:
     def debug_fail_launch(self, after: int):
         """rt_debug_fail_launch: the pipelined sub-launch after `after` more fails (-1: off)."""
         _check(lib().rt_debug_fail_launch(self._h, int(after)), "rt_debug_fail_launch", self._h)
+
+    def debug_set_transfer_chunk(self, doubles: int):
+        """rt_debug_set_transfer_chunk: host transfers in pieces of at most `doubles` doubles
+        (0: the defaults)."""
+        _check(lib().rt_debug_set_transfer_chunk(self._h, int(doubles)), "rt_debug_set_transfer_chunk", self._h)
 
     def pipeline_state(self) -> dict:
         """{"lag_steps", "queued_steps", "pending"} (rt_pipeline_state)."""

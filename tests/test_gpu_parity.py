@@ -240,9 +240,10 @@ def test_time_block_switching(rtsn_mod, oracle_mod, toggle):
         compare_all(gpu, orc)
 
 
-def test_chunked_transfers(rtsn_mod, oracle_mod, monkeypatch):
+def test_chunked_transfers(rtsn_mod, oracle_mod):
     """rt_get_psi / rt_get_ends / rt_set_ends move the reference layouts through a bounded
-    device buffer, a chunk of cells at a time: with 1000-double chunks (4 cells of
+    device buffer, a chunk of cells at a time: with 1000-double chunks
+    (rt_debug_set_transfer_chunk; 4 cells of
     llnl_slab_test's M G = 248, 13 chunks, the last one ragged) the results are bitwise
     those of one chunk, and set_ends(ends()) is the identity; the moments' staged copies
     in 1000-double pieces likewise."""
@@ -250,7 +251,7 @@ def test_chunked_transfers(rtsn_mod, oracle_mod, monkeypatch):
     with rtsn_mod.Solver(p) as s:
         s.solve()
         psi, ends, mom = s.psi(), s.ends(), s.moments()
-        monkeypatch.setenv("RTSN_EXPORT_CHUNK", "1000")
+        s.debug_set_transfer_chunk(1000)
         assert np.array_equal(s.psi(), psi)
         assert np.array_equal(s.ends(), ends)
         for a, b in zip(s.moments(), mom):  # pinned staging in 1000-double pieces (7 per field)
@@ -258,7 +259,7 @@ def test_chunked_transfers(rtsn_mod, oracle_mod, monkeypatch):
         s.set_ends(ends[..., ::-1].copy())  # nodes swapped: a different state, loaded in chunks
         assert np.array_equal(s.ends(), ends[..., ::-1])
         s.set_ends(ends)
-        monkeypatch.delenv("RTSN_EXPORT_CHUNK")
+        s.debug_set_transfer_chunk(0)
         assert np.array_equal(s.ends(), ends)
         assert np.array_equal(s.psi(), psi)
 

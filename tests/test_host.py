@@ -41,7 +41,7 @@ def test_getenv_only_documented():
     import re
     src = REPO / "radiative-transfer_amd" / "csrc"
     allowed = {"TRANSFER_DIR", "RT_TABLE_DIR", "RTSN_QUIET", "RTSN_COMM_TIMEOUT_S", "RTSN_POOL_MB",
-               "RTSN_EXPORT_CHUNK", "RTSN_DEVICE_BASE", "RTSN_FAULT_STALL_RANK", "RTSN_RANKS"}
+               "RTSN_DEVICE_BASE", "RTSN_FAULT_STALL_RANK", "RTSN_RANKS"}
     read, knobs = set(), []
     for f in sorted(src.iterdir()):
         text = f.read_text()
