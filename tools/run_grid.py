@@ -1,6 +1,6 @@
 """Whole-run time of n BDF2 steps on the SL slab with G groups (advance + finish + sync,
 pipelined) over a grid of time block T, waves per segment KW (rt_set_level_waves, used by
-every launch of the run) and segments per line (RTSN_WAVES_PER_CU = w: Sg = CUs w / (2 Q)):
+every launch of the run) and segments per line (rt_set_segmentation(w): Sg = CUs w / (2 Q)):
 the data behind the small-shard schedule.  A fresh handle per configuration
 at dt = 1e-9 (RTSN_GRID_DT), where the reference's BDF2 keeps the SL state finite for more
 than 4000 steps (profiles/archive/r03j_finite_horizon.jsonl; at 1e-7 it overflows within 400 and
@@ -19,13 +19,12 @@ import rtsn  # noqa: E402
 
 G, runs = int(sys.argv[1]), [int(x) for x in sys.argv[2].split(",")]
 Ts, KWs, Ws = ([int(x) for x in a.split(",")] for a in sys.argv[3:6])
-import os as _os
-p = dict(bench.slab_params(G, "v0"), dt=float(_os.environ.get("RTSN_GRID_DT", "1e-9")))
+p = dict(bench.slab_params(G, "v0"), dt=float(os.environ.get("RTSN_GRID_DT", "1e-9")))
 for w in Ws:
-    os.environ["RTSN_WAVES_PER_CU"] = str(w)
     for T in Ts:
         for kw in KWs:
             with rtsn.Solver(p) as s:
+                s.set_segmentation(w)
                 s.pipeline = 2
                 try:
                     s.time_block = T
