@@ -885,125 +885,93 @@ __device__ __forceinline__ bool nearly_equal(double a, double b) {
   return d <= 2.220446049250313e-16 * fabs(a + b) * 2 || d < 2.2250738585072014e-308;
 }
 
-// Bose series of the normalised integral from z1 to z2 (Planck.cpp:94-118):
-// n_terms is the first n >= 32 whose next term falls below the accuracy
-// relative to the leading one (capped so a bad input cannot spin).  The
-// powers e^{-k z} come from one exp and a running product, and
-// P(k z) / k^4 = r (z^3 + r (3 z^2 + r (6 z + 6 r))) with r = 1/k (rk: a
-// table for k <= 64); the terms are summed in ascending k (the reference sums
-// descending): the same value to a few ulps, for two exps per integral
-// instead of two per term.
-__device__ double planck_series(double z1, double z2, double accuracy, const double *rk) {
+// Bose series of the normalised integrals from z1 to z2 of B (Planck.cpp:94-118) and of
+// dB/dT (:170-193), side by side: each series' n_terms is the first n >= 32 whose next term
+// falls below the accuracy relative to its leading one (capped so a bad input cannot spin).
+// The powers e^{-k z} come from one exp and a running product shared by both, and
+// P(k z) / k^4 = r (z^3 + r (3 z^2 + r (6 z + 6 r))), P4(k z) / k^4 = z^4 + r (4 z^3 +
+// r (12 z^2 + r (24 z + 24 r))) with r = 1/k (rk: a table for k <= 64); the terms are summed
+// in ascending k (the reference sums descending): the same values to a few ulps, for two
+// exps per pair of series instead of two per term.  Each sum stops at its own n_terms, so
+// the pair equals the two series evaluated one after the other, bit for bit.
+struct PlanckPair {
+  double b, db;
+};
+
+__device__ PlanckPair planck_series_pair(double z1, double z2, double accuracy, const double *rk) {
   const double e1 = exp(-z1), f1 = exp(-z2);
   const double a1 = z1 * z1 * z1, b1 = 3.0 * (z1 * z1), c1 = 6.0 * z1;
   const double a2 = z2 * z2 * z2, b2 = 3.0 * (z2 * z2), c2 = 6.0 * z2;
+  const double qa1 = (z1 * z1) * (z1 * z1), qb1 = 4.0 * (z1 * z1 * z1), qc1 = 12.0 * (z1 * z1), qd1 = 24.0 * z1;
+  const double qa2 = (z2 * z2) * (z2 * z2), qb2 = 4.0 * (z2 * z2 * z2), qc2 = 12.0 * (z2 * z2), qd2 = 24.0 * z2;
   auto pr = [](double r, double a, double b, double c) { return r * (a + r * (b + r * (c + 6.0 * r))); };
+  auto pq = [](double r, double a, double b, double c, double d) { return a + r * (b + r * (c + r * (d + 24.0 * r))); };
   auto recip = [rk](int k) { return k <= 64 ? rk[k] : 1.0 / k; };
   const double lead = fmax(e1 * (a1 + b1 + c1 + 6.0), 2.220446049250313e-16);
+  const double qlead = fmax(e1 * (qa1 + qb1 + qc1 + qd1 + 24.0), 2.220446049250313e-16);
   const double stop = accuracy * (1.0 - e1) * lead;  // next term <= accuracy, without the divisions
-  int n = 32;
+  const double qstop = accuracy * (1.0 - e1) * qlead;
+  int n = 32, qn = 32;
   for (double em = exp(-33.0 * z1); n < 4096; ++n, em *= e1)
     if (!(em * pr(recip(n + 1), a1, b1, c1) > stop)) break;
-  double s1 = 0.0, s2 = 0.0, p1 = 1.0, p2 = 1.0;
-  for (int k = 1; k <= n; ++k) {
+  for (double em = exp(-33.0 * z1); qn < 4096; ++qn, em *= e1)
+    if (!(em * pq(recip(qn + 1), qa1, qb1, qc1, qd1) > qstop)) break;
+  const int nmax = n > qn ? n : qn;
+  double s1 = 0.0, s2 = 0.0, t1 = 0.0, t2 = 0.0, p1 = 1.0, p2 = 1.0;
+  for (int k = 1; k <= nmax; ++k) {
     p1 *= e1;
     p2 *= f1;
     if (p1 == 0.0) break;  // e^{-k z1} underflowed: so has every later term
     const double r = recip(k);
-    s1 += p1 * pr(r, a1, b1, c1);
-    s2 += p2 * pr(r, a2, b2, c2);
+    if (k <= n) {
+      s1 += p1 * pr(r, a1, b1, c1);
+      s2 += p2 * pr(r, a2, b2, c2);
+    }
+    if (k <= qn) {
+      t1 += p1 * pq(r, qa1, qb1, qc1, qd1);
+      t2 += p2 * pq(r, qa2, qb2, qc2, qd2);
+    }
   }
-  return s1 - s2;
+  return PlanckPair{s1 - s2, t1 - t2};
 }
 
-// The dB/dT series (Planck.cpp:170-193): the same walk with the quartic
-// P4(k z) / k^4 = z^4 + r (4 z^3 + r (12 z^2 + r (24 z + 24 r))), r = 1/k.
-__device__ double planck_series_dBdT(double z1, double z2, double accuracy, const double *rk) {
-  const double e1 = exp(-z1), f1 = exp(-z2);
-  const double a1 = (z1 * z1) * (z1 * z1), b1 = 4.0 * (z1 * z1 * z1), c1 = 12.0 * (z1 * z1), d1 = 24.0 * z1;
-  const double a2 = (z2 * z2) * (z2 * z2), b2 = 4.0 * (z2 * z2 * z2), c2 = 12.0 * (z2 * z2), d2 = 24.0 * z2;
-  auto pr = [](double r, double a, double b, double c, double d) { return a + r * (b + r * (c + r * (d + 24.0 * r))); };
-  auto recip = [rk](int k) { return k <= 64 ? rk[k] : 1.0 / k; };
-  const double lead = fmax(e1 * (a1 + b1 + c1 + d1 + 24.0), 2.220446049250313e-16);
-  const double stop = accuracy * (1.0 - e1) * lead;
-  int n = 32;
-  for (double em = exp(-33.0 * z1); n < 4096; ++n, em *= e1)
-    if (!(em * pr(recip(n + 1), a1, b1, c1, d1) > stop)) break;
-  double s1 = 0.0, s2 = 0.0, p1 = 1.0, p2 = 1.0;
-  for (int k = 1; k <= n; ++k) {
-    p1 *= e1;
-    p2 *= f1;
-    if (p1 == 0.0) break;
-    const double r = recip(k);
-    s1 += p1 * pr(r, a1, b1, c1, d1);
-    s2 += p2 * pr(r, a2, b2, c2, d2);
-  }
-  return s1 - s2;
-}
-
-// 12-point Gauss-Legendre of the Planck density over [mid - hw, mid + hw]
-// (Planck.cpp:129-140; k_B = 1 keV/keV)
-__device__ double planck_gauss(const PlanckCells &pc, double inv_T, double mid, double hw, double pre) {
-  double acc = 0.0;
-#pragma unroll
-  for (int r = 0; r < 12; ++r) {
-    const double E = mid + hw * pc.node[r];
-    acc += hw * pc.weight[r] * (pre * (E * E * E) / (exp(E * inv_T) - 1.0));
-  }
-  return acc;
-}
-
-// ... of its temperature derivative (Planck.h:113-125)
-__device__ double planck_gauss_dBdT(const PlanckCells &pc, double inv_T, double mid, double hw, double pre) {
-  double acc = 0.0;
+// 12-point Gauss-Legendre of the Planck density and of its temperature derivative over
+// [mid - hw, mid + hw] (Planck.cpp:129-140, Planck.h:113-125; k_B = 1 keV/keV), one exp per
+// node for both
+__device__ PlanckPair planck_gauss_pair(const PlanckCells &pc, double inv_T, double mid, double hw, double pre) {
+  double acc = 0.0, dacc = 0.0;
 #pragma unroll
   for (int r = 0; r < 12; ++r) {
     const double E = mid + hw * pc.node[r];
     const double ex = exp(E * inv_T), em1 = ex - 1.0;
-    acc += hw * pc.weight[r] * (pre * ((E * E) * (E * E)) * (inv_T * inv_T) * ex / (em1 * em1));
+    acc += hw * pc.weight[r] * (pre * (E * E * E) / em1);
+    dacc += hw * pc.weight[r] * (pre * ((E * E) * (E * E)) * (inv_T * inv_T) * ex / (em1 * em1));
   }
-  return acc;
+  return PlanckPair{acc, dacc};
 }
 
-// Planck::integrate_dBdT (Planck.cpp:161-229) for T > 0, the branches of planck_integral
-__device__ double planck_integral_dBdT(const PlanckCells &pc, double T, double e_min, double e_max, double pre,
-                                       const double *rk) {
-  if (nearly_equal(e_min, e_max)) return 0.0;
+// Planck::integrate_B (Planck.cpp:85-154) and integrate_dBdT (:161-229) for T > 0, the same
+// branches: Gauss below z = 0.7, series above z = 0.5, split at z = 0.6; x 4 pi.
+// pre = 2 / (h^3 c^2).
+__device__ PlanckPair planck_integral_pair(const PlanckCells &pc, double T, double e_min, double e_max, double pre,
+                                           const double *rk) {
+  if (nearly_equal(e_min, e_max)) return PlanckPair{0.0, 0.0};
   const double inv_T = 1.0 / T;
   const double z1 = e_min * inv_T, z2 = e_max * inv_T;
-  const double t3 = (T * T) * T;
-  double v;
+  const double t3 = (T * T) * T, t4 = (T * T) * (T * T);
+  PlanckPair v;
   if (z2 <= 0.7) {
-    v = planck_gauss_dBdT(pc, inv_T, 0.5 * (e_max + e_min), 0.5 * (e_max - e_min), pre);
+    v = planck_gauss_pair(pc, inv_T, 0.5 * (e_max + e_min), 0.5 * (e_max - e_min), pre);
   } else if (z1 >= 0.5) {
-    v = pre * t3 * planck_series_dBdT(z1, z2, pc.accuracy, rk);
+    const PlanckPair sv = planck_series_pair(z1, z2, pc.accuracy, rk);
+    v = PlanckPair{pre * t4 * sv.b, pre * t3 * sv.db};
   } else {
     const double e6 = 0.6 * T;
-    v = planck_gauss_dBdT(pc, inv_T, 0.5 * (e6 + e_min), 0.5 * (e6 - e_min), pre) +
-        pre * t3 * planck_series_dBdT(0.6, z2, pc.accuracy, rk);
+    const PlanckPair gv = planck_gauss_pair(pc, inv_T, 0.5 * (e6 + e_min), 0.5 * (e6 - e_min), pre);
+    const PlanckPair sv = planck_series_pair(0.6, z2, pc.accuracy, rk);
+    v = PlanckPair{gv.b + pre * t4 * sv.b, gv.db + pre * t3 * sv.db};
   }
-  return v * 4.0 * 3.1415926546;
-}
-
-// Planck::integrate_B (Planck.cpp:85-154) for T > 0: Gauss below z = 0.7,
-// series above z = 0.5, split at z = 0.6; x 4 pi.  pre = 2 / (h^3 c^2).
-__device__ double planck_integral(const PlanckCells &pc, double T, double e_min, double e_max, double pre,
-                                  const double *rk) {
-  if (nearly_equal(e_min, e_max)) return 0.0;
-  const double inv_T = 1.0 / T;
-  const double z1 = e_min * inv_T, z2 = e_max * inv_T;
-  const double t4 = (T * T) * (T * T);
-  double v;
-  if (z2 <= 0.7) {
-    v = planck_gauss(pc, inv_T, 0.5 * (e_max + e_min), 0.5 * (e_max - e_min), pre);
-  } else if (z1 >= 0.5) {
-    v = pre * t4 * planck_series(z1, z2, pc.accuracy, rk);
-  } else {
-    const double e6 = 0.6 * T;
-    v = planck_gauss(pc, inv_T, 0.5 * (e6 + e_min), 0.5 * (e6 - e_min), pre) +
-        pre * t4 * planck_series(0.6, z2, pc.accuracy, rk);
-  }
-  return v * 4.0 * 3.1415926546;
+  return PlanckPair{v.b * 4.0 * 3.1415926546, v.db * 4.0 * 3.1415926546};
 }
 
 // B[x][gl] = kcon * integral over group g_lo + gl at T(x); the last group takes
@@ -1045,14 +1013,14 @@ __global__ __launch_bounds__(kPlanckThreads) void planck_cells_kernel(PlanckCell
         double b = 0.0, db = 0.0;
         if (hot) {
           if (g < pc.G - 1) {
-            b = pc.kcon * planck_integral(pc, T, pc.e_edge[g], pc.e_edge[g + 1], pre, rk);
-            db = pc.kcon * planck_integral_dBdT(pc, T, pc.e_edge[g], pc.e_edge[g + 1], pre, rk);
+            const PlanckPair v = planck_integral_pair(pc, T, pc.e_edge[g], pc.e_edge[g + 1], pre, rk);
+            b = pc.kcon * v.b;
+            db = pc.kcon * v.db;
           } else {
-            const double rest =
-                pc.a_c * ((T * T) * (T * T)) - planck_integral(pc, T, pc.e_edge[0], pc.e_edge[pc.G - 1], pre, rk);
+            const PlanckPair v = planck_integral_pair(pc, T, pc.e_edge[0], pc.e_edge[pc.G - 1], pre, rk);
+            const double rest = pc.a_c * ((T * T) * (T * T)) - v.b;
             b = rest > 0.0 ? pc.kcon * rest : 0.0;
-            const double drest = 4.0 * pc.a_c * ((T * T) * T) -
-                                 planck_integral_dBdT(pc, T, pc.e_edge[0], pc.e_edge[pc.G - 1], pre, rk);
+            const double drest = 4.0 * pc.a_c * ((T * T) * T) - v.db;
             db = drest > 0.0 ? pc.kcon * drest : 0.0;
           }
         }
