@@ -988,9 +988,11 @@ __device__ PlanckPair planck_integral_pair(const PlanckCells &pc, double T, doub
 // A block owns 64 cells (one per lane) and walks the groups wave by wave, so
 // a wave evaluates ONE group at 64 temperatures -- the branch (Gauss / series
 // / split) and the series length are then nearly uniform across the wave --
-// and stages the tiles in LDS to write them back as contiguous [x][g] rows.
-constexpr int kPlanckCells = 64, kPlanckGroups = 64, kPlanckThreads = 256;
-__global__ __launch_bounds__(kPlanckThreads) void planck_cells_kernel(PlanckCells pc, const double *Tc, double *B) {
+// and stages the tiles in LDS to write them back as contiguous [x][g] rows.  Four waves
+// per SIMD (127 VGPRs, 36 KB of LDS per block, 32-group tiles): the exp and series chains
+// are latency-bound at two (SL coupled step: 5.95 -> 4.52 ms, profiles/r06t_material_kernels.json).
+constexpr int kPlanckCells = 64, kPlanckGroups = 32, kPlanckThreads = 256;
+__global__ __launch_bounds__(kPlanckThreads) __attribute__((amdgpu_waves_per_eu(4, 4))) void planck_cells_kernel(PlanckCells pc, const double *Tc, double *B) {
   __shared__ double tile[2][kPlanckCells * (kPlanckGroups + 1)];
   __shared__ double bsum[kPlanckThreads / 64][kPlanckCells];
   __shared__ double rk[65];
