@@ -157,3 +157,53 @@ def test_table_stream_semantics(rtsn_mod, oracle_mod, tmp_path):
                 rtsn_mod.ParameterHandler(f, table_dir=tmp_path)
             with pytest.raises(oracle_mod.OracleError):
                 oracle_mod.parse_prm(f, table_dir=tmp_path)
+
+
+# Random .prm files from the reader's grammar (seeded): keys the reference reads and junk
+# keys, spaces around keys and values, comment and '='-less lines, duplicates, CRLF, and
+# numeric strings from a pool of the conversions' edge shapes (signs, hex, exponents with and
+# without digits, inf / nan, overflow / subnormal, garbage suffixes).  Tables stay off (their
+# files are covered above); M, G and N stay small and positive.
+_NUM = ["0", "1", "2", "4", "-1", "+3", "007", " 5", "6 ", "\t8", "1.5", ".5", "5.", "-0", "1e3", "1e", "2.5e+",
+        "1e-320", "1e-400", "1e999", "-1e999", "0x10", "0x1p-2", "inf", "-inf", "nan", "NaN", "12abc", "abc", "",
+        "2147483647", "2147483648", "-2147483649", "99999999999", "1.2.3", "1,5", "-", "+", "3 4", "0.1e-5x"]
+_BOOL = ["yes", "Yes", "YES", "true", "True", "TRUE", "no", "1", "", " yes", "yes "]
+# (M, G, N > 0: the product's reader refuses others with RT_ERR_PARAM, where the reference's
+# sizes its psi_source matrix and fails later)
+_SMALL = ["1", "2", "3", "4", "6", "8", " 2", "2 ", "+3", "007", "abc", "", "2.9", "1e1"]
+
+
+def _random_prm(rng) -> str:
+    lines = []
+    for _ in range(int(rng.integers(0, 14))):
+        kind = rng.random()
+        if kind < 0.1:
+            lines.append("#" + str(rng.choice(INTS + DOUBLES)) + "=1")
+            continue
+        if kind < 0.15:
+            lines.append(str(rng.choice(["junk line", "", "   ", "M 4"])))
+            continue
+        key = str(rng.choice(INTS + DOUBLES + BOOLS + ("psi_source", "unknown_key")))
+        if key in ("M", "G", "N"):
+            val = str(rng.choice(_SMALL))
+        elif key in BOOLS:
+            val = str(rng.choice(_BOOL))
+        elif key == "psi_source":
+            val = " ".join(str(rng.choice(_NUM)) for _ in range(int(rng.integers(0, 7))))
+        else:
+            val = str(rng.choice(_NUM))
+        pad_k = str(rng.choice(["", "", "", " "]))
+        lines.append(f"{key}{pad_k}={val}" + str(rng.choice(["", "", "", " # c", "=x"])))
+    sep = "\r\n" if rng.random() < 0.2 else "\n"
+    return sep.join(lines) + (sep if rng.random() < 0.8 else "")
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_random_prm_files(rtsn_mod, oracle_mod, tmp_path, seed):
+    """40 random files per seed (320 in all) parse the same through the reference's reader,
+    the product's and the oracle's, values bit for bit, errors exactly where it throws."""
+    rng = np.random.default_rng(20261018 + seed)
+    for i in range(40):
+        f = tmp_path / f"r{seed}_{i}.prm"
+        f.write_bytes(_random_prm(rng).encode())
+        check(f, rtsn_mod, oracle_mod)
