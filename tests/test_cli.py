@@ -82,6 +82,60 @@ def test_eigen_text_format(text_driver, tmp_path, rows, cols, vals):
     assert out.read_text() == eigen_text(a)
 
 
+DRIVER_BIN = r"""
+#include "eigen_text.hpp"
+#include <cstdio>
+#include <cstdlib>
+#include <fstream>
+#include <iostream>
+#include <vector>
+int main(int argc, char **argv) {
+  // argv: in.bin out rows cols left -- doubles ColMajor from in.bin; left: std::left on the stream
+  const size_t r = std::atol(argv[3]), c = std::atol(argv[4]);
+  std::vector<double> v(r * c);
+  FILE *f = std::fopen(argv[1], "rb");
+  if (!f || std::fread(v.data(), sizeof(double), v.size(), f) != v.size()) return 2;
+  std::fclose(f);
+  std::ofstream os(argv[2]);
+  if (std::atoi(argv[5])) os << std::left;
+  rtamd::write_eigen_text(os, v.data(), r, c);
+  os << std::endl;
+  return os ? 0 : 1;
+}
+"""
+
+
+def _c_g6(v: float) -> str:
+    """printf("%.6g") as C prints it (Python drops the sign of a negative NaN)."""
+    return ("-nan" if np.signbit(v) else "nan") if np.isnan(v) else "%.6g" % v
+
+
+@pytest.mark.parametrize("seed", range(4))
+@pytest.mark.parametrize("left", [False, True])
+def test_eigen_text_random(tmp_path, seed, left):
+    """The C++ writer on 4000 random coefficients per case -- random bit patterns (subnormals,
+    huge, inf, nan of either sign), values at the 6-digit rounding edges, plain decimals --
+    against the restatement: the default stream (the one-pass snprintf path) and a stream
+    carrying std::left (the per-coefficient stream path), byte for byte."""
+    rng = np.random.default_rng(7000 + seed)
+    bits = rng.integers(0, 2**63, size=1500, dtype=np.uint64) | (rng.integers(0, 2, 1500, dtype=np.uint64) << 63)
+    edge = np.array([999999.5, 9999995.0, 0.00099999995, 1e-5, 99999.95, 1e16, 1e-7, 123456.5, 5e-324, -0.0])
+    vals = np.concatenate([bits.view(np.float64), rng.choice(edge, 500) * rng.choice([1, -1, 10, 0.1], 500),
+                           np.round(rng.normal(0, 1e3, 2000), rng.integers(0, 9))])
+    rows, cols = 40, 100
+    src, exe = tmp_path / "drv.cpp", tmp_path / "drv"
+    src.write_text(DRIVER_BIN)
+    subprocess.run(["g++", "-std=c++17", "-O1", f"-I{PKG / 'csrc'}", str(src), "-o", str(exe)], check=True)
+    (tmp_path / "in.bin").write_bytes(vals.astype("<f8").tobytes())
+    out = tmp_path / "m.csv"
+    subprocess.run([str(exe), str(tmp_path / "in.bin"), str(out), str(rows), str(cols), str(int(left))], check=True)
+    a = vals.reshape(cols, rows).T
+    s = [[_c_g6(v) for v in row] for row in a]
+    w = max(len(x) for row in s for x in row)
+    pad = (lambda x: x.ljust(w)) if left else (lambda x: x.rjust(w))
+    assert out.read_text() == "\n".join(" ".join(pad(x) for x in row) for row in s) + "\n"
+
+
 def test_tensor_text_layout():
     psi = np.arange(2 * 3 * 4, dtype=float).reshape(2, 3, 4)
     lines = tensor_text(psi).splitlines()
