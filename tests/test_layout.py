@@ -204,3 +204,58 @@ def test_layout_plans_under_address_sanitizer(tmp_path):
     r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "0 failures" in r.stdout
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_random_tilings_round_trip(rtsn_mod, seed):
+    """Seeded random problems and tilings (1-16 ranks; contiguous group shards, some empty,
+    or direction-pair shards of uneven size): random blocks packed by each rank, gathered
+    (stacked / summed) and unpacked land exactly where the whole-problem arrays hold them, and
+    psi / psi_source placement rebuilds the whole arrays bitwise."""
+    rng = np.random.default_rng(900 + seed)
+    modes = []
+    for it in range(12):
+        M = int(rng.choice([2, 4, 8, 16]))
+        G, N = int(rng.integers(1, 40)), int(rng.integers(1, 30))
+        H = M // 2
+        direction = H >= 2 and it % 3 == 0  # a third of the problems on direction-pair shards
+        n = int(rng.integers(2, H + 1)) if direction else int(rng.integers(1, 17))
+        modes.append(direction)
+        if direction:
+            cuts = np.sort(rng.choice(np.arange(1, H), n - 1, replace=False))
+            edges = [0, *map(int, cuts), H]
+            shards = [dict(G=G, M=M, g_lo=0, g_hi=G, d_lo=edges[r], d_hi=edges[r + 1], N=N) for r in range(n)]
+        else:
+            edges = [0, *sorted(map(int, rng.integers(0, G + 1, n - 1))), G]  # empty shards allowed
+            shards = [dict(G=G, M=M, g_lo=edges[r], g_hi=edges[r + 1], d_lo=0, d_hi=H, N=N) for r in range(n)]
+        lay = rtsn_mod.Layout(shards)
+        assert lay.mode == (1 if direction else 0)
+        psi = rng.normal(size=(M, G, N))
+        src = rng.normal(size=(M, G))
+        out, table = np.full(M * G * N, np.nan), np.full(M * G, np.nan)
+        if direction:
+            mom = [rng.normal(size=(n, N, G)) for _ in range(3)]  # per-rank partials
+            blocks = [lay.pack_moments(r, mom[0][r], mom[1][r], mom[2][r]) for r in range(n)]
+            total = sum(blocks[1:], blocks[0].copy())
+            for k, a in enumerate(lay.unpack_moments(total)):
+                assert np.array_equal(a, total[k])
+            for r, sh in enumerate(shards):
+                idx = list(range(H - sh["d_hi"], H - sh["d_lo"])) + list(range(H + sh["d_lo"], H + sh["d_hi"]))
+                lay.place_psi(r, _flat_psi(psi[idx]), out)
+                lay.place_psi_source(r, src[idx].ravel(), table)
+        else:
+            mom = [rng.normal(size=(N, G)) for _ in range(3)]
+            vec = [rng.normal(size=G) for _ in range(2)]
+            blocks = [lay.pack_moments(r, *(m[:, sh["g_lo"]:sh["g_hi"]] for m in mom)) for r, sh in enumerate(shards)]
+            for a, want in zip(lay.unpack_moments(np.stack(blocks)), mom):
+                assert np.array_equal(a, want)
+            vb = [lay.pack_vectors(r, [v[sh["g_lo"]:sh["g_hi"]] for v in vec]) for r, sh in enumerate(shards)]
+            for a, want in zip(lay.unpack_vectors(2, np.stack(vb)), vec):
+                assert np.array_equal(a, want)
+            for r, sh in enumerate(shards):
+                if sh["g_hi"] > sh["g_lo"]:
+                    lay.place_psi(r, _flat_psi(psi[:, sh["g_lo"]:sh["g_hi"]]), out)
+            lay.place_psi_source(0, src.ravel(), table)
+        assert np.array_equal(out, _flat_psi(psi))
+        assert np.array_equal(table, src.ravel())
+    assert any(modes) and not all(modes)
