@@ -173,6 +173,7 @@ class OracleSolver:
             raise OracleError(f"orc_create -> {ORC_ERRORS.get(st.value, st.value)}")
         self.M, self.G, self.N = p.M, p.G, p.N
         self.Gl = L.orc_num_groups_local(self._h)
+        self.g_lo = int(g_lo)  # first group of the handle (its groups: g_lo .. g_lo + Gl - 1)
 
     def __del__(self):
         h = getattr(self, "_h", None)
