@@ -334,11 +334,17 @@ rt_status rt_debug_set_transfer_chunk(rt_solver *s, long long doubles);
  *      relaxes T toward the radiation's temperature at any dt / rho_cv (linear grey
  *      analysis; the explicit dT = dt q / rho_cv of rounds 1-5 needed
  *      dt W b / rho_cv < 2 + sigma c dt) and keeps T > 0 for BE (dT > -T since
- *      B_g <= T dB_g/dT);
+ *      B_g <= T dB_g/dT).  Where dT > T / 4 the tangent of the convex B under-counts
+ *      the emission at the new T (a cold cell beside hot ones absorbs many times its
+ *      energy in a step: the linear update overshoots, then diverges; cooling, it only
+ *      lags): the cell solves rho_cv (T' - T) = dt (A - W S(T'))
+ *      instead, A = q + W S(T^n), S(T) = sum over ALL groups of sigma_g B_g(T) --
+ *      every handle holds every group's edges and opacity, so no second reduction;
+ *      one root (S increases), by Newton's method with bisection;
  *   4. the material thereby emitted dt W sigma_g dB_g/dT dT per group beyond the
- *      sweep's B: it joins the group's owed emission, paid in the next sweeps as
- *      p_g = max(owed_g, -B_g) (Beff >= 0; all of it unless the material cooled by
- *      a large fraction of T in one step).
+ *      sweep's B (B_g(T^{n+1}) - B_g(T^n) where it solved the full emission): it joins
+ *      the group's owed emission, paid in the next sweeps as p_g = max(owed_g, -B_g)
+ *      (Beff >= 0; all of it unless the material cooled by a large fraction of T).
  * With ts_method 1 (BE) radiation + material + owed energy,
  * sum_x dx (sum_g phi_g / c + rho_cv T + rt_get_material_transit), changes by
  * exactly -dt x (net boundary outflow) per step (up to rounding).  Requires the

@@ -560,6 +560,7 @@ struct orc_solver {
   double *owed;       /* N x Gl: emission the material owes the radiation, not yet paid (B units) */
   double *dTlast;     /* N: the last update's temperature change (0 before the first) */
   double *bpart;      /* N: sum over the local groups of sigma_g dB_g/dT(T(c)) */
+  unsigned char *newton; /* N: the last update solved the cell's full emission (material_solve_cell) */
   double rho_cv, wsum;
   int mat_it;         /* substep counter of the coupled steps (_it of solve()) */
   int equil_done;
@@ -811,7 +812,7 @@ void orc_destroy(orc_solver *s) {
   free(s->cB); free(s->cdBdT); free(s->kappa_edge); free(s->dEB); free(s->dsigEdE); free(s->dkapEB);
   free(s->cor1); free(s->cor2); free(s->cor3); free(s->total_correction);
   free(s->psi); free(s->ends); free(s->prev_ends); free(s->half_ends);
-  free(s->Tcell); free(s->Bcell); free(s->dBcell); free(s->Beff); free(s->owed); free(s->dTlast); free(s->bpart);
+  free(s->Tcell); free(s->Bcell); free(s->dBcell); free(s->Beff); free(s->owed); free(s->dTlast); free(s->bpart); free(s->newton);
   free(s);
 }
 
@@ -1122,7 +1123,8 @@ double orc_planck_cell_dBdT(double T, int G, const double *e_edge, int g) {
 }
 
 /* Per cell at the new T(c), per local group: the owed emission grows by dB_g/dT(T_old) dT
- * (what the last implicit update let the material emit beyond the sweep's B); B_g(T); the
+ * (what the last implicit update let the material emit beyond the sweep's B; B_g(T) - B_g(T_old)
+ * for a cell whose update solved the full emission); B_g(T); the
  * next sweep pays p_g = max(owed_g, -B_g) of it -- Beff_g = B_g + p_g >= 0 -- and owed_g
  * keeps the rest; then dB_g/dT(T) and bpart(c) = sum over the local groups (ascending) of
  * sigma_g dB_g/dT. */
@@ -1133,8 +1135,10 @@ static void material_planck(orc_solver *s) {
     for (int gl = 0; gl < s->Gl; ++gl) {
       const int g = s->g_lo + gl;
       const size_t o = (size_t)c * s->Gl + gl;
-      const double owed = s->owed[o] + s->dBcell[o] * s->dTlast[c];
       const double B = planck_cell(&s->planck, s->Tcell[c], s->G, s->e_edge, g);
+      /* what the last update let the material emit beyond the sweep's B: the linearised
+       * dB/dT dT, or B(T^{n+1}) - B(T^n) where it solved the full emission */
+      const double owed = s->newton[c] ? s->owed[o] + (B - s->Bcell[o]) : s->owed[o] + s->dBcell[o] * s->dTlast[c];
       const double dB = planck_cell_dBdT(&s->planck, s->Tcell[c], s->G, s->e_edge, g);
       const double pay = owed > -B ? owed : -B;
       s->Bcell[o] = B;
@@ -1172,10 +1176,12 @@ int orc_material_enable(orc_solver *s, double rho_cv, const double *T_cells) {
   if (!s->dBcell) s->dBcell = (double *)xcalloc((size_t)s->N * s->Gl, sizeof(double), &ok);
   if (!s->Beff) s->Beff = (double *)xcalloc((size_t)s->N * s->Gl, sizeof(double), &ok);
   if (!s->owed) s->owed = (double *)xcalloc((size_t)s->N * s->Gl, sizeof(double), &ok);
+  if (!s->newton) s->newton = (unsigned char *)xcalloc(s->N, 1, &ok);
   if (!ok) return ORC_ERR_NOMEM;
   for (int c = 0; c < s->N; ++c) {
     s->Tcell[c] = T_cells ? T_cells[c] : s->p.T;
     s->dTlast[c] = 0.0;
+    s->newton[c] = 0;
     for (int gl = 0; gl < s->Gl; ++gl) s->owed[(size_t)c * s->Gl + gl] = 0.0;
   }
   s->rho_cv = rho_cv;
@@ -1216,15 +1222,70 @@ int orc_material_sweep(orc_solver *s, double *qb) {
   return ORC_OK;
 }
 
-/* From qb (2N: q and b summed over all groups): dT = dt q / (rho_cv + dt W b), T += dT,
+/* S(T) = sum over ALL G groups of sigma_g B_g(T), and its derivative (planck_cell's groups) */
+static void material_emission_all(const orc_solver *s, double T, double *S, double *dS) {
+  double a = 0.0, d = 0.0;
+  for (int g = 0; g < s->G; ++g) {
+    const double sigma = s->rho[g] * s->kappa[g];
+    a += sigma * planck_cell(&s->planck, T, s->G, s->e_edge, g);
+    d += sigma * planck_cell_dBdT(&s->planck, T, s->G, s->e_edge, g);
+  }
+  *S = a;
+  *dS = d;
+}
+
+/* A cell whose linearised update would heat it by more than MAT_NEWTON_FRAC of T (B is convex
+ * in T, so its tangent at T^n under-counts the emission at T^{n+1}: heating, the linear update
+ * overshoots -- a cold cell beside hot ones absorbs many times its energy in one step and
+ * overshoots by orders of magnitude, then diverges; cooling, it only lags, T staying above the
+ * full solution) solves the full emission instead:
+ *   rho_cv (T' - T) = dt (A - W S(T')),  A = q + W S(T) = sum_g sigma_g phi_g (all groups),
+ * S over ALL groups (every handle holds every group's edges and opacity, so a shard needs no
+ * second reduction).  S is increasing and 0 for T' <= 0, so the root is unique: in
+ * [0, T + dt A / rho_cv] when the material keeps a positive energy, else T + dt A / rho_cv.
+ * Newton's method, bisection where a step leaves the bracket. */
+#define MAT_NEWTON_FRAC 0.25
+static double material_solve_cell(const orc_solver *s, double T, double q) {
+  const double W = s->wsum, dt = s->dt, rc = s->rho_cv;
+  double S0, dS0;
+  material_emission_all(s, T, &S0, &dS0);
+  const double A = q + W * S0;
+  const double hi0 = T + dt * A / rc; /* f(hi0) = dt W S(hi0) >= 0 */
+  if (!(hi0 > 0.0)) return hi0;       /* no emission left to balance: the linear root, <= 0 */
+  double lo = 0.0, hi = hi0, x = T > 0.0 && T < hi0 ? T : 0.5 * hi0;
+  for (int it = 0; it < 200; ++it) {
+    double S, dS;
+    material_emission_all(s, x, &S, &dS);
+    const double f = rc * (x - T) + dt * W * S - dt * A;
+    if (f > 0.0) hi = x; else lo = x;
+    const double fp = rc + dt * W * dS;
+    double xn = x - f / fp;
+    if (!(xn > lo && xn < hi)) xn = 0.5 * (lo + hi);
+    if (fabs(xn - x) <= 1e-15 * fabs(xn) || hi - lo <= 1e-15 * hi) return xn;
+    x = xn;
+  }
+  return x;
+}
+
+/* From qb (2N: q and b summed over all groups): dT = dt q / (rho_cv + dt W b), T += dT --
+ * or, where dT > MAT_NEWTON_FRAC T, the root of the full emission (material_solve_cell) --
  * then the Planck terms at the new T and the next emission (see orc_material_enable). */
 void orc_material_update(orc_solver *s, const double *qb) {
   const double W = s->wsum, dt = s->dt, rc = s->rho_cv;
   for (int c = 0; c < s->N; ++c) {
     const double q = qb[c], b = qb[(size_t)s->N + c];
+    const double T = s->Tcell[c];
     const double dT = dt * q / (rc + dt * W * b);
-    s->Tcell[c] = s->Tcell[c] + dT;
-    s->dTlast[c] = dT;
+    if (dT <= MAT_NEWTON_FRAC * T) {
+      s->Tcell[c] = T + dT;
+      s->dTlast[c] = dT;
+      s->newton[c] = 0;
+    } else {
+      const double Tn = material_solve_cell(s, T, q);
+      s->Tcell[c] = Tn;
+      s->dTlast[c] = Tn - T;
+      s->newton[c] = 1;
+    }
   }
   material_planck(s);
 }

@@ -974,6 +974,23 @@ __device__ PlanckPair planck_integral_pair(const PlanckCells &pc, double T, doub
   return PlanckPair{v.b * 4.0 * 3.1415926546, v.db * 4.0 * 3.1415926546};
 }
 
+// kcon B_g(T) and kcon dB_g/dT(T) of group g (0 .. G-1): the integral over the group, the last
+// group the grey remainder a c T^4 - (the integral over groups 0..G-2 as one) and its
+// derivative, each only where positive; T <= 0 (or nearly 0, Planck.h:84-90) or not finite: 0
+__device__ PlanckPair cell_group_planck(const PlanckCells &pc, double T, int g, double pre, const double *rk) {
+  if (!(T > 0.0 && isfinite(T) && !nearly_equal(T, 0.0))) return PlanckPair{0.0, 0.0};
+  if (g < pc.G - 1) {
+    const PlanckPair v = planck_integral_pair(pc, T, pc.e_edge[g], pc.e_edge[g + 1], pre, rk);
+    return PlanckPair{pc.kcon * v.b, pc.kcon * v.db};
+  }
+  const PlanckPair v = planck_integral_pair(pc, T, pc.e_edge[0], pc.e_edge[pc.G - 1], pre, rk);
+  const double rest = pc.a_c * ((T * T) * (T * T)) - v.b;
+  const double drest = 4.0 * pc.a_c * ((T * T) * T) - v.db;
+  return PlanckPair{rest > 0.0 ? pc.kcon * rest : 0.0, drest > 0.0 ? pc.kcon * drest : 0.0};
+}
+
+constexpr double kPlanckPre = 2.0 / ((4.141895e-10 * 4.141895e-10 * 4.141895e-10) * (299.792458 * 299.792458));
+
 // B[x][gl] = kcon * integral over group g_lo + gl at T(x); the last group takes
 // the grey remainder a c T^4 - (integral over groups 0..G-2) when positive
 // (Planck.cpp:73-76; the sum of the other groups as one integral over their
@@ -996,8 +1013,7 @@ __global__ __launch_bounds__(kPlanckThreads) __attribute__((amdgpu_waves_per_eu(
   __shared__ double tile[2][kPlanckCells * (kPlanckGroups + 1)];
   __shared__ double bsum[kPlanckThreads / 64][kPlanckCells];
   __shared__ double rk[65];
-  const double hc = 4.141895e-10, c = 299.792458;
-  const double pre = 2.0 / ((hc * hc * hc) * (c * c));
+  const double pre = kPlanckPre;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nwave = blockDim.x >> 6;
   if (threadIdx.x <= 64) rk[threadIdx.x] = threadIdx.x ? 1.0 / threadIdx.x : 0.0;
   const int ntiles = (pc.N + kPlanckCells - 1) / kPlanckCells;
@@ -1005,6 +1021,7 @@ __global__ __launch_bounds__(kPlanckThreads) __attribute__((amdgpu_waves_per_eu(
     const int x0 = t * kPlanckCells, nx = min(kPlanckCells, pc.N - x0);
     const double T = lane < nx ? Tc[x0 + lane] : 0.0;
     const double dT = lane < nx ? pc.dTlast[x0 + lane] : 0.0;
+    const bool newton = lane < nx && pc.newton[x0 + lane];
     const bool hot = T > 0.0 && isfinite(T) && !nearly_equal(T, 0.0);
     double bacc = 0.0;  // this wave's groups of sigma_g dB_g/dT at cell lane
     for (int g0 = 0; g0 < pc.Gl; g0 += kPlanckGroups) {
@@ -1014,23 +1031,19 @@ __global__ __launch_bounds__(kPlanckThreads) __attribute__((amdgpu_waves_per_eu(
         const int g = pc.g_lo + g0 + j;
         double b = 0.0, db = 0.0;
         if (hot) {
-          if (g < pc.G - 1) {
-            const PlanckPair v = planck_integral_pair(pc, T, pc.e_edge[g], pc.e_edge[g + 1], pre, rk);
-            b = pc.kcon * v.b;
-            db = pc.kcon * v.db;
-          } else {
-            const PlanckPair v = planck_integral_pair(pc, T, pc.e_edge[0], pc.e_edge[pc.G - 1], pre, rk);
-            const double rest = pc.a_c * ((T * T) * (T * T)) - v.b;
-            b = rest > 0.0 ? pc.kcon * rest : 0.0;
-            const double drest = 4.0 * pc.a_c * ((T * T) * T) - v.db;
-            db = drest > 0.0 ? pc.kcon * drest : 0.0;
-          }
+          const PlanckPair v = cell_group_planck(pc, T, g, pre, rk);
+          b = v.b;
+          db = v.db;
         }
         double pay = 0.0;
         if (lane < nx) {
 #pragma clang fp contract(off)
           const size_t o = static_cast<size_t>(g0 + j) * pc.N + x0 + lane;
-          const double owed = pc.owed[o] + pc.dB[o] * dT;
+          // what the last update let the material emit beyond the sweep's B: the linearised
+          // dB/dT dT, or B(T^{n+1}) - B(T^n) where it solved the full emission (B still holds
+          // B(T^n): this block writes its cells' rows after the sync below)
+          const double owed = newton ? pc.owed[o] + (b - B[static_cast<size_t>(x0 + lane) * pc.Gl + g0 + j])
+                                     : pc.owed[o] + pc.dB[o] * dT;
           pay = owed > -b ? owed : -b;
           pc.owed[o] = owed - pay;
           pc.dB[o] = db;
@@ -1580,14 +1593,66 @@ __global__ void material_q_kernel(const double *phi, int nparts, const double *B
 
 // dT = dt q / (rho_cv + dt W b), T += dT (rt_oracle.c orc_material_update, the same
 // expressions unfused); dT kept for the next Planck pass's owed emission
-__global__ void material_update_kernel(double *T, const double *qb, double *dTlast, double dt, double rho_cv, double W,
-                                       int N) {
-#pragma clang fp contract(off)
+// S(T) = sum over ALL G groups of sigma_g B_g(T) and its derivative (rt_oracle.c
+// material_emission_all)
+__device__ PlanckPair material_emission_all(const PlanckCells &pc, double T, const double *rk) {
+  double a = 0.0, d = 0.0;
+  for (int g = 0; g < pc.G; ++g) {
+    const PlanckPair v = cell_group_planck(pc, T, g, kPlanckPre, rk);
+    a += pc.sigma_all[g] * v.b;
+    d += pc.sigma_all[g] * v.db;
+  }
+  return PlanckPair{a, d};
+}
+
+// dT = dt q / (rho_cv + dt W b), T += dT (rt_oracle.c orc_material_update, the same
+// expressions unfused); dT kept for the next Planck pass's owed emission.  Where dT > T / 4
+// the tangent of the convex B under-counts the emission at the new T (heating a cold cell
+// beside hot ones, the linear update overshot by 10^3 and diverged; cooling it only lags):
+// the cell solves rho_cv (T' - T) = dt (A - W S(T')),
+// A = q + W S(T), S over all groups -- increasing, 0 for T' <= 0: one root, bracketed in
+// [0, T + dt A / rho_cv] -- by Newton's method with bisection (rt_oracle.c material_solve_cell).
+constexpr double kNewtonFrac = 0.25;
+__global__ void material_update_kernel(PlanckCells pc, double *T, const double *qb, double *dTlast,
+                                       unsigned char *newton, double dt, double rho_cv, double W, int N) {
+  __shared__ double rk[65];
+  if (threadIdx.x <= 64) rk[threadIdx.x] = threadIdx.x ? 1.0 / threadIdx.x : 0.0;
+  __syncthreads();
   for (int x = blockIdx.x * blockDim.x + threadIdx.x; x < N; x += gridDim.x * blockDim.x) {
-    const double q = qb[x], b = qb[N + x];
-    const double dT = dt * q / (rho_cv + dt * W * b);
-    T[x] = T[x] + dT;
-    dTlast[x] = dT;
+    const double q = qb[x], b = qb[N + x], T0 = T[x];
+    double dT;
+    {
+#pragma clang fp contract(off)
+      dT = dt * q / (rho_cv + dt * W * b);
+    }
+    if (dT <= kNewtonFrac * T0) {
+#pragma clang fp contract(off)
+      T[x] = T0 + dT;
+      dTlast[x] = dT;
+      newton[x] = 0;
+      continue;
+    }
+    const PlanckPair s0 = material_emission_all(pc, T0, rk);
+    const double A = q + W * s0.b;
+    const double hi0 = T0 + dt * A / rho_cv;  // f(hi0) = dt W S(hi0) >= 0
+    double Tn = hi0;
+    if (hi0 > 0.0) {
+      double lo = 0.0, hi = hi0, t = T0 > 0.0 && T0 < hi0 ? T0 : 0.5 * hi0;
+      Tn = t;
+      for (int it = 0; it < 200; ++it) {
+        const PlanckPair sv = material_emission_all(pc, t, rk);
+        const double f = rho_cv * (t - T0) + dt * W * sv.b - dt * A;
+        if (f > 0.0) hi = t; else lo = t;
+        double tn = t - f / (rho_cv + dt * W * sv.db);
+        if (!(tn > lo && tn < hi)) tn = 0.5 * (lo + hi);
+        Tn = tn;
+        if (fabs(tn - t) <= 1e-15 * fabs(tn) || hi - lo <= 1e-15 * hi) break;
+        t = tn;
+      }
+    }
+    T[x] = Tn;
+    dTlast[x] = Tn - T0;
+    newton[x] = 1;
   }
 }
 
@@ -1927,10 +1992,10 @@ hipError_t launch_material_q(const double *phi, int nparts, const double *B, con
   return hipGetLastError();
 }
 
-hipError_t launch_material_update(double *T, const double *qb, double *dTlast, double dt, double rho_cv, double W,
-                                  int N, hipStream_t st) {
-  hipLaunchKernelGGL(material_update_kernel, dim3(grid_for(static_cast<size_t>(N), 256)), dim3(256), 0, st, T, qb,
-                     dTlast, dt, rho_cv, W, N);
+hipError_t launch_material_update(const PlanckCells &pc, double *T, const double *qb, double *dTlast,
+                                  unsigned char *newton, double dt, double rho_cv, double W, int N, hipStream_t st) {
+  hipLaunchKernelGGL(material_update_kernel, dim3(grid_for(static_cast<size_t>(N), 256)), dim3(256), 0, st, pc, T,
+                     qb, dTlast, newton, dt, rho_cv, W, N);
   return hipGetLastError();
 }
 

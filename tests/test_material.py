@@ -146,6 +146,37 @@ def test_stiff_emission_stays_stable(oracle_mod, kappa, T_rad, T_mat):
         assert abs(resid) <= 1e-12 * max(abs(e0), abs(e1)), (n, resid, e0)
 
 
+@pytest.mark.parametrize("rho_cv,kappa", [(0.63, 32.0), (0.04, 5.0), (0.013, 83.0)])
+def test_far_from_equilibrium_cells_stay_bounded(oracle_mod, rho_cv, kappa):
+    """Cells at 0.35-28 keV, cell to cell at random, small heat capacity, BE: a cold cell
+    beside hot ones absorbs many times its energy in one step, where the update linearised
+    about T^n overshot by 10^3 and diverged within four steps (T -> inf, found by
+    tests/test_random_gpu.py).  Those cells solve the full emission (dT > T / 4): T stays
+    finite, > 0 and below the hottest initial temperature, the emission >= 0, and radiation +
+    material + owed energy balance the boundary outflow to rounding every step."""
+    p = params(oracle_mod, ts=1, G=10, N=42, M=2, bc_left=2, bc_right=1, kappa=kappa, dt=1.3e-4, T=1.5,
+               efirst=0.35, elast=11.5)
+    rng = np.random.default_rng(5)
+    p["psi_source"] = rng.uniform(0.0, 2.0, size=(p["M"], p["G"]))
+    T0 = 10.0 ** rng.uniform(np.log10(0.35), np.log10(28.0), size=p["N"])
+    s = oracle_mod.OracleSolver(p)
+    s.material_enable(rho_cv, T0)
+    def parts(s):  # the energy's terms by magnitude: the residual's rounding scale
+        phi = s.moments()[0]
+        return p["dx"] * float((np.abs(phi).sum(axis=0) / C_LIGHT + rho_cv * np.abs(s.temperature())
+                                + np.abs(s.material_transit())).sum())
+
+    for n in range(12):
+        e0, m0 = total_energy(s, p, rho_cv), parts(s)
+        s.material_step(1)
+        e1, m1 = total_energy(s, p, rho_cv), parts(s)
+        T = s.temperature()
+        assert np.isfinite(T).all() and np.all(T > 0.0) and T.max() <= T0.max(), (n, T.min(), T.max())
+        assert np.all(s.cell_emission() >= 0.0), n
+        resid = (e1 - e0) + p["dt"] * net_outflow(s, p)
+        assert abs(resid) <= 1e-12 * (m0 + m1), (n, resid, e0, m0, m1)
+
+
 def test_cell_planck_edge_temperatures(oracle_mod):
     e = np.array([0.0, 0.1, 1.0, 10.0])
     for T in (0.0, -1.0, float("nan"), float("inf")):

@@ -76,3 +76,37 @@ def test_random_configuration(rtsn_mod, oracle_mod, seed):
                 orc = oracle_mod.OracleSolver(dict(p, max_timesteps=done))
                 orc.solve()
                 compare_all(gpu, orc)
+
+
+def _material_case(oracle_mod, seed):
+    from test_material import params
+    rng = np.random.default_rng(47000 + seed)
+    M = int(rng.choice([2, 4, 6, 8, 16]))
+    G = int(rng.integers(1, 11))
+    N = int(np.exp(rng.uniform(0.0, np.log(2000.0))))
+    ts = int(rng.choice([1, 1, 2, 3]))
+    bc_left, bc_right = BC_PAIRS[int(rng.integers(len(BC_PAIRS)))]
+    dt = float(10.0 ** rng.uniform(-5, -4 if ts == 3 else -3))
+    p = params(oracle_mod, ts=ts, dt=dt, M=M, G=G, N=N, bc_left=bc_left, bc_right=bc_right,
+               kappa=float(10.0 ** rng.uniform(-1, 3)), T=float(10.0 ** rng.uniform(-0.5, 1.5)),
+               efirst=float(10.0 ** rng.uniform(-2, -0.3)), elast=float(10.0 ** rng.uniform(0.7, 2)))
+    p["psi_source"] = rng.uniform(0.0, 2.0, size=(M, G))
+    T0 = 10.0 ** rng.uniform(-0.5, 1.5, size=N)
+    if rng.random() < 0.5:  # a smooth profile instead of cell-to-cell noise
+        T0 = np.sort(T0) if rng.random() < 0.5 else np.full(N, float(T0[0]))
+    return p, T0, float(10.0 ** rng.uniform(-2, 2)), int(rng.integers(1, 7)), int(rng.choice([0, 0, 1, 4, 16]))
+
+
+@pytest.mark.parametrize("seed", range(60))
+def test_random_material_configuration(rtsn_mod, oracle_mod, seed):
+    """The material coupling on seeded random configurations: quadrature, groups, cells,
+    scheme, boundaries, opacity (0.1 .. 1e3), radiation and cell temperatures (0.3 .. 30 keV,
+    noisy, sorted or uniform), rho c_v (0.01 .. 100: stiffness from ~0 to ~1e6), group grid,
+    dt, steps and segmentation: T, psi, B, Beff and the owed energy against the oracle
+    (test_material_gpu.compare)."""
+    from test_material_gpu import compare, run_pair
+    p, T0, rho_cv, steps, wgs = _material_case(oracle_mod, seed)
+    gpu, orc = run_pair(rtsn_mod, oracle_mod, p, steps, rho_cv=rho_cv, T0=T0, wgs_per_cu=wgs)
+    with gpu:
+        compare(gpu, orc)
+        assert np.isfinite(gpu.temperature()).all()
