@@ -560,7 +560,6 @@ struct orc_solver {
   double *owed;       /* N x Gl: emission the material owes the radiation, not yet paid (B units) */
   double *dTlast;     /* N: the last update's temperature change (0 before the first) */
   double *bpart;      /* N: sum over the local groups of sigma_g dB_g/dT(T(c)) */
-  unsigned char *newton; /* N: the last update solved the cell's full emission (material_solve_cell) */
   double rho_cv, wsum;
   int mat_it;         /* substep counter of the coupled steps (_it of solve()) */
   int equil_done;
@@ -812,7 +811,7 @@ void orc_destroy(orc_solver *s) {
   free(s->cB); free(s->cdBdT); free(s->kappa_edge); free(s->dEB); free(s->dsigEdE); free(s->dkapEB);
   free(s->cor1); free(s->cor2); free(s->cor3); free(s->total_correction);
   free(s->psi); free(s->ends); free(s->prev_ends); free(s->half_ends);
-  free(s->Tcell); free(s->Bcell); free(s->dBcell); free(s->Beff); free(s->owed); free(s->dTlast); free(s->bpart); free(s->newton);
+  free(s->Tcell); free(s->Bcell); free(s->dBcell); free(s->Beff); free(s->owed); free(s->dTlast); free(s->bpart);
   free(s);
 }
 
@@ -1123,8 +1122,8 @@ double orc_planck_cell_dBdT(double T, int G, const double *e_edge, int g) {
 }
 
 /* Per cell at the new T(c), per local group: the owed emission grows by dB_g/dT(T_old) dT
- * (what the last implicit update let the material emit beyond the sweep's B; B_g(T) - B_g(T_old)
- * for a cell whose update solved the full emission); B_g(T); the
+ * (what the last implicit update let the material emit beyond the sweep's B; a cell whose
+ * update solved the full emission added B_g(T) - B_g(T_old) there and left dT 0); B_g(T); the
  * next sweep pays p_g = max(owed_g, -B_g) of it -- Beff_g = B_g + p_g >= 0 -- and owed_g
  * keeps the rest; then dB_g/dT(T) and bpart(c) = sum over the local groups (ascending) of
  * sigma_g dB_g/dT. */
@@ -1135,10 +1134,8 @@ static void material_planck(orc_solver *s) {
     for (int gl = 0; gl < s->Gl; ++gl) {
       const int g = s->g_lo + gl;
       const size_t o = (size_t)c * s->Gl + gl;
+      const double owed = s->owed[o] + s->dBcell[o] * s->dTlast[c];
       const double B = planck_cell(&s->planck, s->Tcell[c], s->G, s->e_edge, g);
-      /* what the last update let the material emit beyond the sweep's B: the linearised
-       * dB/dT dT, or B(T^{n+1}) - B(T^n) where it solved the full emission */
-      const double owed = s->newton[c] ? s->owed[o] + (B - s->Bcell[o]) : s->owed[o] + s->dBcell[o] * s->dTlast[c];
       const double dB = planck_cell_dBdT(&s->planck, s->Tcell[c], s->G, s->e_edge, g);
       const double pay = owed > -B ? owed : -B;
       s->Bcell[o] = B;
@@ -1176,12 +1173,10 @@ int orc_material_enable(orc_solver *s, double rho_cv, const double *T_cells) {
   if (!s->dBcell) s->dBcell = (double *)xcalloc((size_t)s->N * s->Gl, sizeof(double), &ok);
   if (!s->Beff) s->Beff = (double *)xcalloc((size_t)s->N * s->Gl, sizeof(double), &ok);
   if (!s->owed) s->owed = (double *)xcalloc((size_t)s->N * s->Gl, sizeof(double), &ok);
-  if (!s->newton) s->newton = (unsigned char *)xcalloc(s->N, 1, &ok);
   if (!ok) return ORC_ERR_NOMEM;
   for (int c = 0; c < s->N; ++c) {
     s->Tcell[c] = T_cells ? T_cells[c] : s->p.T;
     s->dTlast[c] = 0.0;
-    s->newton[c] = 0;
     for (int gl = 0; gl < s->Gl; ++gl) s->owed[(size_t)c * s->Gl + gl] = 0.0;
   }
   s->rho_cv = rho_cv;
@@ -1279,12 +1274,15 @@ void orc_material_update(orc_solver *s, const double *qb) {
     if (dT <= MAT_NEWTON_FRAC * T) {
       s->Tcell[c] = T + dT;
       s->dTlast[c] = dT;
-      s->newton[c] = 0;
     } else {
+      /* the material emitted B_g(T') - B_g(T) beyond the sweep's B: owed now, no dT term */
       const double Tn = material_solve_cell(s, T, q);
+      for (int gl = 0; gl < s->Gl; ++gl) {
+        const size_t o = (size_t)c * s->Gl + gl;
+        s->owed[o] = s->owed[o] + (planck_cell(&s->planck, Tn, s->G, s->e_edge, s->g_lo + gl) - s->Bcell[o]);
+      }
       s->Tcell[c] = Tn;
-      s->dTlast[c] = Tn - T;
-      s->newton[c] = 1;
+      s->dTlast[c] = 0.0;
     }
   }
   material_planck(s);

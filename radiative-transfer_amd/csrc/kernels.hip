@@ -1021,7 +1021,6 @@ __global__ __launch_bounds__(kPlanckThreads) __attribute__((amdgpu_waves_per_eu(
     const int x0 = t * kPlanckCells, nx = min(kPlanckCells, pc.N - x0);
     const double T = lane < nx ? Tc[x0 + lane] : 0.0;
     const double dT = lane < nx ? pc.dTlast[x0 + lane] : 0.0;
-    const bool newton = lane < nx && pc.newton[x0 + lane];
     const bool hot = T > 0.0 && isfinite(T) && !nearly_equal(T, 0.0);
     double bacc = 0.0;  // this wave's groups of sigma_g dB_g/dT at cell lane
     for (int g0 = 0; g0 < pc.Gl; g0 += kPlanckGroups) {
@@ -1039,11 +1038,7 @@ __global__ __launch_bounds__(kPlanckThreads) __attribute__((amdgpu_waves_per_eu(
         if (lane < nx) {
 #pragma clang fp contract(off)
           const size_t o = static_cast<size_t>(g0 + j) * pc.N + x0 + lane;
-          // what the last update let the material emit beyond the sweep's B: the linearised
-          // dB/dT dT, or B(T^{n+1}) - B(T^n) where it solved the full emission (B still holds
-          // B(T^n): this block writes its cells' rows after the sync below)
-          const double owed = newton ? pc.owed[o] + (b - B[static_cast<size_t>(x0 + lane) * pc.Gl + g0 + j])
-                                     : pc.owed[o] + pc.dB[o] * dT;
+          const double owed = pc.owed[o] + pc.dB[o] * dT;
           pay = owed > -b ? owed : -b;
           pc.owed[o] = owed - pay;
           pc.dB[o] = db;
@@ -1611,10 +1606,11 @@ __device__ PlanckPair material_emission_all(const PlanckCells &pc, double T, con
 // beside hot ones, the linear update overshot by 10^3 and diverged; cooling it only lags):
 // the cell solves rho_cv (T' - T) = dt (A - W S(T')),
 // A = q + W S(T), S over all groups -- increasing, 0 for T' <= 0: one root, bracketed in
-// [0, T + dt A / rho_cv] -- by Newton's method with bisection (rt_oracle.c material_solve_cell).
+// [0, T + dt A / rho_cv] -- by Newton's method with bisection (rt_oracle.c material_solve_cell);
+// its owed emission grows by B_g(T') - B_g(T) here and dTlast is 0 (no dB/dT dT term).
 constexpr double kNewtonFrac = 0.25;
-__global__ void material_update_kernel(PlanckCells pc, double *T, const double *qb, double *dTlast,
-                                       unsigned char *newton, double dt, double rho_cv, double W, int N) {
+__global__ void material_update_kernel(PlanckCells pc, double *T, const double *qb, double *dTlast, double dt,
+                                       double rho_cv, double W, int N) {
   __shared__ double rk[65];
   if (threadIdx.x <= 64) rk[threadIdx.x] = threadIdx.x ? 1.0 / threadIdx.x : 0.0;
   __syncthreads();
@@ -1629,7 +1625,6 @@ __global__ void material_update_kernel(PlanckCells pc, double *T, const double *
 #pragma clang fp contract(off)
       T[x] = T0 + dT;
       dTlast[x] = dT;
-      newton[x] = 0;
       continue;
     }
     const PlanckPair s0 = material_emission_all(pc, T0, rk);
@@ -1638,6 +1633,22 @@ __global__ void material_update_kernel(PlanckCells pc, double *T, const double *
     double Tn = hi0;
     if (hi0 > 0.0) {
       double lo = 0.0, hi = hi0, t = T0 > 0.0 && T0 < hi0 ? T0 : 0.5 * hi0;
+      if (T0 > 0.0 && s0.b > 0.0) {
+        // start at the root of the grey model S(T') ~ S(T0) (T'/T0)^4 (no Planck terms; from
+        // the linear update, above it: Newton on the convex model converges from the right)
+        const double k = dt * W * s0.b / (T0 * T0 * T0 * T0);
+        double m = fmin(T0 + dT, hi0);
+        for (int it = 0; it < 60; ++it) {
+          const double m2 = m * m, fm = rho_cv * (m - T0) + k * m2 * m2 - dt * A;
+          const double mn = m - fm / (rho_cv + 4.0 * k * m2 * m);
+          if (!(mn > 0.0) || fabs(mn - m) <= 1e-3 * m) {
+            m = mn > 0.0 ? mn : m;
+            break;
+          }
+          m = mn;
+        }
+        if (m > lo && m < hi) t = m;
+      }
       Tn = t;
       for (int it = 0; it < 200; ++it) {
         const PlanckPair sv = material_emission_all(pc, t, rk);
@@ -1650,9 +1661,15 @@ __global__ void material_update_kernel(PlanckCells pc, double *T, const double *
         t = tn;
       }
     }
+    // the material emitted B_g(T') - B_g(T0) beyond the sweep's B: owed now, no dT term next
+    for (int gl = 0; gl < pc.Gl; ++gl) {
+#pragma clang fp contract(off)
+      const size_t o = static_cast<size_t>(gl) * N + x;
+      pc.owed[o] = pc.owed[o] + (cell_group_planck(pc, Tn, pc.g_lo + gl, kPlanckPre, rk).b -
+                                 pc.Bcell[static_cast<size_t>(x) * pc.Gl + gl]);
+    }
     T[x] = Tn;
-    dTlast[x] = Tn - T0;
-    newton[x] = 1;
+    dTlast[x] = 0.0;
   }
 }
 
@@ -1992,10 +2009,10 @@ hipError_t launch_material_q(const double *phi, int nparts, const double *B, con
   return hipGetLastError();
 }
 
-hipError_t launch_material_update(const PlanckCells &pc, double *T, const double *qb, double *dTlast,
-                                  unsigned char *newton, double dt, double rho_cv, double W, int N, hipStream_t st) {
+hipError_t launch_material_update(const PlanckCells &pc, double *T, const double *qb, double *dTlast, double dt,
+                                  double rho_cv, double W, int N, hipStream_t st) {
   hipLaunchKernelGGL(material_update_kernel, dim3(grid_for(static_cast<size_t>(N), 256)), dim3(256), 0, st, pc, T,
-                     qb, dTlast, newton, dt, rho_cv, W, N);
+                     qb, dTlast, dt, rho_cv, W, N);
   return hipGetLastError();
 }
 

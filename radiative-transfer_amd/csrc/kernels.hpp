@@ -141,10 +141,8 @@ struct PlanckCells {
   double *Beff;                 // [N][Gl]
   double *bpart;                // [N]
   double b_scale;               // 1, or 0 on a direction shard without pair 0 (b counted once)
-  // the update's full-emission cells (material_update_kernel): flag per cell; there the
-  // owed emission grows by B(T^{n+1}) - B(T^n) instead of dB/dT dT
-  const unsigned char *newton;  // [N]
-  const double *sigma_all;      // [G] rho kappa of every group (S(T) over all groups)
+  const double *sigma_all;      // [G] rho kappa of every group (the update's S(T), all groups)
+  const double *Bcell;          // [N][Gl] B_g(T^n) (the update's full-emission cells: owed += B(T') - B(T^n))
 };
 // B[N][Gl] = B_g(T(x)) and the fields above
 hipError_t launch_planck_cells(const PlanckCells &pc, const double *T, double *B, hipStream_t st);
@@ -170,10 +168,10 @@ hipError_t launch_correction_power(int scheme, const double *map, double *pow, i
 hipError_t launch_material_q(const double *phi, int nparts, const double *B, const double *sigma, double W,
                              const double *bpart, double *q, int Gl, int N, hipStream_t st);
 // from qb = [q, b] summed over all groups: dT = dt q / (rho_cv + dt W b), T(x) += dT, dTlast = dT
-// T += dt q / (rho_cv + dt W b), or the root of the full emission where dT > T / 4 (flag in
-// newton[x]): rt_oracle.c orc_material_update
-hipError_t launch_material_update(const PlanckCells &pc, double *T, const double *qb, double *dTlast,
-                                  unsigned char *newton, double dt, double rho_cv, double W, int N, hipStream_t st);
+// T += dt q / (rho_cv + dt W b), or the root of the full emission where dT > T / 4 (its owed
+// emission added there, dT 0): rt_oracle.c orc_material_update
+hipError_t launch_material_update(const PlanckCells &pc, double *T, const double *qb, double *dTlast, double dt,
+                                  double rho_cv, double W, int N, hipStream_t st);
 // E[x] = scale sum_gl sigma[gl] ((Beff - B) + owed[gl][x]) (rt_get_material_transit)
 hipError_t launch_material_transit(const double *B, const double *Beff, const double *owed, const double *sigma,
                                    double scale, double *E, int Gl, int N, hipStream_t st);

@@ -250,7 +250,7 @@ struct rt_solver {
   // owed, dBcell [Gl][N] the owed emission and dB_g/dT; dTlast [N] the last update's dT; bpart
   // [N] sum_gl sigma dB/dT; qbuf [2N] the exchange buffer (q, b)
   rtsn_detail::DeviceBuf Tcell, Bcell, Beff, owed, dBcell, dTlast, bpart, qbuf, edges, map_unit, hmap_unit, phi_part;
-  rtsn_detail::DeviceBuf newton, sigma_all;  // [N] full-emission update flags; [G] rho kappa of every group
+  rtsn_detail::DeviceBuf sigma_all;  // [G] rho kappa of every group (the update's full-emission cells)
   rtsn_detail::DeviceBuf corr_pow;            // A^Lsub per line for phi_correction_kernel's sub-segments
   int corr_pow_L = 0;            // the Lsub it holds (0: none)
   rtsn_detail::DeviceBuf corr_rows;           // BDF2: rows b A^j and A^64 per line (phi_correction_rows_kernel)

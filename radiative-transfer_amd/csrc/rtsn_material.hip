@@ -70,7 +70,6 @@ extern "C" rt_status rt_material_enable(rt_solver *s, double rho_cv, const doubl
     if (!e) e = dalloc(s->bpart, sizeof(double) * N);
     if (!e) e = dalloc(s->qbuf, sizeof(double) * 2 * N);
     if (!e) e = dalloc(s->edges, sizeof(double) * (s->p.G + 1));
-    if (!e) e = dalloc(s->newton, N);
     if (!e) e = dalloc(s->sigma_all, sizeof(double) * s->p.G);
     if (!e) e = dalloc(s->map_unit, s->map.bytes);
     if (!e) e = dalloc(s->hmap_unit, s->hmap.bytes);
@@ -110,7 +109,6 @@ extern "C" rt_status rt_material_enable(rt_solver *s, double rho_cv, const doubl
   HIP_TRY(s, hipMemsetAsync(s->owed.p, 0, sizeof(double) * NG, s->stream));
   HIP_TRY(s, hipMemsetAsync(s->dBcell.p, 0, sizeof(double) * NG, s->stream));
   if ((st = upload(s, s->edges, s->gt.e_edge.data(), (s->p.G + 1) * sizeof(double)))) return st;
-  HIP_TRY(s, hipMemsetAsync(s->newton.p, 0, N, s->stream));
   {
     std::vector<double> sig(s->p.G);
     for (int g = 0; g < s->p.G; ++g) sig[g] = s->gt.rho[g] * s->gt.kappa[g];
@@ -133,8 +131,8 @@ extern "C" rt_status rt_material_enable(rt_solver *s, double rho_cv, const doubl
   pc.Beff = static_cast<double *>(s->Beff.p);
   pc.bpart = static_cast<double *>(s->bpart.p);
   pc.b_scale = s->d_lo == 0 ? 1.0 : 0.0;  // direction shards: every one holds all groups, count b once
-  pc.newton = static_cast<const unsigned char *>(s->newton.p);
   pc.sigma_all = static_cast<const double *>(s->sigma_all.p);
+  pc.Bcell = static_cast<const double *>(s->Bcell.p);
   s->wsum = 0.0;
   for (double w : s->wt) s->wsum += w;
   {
@@ -227,8 +225,8 @@ extern "C" rt_status rt_material_update(rt_solver *s, const double *d_q) {
   HIP_TRY(s, hipSetDevice(s->device));
   HIP_TRY(s, launch_material_update(s->pc, static_cast<double *>(s->Tcell.p),
                                     d_q ? d_q : static_cast<const double *>(s->qbuf.p),
-                                    static_cast<double *>(s->dTlast.p), static_cast<unsigned char *>(s->newton.p),
-                                    s->p.dt, s->rho_cv, s->wsum_all, s->p.N, s->stream));
+                                    static_cast<double *>(s->dTlast.p), s->p.dt, s->rho_cv, s->wsum_all, s->p.N,
+                                    s->stream));
   return material_planck(s);
 }
 
