@@ -46,13 +46,17 @@ def _case(oracle_mod, seed):
     if rng.random() < 0.4 and steps > 1:
         cuts = sorted(set(int(c) for c in rng.integers(1, steps, size=int(rng.integers(1, 4)))))
         chunks = [b - a for a, b in zip([0] + cuts, cuts + [steps])]
-    return p, sched, chunks
+    shard = (0, 0)
+    if G > 1 and rng.random() < 0.3:  # a group shard [g_lo, g_hi) of the configuration
+        lo = int(rng.integers(0, G))
+        shard = (lo, int(rng.integers(lo + 1, G + 1)))
+    return p, sched, chunks, shard
 
 
 @pytest.mark.parametrize("seed", range(200))
 def test_random_configuration(rtsn_mod, oracle_mod, seed):
-    p, sched, chunks = _case(oracle_mod, seed)
-    with rtsn_mod.Solver(to_rt(p)) as gpu:
+    p, sched, chunks, (g_lo, g_hi) = _case(oracle_mod, seed)
+    with rtsn_mod.Solver(to_rt(p), g_lo=g_lo, g_hi=g_hi) as gpu:
         if "time_block" in sched:
             try:
                 gpu.time_block = sched["time_block"]
@@ -65,7 +69,7 @@ def test_random_configuration(rtsn_mod, oracle_mod, seed):
             gpu.set_segmentation(sched["segmentation"])
         if chunks is None:
             gpu.solve()
-            orc = oracle_mod.OracleSolver(p)
+            orc = oracle_mod.OracleSolver(p, g_lo=g_lo, g_hi=g_hi)
             orc.solve()
             compare_all(gpu, orc)
         else:
@@ -73,7 +77,7 @@ def test_random_configuration(rtsn_mod, oracle_mod, seed):
             for n in chunks:
                 gpu.advance(n)
                 done += n
-                orc = oracle_mod.OracleSolver(dict(p, max_timesteps=done))
+                orc = oracle_mod.OracleSolver(dict(p, max_timesteps=done), g_lo=g_lo, g_hi=g_hi)
                 orc.solve()
                 compare_all(gpu, orc)
 
@@ -94,7 +98,11 @@ def _material_case(oracle_mod, seed):
     T0 = 10.0 ** rng.uniform(-0.5, 1.5, size=N)
     if rng.random() < 0.5:  # a smooth profile instead of cell-to-cell noise
         T0 = np.sort(T0) if rng.random() < 0.5 else np.full(N, float(T0[0]))
-    return p, T0, float(10.0 ** rng.uniform(-2, 2)), int(rng.integers(1, 7)), int(rng.choice([0, 0, 1, 4, 16]))
+    shard = (0, 0)
+    if G > 1 and rng.random() < 0.3:  # a group shard: its own q, as the oracle shard does
+        lo = int(rng.integers(0, G))
+        shard = (lo, int(rng.integers(lo + 1, G + 1)))
+    return p, T0, float(10.0 ** rng.uniform(-2, 2)), int(rng.integers(1, 7)), int(rng.choice([0, 0, 1, 4, 16])), shard
 
 
 @pytest.mark.parametrize("seed", range(60))
@@ -105,8 +113,8 @@ def test_random_material_configuration(rtsn_mod, oracle_mod, seed):
     dt, steps and segmentation: T, psi, B, Beff and the owed energy against the oracle
     (test_material_gpu.compare)."""
     from test_material_gpu import compare, run_pair
-    p, T0, rho_cv, steps, wgs = _material_case(oracle_mod, seed)
-    gpu, orc = run_pair(rtsn_mod, oracle_mod, p, steps, rho_cv=rho_cv, T0=T0, wgs_per_cu=wgs)
+    p, T0, rho_cv, steps, wgs, (g_lo, g_hi) = _material_case(oracle_mod, seed)
+    gpu, orc = run_pair(rtsn_mod, oracle_mod, p, steps, rho_cv=rho_cv, T0=T0, g_lo=g_lo, g_hi=g_hi, wgs_per_cu=wgs)
     with gpu:
         compare(gpu, orc)
         assert np.isfinite(gpu.temperature()).all()

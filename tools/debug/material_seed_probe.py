@@ -13,10 +13,10 @@ import rtsn  # noqa: E402
 import test_random_gpu as t  # noqa: E402
 from test_material_gpu import run_pair  # noqa: E402
 
-p, T0, rc, steps, w = t._material_case(om, int(sys.argv[1]))
+p, T0, rc, steps, w, (lo, hi) = t._material_case(om, int(sys.argv[1]))
 print({k: p[k] for k in ("M", "G", "N", "ts_method", "bc_left", "bc_right", "kappa_grey", "T", "dt", "efirst", "elast")},
       "rho_cv", rc, "steps", steps, "wgs", w)
-gpu, orc = run_pair(rtsn, om, p, steps, rho_cv=rc, T0=T0, wgs_per_cu=w)
+gpu, orc = run_pair(rtsn, om, p, steps, rho_cv=rc, T0=T0, g_lo=lo, g_hi=hi, wgs_per_cu=w)
 with gpu:
     Tg, To = gpu.temperature(), orc.temperature()
     Bg, Bo = gpu.cell_planck(), orc.cell_planck()
